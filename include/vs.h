@@ -1,0 +1,109 @@
+/*
+ * vs.h -- C ABI of the MI355X-native exact flat k-NN backend (libvs.so).
+ *
+ * Drop-in boundary for the vector arithmetic behind the reference's VectorStore
+ * (/root/reference/utils/vector_store.py).  The reference reaches faiss through SWIG at these
+ * call sites; each entry point below replaces one of them:
+ *
+ *   faiss.IndexFlatIP(d) / faiss.IndexFlatL2(d)   utils/vector_store.py:79-81   -> vs_create
+ *   index.add(vector)                             utils/vector_store.py:163-164 -> vs_add
+ *   index.search(vector, k)                       utils/vector_store.py:190-191 -> vs_search
+ *   index.reconstruct(i)                          utils/vector_store.py:207     -> vs_reconstruct
+ *   index.ntotal / index.d                        utils/vector_store.py:183,188,255-258,271 -> vs_ntotal, vs_dim
+ *   _create_index() on clear()                    utils/vector_store.py:277     -> vs_reset
+ *   faiss.write_index (storage payload)           utils/vector_store.py:234     -> vs_reconstruct_n
+ *
+ * Plain pointers and sizes only; no torch types.  Rows are row-major n x d fp32, already
+ * normalised by the Python layer exactly as the reference does it (utils/vector_store.py:83-90).
+ *
+ * Semantics of vs_search (faiss IndexFlat semantics, made exact):
+ *   - IP: D descending, L2: D ascending (squared L2), ties -> lower id.
+ *   - The returned ids are the exact top-k under the canonical fp64 score (oracle/vs_oracle.c);
+ *     D is that score rounded to fp32 (|D - faiss fp32 D| <= 1e-5 for unit vectors).
+ *   - Unfilled slots (k > ntotal): I = -1, D = -FLT_MAX (IP) / +FLT_MAX (L2).
+ *
+ * Errors: every int-returning function returns 0 on success, < 0 on failure; the message is
+ * in vs_last_error() (thread-local).  No C++ exception crosses the ABI.
+ *
+ * Threading: concurrent vs_search* calls on one handle are safe (shared corpus, one stream +
+ * workspace per call from a pool).  vs_add, vs_add_device, vs_add_synthetic and vs_reset take an exclusive lock.
+ */
+#ifndef VS_H_
+#define VS_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct vs_index vs_index;
+
+enum { VS_METRIC_IP = 0, VS_METRIC_L2 = 1 };
+enum { VS_DTYPE_F32 = 0, VS_DTYPE_BF16 = 1, VS_DTYPE_F16 = 2 };
+
+enum {
+    VS_OK = 0,
+    VS_ERR_ARG = -1,          /* bad argument (dims, k, null pointer) */
+    VS_ERR_DEVICE = -2,       /* no HIP device / HIP runtime failure */
+    VS_ERR_OOM = -3,          /* device allocation failed */
+    VS_ERR_UNCERTIFIED = -4,  /* exactness certificate could not be established */
+    VS_ERR_INTERNAL = -5
+};
+
+/* ---- lifecycle (faiss.IndexFlatIP / IndexFlatL2 constructors, utils/vector_store.py:79-81) */
+int vs_create(int d, int metric, int dtype, int device, vs_index** out);
+void vs_destroy(vs_index* index);
+int vs_reset(vs_index* index);                    /* clear(): utils/vector_store.py:273-280 */
+
+/* ---- add (index.add, utils/vector_store.py:164) */
+int vs_add(vs_index* index, const float* x, int64_t n);                 /* host fp32 n x d */
+int vs_add_device(vs_index* index, const float* x_dev, int64_t n, void* stream); /* device fp32 */
+/* Fill rows [ntotal, ntotal+n) with synthetic rows global_row0.. of the counter-hash generator
+ * (bench / tests; bit-identical to oracle/vs_oracle.c orc_synth_rows). */
+int vs_add_synthetic(vs_index* index, uint64_t seed, int64_t global_row0, int64_t n, int normalize);
+/* Same generator, written as row-major fp32 (values rounded to `dtype`) into device memory on
+ * `device`: synthetic query batches for bench.py / tests. */
+int vs_synthesize(int device, uint64_t seed, int64_t global_row0, int64_t n, int d, int normalize, int dtype,
+                  float* out_dev, void* stream);
+
+/* ---- search (index.search, utils/vector_store.py:191) */
+int vs_search(vs_index* index, const float* q, int64_t nq, int32_t k, float* D, int64_t* I);
+/* All pointers device-resident; enqueued on `stream` (NULL = the index's own stream), no host
+ * sync.  S64 (optional, may be NULL) receives the exact fp64 scores; id_offset is added to every
+ * returned id (row-sharded corpora).  Certification failures are counted on the device
+ * (vs_uncertified_count) and are NOT retried on this path. */
+int vs_search_device(vs_index* index, const float* q_dev, int64_t nq, int32_t k, float* D_dev,
+                     int64_t* I_dev, double* S64_dev, int64_t id_offset, void* stream);
+
+/* ---- merge of per-shard results (all-gather + K3 merge).
+ * S_in/I_in: G x nq x k (device), each list sorted best-first; output nq x k best-first under
+ * (score desc | asc for L2, id asc).  D_out is S_out rounded to fp32 (may be NULL). */
+int vs_merge_shards_device(int metric, const double* S_in, const int64_t* I_in, int G, int64_t nq,
+                           int32_t k, double* S_out, int64_t* I_out, float* D_out, void* stream);
+
+/* ---- reconstruct (index.reconstruct, utils/vector_store.py:207) */
+int vs_reconstruct(vs_index* index, int64_t id, float* out);
+int vs_reconstruct_n(vs_index* index, int64_t i0, int64_t n, float* out); /* host n x d */
+
+/* ---- introspection */
+int64_t vs_ntotal(const vs_index* index);
+int vs_dim(const vs_index* index);
+int vs_metric(const vs_index* index);
+int vs_dtype(const vs_index* index);
+int vs_device(const vs_index* index);
+const char* vs_last_error(void);
+const char* vs_version(void);
+
+/* ---- measurement hooks (bench.py): HIP events around the dominant screen kernel, recorded on
+ * the stream it is launched on.  vs_timing_fetch synchronises those events and returns up to
+ * `cap` per-launch durations (ms), oldest first, then clears them. */
+int vs_set_timing(vs_index* index, int enable);
+int vs_timing_fetch(vs_index* index, float* ms, int cap, int* kernel_kind);
+int64_t vs_uncertified_count(vs_index* index);   /* synchronises the device counter */
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* VS_H_ */

@@ -1,0 +1,120 @@
+"""ctypes binding of libvs.so (include/vs.h).
+
+The library is the product path: if it is missing or cannot be loaded this module raises, loudly.
+There is no CPU fallback anywhere in ``photo_search_engine_amd``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+import sys
+import threading
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libvs.so")
+HEADER_PATH = os.path.join(HERE, "..", "include", "vs.h")
+
+METRIC_IP = 0
+METRIC_L2 = 1
+DTYPE_F32 = 0
+DTYPE_BF16 = 1
+DTYPE_F16 = 2
+DTYPE_CODES = {"f32": DTYPE_F32, "fp32": DTYPE_F32, "float32": DTYPE_F32,
+               "bf16": DTYPE_BF16, "bfloat16": DTYPE_BF16,
+               "f16": DTYPE_F16, "fp16": DTYPE_F16, "float16": DTYPE_F16}
+
+VS_OK = 0
+VS_ERR_ARG = -1
+VS_ERR_DEVICE = -2
+VS_ERR_OOM = -3
+VS_ERR_UNCERTIFIED = -4
+VS_ERR_INTERNAL = -5
+
+
+class VsError(RuntimeError):
+    """A libvs call failed (device, allocation, argument or certification error)."""
+
+    def __init__(self, code: int, message: str) -> None:
+        super().__init__(f"libvs error {code}: {message}")
+        self.code = code
+
+
+_lock = threading.Lock()
+_lib = None
+
+_c_i64 = ctypes.c_int64
+_vp = ctypes.c_void_p
+_SIGS = {
+    # name: (restype, argtypes)
+    "vs_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_vp)]),
+    "vs_destroy": (None, [_vp]),
+    "vs_reset": (ctypes.c_int, [_vp]),
+    "vs_add": (ctypes.c_int, [_vp, _vp, _c_i64]),
+    "vs_add_device": (ctypes.c_int, [_vp, _vp, _c_i64, _vp]),
+    "vs_add_synthetic": (ctypes.c_int, [_vp, ctypes.c_uint64, _c_i64, _c_i64, ctypes.c_int]),
+    "vs_synthesize": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint64, _c_i64, _c_i64, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_int, _vp, _vp]),
+    "vs_search": (ctypes.c_int, [_vp, _vp, _c_i64, ctypes.c_int32, _vp, _vp]),
+    "vs_search_device": (ctypes.c_int, [_vp, _vp, _c_i64, ctypes.c_int32, _vp, _vp, _vp, _c_i64, _vp]),
+    "vs_merge_shards_device": (ctypes.c_int, [ctypes.c_int, _vp, _vp, ctypes.c_int, _c_i64, ctypes.c_int32, _vp,
+                                              _vp, _vp, _vp]),
+    "vs_reconstruct": (ctypes.c_int, [_vp, _c_i64, _vp]),
+    "vs_reconstruct_n": (ctypes.c_int, [_vp, _c_i64, _c_i64, _vp]),
+    "vs_ntotal": (_c_i64, [_vp]),
+    "vs_dim": (ctypes.c_int, [_vp]),
+    "vs_metric": (ctypes.c_int, [_vp]),
+    "vs_dtype": (ctypes.c_int, [_vp]),
+    "vs_device": (ctypes.c_int, [_vp]),
+    "vs_last_error": (ctypes.c_char_p, []),
+    "vs_version": (ctypes.c_char_p, []),
+    "vs_set_timing": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "vs_timing_fetch": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
+    "vs_uncertified_count": (_c_i64, [_vp]),
+}
+
+
+def header_functions(path: str = HEADER_PATH):
+    """Names of every function include/vs.h declares (used by the symbol-export test)."""
+    text = open(path, encoding="utf-8").read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(vs_[a-z0-9_]+)\s*\(", text)))
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libvs.so and bind every entry point; raises if the library is absent."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        # One HIP runtime per process: torch wheels bundle their own libamdhip64.so.7 /
+        # libhsa-runtime64.so.1.  If torch is importable, load it first so libvs binds to the
+        # SAME runtime (same SONAME) instead of /opt/rocm's copy; two HSA runtimes in one process
+        # leave the second one without devices.  VS_NO_TORCH=1 skips this (pure C-ABI users).
+        if os.environ.get("VS_NO_TORCH", "0") != "1" and "torch" not in sys.modules:
+            try:
+                import torch  # noqa: F401
+            except ImportError:
+                pass
+        if not os.path.exists(path):
+            raise ImportError(
+                f"libvs.so not found at {path}: the HIP library is the only implementation of this path; "
+                "build it with `python -m photo_search_engine_amd.build` (hipcc, gfx950)")
+        L = ctypes.CDLL(path)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+        return L
+
+
+def last_error() -> str:
+    msg = load().vs_last_error()
+    return msg.decode("utf-8", "replace") if msg else ""
+
+
+def check(rc: int) -> int:
+    if rc < 0:
+        raise VsError(rc, last_error())
+    return rc

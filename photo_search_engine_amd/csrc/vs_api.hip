@@ -1,0 +1,635 @@
+// vs_api.hip -- C ABI of libvs (include/vs.h): index object, HBM residency, search orchestration.
+//
+// Replaces faiss.IndexFlatIP/IndexFlatL2 behind /root/reference/utils/vector_store.py
+// (construct :79-81, add :164, search :191, reconstruct :207, ntotal :183/:271, clear :277).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <condition_variable>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <shared_mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/vs.h"
+#include "vs_internal.h"
+
+using namespace vs;
+
+namespace {
+
+thread_local std::string g_err;
+
+struct VsError : std::runtime_error {
+    int code;
+    VsError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define HIP_CHECK(expr)                                                                                    \
+    do {                                                                                                   \
+        hipError_t _e = (expr);                                                                            \
+        if (_e != hipSuccess)                                                                              \
+            throw VsError(_e == hipErrorOutOfMemory ? VS_ERR_OOM : VS_ERR_DEVICE,                          \
+                          std::string(#expr) + ": " + hipGetErrorString(_e));                              \
+    } while (0)
+
+template <typename F>
+int guarded(F&& f) {
+    try {
+        f();
+        return VS_OK;
+    } catch (const VsError& e) {
+        g_err = e.what();
+        return e.code;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return VS_ERR_INTERNAL;
+    } catch (...) {
+        g_err = "unknown error";
+        return VS_ERR_INTERNAL;
+    }
+}
+
+inline int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
+
+// device buffer that only grows
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    void ensure(size_t want) {
+        if (want <= bytes) return;
+        if (p) hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        HIP_CHECK(hipMalloc(&p, want));
+        bytes = want;
+    }
+    template <typename T>
+    T* as() const { return (T*)p; }
+    void release() {
+        if (p) hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+};
+
+// per-call execution context: stream + workspace (pooled; one per concurrent search)
+struct Ctx {
+    hipStream_t stream = nullptr;
+    DevBuf qdev, qtile, qinfo, qpad, cand, part, merge_a, merge_b, outD, outI, outS, cert;
+    std::vector<int> cert_host;
+    ~Ctx() {
+        for (DevBuf* b : {&qdev, &qtile, &qinfo, &qpad, &cand, &part, &merge_a, &merge_b, &outD, &outI, &outS, &cert})
+            b->release();
+        if (stream) hipStreamDestroy(stream);
+    }
+};
+
+}  // namespace
+
+struct vs_index {
+    int d = 0, dpad = 0, metric = 0, dtype = 0, device = 0, es = 4;
+    int num_cu = 256;
+    int64_t ntotal = 0, cap_rows = 0;
+    uint8_t* data = nullptr;
+    float* sqn = nullptr;
+    unsigned* d_maxsq = nullptr;
+    unsigned* d_uncert = nullptr;
+    float maxsq = 0.0f;
+    hipStream_t own = nullptr;  // ingest stream
+    DevBuf stage;               // host->device staging for vs_add
+    std::shared_mutex rw;       // shared: search; exclusive: add/reset
+    std::mutex pool_mtx;
+    std::vector<Ctx*> pool_free;
+    std::vector<Ctx*> pool_all;
+    // timing (bench): events around the screen kernel
+    std::atomic<bool> timing{false};
+    std::mutex tmtx;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> tev;
+    int last_kernel_kind = 0;  // 1 = mfma, 2 = gemv
+};
+
+namespace {
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        hipGetDevice(&prev);
+        if (prev != dev) HIP_CHECK(hipSetDevice(dev));
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        hipGetDevice(&cur);
+        if (prev >= 0 && cur != prev) hipSetDevice(prev);
+    }
+};
+
+Ctx* acquire_ctx(vs_index* ix) {
+    std::lock_guard<std::mutex> g(ix->pool_mtx);
+    if (!ix->pool_free.empty()) {
+        Ctx* c = ix->pool_free.back();
+        ix->pool_free.pop_back();
+        return c;
+    }
+    Ctx* c = new Ctx();
+    HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    ix->pool_all.push_back(c);
+    return c;
+}
+void release_ctx(vs_index* ix, Ctx* c) {
+    std::lock_guard<std::mutex> g(ix->pool_mtx);
+    ix->pool_free.push_back(c);
+}
+struct CtxLease {
+    vs_index* ix;
+    Ctx* c;
+    explicit CtxLease(vs_index* i) : ix(i), c(acquire_ctx(i)) {}
+    ~CtxLease() { release_ctx(ix, c); }
+};
+
+void ensure_capacity(vs_index* ix, int64_t rows_needed) {
+    const int64_t want = round_up(rows_needed, TR);
+    if (want <= ix->cap_rows) return;
+    int64_t ncap = std::max(want, ix->cap_rows + ix->cap_rows / 2);
+    ncap = round_up(ncap, TR);
+    const int64_t tb = tile_bytes(ix->dpad, ix->dtype);
+    uint8_t* nd = nullptr;
+    float* ns = nullptr;
+    HIP_CHECK(hipMalloc(&nd, (size_t)(ncap / TR) * tb));
+    hipError_t e = hipMalloc(&ns, (size_t)ncap * sizeof(float));
+    if (e != hipSuccess) {
+        hipFree(nd);
+        HIP_CHECK(e);
+    }
+    HIP_CHECK(hipMemsetAsync(nd, 0, (size_t)(ncap / TR) * tb, ix->own));
+    HIP_CHECK(hipMemsetAsync(ns, 0, (size_t)ncap * sizeof(float), ix->own));
+    if (ix->data && ix->ntotal > 0) {
+        const int64_t used_tiles = (ix->ntotal + TR - 1) / TR;
+        HIP_CHECK(hipMemcpyAsync(nd, ix->data, (size_t)used_tiles * tb, hipMemcpyDeviceToDevice, ix->own));
+        HIP_CHECK(hipMemcpyAsync(ns, ix->sqn, (size_t)ix->ntotal * sizeof(float), hipMemcpyDeviceToDevice, ix->own));
+    }
+    HIP_CHECK(hipStreamSynchronize(ix->own));
+    if (ix->data) hipFree(ix->data);
+    if (ix->sqn) hipFree(ix->sqn);
+    ix->data = nd;
+    ix->sqn = ns;
+    ix->cap_rows = ncap;
+}
+
+void refresh_maxsq(vs_index* ix) {
+    unsigned bits = 0;
+    HIP_CHECK(hipMemcpyAsync(&bits, ix->d_maxsq, sizeof(unsigned), hipMemcpyDeviceToHost, ix->own));
+    HIP_CHECK(hipStreamSynchronize(ix->own));
+    float f;
+    std::memcpy(&f, &bits, 4);
+    ix->maxsq = f;
+}
+
+// screening depth: k plus a margin that certifies exactness for all but pathological inputs
+int screen_depth(int k) {
+    int kp = k + std::max(16, k / 4);
+    kp = (int)round_up(kp, 16);
+    return std::min(kp, KP_MAX);
+}
+
+float gamma_of(int d) {
+    const double u = 5.9604644775390625e-08;  // 2^-24
+    const double n = (double)d + 64.0;
+    return (float)(n * u / (1.0 - n * u));
+}
+
+// Enqueue one query block through screen -> merge -> refine.  q: device fp32 [nqb][d].
+void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, float* D, int64_t* I, double* S64,
+                  int* cert, int64_t id_offset, hipStream_t st) {
+    const int64_t tiles = (ix->ntotal + TR - 1) / TR;
+    const bool use_mfma = ix->dtype != DT_F32 && nqb > GEMV_NQ_MAX && Kp <= MFMA_KP_MAX;
+    ScreenArgs a{};
+    a.corpus = ix->data;
+    a.n_valid = ix->ntotal;
+    a.tiles = (int)tiles;
+    a.dpad = ix->dpad;
+    a.d = ix->d;
+    a.metric = ix->metric;
+    a.sqn = ix->sqn;
+    a.Kp = Kp;
+    int QB;
+    c->qinfo.ensure(sizeof(float) * 2 * MFMA_QB);
+    if (use_mfma) {
+        QB = MFMA_QB;
+        a.cap = MFMA_CAP;
+        a.G = (int)std::min<int64_t>(tiles, ix->num_cu);
+        c->qtile.ensure((size_t)MFMA_QB * ix->dpad * 2);
+        HIP_CHECK(launch_pack_qtile(ix->dtype, q, nqb, ix->d, ix->dpad, c->qtile.as<uint8_t>(), c->qinfo.as<float>(), st));
+    } else {
+        QB = nqb <= 1 ? 1 : nqb <= 2 ? 2 : nqb <= 4 ? 4 : 8;
+        a.cap = (int)round_up(Kp + 2 * TR, 256);
+        a.G = (int)std::min<int64_t>(tiles, (int64_t)ix->num_cu * 8);
+        c->qpad.ensure((size_t)QB * ix->dpad * sizeof(float));
+        HIP_CHECK(launch_pack_qf32(q, nqb, QB, ix->d, ix->dpad, c->qpad.as<float>(), c->qinfo.as<float>(), st));
+    }
+    a.G = std::max(a.G, 1);
+    c->cand.ensure((size_t)a.G * QB * a.cap * sizeof(u64));
+    c->part.ensure((size_t)a.G * QB * Kp * sizeof(u64));
+    a.cand = c->cand.as<u64>();
+    a.part = c->part.as<u64>();
+
+    const bool timing = ix->timing.load();
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (timing) {
+        HIP_CHECK(hipEventCreate(&e0));
+        HIP_CHECK(hipEventCreate(&e1));
+        HIP_CHECK(hipEventRecord(e0, st));
+    }
+    if (use_mfma) HIP_CHECK(launch_screen_mfma(ix->dtype, a, c->qtile.as<uint8_t>(), nqb, st));
+    else HIP_CHECK(launch_screen_gemv(ix->dtype, a, c->qpad.as<float>(), nqb, QB, st));
+    if (timing) {
+        HIP_CHECK(hipEventRecord(e1, st));
+        std::lock_guard<std::mutex> g(ix->tmtx);
+        ix->tev.emplace_back(e0, e1);
+        ix->last_kernel_kind = use_mfma ? 1 : 2;
+    }
+
+    // merge partial lists [G][QB][Kp] down to one list per query
+    const u64* cur = a.part;
+    int nseg = a.G, qstride = QB;
+    const int spb = (256 * 16) / Kp;  // k_merge: 4096 keys per block
+    const size_t mbytes = (size_t)std::max(1, (a.G + spb - 1) / spb) * nqb * Kp * sizeof(u64);
+    c->merge_a.ensure(mbytes);
+    c->merge_b.ensure(mbytes);
+    u64* bufs[2] = {c->merge_a.as<u64>(), c->merge_b.as<u64>()};
+    int which = 0;
+    while (nseg > 1) {
+        int nout = 0;
+        HIP_CHECK(launch_merge(cur, nseg, qstride, nqb, Kp, bufs[which], &nout, st));
+        cur = bufs[which];
+        which ^= 1;
+        nseg = nout;
+        qstride = nqb;
+    }
+    // refine expects cand[q*Kp + j] (qstride == nqb) or part[0][q][Kp] (qstride QB, same row offset)
+    RefineArgs r{};
+    r.cand = cur;
+    r.Kp = Kp;
+    r.q = q;
+    r.d = ix->d;
+    r.dpad = ix->dpad;
+    r.dt = ix->dtype;
+    r.metric = ix->metric;
+    r.corpus = ix->data;
+    r.qinfo = c->qinfo.as<float>();
+    r.xmax = (float)(std::sqrt((double)ix->maxsq) * (1.0 + 1e-5)) + 1e-30f;
+    r.gamma = gamma_of(ix->d);
+    r.k = k;
+    r.n_valid = ix->ntotal;
+    r.id_offset = id_offset;
+    r.D = D;
+    r.I = I;
+    r.S64 = S64;
+    r.cert = cert;
+    r.uncert = ix->d_uncert;
+    HIP_CHECK(launch_refine(r, nqb, st));
+}
+
+// Full search of nq device queries; outputs device [nq][k].
+void search_all(vs_index* ix, Ctx* c, const float* q, int64_t nq, int k, int Kp, float* D, int64_t* I, double* S64,
+                int* cert, int64_t id_offset, hipStream_t st) {
+    const int64_t tiles = (ix->ntotal + TR - 1) / TR;
+    (void)tiles;
+    const bool mfma_ok = ix->dtype != DT_F32 && Kp <= MFMA_KP_MAX;
+    int64_t done = 0;
+    while (done < nq) {
+        const int64_t rem = nq - done;
+        int nqb;
+        if (mfma_ok && rem > GEMV_NQ_MAX) nqb = (int)std::min<int64_t>(rem, MFMA_QB);
+        else nqb = (int)std::min<int64_t>(rem, GEMV_NQ_MAX);
+        search_block(ix, c, q + done * ix->d, nqb, k, Kp, D ? D + done * k : nullptr, I + done * k,
+                     S64 ? S64 + done * k : nullptr, cert ? cert + done : nullptr, id_offset, st);
+        done += nqb;
+    }
+}
+
+void check_index(const vs_index* ix) {
+    if (!ix) throw VsError(VS_ERR_ARG, "null index");
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* vs_last_error(void) { return g_err.c_str(); }
+const char* vs_version(void) { return "libvs 0.1 (gfx950)"; }
+
+int vs_create(int d, int metric, int dtype, int device, vs_index** out) {
+    return guarded([&] {
+        if (!out) throw VsError(VS_ERR_ARG, "out is null");
+        *out = nullptr;
+        if (d <= 0) throw VsError(VS_ERR_ARG, "dimension must be > 0");
+        if (metric != VS_METRIC_IP && metric != VS_METRIC_L2) throw VsError(VS_ERR_ARG, "metric must be IP(0) or L2(1)");
+        if (dtype < VS_DTYPE_F32 || dtype > VS_DTYPE_F16) throw VsError(VS_ERR_ARG, "dtype must be 0 (f32), 1 (bf16), 2 (f16)");
+        int ndev = 0;
+        hipError_t e = hipGetDeviceCount(&ndev);
+        if (e != hipSuccess || ndev <= 0) throw VsError(VS_ERR_DEVICE, "no HIP device available (libvs needs an MI355X)");
+        if (device < 0 || device >= ndev) throw VsError(VS_ERR_ARG, "device ordinal out of range");
+        DeviceGuard dg(device);
+        hipDeviceProp_t prop;
+        HIP_CHECK(hipGetDeviceProperties(&prop, device));
+        if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+            throw VsError(VS_ERR_DEVICE, std::string("libvs is built for gfx950, device is ") + prop.gcnArchName);
+        vs_index* ix = new vs_index();
+        ix->d = d;
+        ix->dpad = (int)round_up(d, CH);
+        ix->metric = metric;
+        ix->dtype = dtype;
+        ix->device = device;
+        ix->es = es_of(dtype);
+        ix->num_cu = prop.multiProcessorCount;
+        try {
+            HIP_CHECK(hipStreamCreateWithFlags(&ix->own, hipStreamNonBlocking));
+            HIP_CHECK(hipMalloc(&ix->d_maxsq, sizeof(unsigned) * 2));
+            HIP_CHECK(hipMemset(ix->d_maxsq, 0, sizeof(unsigned) * 2));
+            ix->d_uncert = ix->d_maxsq + 1;
+        } catch (...) {
+            delete ix;
+            throw;
+        }
+        *out = ix;
+    });
+}
+
+void vs_destroy(vs_index* ix) {
+    if (!ix) return;
+    {
+        DeviceGuard dg(ix->device);
+        hipDeviceSynchronize();
+        for (Ctx* c : ix->pool_all) delete c;
+        for (auto& pr : ix->tev) {
+            hipEventDestroy(pr.first);
+            hipEventDestroy(pr.second);
+        }
+        ix->stage.release();
+        if (ix->data) hipFree(ix->data);
+        if (ix->sqn) hipFree(ix->sqn);
+        if (ix->d_maxsq) hipFree(ix->d_maxsq);
+        if (ix->own) hipStreamDestroy(ix->own);
+    }
+    delete ix;
+}
+
+int vs_reset(vs_index* ix) {
+    return guarded([&] {
+        check_index(ix);
+        std::unique_lock<std::shared_mutex> lk(ix->rw);
+        DeviceGuard dg(ix->device);
+        ix->ntotal = 0;
+        ix->maxsq = 0.0f;
+        HIP_CHECK(hipMemsetAsync(ix->d_maxsq, 0, sizeof(unsigned), ix->own));
+        HIP_CHECK(hipStreamSynchronize(ix->own));
+    });
+}
+
+int vs_add(vs_index* ix, const float* x, int64_t n) {
+    return guarded([&] {
+        check_index(ix);
+        if (n < 0) throw VsError(VS_ERR_ARG, "n must be >= 0");
+        if (n == 0) return;
+        if (!x) throw VsError(VS_ERR_ARG, "x is null");
+        std::unique_lock<std::shared_mutex> lk(ix->rw);
+        DeviceGuard dg(ix->device);
+        if (ix->ntotal + n > (int64_t)0xFFFFFFF0LL) throw VsError(VS_ERR_ARG, "shard exceeds 2^32 rows");
+        ensure_capacity(ix, ix->ntotal + n);
+        const int64_t rows_per_chunk = std::max<int64_t>(1, (int64_t)(64 << 20) / ((int64_t)ix->d * 4));
+        ix->stage.ensure((size_t)std::min(n, rows_per_chunk) * ix->d * sizeof(float));
+        for (int64_t r0 = 0; r0 < n; r0 += rows_per_chunk) {
+            const int64_t m = std::min(rows_per_chunk, n - r0);
+            HIP_CHECK(hipMemcpyAsync(ix->stage.p, x + r0 * ix->d, (size_t)m * ix->d * sizeof(float),
+                                     hipMemcpyHostToDevice, ix->own));
+            HIP_CHECK(launch_pack_rows(ix->dtype, ix->stage.as<float>(), m, ix->d, ix->dpad, ix->data,
+                                       ix->ntotal + r0, ix->sqn, ix->d_maxsq, ix->own));
+            HIP_CHECK(hipStreamSynchronize(ix->own));  // staging buffer reuse
+        }
+        ix->ntotal += n;
+        refresh_maxsq(ix);
+    });
+}
+
+int vs_add_device(vs_index* ix, const float* x_dev, int64_t n, void* stream) {
+    return guarded([&] {
+        check_index(ix);
+        if (n < 0) throw VsError(VS_ERR_ARG, "n must be >= 0");
+        if (n == 0) return;
+        if (!x_dev) throw VsError(VS_ERR_ARG, "x_dev is null");
+        std::unique_lock<std::shared_mutex> lk(ix->rw);
+        DeviceGuard dg(ix->device);
+        if (ix->ntotal + n > (int64_t)0xFFFFFFF0LL) throw VsError(VS_ERR_ARG, "shard exceeds 2^32 rows");
+        ensure_capacity(ix, ix->ntotal + n);
+        hipStream_t st = stream ? (hipStream_t)stream : ix->own;
+        HIP_CHECK(launch_pack_rows(ix->dtype, x_dev, n, ix->d, ix->dpad, ix->data, ix->ntotal, ix->sqn, ix->d_maxsq, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+        ix->ntotal += n;
+        refresh_maxsq(ix);
+    });
+}
+
+int vs_add_synthetic(vs_index* ix, uint64_t seed, int64_t global_row0, int64_t n, int normalize) {
+    return guarded([&] {
+        check_index(ix);
+        if (n < 0 || global_row0 < 0) throw VsError(VS_ERR_ARG, "bad synthetic range");
+        if (n == 0) return;
+        std::unique_lock<std::shared_mutex> lk(ix->rw);
+        DeviceGuard dg(ix->device);
+        if (ix->ntotal + n > (int64_t)0xFFFFFFF0LL) throw VsError(VS_ERR_ARG, "shard exceeds 2^32 rows");
+        ensure_capacity(ix, ix->ntotal + n);
+        HIP_CHECK(launch_synth_rows(ix->dtype, seed, global_row0, n, ix->d, ix->dpad, ix->data, ix->ntotal, normalize,
+                                    ix->sqn, ix->d_maxsq, ix->own));
+        HIP_CHECK(hipStreamSynchronize(ix->own));
+        ix->ntotal += n;
+        refresh_maxsq(ix);
+    });
+}
+
+int vs_synthesize(int device, uint64_t seed, int64_t global_row0, int64_t n, int d, int normalize, int dtype,
+                  float* out_dev, void* stream) {
+    return guarded([&] {
+        if (n < 0 || d <= 0 || global_row0 < 0) throw VsError(VS_ERR_ARG, "bad synthetic shape");
+        if (dtype < VS_DTYPE_F32 || dtype > VS_DTYPE_F16) throw VsError(VS_ERR_ARG, "bad dtype");
+        if (n == 0) return;
+        if (!out_dev) throw VsError(VS_ERR_ARG, "out_dev is null");
+        int ndev = 0;
+        if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) throw VsError(VS_ERR_DEVICE, "no HIP device available");
+        DeviceGuard dg(device);
+        HIP_CHECK(launch_synth_f32(dtype, seed, global_row0, n, d, normalize, out_dev, (hipStream_t)stream));
+    });
+}
+
+int vs_search_device(vs_index* ix, const float* q_dev, int64_t nq, int32_t k, float* D_dev, int64_t* I_dev,
+                     double* S64_dev, int64_t id_offset, void* stream) {
+    return guarded([&] {
+        check_index(ix);
+        if (nq < 0) throw VsError(VS_ERR_ARG, "nq must be >= 0");
+        if (k <= 0) throw VsError(VS_ERR_ARG, "k must be > 0");
+        if (screen_depth(k) < k) throw VsError(VS_ERR_ARG, "k too large (max " + std::to_string(KP_MAX * 4 / 5) + ")");
+        if (nq == 0) return;
+        if (!q_dev || !I_dev) throw VsError(VS_ERR_ARG, "null device buffer");
+        std::shared_lock<std::shared_mutex> lk(ix->rw);
+        DeviceGuard dg(ix->device);
+        hipStream_t st = stream ? (hipStream_t)stream : ix->own;
+        if (ix->ntotal == 0) throw VsError(VS_ERR_ARG, "index is empty");
+        CtxLease L(ix);
+        search_all(ix, L.c, q_dev, nq, k, screen_depth(k), D_dev, I_dev, S64_dev, nullptr, id_offset, st);
+    });
+}
+
+int vs_search(vs_index* ix, const float* q, int64_t nq, int32_t k, float* D, int64_t* I) {
+    return guarded([&] {
+        check_index(ix);
+        if (nq < 0) throw VsError(VS_ERR_ARG, "nq must be >= 0");
+        if (k <= 0) throw VsError(VS_ERR_ARG, "k must be > 0");
+        if (nq == 0) return;
+        if (!q || !D || !I) throw VsError(VS_ERR_ARG, "null host buffer");
+        std::shared_lock<std::shared_mutex> lk(ix->rw);
+        DeviceGuard dg(ix->device);
+        const float fillD = ix->metric == VS_METRIC_IP ? -3.402823466e+38f : 3.402823466e+38f;
+        if (ix->ntotal == 0) {
+            for (int64_t i = 0; i < nq * k; ++i) {
+                D[i] = fillD;
+                I[i] = -1;
+            }
+            return;
+        }
+        // k beyond the rows present: search min(k, ntotal), pad the rest (faiss layout)
+        const int kk = (int)std::min<int64_t>(k, ix->ntotal);
+        if (kk > KP_MAX * 4 / 5) throw VsError(VS_ERR_ARG, "k too large (max " + std::to_string(KP_MAX * 4 / 5) + ")");
+        CtxLease L(ix);
+        Ctx* c = L.c;
+        hipStream_t st = c->stream;
+        c->qdev.ensure((size_t)nq * ix->d * sizeof(float));
+        c->outD.ensure((size_t)nq * kk * sizeof(float));
+        c->outI.ensure((size_t)nq * kk * sizeof(int64_t));
+        c->cert.ensure((size_t)nq * sizeof(int));
+        HIP_CHECK(hipMemcpyAsync(c->qdev.p, q, (size_t)nq * ix->d * sizeof(float), hipMemcpyHostToDevice, st));
+        int Kp = screen_depth(kk);
+        std::vector<float> Dk((size_t)nq * kk);
+        std::vector<int64_t> Ik((size_t)nq * kk);
+        c->cert_host.resize((size_t)nq);
+        search_all(ix, c, c->qdev.as<float>(), nq, kk, Kp, c->outD.as<float>(), c->outI.as<int64_t>(), nullptr,
+                   c->cert.as<int>(), 0, st);
+        HIP_CHECK(hipMemcpyAsync(Dk.data(), c->outD.p, Dk.size() * sizeof(float), hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipMemcpyAsync(Ik.data(), c->outI.p, Ik.size() * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipMemcpyAsync(c->cert_host.data(), c->cert.p, (size_t)nq * sizeof(int), hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+        // exactness certificate failed for some queries (near-ties deeper than the margin):
+        // re-screen those queries one at a time with a 4x deeper candidate set.
+        for (int64_t qi = 0; qi < nq; ++qi) {
+            int Kr = Kp;
+            while (!c->cert_host[qi]) {
+                if (Kr >= KP_MAX || Kr >= ix->ntotal)
+                    throw VsError(VS_ERR_UNCERTIFIED, "exactness certificate failed at maximum screening depth");
+                Kr = (int)std::min<int64_t>(std::min<int64_t>((int64_t)Kr * 4, KP_MAX), round_up(ix->ntotal, 16));
+                search_all(ix, c, c->qdev.as<float>() + qi * ix->d, 1, kk, Kr, c->outD.as<float>(),
+                           c->outI.as<int64_t>(), nullptr, c->cert.as<int>(), 0, st);
+                HIP_CHECK(hipMemcpyAsync(Dk.data() + qi * kk, c->outD.p, kk * sizeof(float), hipMemcpyDeviceToHost, st));
+                HIP_CHECK(hipMemcpyAsync(Ik.data() + qi * kk, c->outI.p, kk * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+                HIP_CHECK(hipMemcpyAsync(&c->cert_host[qi], c->cert.p, sizeof(int), hipMemcpyDeviceToHost, st));
+                HIP_CHECK(hipStreamSynchronize(st));
+            }
+        }
+        for (int64_t qi = 0; qi < nq; ++qi)
+            for (int j = 0; j < k; ++j) {
+                if (j < kk) {
+                    D[qi * k + j] = Dk[qi * kk + j];
+                    I[qi * k + j] = Ik[qi * kk + j];
+                } else {
+                    D[qi * k + j] = fillD;
+                    I[qi * k + j] = -1;
+                }
+            }
+    });
+}
+
+int vs_merge_shards_device(int metric, const double* S_in, const int64_t* I_in, int G, int64_t nq, int32_t k,
+                           double* S_out, int64_t* I_out, float* D_out, void* stream) {
+    return guarded([&] {
+        if (G <= 0 || G > 64) throw VsError(VS_ERR_ARG, "G must be in [1, 64]");
+        if (k <= 0 || nq < 0) throw VsError(VS_ERR_ARG, "bad k / nq");
+        if (nq == 0) return;
+        HIP_CHECK(launch_merge_shards(metric, S_in, I_in, G, nq, k, S_out, I_out, D_out, (hipStream_t)stream));
+    });
+}
+
+int vs_reconstruct_n(vs_index* ix, int64_t i0, int64_t n, float* out) {
+    return guarded([&] {
+        check_index(ix);
+        if (n == 0) return;
+        if (!out) throw VsError(VS_ERR_ARG, "out is null");
+        std::shared_lock<std::shared_mutex> lk(ix->rw);
+        if (i0 < 0 || n < 0 || i0 + n > ix->ntotal) throw VsError(VS_ERR_ARG, "reconstruct range out of bounds");
+        DeviceGuard dg(ix->device);
+        CtxLease L(ix);
+        Ctx* c = L.c;
+        const int64_t rows_per_chunk = std::max<int64_t>(1, (int64_t)(64 << 20) / ((int64_t)ix->d * 4));
+        c->outD.ensure((size_t)std::min(n, rows_per_chunk) * ix->d * sizeof(float));
+        for (int64_t r0 = 0; r0 < n; r0 += rows_per_chunk) {
+            const int64_t m = std::min(rows_per_chunk, n - r0);
+            HIP_CHECK(launch_unpack_rows(ix->dtype, ix->data, i0 + r0, m, ix->d, ix->dpad, c->outD.as<float>(), c->stream));
+            HIP_CHECK(hipMemcpyAsync(out + r0 * ix->d, c->outD.p, (size_t)m * ix->d * sizeof(float),
+                                     hipMemcpyDeviceToHost, c->stream));
+            HIP_CHECK(hipStreamSynchronize(c->stream));
+        }
+    });
+}
+
+int vs_reconstruct(vs_index* ix, int64_t id, float* out) { return vs_reconstruct_n(ix, id, 1, out); }
+
+int64_t vs_ntotal(const vs_index* ix) { return ix ? ix->ntotal : -1; }
+int vs_dim(const vs_index* ix) { return ix ? ix->d : -1; }
+int vs_metric(const vs_index* ix) { return ix ? ix->metric : -1; }
+int vs_dtype(const vs_index* ix) { return ix ? ix->dtype : -1; }
+int vs_device(const vs_index* ix) { return ix ? ix->device : -1; }
+
+int vs_set_timing(vs_index* ix, int enable) {
+    return guarded([&] {
+        check_index(ix);
+        ix->timing.store(enable != 0);
+    });
+}
+
+int vs_timing_fetch(vs_index* ix, float* ms, int cap, int* kernel_kind) {
+    int count = 0;
+    int rc = guarded([&] {
+        check_index(ix);
+        DeviceGuard dg(ix->device);
+        std::lock_guard<std::mutex> g(ix->tmtx);
+        for (auto& pr : ix->tev) {
+            HIP_CHECK(hipEventSynchronize(pr.second));
+            float t = 0.0f;
+            HIP_CHECK(hipEventElapsedTime(&t, pr.first, pr.second));
+            if (ms && count < cap) ms[count] = t;
+            ++count;
+            hipEventDestroy(pr.first);
+            hipEventDestroy(pr.second);
+        }
+        ix->tev.clear();
+        if (kernel_kind) *kernel_kind = ix->last_kernel_kind;
+    });
+    return rc == VS_OK ? std::min(count, cap) : rc;
+}
+
+int64_t vs_uncertified_count(vs_index* ix) {
+    int64_t v = -1;
+    int rc = guarded([&] {
+        check_index(ix);
+        DeviceGuard dg(ix->device);
+        HIP_CHECK(hipDeviceSynchronize());
+        unsigned u = 0;
+        HIP_CHECK(hipMemcpy(&u, ix->d_uncert, sizeof(unsigned), hipMemcpyDeviceToHost));
+        v = u;
+    });
+    return rc == VS_OK ? v : rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,99 @@
+// vs_internal.h -- shared constants, HBM layout and kernel launchers of libvs (gfx950 only).
+//
+// HBM layout of a corpus shard ("row tiles"):
+//   rows are grouped in tiles of TR = 256; d is padded to dpad = roundup(d, 64);
+//   inside a tile the matrix is stored chunk-major: [chunk c = i / 64][row r in tile][64 elements]
+//   so element (r, i) of a tile lives at  c*(TR*CB) + (r % TR)*CB + (i % 64)*es,
+//   CB = 64*es bytes (128 B bf16/f16, 256 B f32).
+// One K-step of the MFMA screen (256 rows x 64 elements) is therefore one contiguous 32 KiB
+// (bf16) block, every global load is a full 16 B/lane coalesced piece, and a row's 64-element
+// chunk is one 128 B line for the exact-rescoring gather.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace vs {
+
+constexpr int TR = 256;        // rows per tile
+constexpr int CH = 64;         // elements per chunk (= one MFMA K-step)
+constexpr int DT_F32 = 0, DT_BF16 = 1, DT_F16 = 2;
+constexpr int METRIC_IP = 0, METRIC_L2 = 1;
+
+constexpr int MFMA_QB = 256;   // queries per MFMA screen launch
+constexpr int MFMA_CAP = 768;  // candidate slots per (workgroup, query) in the MFMA screen
+constexpr int MFMA_KP_MAX = 256;
+constexpr int GEMV_NQ_MAX = 8; // queries per GEMV screen launch
+constexpr int KP_MAX = 2048;   // largest screening depth (merge: >= 2 lists per block)
+constexpr int SELECT_E = 16;   // keys per thread in block selection (256 threads -> 4096 keys)
+
+inline int es_of(int dt) { return dt == DT_F32 ? 4 : 2; }
+inline int64_t tile_bytes(int dpad, int dt) { return (int64_t)TR * dpad * es_of(dt); }
+
+// candidate key: (orderable score << 32) | (0xFFFFFFFF - local id); larger key = better,
+// equal scores -> lower id first; key 0 = empty slot.
+typedef unsigned long long u64;
+
+struct ScreenArgs {
+    const uint8_t* corpus;   // tiled shard
+    int64_t n_valid;         // rows in the shard
+    int tiles;               // ceil(n_valid / TR)
+    int dpad, d;
+    int metric;
+    const float* sqn;        // per-row ||x||^2 (fp32) for L2 screening
+    int Kp;                  // screening depth per (workgroup, query)
+    int cap;                 // candidate buffer slots per (workgroup, query)
+    u64* cand;               // [G][QB][cap]
+    u64* part;               // [G][QB][Kp]
+    int G;                   // workgroups
+};
+
+// ---- launchers (vs_kernels.hip) -------------------------------------------------------------
+hipError_t launch_pack_rows(int dt, const float* src, int64_t n, int d, int dpad, uint8_t* data, int64_t lrow0,
+                            float* sqn, unsigned* maxsq, hipStream_t st);
+hipError_t launch_synth_rows(int dt, uint64_t seed, int64_t grow0, int64_t n, int d, int dpad, uint8_t* data,
+                             int64_t lrow0, int normalize, float* sqn, unsigned* maxsq, hipStream_t st);
+hipError_t launch_synth_f32(int dt, uint64_t seed, int64_t grow0, int64_t n, int d, int normalize, float* out,
+                            hipStream_t st);
+hipError_t launch_unpack_rows(int dt, const uint8_t* data, int64_t lrow0, int64_t n, int d, int dpad, float* out,
+                              hipStream_t st);
+hipError_t launch_gather_rows(int dt, const uint8_t* data, const int64_t* ids, int64_t n, int d, int dpad,
+                              float* out, hipStream_t st);
+
+// queries: MFMA tile (dtype, [nks][256][64]) or fp32 padded [NQ][dpad]; qinfo[q*2] = ||q_hat||,
+// qinfo[q*2+1] = ||q_hat - q|| (upper bounds, fp32)
+hipError_t launch_pack_qtile(int dt, const float* q, int nqb, int d, int dpad, uint8_t* qt, float* qinfo,
+                             hipStream_t st);
+hipError_t launch_pack_qf32(const float* q, int nqb, int nqpad, int d, int dpad, float* qp, float* qinfo,
+                            hipStream_t st);
+
+hipError_t launch_screen_mfma(int dt, const ScreenArgs& a, const uint8_t* qt, int nqb, hipStream_t st);
+hipError_t launch_screen_gemv(int dt, const ScreenArgs& a, const float* qp, int nqb, int nqpad, hipStream_t st);
+
+// one merge stage: in[(s*qstride + q)*Kp + j], s < nseg  ->  out[(b*nq + q)*Kp + j]
+hipError_t launch_merge(const u64* in, int nseg, int qstride, int nq, int Kp, u64* out, int* nseg_out,
+                        hipStream_t st);
+
+struct RefineArgs {
+    const u64* cand;       // [nq][Kp] (qstride = nq)
+    int Kp;
+    const float* q;        // [nq][d] fp32 (original queries)
+    int d, dpad, dt, metric;
+    const uint8_t* corpus;
+    const float* qinfo;    // [nq][2]
+    float xmax;            // upper bound on ||x|| over the shard
+    float gamma;           // fp32 accumulation error factor
+    int k;
+    int64_t n_valid;
+    int64_t id_offset;
+    float* D;              // [nq][k] (may be null)
+    int64_t* I;            // [nq][k]
+    double* S64;           // [nq][k] (may be null)
+    int* cert;             // [nq] 1 = certified exact (may be null)
+    unsigned* uncert;      // device counter (may be null)
+};
+hipError_t launch_refine(const RefineArgs& a, int nq, hipStream_t st);
+
+hipError_t launch_merge_shards(int metric, const double* S_in, const int64_t* I_in, int G, int64_t nq, int k,
+                               double* S_out, int64_t* I_out, float* D_out, hipStream_t st);
+
+}  // namespace vs

@@ -1,0 +1,1172 @@
+// vs_kernels.hip -- gfx950 (CDNA4) kernels of the exact flat k-NN backend.
+//
+// Pipeline of one search:
+//   pack_q  -> screen (K1 MFMA bf16/f16, or K2 GEMV) -> merge (K3, 1-2 stages) -> refine (K5)
+//
+//   screen: streams the shard once from HBM, computes fp32 scores (bf16/f16 MFMA, or fp32 FMA),
+//           and keeps per (workgroup, query) the top-Kp candidates by a running threshold;
+//           survivors are rare after the first tiles, so the score matrix never leaves registers.
+//   merge:  block-wide radix-bisection select of the best Kp keys of many partial lists.
+//   refine: exact fp64 rescoring of the Kp survivors in the canonical expression tree
+//           (oracle/vs_oracle.c canon_score), sort, exactness certificate, faiss-layout output.
+//
+// Candidate key (u64): (orderable fp32 score << 32) | (0xFFFFFFFF - local row id); larger is
+// better, equal score -> lower id (faiss' effective tie order), 0 = empty.
+#include "vs_internal.h"
+
+#include <math.h>
+
+namespace vs {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+// ------------------------------------------------------------------------------------------------
+// scalar helpers (bit-identical with oracle/vs_oracle.c)
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t ord_f32(float f) {
+    uint32_t u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float unord_f32(uint32_t o) {
+    uint32_t u = (o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o;
+    return __uint_as_float(u);
+}
+__device__ __forceinline__ u64 mk_key(float s, uint32_t id) {
+    return ((u64)ord_f32(s) << 32) | (u64)(0xFFFFFFFFu - id);
+}
+__device__ __forceinline__ uint32_t key_id(u64 k) { return 0xFFFFFFFFu - (uint32_t)k; }
+__device__ __forceinline__ float key_score(u64 k) { return unord_f32((uint32_t)(k >> 32)); }
+
+__device__ __forceinline__ uint16_t f32_to_bf16_rne(float f) {
+    uint32_t u = __float_as_uint(f);
+    if ((u & 0x7FFFFFFFu) > 0x7F800000u) return (uint16_t)((u >> 16) | 0x40u);
+    u += 0x7FFFu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+__device__ __forceinline__ uint16_t f32_to_f16_rne(float f) {
+    uint32_t x = __float_as_uint(f);
+    uint32_t sign = (x >> 16) & 0x8000u;
+    uint32_t ax = x & 0x7FFFFFFFu;
+    if (ax >= 0x7F800000u) return (uint16_t)(sign | (ax > 0x7F800000u ? 0x7E00u : 0x7C00u));
+    if (ax >= 0x477FF000u) return (uint16_t)(sign | 0x7C00u);
+    if (ax < 0x38800000u) {
+        float v = __uint_as_float(ax) * 16777216.0f;
+        return (uint16_t)(sign | (uint32_t)rintf(v));
+    }
+    uint32_t e = (ax >> 23) - 127u + 15u;
+    uint32_t mant = ax & 0x7FFFFFu;
+    uint32_t r = (e << 10) | (mant >> 13);
+    uint32_t rem = mant & 0x1FFFu;
+    if (rem > 0x1000u || (rem == 0x1000u && (r & 1u))) r++;
+    return (uint16_t)(sign | r);
+}
+__device__ __forceinline__ float bf16_bits_to_f32(uint32_t h) { return __uint_as_float(h << 16); }
+__device__ __forceinline__ float f16_bits_to_f32(uint32_t h) {
+    _Float16 v = __builtin_bit_cast(_Float16, (uint16_t)h);
+    return (float)v;
+}
+
+template <int DT>
+__device__ __forceinline__ float round_store(float v, uint8_t* p);
+template <>
+__device__ __forceinline__ float round_store<DT_F32>(float v, uint8_t* p) {
+    *(float*)p = v;
+    return v;
+}
+template <>
+__device__ __forceinline__ float round_store<DT_BF16>(float v, uint8_t* p) {
+    uint16_t h = f32_to_bf16_rne(v);
+    *(uint16_t*)p = h;
+    return bf16_bits_to_f32(h);
+}
+template <>
+__device__ __forceinline__ float round_store<DT_F16>(float v, uint8_t* p) {
+    uint16_t h = f32_to_f16_rne(v);
+    *(uint16_t*)p = h;
+    return f16_bits_to_f32(h);
+}
+template <int DT>
+__device__ __forceinline__ float round_only(float v) {
+    if constexpr (DT == DT_BF16) return bf16_bits_to_f32(f32_to_bf16_rne(v));
+    else if constexpr (DT == DT_F16) return f16_bits_to_f32(f32_to_f16_rne(v));
+    else return v;
+}
+template <int DT>
+__device__ __forceinline__ float load_elem(const uint8_t* p) {
+    if constexpr (DT == DT_F32) return *(const float*)p;
+    else if constexpr (DT == DT_BF16) return bf16_bits_to_f32(*(const uint16_t*)p);
+    else return f16_bits_to_f32(*(const uint16_t*)p);
+}
+// 16 B unit -> fp32 values (4 for f32, 8 for bf16/f16)
+template <int DT>
+__device__ __forceinline__ void unpack16(const uint4 r, float* v) {
+    if constexpr (DT == DT_F32) {
+        v[0] = __uint_as_float(r.x); v[1] = __uint_as_float(r.y);
+        v[2] = __uint_as_float(r.z); v[3] = __uint_as_float(r.w);
+    } else if constexpr (DT == DT_BF16) {
+        v[0] = __uint_as_float(r.x << 16); v[1] = __uint_as_float(r.x & 0xFFFF0000u);
+        v[2] = __uint_as_float(r.y << 16); v[3] = __uint_as_float(r.y & 0xFFFF0000u);
+        v[4] = __uint_as_float(r.z << 16); v[5] = __uint_as_float(r.z & 0xFFFF0000u);
+        v[6] = __uint_as_float(r.w << 16); v[7] = __uint_as_float(r.w & 0xFFFF0000u);
+    } else {
+        v[0] = f16_bits_to_f32(r.x & 0xFFFFu); v[1] = f16_bits_to_f32(r.x >> 16);
+        v[2] = f16_bits_to_f32(r.y & 0xFFFFu); v[3] = f16_bits_to_f32(r.y >> 16);
+        v[4] = f16_bits_to_f32(r.z & 0xFFFFu); v[5] = f16_bits_to_f32(r.z >> 16);
+        v[6] = f16_bits_to_f32(r.w & 0xFFFFu); v[7] = f16_bits_to_f32(r.w >> 16);
+    }
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+#define SYNTH_SCALE ((float)(1.7320508075688772 / 4194304.0))
+__device__ __forceinline__ float synth_raw(uint64_t base, uint64_t ctr) {
+    uint64_t h1 = splitmix64(base + 2u * ctr);
+    uint64_t h2 = splitmix64(base + 2u * ctr + 1u);
+    uint32_t a = (uint32_t)(h1 & 0x3FFFFFu), b = (uint32_t)((h1 >> 22) & 0x3FFFFFu);
+    uint32_t c = (uint32_t)(h2 & 0x3FFFFFu), d = (uint32_t)((h2 >> 22) & 0x3FFFFFu);
+    int32_t s = (int32_t)(a + b + c + d) - (1 << 23);
+    return (float)s * SYNTH_SCALE;
+}
+
+// ------------------------------------------------------------------------------------------------
+// wave64 / block reductions and selection
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ int wave_sum_i(int v) {
+#pragma unroll
+    for (int s = 32; s > 0; s >>= 1) v += __shfl_xor(v, s, 64);
+    return v;
+}
+__device__ __forceinline__ float wave_sum_fp32_canon(float v) {
+    // xor butterfly 32..1: identical expression tree to the oracle's part[j] + part[j ^ s]
+#pragma unroll
+    for (int s = 32; s > 0; s >>= 1) v = v + __shfl_xor(v, s, 64);
+    return v;
+}
+__device__ __forceinline__ u64 wave_min_u64(u64 v) {
+#pragma unroll
+    for (int s = 32; s > 0; s >>= 1) {
+        u64 o = __shfl_xor(v, s, 64);
+        v = o < v ? o : v;
+    }
+    return v;
+}
+__device__ __forceinline__ int lane_prefix(u64 mask) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+// K-th largest key among the wave's keys (keys unique, 0 = empty, at least K non-empty).
+// Bit-serial bisection with early exit once exactly K keys are >= the prefix.
+template <int E>
+__device__ __forceinline__ u64 wave_kth(const u64 (&keys)[E], int K) {
+    u64 t = 0;
+    for (int b = 63; b >= 0; --b) {
+        const u64 cand = t | (1ull << b);
+        int c = 0;
+#pragma unroll
+        for (int e = 0; e < E; ++e) c += keys[e] >= cand ? 1 : 0;
+        c = wave_sum_i(c);
+        if (c >= K) {
+            t = cand;
+            if (c == K) break;
+        }
+    }
+    return t;
+}
+
+// Same over a 256-thread block; red = 8 ints of LDS.
+template <int E>
+__device__ __forceinline__ u64 block_kth(const u64 (&keys)[E], int K, int* red) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    u64 t = 0;
+    for (int b = 63; b >= 0; --b) {
+        const u64 cand = t | (1ull << b);
+        int c = 0;
+#pragma unroll
+        for (int e = 0; e < E; ++e) c += keys[e] >= cand ? 1 : 0;
+        c = wave_sum_i(c);
+        if (lane == 0) red[w] = c;
+        __syncthreads();
+        int tot = 0;
+        for (int i = 0; i < nw; ++i) tot += red[i];
+        __syncthreads();
+        if (tot >= K) {
+            t = cand;
+            if (tot == K) break;
+        }
+    }
+    return t;
+}
+
+// Write the block's keys >= t (t > 0) compactly to out[0..total), returns total.
+template <int E>
+__device__ __forceinline__ int block_write_kept(const u64 (&keys)[E], u64 t, u64* out, int* red) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    int c = 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) c += keys[e] >= t ? 1 : 0;
+    int incl = c;
+#pragma unroll
+    for (int s = 1; s < 64; s <<= 1) {
+        int v = __shfl_up(incl, s, 64);
+        if (lane >= s) incl += v;
+    }
+    if (lane == 63) red[w] = incl;
+    __syncthreads();
+    int base = 0, total = 0;
+    for (int i = 0; i < nw; ++i) {
+        if (i < w) base += red[i];
+        total += red[i];
+    }
+    __syncthreads();
+    int pos = base + incl - c;
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+        if (keys[e] >= t) out[pos++] = keys[e];
+    return total;
+}
+
+// K-th largest key of buf[0..n) by a 256-thread block, keys re-read from memory every bisection
+// step (rare compaction path: keeps the streaming kernel's register budget small).
+__device__ __forceinline__ u64 block_kth_mem(const u64* buf, int n, int K, int* red) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    u64 t = 0;
+    for (int b = 63; b >= 0; --b) {
+        const u64 cand = t | (1ull << b);
+        int c = 0;
+        for (int idx = threadIdx.x; idx < n; idx += blockDim.x) c += buf[idx] >= cand ? 1 : 0;
+        c = wave_sum_i(c);
+        if (lane == 0) red[w] = c;
+        __syncthreads();
+        int tot = 0;
+        for (int i = 0; i < nw; ++i) tot += red[i];
+        __syncthreads();
+        if (tot >= K) {
+            t = cand;
+            if (tot == K) break;
+        }
+    }
+    return t;
+}
+// Order-preserving compaction of src[0..n) keys >= t (t > 0) into dst[0..); dst may alias src
+// (a kept key moves to a position <= its own, and every round reads before it writes).
+__device__ __forceinline__ int block_compact_mem(const u64* src, u64* dst, int n, u64 t, int* red) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    int base = 0;
+    for (int r0 = 0; r0 < n; r0 += blockDim.x) {
+        const int idx = r0 + threadIdx.x;
+        const u64 k = idx < n ? src[idx] : 0ull;
+        const bool keep = k >= t;
+        const u64 m = __ballot(keep);
+        if (lane == 0) red[w] = __popcll(m);
+        __syncthreads();
+        int wb = 0, tot = 0;
+        for (int i = 0; i < nw; ++i) {
+            if (i < w) wb += red[i];
+            tot += red[i];
+        }
+        __syncthreads();
+        if (keep) dst[base + wb + lane_prefix(m)] = k;
+        base += tot;
+    }
+    return base;
+}
+
+// ------------------------------------------------------------------------------------------------
+// ingest: pack host/device fp32 rows into the tiled layout; synthetic rows; unpack
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ int64_t tiled_off(int64_t row, int i, int dpad, int es) {
+    return (row / TR) * (int64_t)TR * dpad * es + (int64_t)(i >> 6) * TR * 64 * es + (row % TR) * 64 * es +
+           (int64_t)(i & 63) * es;
+}
+
+// one wave per row; element i handled by lane i & 63 (the canonical fp32 order for sqn)
+template <int DT>
+__global__ void __launch_bounds__(256) k_pack_rows(const float* __restrict__ src, int64_t n, int d, int dpad,
+                                                    uint8_t* __restrict__ data, int64_t lrow0, float* __restrict__ sqn,
+                                                    unsigned* __restrict__ maxsq) {
+    constexpr int ES = DT == DT_F32 ? 4 : 2;
+    const int lane = threadIdx.x & 63;
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= n) return;
+    const float* s = src + r * (int64_t)d;
+    const int64_t row = lrow0 + r;
+    float ss = 0.0f;
+    for (int i = lane; i < dpad; i += 64) {
+        float v = i < d ? s[i] : 0.0f;
+        float st = round_store<DT>(v, data + tiled_off(row, i, dpad, ES));
+        ss = fmaf(st, st, ss);
+    }
+    ss = wave_sum_fp32_canon(ss);
+    if (lane == 0) {
+        sqn[row] = ss;
+        atomicMax(maxsq, __float_as_uint(ss));
+    }
+}
+
+template <int DT>
+__global__ void __launch_bounds__(256) k_synth_rows(uint64_t base, int64_t grow0, int64_t n, int d, int dpad,
+                                                     uint8_t* __restrict__ data, int64_t lrow0, int normalize,
+                                                     float* __restrict__ sqn, unsigned* __restrict__ maxsq) {
+    constexpr int ES = DT == DT_F32 ? 4 : 2;
+    const int lane = threadIdx.x & 63;
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= n) return;
+    const uint64_t ctr0 = (uint64_t)(grow0 + r) * (uint64_t)d;
+    float nrm = 0.0f;
+    if (normalize) {
+        float part = 0.0f;
+        for (int i = lane; i < d; i += 64) {
+            float v = synth_raw(base, ctr0 + (uint64_t)i);
+            part = fmaf(v, v, part);
+        }
+        nrm = sqrtf(wave_sum_fp32_canon(part));
+    }
+    const int64_t row = lrow0 + r;
+    float ss = 0.0f;
+    for (int i = lane; i < dpad; i += 64) {
+        float v = 0.0f;
+        if (i < d) {
+            v = synth_raw(base, ctr0 + (uint64_t)i);
+            if (normalize && nrm != 0.0f) v = v / nrm;
+        }
+        float st = round_store<DT>(v, data + tiled_off(row, i, dpad, ES));
+        ss = fmaf(st, st, ss);
+    }
+    ss = wave_sum_fp32_canon(ss);
+    if (lane == 0) {
+        sqn[row] = ss;
+        atomicMax(maxsq, __float_as_uint(ss));
+    }
+}
+
+// same generator, row-major fp32 output (values rounded to DT), for synthetic query batches
+template <int DT>
+__global__ void __launch_bounds__(256) k_synth_f32(uint64_t base, int64_t grow0, int64_t n, int d, int normalize,
+                                                    float* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= n) return;
+    const uint64_t ctr0 = (uint64_t)(grow0 + r) * (uint64_t)d;
+    float nrm = 0.0f;
+    if (normalize) {
+        float part = 0.0f;
+        for (int i = lane; i < d; i += 64) {
+            float v = synth_raw(base, ctr0 + (uint64_t)i);
+            part = fmaf(v, v, part);
+        }
+        nrm = sqrtf(wave_sum_fp32_canon(part));
+    }
+    for (int i = lane; i < d; i += 64) {
+        float v = synth_raw(base, ctr0 + (uint64_t)i);
+        if (normalize && nrm != 0.0f) v = v / nrm;
+        out[r * (int64_t)d + i] = round_only<DT>(v);
+    }
+}
+
+template <int DT>
+__global__ void __launch_bounds__(256) k_unpack_rows(const uint8_t* __restrict__ data, int64_t lrow0, int64_t n,
+                                                      int d, int dpad, float* __restrict__ out) {
+    constexpr int ES = DT == DT_F32 ? 4 : 2;
+    const int lane = threadIdx.x & 63;
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= n) return;
+    const int64_t row = lrow0 + r;
+    for (int i = lane; i < d; i += 64) out[r * (int64_t)d + i] = load_elem<DT>(data + tiled_off(row, i, dpad, ES));
+}
+
+template <int DT>
+__global__ void __launch_bounds__(256) k_gather_rows(const uint8_t* __restrict__ data, const int64_t* __restrict__ ids,
+                                                      int64_t n, int d, int dpad, float* __restrict__ out) {
+    constexpr int ES = DT == DT_F32 ? 4 : 2;
+    const int lane = threadIdx.x & 63;
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= n) return;
+    const int64_t row = ids[r];
+    for (int i = lane; i < d; i += 64)
+        out[r * (int64_t)d + i] = row < 0 ? 0.0f : load_elem<DT>(data + tiled_off(row, i, dpad, ES));
+}
+
+// ------------------------------------------------------------------------------------------------
+// query packing
+// ------------------------------------------------------------------------------------------------
+// MFMA query tile [nks][256][64] in the corpus dtype; qinfo = (||q_hat||, ||q_hat - q||) in fp64,
+// rounded up to fp32.
+template <int DT>
+__global__ void __launch_bounds__(256) k_pack_qtile(const float* __restrict__ q, int nqb, int d, int dpad,
+                                                     uint8_t* __restrict__ qt, float* __restrict__ qinfo) {
+    const int lane = threadIdx.x & 63;
+    const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= MFMA_QB) return;
+    double n2 = 0.0, e2 = 0.0;
+    for (int i = lane; i < dpad; i += 64) {
+        float v = (r < nqb && i < d) ? q[(int64_t)r * d + i] : 0.0f;
+        float st = round_store<DT>(v, qt + (int64_t)(i >> 6) * MFMA_QB * 128 + (int64_t)r * 128 + (i & 63) * 2);
+        n2 += (double)st * st;
+        double df = (double)st - (double)v;
+        e2 += df * df;
+    }
+#pragma unroll
+    for (int s = 32; s > 0; s >>= 1) {
+        n2 += __shfl_xor(n2, s, 64);
+        e2 += __shfl_xor(e2, s, 64);
+    }
+    if (lane == 0 && r < nqb) {
+        qinfo[2 * r] = (float)(sqrt(n2) * (1.0 + 1e-6)) + 1e-30f;
+        qinfo[2 * r + 1] = (float)(sqrt(e2) * (1.0 + 1e-6));
+    }
+}
+
+// GEMV queries: fp32, [nqpad][dpad] zero padded; q_hat = q
+__global__ void __launch_bounds__(256) k_pack_qf32(const float* __restrict__ q, int nqb, int nqpad, int d, int dpad,
+                                                    float* __restrict__ qp, float* __restrict__ qinfo) {
+    const int lane = threadIdx.x & 63;
+    const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= nqpad) return;
+    double n2 = 0.0;
+    for (int i = lane; i < dpad; i += 64) {
+        float v = (r < nqb && i < d) ? q[(int64_t)r * d + i] : 0.0f;
+        qp[(int64_t)r * dpad + i] = v;
+        n2 += (double)v * v;
+    }
+#pragma unroll
+    for (int s = 32; s > 0; s >>= 1) n2 += __shfl_xor(n2, s, 64);
+    if (lane == 0 && r < nqb) {
+        qinfo[2 * r] = (float)(sqrt(n2) * (1.0 + 1e-6)) + 1e-30f;
+        qinfo[2 * r + 1] = 0.0f;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// K1: MFMA screen (bf16 / f16 corpus, up to 256 queries per launch)
+// ------------------------------------------------------------------------------------------------
+// Workgroup = 512 threads = 8 waves, one per CU (132 KiB LDS), persistent over a contiguous range
+// of row tiles.  Output tile per K-step pass: 256 corpus rows (M) x 256 queries (N), K = dpad.
+// Waves 4(M) x 2(N): each wave 64 rows x 128 queries = 4 x 8 MFMA 16x16x32 tiles, 128 acc VGPRs.
+// Staging: both operands are contiguous 32 KiB blocks per K-step (tiled layout), copied by
+// global_load_lds (16 B/lane) into a lane-linear LDS image whose 16 B pieces are XOR-swizzled
+// on the SOURCE address (piece p of row r holds chunk p ^ ((r >> 1) & 7)), so every ds_read_b128
+// fragment read is bank-conflict free.  Two LDS stages: the next K-step streams in while the
+// current one is multiplied.
+constexpr int MF_STAGE = 65536;  // A (corpus) 32 KiB + B (queries) 32 KiB
+constexpr int MF_LDS = 2 * MF_STAGE + 256 * 8 + 256 * 4 + 256 * 4;
+
+typedef __attribute__((address_space(3))) uint8_t* lds_u8_t;
+
+// LDS-DMA of 16 B per lane: LDS[m0 + lane*16] <- global[gptr].  Issued as inline asm so the
+// compiler does not fence every later ds_read with vmcnt(0) (it cannot tell which LDS bytes a
+// builtin DMA writes); the kernel waits for these with its own s_waitcnt vmcnt before the barrier
+// that publishes the stage.
+__device__ __forceinline__ void glds16(const void* gptr, uint32_t lds_base) {
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gptr), "s"(lds_base)
+                 : "memory", "m0");
+}
+__device__ __forceinline__ uint32_t lds_addr(const uint8_t* p) {
+    return (uint32_t)(uintptr_t)(lds_u8_t)(p);
+}
+
+__device__ __forceinline__ void mf_stage(const uint8_t* __restrict__ gA, const uint8_t* __restrict__ gB, uint8_t* lds,
+                                         int tid) {
+    const int w = tid >> 6, lane = tid & 63;
+    const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(lds) + (uint32_t)(w * 64 * 16));
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+        const int g = it * 512 + w * 64 + lane;  // LDS piece written by this lane
+        const int row = g >> 3, pos = g & 7;
+        const int src = (row << 3) + (pos ^ ((row >> 1) & 7));
+        glds16(gA + (size_t)src * 16, base + it * 512 * 16);
+        glds16(gB + (size_t)src * 16, base + it * 512 * 16 + 32768);
+    }
+}
+
+template <int DT>
+__device__ __forceinline__ floatx4 mfma16(const uint4 a, const uint4 b, floatx4 c) {
+    if constexpr (DT == DT_BF16)
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                       0, 0, 0);
+    else
+        return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0,
+                                                      0, 0);
+}
+
+template <int DT>
+__device__ __forceinline__ void mf_compute(const uint8_t* buf, floatx4 (&acc)[4][8], int wm, int wn, int lane) {
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+        const int c = kh * 4 + (lane >> 4);
+        uint4 af[4], bfr[8];
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) {
+            const int row = wm * 64 + mi * 16 + (lane & 15);
+            af[mi] = *(const uint4*)(buf + row * 128 + ((c ^ ((row >> 1) & 7)) << 4));
+        }
+#pragma unroll
+        for (int ni = 0; ni < 8; ++ni) {
+            const int row = wn * 128 + ni * 16 + (lane & 15);
+            bfr[ni] = *(const uint4*)(buf + 32768 + row * 128 + ((c ^ ((row >> 1) & 7)) << 4));
+        }
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 8; ++ni) acc[mi][ni] = mfma16<DT>(af[mi], bfr[ni], acc[mi][ni]);
+    }
+}
+
+// compact one (workgroup, query) candidate buffer to its best K keys (one wave)
+template <int E>
+__device__ __forceinline__ void mf_wave_compact(u64* __restrict__ buf, int n, int K, u64* thr_key, float* thr_f,
+                                             int lane) {
+    u64 keys[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int idx = lane + 64 * e;
+        keys[e] = idx < n ? buf[idx] : 0ull;
+    }
+    const u64 t = wave_kth<E>(keys, K);
+    int base = 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const bool keep = keys[e] >= t;
+        const u64 m = __ballot(keep);
+        const int pos = base + lane_prefix(m);
+        if (keep) buf[pos] = keys[e];
+        base += __popcll(m);
+    }
+    if (lane == 0) {
+        *thr_key = t;
+        *thr_f = key_score(t);
+    }
+}
+
+template <int DT>
+__global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    u64* thr_key = (u64*)(smem + 2 * MF_STAGE);
+    float* thr_f = (float*)(smem + 2 * MF_STAGE + 256 * 8);
+    int* cnt = (int*)(smem + 2 * MF_STAGE + 256 * 12);
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid & 3, wn = wid >> 2;
+    const int blk = blockIdx.x;
+    const int t0 = (int)((int64_t)a.tiles * blk / a.G);
+    const int t1 = (int)((int64_t)a.tiles * (blk + 1) / a.G);
+    if (tid < 256) {
+        const bool real = tid < nqb;
+        thr_key[tid] = real ? 0ull : ~0ull;
+        thr_f[tid] = real ? -INFINITY : INFINITY;
+        cnt[tid] = 0;
+    }
+    const int nks = a.dpad / 64;
+    const int64_t tbytes = (int64_t)TR * a.dpad * 2;
+    const int S = (t1 - t0) * nks;
+    u64* cand = a.cand + (size_t)blk * MFMA_QB * a.cap;
+    const int trigger = a.cap - TR;
+
+    floatx4 acc[4][8];
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 8; ++ni) acc[mi][ni] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    if (S > 0) mf_stage(a.corpus + (int64_t)t0 * tbytes, qt, smem, tid);
+    int ti = t0, ks = 0;
+    for (int s = 0; s < S; ++s) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        {
+            int ks1 = ks + 1, ti1 = ti;
+            if (ks1 == nks) { ks1 = 0; ++ti1; }
+            if (s + 1 < S)
+                mf_stage(a.corpus + (int64_t)ti1 * tbytes + (int64_t)ks1 * 32768, qt + (int64_t)ks1 * 32768,
+                         smem + ((s + 1) & 1) * MF_STAGE, tid);
+        }
+        mf_compute<DT>(smem + (s & 1) * MF_STAGE, acc, wm, wn, lane);
+        if (ks == nks - 1) {
+            // ---- fused top-k epilogue: threshold filter, rare inserts ----
+            const int64_t rowbase = (int64_t)ti * TR;
+            const bool full = rowbase + TR <= a.n_valid;
+            float sq[4][4];
+            if (a.metric == METRIC_L2) {
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int64_t gr = rowbase + wm * 64 + mi * 16 + (lane >> 4) * 4 + r;
+                        sq[mi][r] = gr < a.n_valid ? a.sqn[gr] : 0.0f;
+                    }
+            }
+#pragma unroll
+            for (int ni = 0; ni < 8; ++ni) {
+                const int q = wn * 128 + ni * 16 + (lane & 15);
+                const float tf = thr_f[q];
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int rit = wm * 64 + mi * 16 + (lane >> 4) * 4 + r;
+                        float sc = acc[mi][ni][r];
+                        if (a.metric == METRIC_L2) sc = 2.0f * sc - sq[mi][r];
+                        const bool valid = full || (rowbase + rit < a.n_valid);
+                        if (valid && sc >= tf) {
+                            const u64 key = mk_key(sc, (uint32_t)(rowbase + rit));
+                            if (key > thr_key[q]) {
+                                const int slot = atomicAdd(&cnt[q], 1);
+                                if (slot < a.cap) cand[(size_t)q * a.cap + slot] = key;
+                            }
+                        }
+                    }
+            }
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < 8; ++ni) acc[mi][ni] = floatx4{0.f, 0.f, 0.f, 0.f};
+            __syncthreads();
+            for (int q = wid; q < nqb; q += 8) {
+                const int n = cnt[q];
+                if (n > trigger) {
+                    mf_wave_compact<MFMA_CAP / 64>(cand + (size_t)q * a.cap, n, a.Kp, &thr_key[q], &thr_f[q], lane);
+                    if (lane == 0) cnt[q] = a.Kp;
+                }
+            }
+        }
+        if (++ks == nks) { ks = 0; ++ti; }
+    }
+    // ---- flush: best Kp per query -> part[blk][q][Kp] ----
+    __syncthreads();
+    for (int q = wid; q < MFMA_QB; q += 8) {
+        u64* pq = a.part + ((size_t)blk * MFMA_QB + q) * a.Kp;
+        int n = q < nqb ? cnt[q] : 0;
+        if (n > a.Kp) {
+            mf_wave_compact<MFMA_CAP / 64>(cand + (size_t)q * a.cap, n, a.Kp, &thr_key[q], &thr_f[q], lane);
+            n = a.Kp;
+        }
+        for (int j = lane; j < a.Kp; j += 64) pq[j] = j < n ? cand[(size_t)q * a.cap + j] : 0ull;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// K2: GEMV screen (any dtype, up to 8 queries per launch) -- HBM streaming, fp32 FMA
+// ------------------------------------------------------------------------------------------------
+// 256 threads, persistent over a contiguous tile range.  A row's 64-element chunk is LPR 16 B
+// units, read by LPR consecutive lanes, so every wave-instruction is a contiguous 1 KiB piece.
+template <int DT, int NQ>
+__global__ void __launch_bounds__(256) k_screen_gemv(ScreenArgs a, const float* __restrict__ qp, int nqb) {
+    constexpr int ES = DT == DT_F32 ? 4 : 2;
+    constexpr int CB = 64 * ES;
+    constexpr int LPR = CB / 16;
+    constexpr int RPI = 64 / LPR;
+    constexpr int EPU = 16 / ES;
+    constexpr int RG = 64 / RPI;
+    constexpr int RB = (NQ <= 2) ? 8 : 4;  // rows per pass (register budget)
+    static_assert(RG % RB == 0, "row groups");
+
+    __shared__ u64 thr_key[NQ];
+    __shared__ float thr_f[NQ];
+    __shared__ int cnt[NQ];
+    __shared__ int red[8];
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int unit = lane % LPR, rsub = lane / LPR;
+    const int blk = blockIdx.x;
+    const int t0 = (int)((int64_t)a.tiles * blk / a.G);
+    const int t1 = (int)((int64_t)a.tiles * (blk + 1) / a.G);
+    if (tid < NQ) {
+        const bool real = tid < nqb;
+        thr_key[tid] = real ? 0ull : ~0ull;
+        thr_f[tid] = real ? -INFINITY : INFINITY;
+        cnt[tid] = 0;
+    }
+    __syncthreads();
+    const int nch = a.dpad / 64;
+    const int64_t tbytes = (int64_t)TR * a.dpad * ES;
+    u64* cand = a.cand + (size_t)blk * NQ * a.cap;
+    const int trigger = a.cap - TR;
+
+    for (int ti = t0; ti < t1; ++ti) {
+        const uint8_t* tb = a.corpus + (int64_t)ti * tbytes;
+        const int64_t rowbase = (int64_t)ti * TR;
+        for (int gb = 0; gb < RG / RB; ++gb) {
+            float acc[RB][NQ];
+#pragma unroll
+            for (int r = 0; r < RB; ++r)
+#pragma unroll
+                for (int qi = 0; qi < NQ; ++qi) acc[r][qi] = 0.0f;
+#pragma unroll 2
+            for (int c = 0; c < nch; ++c) {
+                float qv[NQ][EPU];
+#pragma unroll
+                for (int qi = 0; qi < NQ; ++qi) {
+                    const float4* qs = (const float4*)(qp + (int64_t)qi * a.dpad + c * 64 + unit * EPU);
+#pragma unroll
+                    for (int h = 0; h < EPU / 4; ++h) {
+                        float4 t = qs[h];
+                        qv[qi][4 * h + 0] = t.x; qv[qi][4 * h + 1] = t.y;
+                        qv[qi][4 * h + 2] = t.z; qv[qi][4 * h + 3] = t.w;
+                    }
+                }
+                uint4 raw[RB];
+#pragma unroll
+                for (int r = 0; r < RB; ++r) {
+                    const int rit = wid * 64 + (gb * RB + r) * RPI + rsub;
+                    raw[r] = *(const uint4*)(tb + (int64_t)c * TR * CB + rit * CB + unit * 16);
+                }
+#pragma unroll
+                for (int r = 0; r < RB; ++r) {
+                    float xv[EPU];
+                    unpack16<DT>(raw[r], xv);
+#pragma unroll
+                    for (int qi = 0; qi < NQ; ++qi)
+#pragma unroll
+                        for (int e = 0; e < EPU; ++e) acc[r][qi] = fmaf(xv[e], qv[qi][e], acc[r][qi]);
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < RB; ++r)
+#pragma unroll
+                for (int qi = 0; qi < NQ; ++qi) {
+                    float v = acc[r][qi];
+#pragma unroll
+                    for (int s = 1; s < LPR; s <<= 1) v += __shfl_xor(v, s, 64);
+                    acc[r][qi] = v;
+                }
+            if (unit == 0) {
+#pragma unroll
+                for (int r = 0; r < RB; ++r) {
+                    const int rit = wid * 64 + (gb * RB + r) * RPI + rsub;
+                    const int64_t gr = rowbase + rit;
+                    if (gr >= a.n_valid) continue;
+                    const float sq = a.metric == METRIC_L2 ? a.sqn[gr] : 0.0f;
+#pragma unroll
+                    for (int qi = 0; qi < NQ; ++qi) {
+                        float sc = acc[r][qi];
+                        if (a.metric == METRIC_L2) sc = 2.0f * sc - sq;
+                        if (sc >= thr_f[qi]) {
+                            const u64 key = mk_key(sc, (uint32_t)gr);
+                            if (key > thr_key[qi]) {
+                                const int slot = atomicAdd(&cnt[qi], 1);
+                                if (slot < a.cap) cand[(size_t)qi * a.cap + slot] = key;
+                            }
+                        }
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        for (int qi = 0; qi < nqb; ++qi) {
+            const int n = cnt[qi];
+            if (n > trigger) {  // block-uniform
+                u64* buf = cand + (size_t)qi * a.cap;
+                const u64 t = block_kth_mem(buf, n, a.Kp, red);
+                block_compact_mem(buf, buf, n, t, red);
+                if (tid == 0) {
+                    thr_key[qi] = t;
+                    thr_f[qi] = key_score(t);
+                    cnt[qi] = a.Kp;
+                }
+                __syncthreads();
+            }
+        }
+    }
+    __syncthreads();
+    for (int qi = 0; qi < NQ; ++qi) {
+        u64* pq = a.part + ((size_t)blk * NQ + qi) * a.Kp;
+        u64* buf = cand + (size_t)qi * a.cap;
+        int n = qi < nqb ? cnt[qi] : 0;
+        if (n > a.Kp) {
+            const u64 t = block_kth_mem(buf, n, a.Kp, red);
+            n = block_compact_mem(buf, pq, n, t, red);
+        } else {
+            for (int j = tid; j < n; j += 256) pq[j] = buf[j];
+        }
+        for (int j = n + tid; j < a.Kp; j += 256) pq[j] = 0ull;
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// K3: merge of partial candidate lists (block-wide selection)
+// ------------------------------------------------------------------------------------------------
+constexpr int MERGE_E = 16;  // 4096 keys per block
+__global__ void __launch_bounds__(256) k_merge(const u64* __restrict__ in, int nseg, int qstride, int nq, int Kp,
+                                               int spb, u64* __restrict__ out) {
+    __shared__ int red[8];
+    const int q = blockIdx.y, b = blockIdx.x, tid = threadIdx.x;
+    const int s0 = b * spb;
+    const int s1 = min(nseg, s0 + spb);
+    const int n = (s1 - s0) * Kp;
+    u64 keys[MERGE_E];
+    int nvalid = 0;
+#pragma unroll
+    for (int e = 0; e < MERGE_E; ++e) {
+        const int idx = tid + 256 * e;
+        u64 k = 0ull;
+        if (idx < n) {
+            const int s = s0 + idx / Kp, j = idx % Kp;
+            k = in[((size_t)s * qstride + q) * Kp + j];
+        }
+        keys[e] = k;
+        nvalid += k != 0ull;
+    }
+    nvalid = wave_sum_i(nvalid);
+    if ((tid & 63) == 0) red[tid >> 6] = nvalid;
+    __syncthreads();
+    int tot = 0;
+    for (int i = 0; i < 4; ++i) tot += red[i];
+    __syncthreads();
+    const u64 t = tot > Kp ? block_kth<MERGE_E>(keys, Kp, red) : 1ull;
+    u64* o = out + ((size_t)b * nq + q) * Kp;
+    const int kept = block_write_kept<MERGE_E>(keys, t, o, red);
+    for (int j = kept + tid; j < Kp; j += 256) o[j] = 0ull;
+}
+
+// ------------------------------------------------------------------------------------------------
+// K5: exact refine -- canonical fp64 rescoring, sort, certificate, faiss-layout output
+// ------------------------------------------------------------------------------------------------
+template <int DT>
+__device__ __forceinline__ double exact_score(const uint8_t* __restrict__ corpus, int64_t row,
+                                              const float* __restrict__ q, int d, int dpad, int metric, int lane) {
+#pragma clang fp contract(off)
+    constexpr int ES = DT == DT_F32 ? 4 : 2;
+    const uint8_t* rb = corpus + (row / TR) * (int64_t)TR * dpad * ES + (row % TR) * (64 * ES);
+    double acc = 0.0;
+    for (int g = lane; 8 * g < d; g += 64) {
+        const int e0 = 8 * g;
+        const uint8_t* p = rb + (int64_t)(e0 >> 6) * TR * 64 * ES + (e0 & 63) * ES;
+        float xv[8];
+        if constexpr (DT == DT_F32) {
+            unpack16<DT>(*(const uint4*)p, xv);
+            unpack16<DT>(*(const uint4*)(p + 16), xv + 4);
+        } else {
+            unpack16<DT>(*(const uint4*)p, xv);
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int i = e0 + e;
+            if (i < d) {
+                const double x = (double)xv[e];
+                const double qq = (double)q[i];
+                if (metric == METRIC_IP) {
+                    const double pr = x * qq;
+                    acc = acc + pr;
+                } else {
+                    const double dl = x - qq;
+                    const double pr = dl * dl;
+                    acc = acc + pr;
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int s = 32; s > 0; s >>= 1) {
+        const double o = __shfl_xor(acc, s, 64);
+        acc = acc + o;
+    }
+    return acc;
+}
+
+__device__ __forceinline__ bool better_exact(double sa, uint32_t ia, double sb, uint32_t ib, int metric) {
+    if (sa != sb) return metric == METRIC_IP ? (sa > sb) : (sa < sb);
+    return ia < ib;
+}
+
+template <int DT>
+__global__ void __launch_bounds__(256) k_refine(RefineArgs a, int KP2) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    double* sc = (double*)smem;
+    uint32_t* ids = (uint32_t*)(smem + (size_t)KP2 * 8);
+    __shared__ int nv_s;
+    __shared__ u64 minkey_s;
+    __shared__ double qq_s;
+    const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const u64* cq = a.cand + (size_t)q * a.Kp;
+    const float* qv = a.q + (int64_t)q * a.d;
+    if (tid == 0) {
+        nv_s = 0;
+        minkey_s = ~0ull;
+    }
+    __syncthreads();
+    // candidates are compacted (non-empty first)
+    int myv = 0;
+    u64 mymin = ~0ull;
+    for (int j = tid; j < a.Kp; j += 256) {
+        const u64 k = cq[j];
+        if (k != 0ull) {
+            ++myv;
+            mymin = k < mymin ? k : mymin;
+        }
+    }
+    myv = wave_sum_i(myv);
+    mymin = wave_min_u64(mymin);
+    if (lane == 0) {
+        atomicAdd(&nv_s, myv);
+        atomicMin(&minkey_s, mymin);
+    }
+    if (wid == 0) {
+        double s2 = 0.0;
+        for (int i = lane; i < a.d; i += 64) s2 += (double)qv[i] * (double)qv[i];
+#pragma unroll
+        for (int s = 32; s > 0; s >>= 1) s2 += __shfl_xor(s2, s, 64);
+        if (lane == 0) qq_s = s2;
+    }
+    __syncthreads();
+    const int nv = nv_s;
+    for (int j = wid; j < nv; j += 4) {
+        const uint32_t id = key_id(cq[j]);
+        double s;
+        if (a.dt == DT_F32) s = exact_score<DT_F32>(a.corpus, id, qv, a.d, a.dpad, a.metric, lane);
+        else if (a.dt == DT_BF16) s = exact_score<DT_BF16>(a.corpus, id, qv, a.d, a.dpad, a.metric, lane);
+        else s = exact_score<DT_F16>(a.corpus, id, qv, a.d, a.dpad, a.metric, lane);
+        if (lane == 0) {
+            sc[j] = s;
+            ids[j] = id;
+        }
+    }
+    const double worst = a.metric == METRIC_IP ? -INFINITY : INFINITY;
+    for (int j = nv + tid; j < KP2; j += 256) {
+        sc[j] = worst;
+        ids[j] = 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    // bitonic sort, best first
+    for (int size = 2; size <= KP2; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int i = tid; i < KP2; i += 256) {
+                const int j = i ^ stride;
+                if (j > i) {
+                    const bool up = (i & size) == 0;
+                    const double si = sc[i], sj = sc[j];
+                    const uint32_t ii = ids[i], ij = ids[j];
+                    const bool jb = better_exact(sj, ij, si, ii, a.metric);
+                    if (up ? jb : !jb) {
+                        sc[i] = sj; sc[j] = si;
+                        ids[i] = ij; ids[j] = ii;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    // exactness certificate: every non-candidate row has exact transformed score <= smin + eps
+    if (tid == 0) {
+        int cert = 1;
+        if (nv >= a.Kp && a.k <= nv) {
+            const double smin = (double)key_score(minkey_s);
+            const double qh = (double)a.qinfo[2 * q], dq = (double)a.qinfo[2 * q + 1];
+            const double xm = (double)a.xmax;
+            double eps = ((double)a.gamma * qh + dq) * xm * 1.01 + 1e-30;
+            double tk = sc[a.k - 1];
+            if (a.metric == METRIC_L2) {
+                eps = 2.0 * eps + ((double)a.gamma + 4.0 * 5.9604644775390625e-08) * (xm * xm + 2.0 * xm * qh) * 1.01 +
+                      1e-12 * (qq_s + xm * xm);
+                tk = qq_s - tk;
+            }
+            cert = tk > smin + eps ? 1 : 0;
+        }
+        if (a.cert) a.cert[q] = cert;
+        if (!cert && a.uncert) atomicAdd(a.uncert, 1u);
+    }
+    for (int j = tid; j < a.k; j += 256) {
+        const size_t o = (size_t)q * a.k + j;
+        if (j < nv) {
+            if (a.D) a.D[o] = (float)sc[j];
+            a.I[o] = (int64_t)ids[j] + a.id_offset;
+            if (a.S64) a.S64[o] = sc[j];
+        } else {
+            if (a.D) a.D[o] = a.metric == METRIC_IP ? -3.402823466e+38f : 3.402823466e+38f;
+            a.I[o] = -1;
+            if (a.S64) a.S64[o] = a.metric == METRIC_IP ? -1.7976931348623157e308 : 1.7976931348623157e308;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// merge of per-shard sorted results (after the RCCL all-gather)
+// ------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) k_merge_shards(int metric, const double* __restrict__ S_in,
+                                                     const int64_t* __restrict__ I_in, int G, int64_t nq, int k,
+                                                     double* __restrict__ S_out, int64_t* __restrict__ I_out,
+                                                     float* __restrict__ D_out) {
+    const int64_t q = (int64_t)blockIdx.x * 64 + threadIdx.x;
+    if (q >= nq) return;
+    int pos[64];
+    for (int g = 0; g < G; ++g) pos[g] = 0;
+    for (int j = 0; j < k; ++j) {
+        int bg = -1;
+        double bs = 0.0;
+        int64_t bi = 0;
+        for (int g = 0; g < G; ++g) {
+            if (pos[g] >= k) continue;
+            const size_t o = ((size_t)g * nq + q) * k + pos[g];
+            const int64_t id = I_in[o];
+            if (id < 0) continue;
+            const double s = S_in[o];
+            bool take = bg < 0;
+            if (!take) take = (s != bs) ? (metric == METRIC_IP ? s > bs : s < bs) : id < bi;
+            if (take) { bg = g; bs = s; bi = id; }
+        }
+        const size_t oo = (size_t)q * k + j;
+        if (bg < 0) {
+            S_out[oo] = metric == METRIC_IP ? -1.7976931348623157e308 : 1.7976931348623157e308;
+            I_out[oo] = -1;
+            if (D_out) D_out[oo] = metric == METRIC_IP ? -3.402823466e+38f : 3.402823466e+38f;
+        } else {
+            S_out[oo] = bs;
+            I_out[oo] = bi;
+            if (D_out) D_out[oo] = (float)bs;
+            pos[bg]++;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// launchers
+// ------------------------------------------------------------------------------------------------
+#define VS_DISPATCH_DT(dt, KERNEL, ...)                                       \
+    do {                                                                      \
+        if ((dt) == DT_F32) hipLaunchKernelGGL(KERNEL<DT_F32>, __VA_ARGS__);  \
+        else if ((dt) == DT_BF16) hipLaunchKernelGGL(KERNEL<DT_BF16>, __VA_ARGS__); \
+        else hipLaunchKernelGGL(KERNEL<DT_F16>, __VA_ARGS__);                 \
+    } while (0)
+
+static inline unsigned blocks4(int64_t n) { return (unsigned)((n + 3) / 4); }
+
+hipError_t launch_pack_rows(int dt, const float* src, int64_t n, int d, int dpad, uint8_t* data, int64_t lrow0,
+                            float* sqn, unsigned* maxsq, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    VS_DISPATCH_DT(dt, k_pack_rows, dim3(blocks4(n)), dim3(256), 0, st, src, n, d, dpad, data, lrow0, sqn, maxsq);
+    return hipGetLastError();
+}
+
+hipError_t launch_synth_rows(int dt, uint64_t seed, int64_t grow0, int64_t n, int d, int dpad, uint8_t* data,
+                             int64_t lrow0, int normalize, float* sqn, unsigned* maxsq, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    // base = splitmix64(seed), computed on the host exactly as the oracle does
+    uint64_t x = seed + 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    const uint64_t base = x ^ (x >> 31);
+    const int64_t CHUNK = 1 << 22;  // rows per launch (grid-size bound)
+    for (int64_t r0 = 0; r0 < n; r0 += CHUNK) {
+        const int64_t m = n - r0 < CHUNK ? n - r0 : CHUNK;
+        VS_DISPATCH_DT(dt, k_synth_rows, dim3(blocks4(m)), dim3(256), 0, st, base, grow0 + r0, m, d, dpad, data,
+                       lrow0 + r0, normalize, sqn, maxsq);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+static inline uint64_t host_splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+hipError_t launch_synth_f32(int dt, uint64_t seed, int64_t grow0, int64_t n, int d, int normalize, float* out,
+                            hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    VS_DISPATCH_DT(dt, k_synth_f32, dim3(blocks4(n)), dim3(256), 0, st, host_splitmix64(seed), grow0, n, d, normalize,
+                   out);
+    return hipGetLastError();
+}
+
+hipError_t launch_unpack_rows(int dt, const uint8_t* data, int64_t lrow0, int64_t n, int d, int dpad, float* out,
+                              hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    VS_DISPATCH_DT(dt, k_unpack_rows, dim3(blocks4(n)), dim3(256), 0, st, data, lrow0, n, d, dpad, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_rows(int dt, const uint8_t* data, const int64_t* ids, int64_t n, int d, int dpad,
+                              float* out, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    VS_DISPATCH_DT(dt, k_gather_rows, dim3(blocks4(n)), dim3(256), 0, st, data, ids, n, d, dpad, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_pack_qtile(int dt, const float* q, int nqb, int d, int dpad, uint8_t* qt, float* qinfo,
+                             hipStream_t st) {
+    if (dt == DT_BF16)
+        hipLaunchKernelGGL(k_pack_qtile<DT_BF16>, dim3(MFMA_QB / 4), dim3(256), 0, st, q, nqb, d, dpad, qt, qinfo);
+    else
+        hipLaunchKernelGGL(k_pack_qtile<DT_F16>, dim3(MFMA_QB / 4), dim3(256), 0, st, q, nqb, d, dpad, qt, qinfo);
+    return hipGetLastError();
+}
+
+hipError_t launch_pack_qf32(const float* q, int nqb, int nqpad, int d, int dpad, float* qp, float* qinfo,
+                            hipStream_t st) {
+    hipLaunchKernelGGL(k_pack_qf32, dim3(blocks4(nqpad)), dim3(256), 0, st, q, nqb, nqpad, d, dpad, qp, qinfo);
+    return hipGetLastError();
+}
+
+hipError_t launch_screen_mfma(int dt, const ScreenArgs& a, const uint8_t* qt, int nqb, hipStream_t st) {
+    static bool attr_set[3] = {false, false, false};
+    if (dt == DT_BF16) {
+        if (!attr_set[1]) {
+            hipFuncSetAttribute((const void*)k_screen_mfma<DT_BF16>, hipFuncAttributeMaxDynamicSharedMemorySize, MF_LDS);
+            attr_set[1] = true;
+        }
+        hipLaunchKernelGGL(k_screen_mfma<DT_BF16>, dim3(a.G), dim3(512), MF_LDS, st, a, qt, nqb);
+    } else {
+        if (!attr_set[2]) {
+            hipFuncSetAttribute((const void*)k_screen_mfma<DT_F16>, hipFuncAttributeMaxDynamicSharedMemorySize, MF_LDS);
+            attr_set[2] = true;
+        }
+        hipLaunchKernelGGL(k_screen_mfma<DT_F16>, dim3(a.G), dim3(512), MF_LDS, st, a, qt, nqb);
+    }
+    return hipGetLastError();
+}
+
+template <int DT>
+static void launch_gemv_dt(const ScreenArgs& a, const float* qp, int nqb, int nqpad, hipStream_t st) {
+    switch (nqpad) {
+        case 1: hipLaunchKernelGGL((k_screen_gemv<DT, 1>), dim3(a.G), dim3(256), 0, st, a, qp, nqb); break;
+        case 2: hipLaunchKernelGGL((k_screen_gemv<DT, 2>), dim3(a.G), dim3(256), 0, st, a, qp, nqb); break;
+        case 4: hipLaunchKernelGGL((k_screen_gemv<DT, 4>), dim3(a.G), dim3(256), 0, st, a, qp, nqb); break;
+        default: hipLaunchKernelGGL((k_screen_gemv<DT, 8>), dim3(a.G), dim3(256), 0, st, a, qp, nqb); break;
+    }
+}
+hipError_t launch_screen_gemv(int dt, const ScreenArgs& a, const float* qp, int nqb, int nqpad, hipStream_t st) {
+    if (dt == DT_F32) launch_gemv_dt<DT_F32>(a, qp, nqb, nqpad, st);
+    else if (dt == DT_BF16) launch_gemv_dt<DT_BF16>(a, qp, nqb, nqpad, st);
+    else launch_gemv_dt<DT_F16>(a, qp, nqb, nqpad, st);
+    return hipGetLastError();
+}
+
+hipError_t launch_merge(const u64* in, int nseg, int qstride, int nq, int Kp, u64* out, int* nseg_out,
+                        hipStream_t st) {
+    const int spb = (256 * MERGE_E) / Kp;  // segments per block (Kp <= 4096)
+    const int nb = (nseg + spb - 1) / spb;
+    hipLaunchKernelGGL(k_merge, dim3(nb, nq), dim3(256), 0, st, in, nseg, qstride, nq, Kp, spb, out);
+    *nseg_out = nb;
+    return hipGetLastError();
+}
+
+hipError_t launch_refine(const RefineArgs& a, int nq, hipStream_t st) {
+    int KP2 = 1;
+    while (KP2 < a.Kp) KP2 <<= 1;
+    const size_t lds = (size_t)KP2 * 12;
+    static bool attr = false;
+    if (!attr) {
+        hipFuncSetAttribute((const void*)k_refine<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_refine<0>, dim3(nq), dim3(256), lds, st, a, KP2);
+    return hipGetLastError();
+}
+
+hipError_t launch_merge_shards(int metric, const double* S_in, const int64_t* I_in, int G, int64_t nq, int k,
+                               double* S_out, int64_t* I_out, float* D_out, hipStream_t st) {
+    if (G > 64) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_merge_shards, dim3((unsigned)((nq + 63) / 64)), dim3(64), 0, st, metric, S_in, I_in, G, nq,
+                       k, S_out, I_out, D_out);
+    return hipGetLastError();
+}
+
+}  // namespace vs

@@ -1,0 +1,140 @@
+"""``FlatIndex``: the faiss-IndexFlat-shaped handle over libvs (one GPU shard).
+
+It is what ``VectorStore`` holds in ``.index`` where the reference holds a
+``faiss.IndexFlatIP`` / ``faiss.IndexFlatL2`` (/root/reference/utils/vector_store.py:72-81):
+``ntotal``, ``d``, ``metric_type``, ``add``, ``search``, ``reconstruct``, ``reset``.  Host
+methods take numpy arrays; ``*_device`` methods take raw device pointers (ints) so callers may
+hand in torch tensors' ``data_ptr()`` without torch types crossing the C ABI.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Tuple
+
+import numpy as np
+
+from . import _lib
+from ._lib import DTYPE_CODES, METRIC_IP, METRIC_L2, check
+
+METRIC_INNER_PRODUCT = METRIC_IP  # faiss.METRIC_INNER_PRODUCT == 0
+METRIC_L2_ = METRIC_L2            # faiss.METRIC_L2 == 1
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+class FlatIndex:
+    """Exact flat inner-product / squared-L2 index resident in one GPU's HBM."""
+
+    def __init__(self, d: int, metric: str = "ip", dtype: str = "f32", device: int = 0) -> None:
+        self._h = None
+        L = _lib.load()
+        m = metric.lower()
+        if m in ("ip", "cosine", "inner_product"):
+            code = METRIC_IP
+        elif m in ("l2", "euclidean"):
+            code = METRIC_L2
+        else:
+            raise ValueError(f"unknown metric {metric!r}")
+        if dtype not in DTYPE_CODES:
+            raise ValueError(f"unknown dtype {dtype!r}")
+        h = ctypes.c_void_p()
+        check(L.vs_create(int(d), code, DTYPE_CODES[dtype], int(device), ctypes.byref(h)))
+        self._h = h
+        self._L = L
+        self.d = int(d)
+        self.metric_type = code
+        self.dtype = dtype
+        self.device = int(device)
+
+    # -- faiss-like surface ------------------------------------------------------------------
+    @property
+    def ntotal(self) -> int:
+        return int(self._L.vs_ntotal(self._h))
+
+    def add(self, x) -> None:
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        if x.ndim != 2 or x.shape[1] != self.d:
+            raise ValueError(f"add expects an (n, {self.d}) array, got {x.shape}")
+        check(self._L.vs_add(self._h, _ptr(x), x.shape[0]))
+
+    def search(self, q, k: int) -> Tuple[np.ndarray, np.ndarray]:
+        q = np.ascontiguousarray(q, dtype=np.float32)
+        if q.ndim != 2 or q.shape[1] != self.d:
+            raise ValueError(f"search expects an (nq, {self.d}) array, got {q.shape}")
+        nq = q.shape[0]
+        k = int(k)
+        if k <= 0:
+            raise _lib.VsError(_lib.VS_ERR_ARG, "k must be > 0")
+        D = np.empty((nq, k), dtype=np.float32)
+        I = np.empty((nq, k), dtype=np.int64)
+        check(self._L.vs_search(self._h, _ptr(q), nq, k, _ptr(D), _ptr(I)))
+        return D, I
+
+    def reconstruct(self, i: int) -> np.ndarray:
+        out = np.empty((self.d,), dtype=np.float32)
+        check(self._L.vs_reconstruct(self._h, int(i), _ptr(out)))
+        return out
+
+    def reconstruct_n(self, i0: int, n: int) -> np.ndarray:
+        out = np.empty((int(n), self.d), dtype=np.float32)
+        if n:
+            check(self._L.vs_reconstruct_n(self._h, int(i0), int(n), _ptr(out)))
+        return out
+
+    def reset(self) -> None:
+        check(self._L.vs_reset(self._h))
+
+    # -- device-resident surface (bench / multi-GPU) -----------------------------------------
+    def add_device(self, x_ptr: int, n: int, stream: Optional[int] = None) -> None:
+        check(self._L.vs_add_device(self._h, x_ptr, int(n), stream or None))
+
+    def add_synthetic(self, seed: int, global_row0: int, n: int, normalize: bool = True) -> None:
+        check(self._L.vs_add_synthetic(self._h, int(seed), int(global_row0), int(n), int(bool(normalize))))
+
+    def search_device(self, q_ptr: int, nq: int, k: int, D_ptr: Optional[int], I_ptr: int,
+                      S64_ptr: Optional[int] = None, id_offset: int = 0, stream: Optional[int] = None) -> None:
+        check(self._L.vs_search_device(self._h, q_ptr, int(nq), int(k), D_ptr or None, I_ptr, S64_ptr or None,
+                                       int(id_offset), stream or None))
+
+    def set_timing(self, enable: bool) -> None:
+        check(self._L.vs_set_timing(self._h, int(bool(enable))))
+
+    def timing_fetch(self, cap: int = 4096):
+        buf = (ctypes.c_float * cap)()
+        kind = ctypes.c_int(0)
+        n = check(self._L.vs_timing_fetch(self._h, buf, cap, ctypes.byref(kind)))
+        return [float(buf[i]) for i in range(n)], {1: "mfma", 2: "gemv"}.get(kind.value, "none")
+
+    def uncertified_count(self) -> int:
+        return int(check(self._L.vs_uncertified_count(self._h)))
+
+    # -- lifecycle ----------------------------------------------------------------------------
+    def close(self) -> None:
+        if self._h is not None and self._h.value:
+            self._L.vs_destroy(self._h)
+        self._h = None
+
+    def __del__(self) -> None:  # pragma: no cover - interpreter shutdown ordering
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def merge_shards_device(metric_type: int, S_ptr: int, I_ptr: int, G: int, nq: int, k: int, S_out: int, I_out: int,
+                        D_out: Optional[int] = None, stream: Optional[int] = None) -> None:
+    """Merge G per-shard sorted (S64, id) lists [G][nq][k] on the device (after an all-gather)."""
+    L = _lib.load()
+    check(L.vs_merge_shards_device(int(metric_type), S_ptr, I_ptr, int(G), int(nq), int(k), S_out, I_out,
+                                   D_out or None, stream or None))
+
+
+def synthesize_device(device: int, seed: int, global_row0: int, n: int, d: int, out_ptr: int, normalize: bool = True,
+                      dtype: str = "f32", stream: Optional[int] = None) -> None:
+    """Write synthetic rows [global_row0, +n) as row-major fp32 (rounded to ``dtype``) to device
+    memory -- the same counter-hash generator as ``FlatIndex.add_synthetic``."""
+    L = _lib.load()
+    check(L.vs_synthesize(int(device), int(seed), int(global_row0), int(n), int(d), int(bool(normalize)),
+                          DTYPE_CODES[dtype], out_ptr, stream or None))

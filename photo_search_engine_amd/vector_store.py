@@ -1,0 +1,310 @@
+"""Drop-in ``VectorStore`` backed by the MI355X flat k-NN library.
+
+Same class name, constructor keywords, methods, attributes, error types/messages and sidecar
+files as /root/reference/utils/vector_store.py:15-280, so ``core/indexer.py`` and
+``core/searcher.py`` run unchanged.  Integration: replace the reference's
+``utils/vector_store.py`` body with ``from photo_search_engine_amd.vector_store import VectorStore``
+(INTEGRATION.md).
+
+What changes underneath:
+  * ``self.index`` is a :class:`~photo_search_engine_amd.index.FlatIndex` (HBM-resident shard on
+    one GPU) instead of a faiss CPU index; searches are exact (see include/vs.h).
+  * ``index_type="hnsw"`` is accepted, validated and recorded in the sidecar exactly as before,
+    but served by exact flat search (recall 1.0 >= HNSW); ``save()`` writes a flat IxFI/IxF2
+    payload for it.  ``load()`` reads flat files and the reference's HNSW (IHNf) files.
+  * ``_embeddings`` caches only rows added in this process (a dict), not one Python list per row.
+  * Bulk additions: :meth:`add` (n x d array) and :meth:`search_batch` (faiss (D, I) layout).
+
+Normalisation stays on the host in numpy, bit-identical to the reference
+(utils/vector_store.py:83-90), so stored vectors and query vectors are the same fp32 values.
+
+Environment knobs (new, optional): ``VECTOR_DEVICE`` (GPU ordinal, default 0) and
+``VECTOR_DTYPE`` (f32 | bf16 | f16 storage, default f32 = the reference's storage precision).
+"""
+from __future__ import annotations
+
+import json
+import os
+from typing import Any, Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import faiss_format
+from .index import FlatIndex
+
+METRIC_INNER_PRODUCT = 0
+METRIC_L2 = 1
+
+
+def _default_index_factory(dimension: int, metric: str) -> FlatIndex:
+    device = int(os.environ.get("VECTOR_DEVICE", "0") or 0)
+    dtype = (os.environ.get("VECTOR_DTYPE", "f32") or "f32").strip().lower()
+    return FlatIndex(dimension, metric="ip" if metric == "cosine" else "l2", dtype=dtype, device=device)
+
+
+# Module-level hook: tests may substitute a checker-backed index with the same surface.
+_index_factory = _default_index_factory
+
+
+class VectorStore:
+    """
+    向量存储与检索封装 (vector storage and retrieval).
+
+    Attributes:
+        dimension (Optional[int]): 向量维度
+        index_path (str): 索引文件路径
+        metadata_path (str): 元数据文件路径
+    """
+
+    def __init__(
+        self,
+        dimension: Optional[int],
+        index_path: str,
+        metadata_path: str,
+        metric: str = "cosine",
+        index_type: str = "flat",
+        hnsw_m: int = 32,
+        hnsw_ef_construction: int = 200,
+        hnsw_ef_search: int = 96,
+    ) -> None:
+        # utils/vector_store.py:44-62
+        self.dimension = dimension
+        self.index_path = index_path
+        self.metadata_path = metadata_path
+        self.meta_path = f"{self.index_path}.meta.json"
+        self.metric = metric.lower().strip() if metric else "l2"
+        if self.metric not in {"l2", "cosine"}:
+            raise ValueError("metric仅支持l2或cosine")
+        self.index_type = (index_type or "flat").strip().lower()
+        if self.index_type not in {"flat", "hnsw"}:
+            raise ValueError("index_type仅支持flat或hnsw")
+        self.hnsw_m = max(4, int(hnsw_m))
+        self.hnsw_ef_construction = max(8, int(hnsw_ef_construction))
+        self.hnsw_ef_search = max(8, int(hnsw_ef_search))
+
+        self.index = self._create_index(dimension) if dimension else None
+        self.metadata: List[Dict] = []
+        self._normalize = self.metric == "cosine"
+        self._embeddings: Dict[int, List[float]] = {}
+        self._path_to_index: Dict[str, int] = {}
+
+    # ------------------------------------------------------------------ internals
+    def _rebuild_path_index(self) -> None:
+        path_to_index: Dict[str, int] = {}
+        for index, metadata in enumerate(self.metadata):
+            photo_path = metadata.get("photo_path")
+            if isinstance(photo_path, str) and photo_path:
+                path_to_index[photo_path] = index
+        self._path_to_index = path_to_index
+
+    def _create_index(self, dimension: int):
+        return _index_factory(int(dimension), self.metric)
+
+    def _normalize_vector(self, vector: List[float]) -> List[float]:
+        # utils/vector_store.py:83-90, verbatim semantics (fp32, np.linalg.norm, zero passthrough)
+        if not self._normalize:
+            return vector
+        array = np.array(vector, dtype="float32")
+        norm = np.linalg.norm(array)
+        if norm == 0:
+            return vector
+        return (array / norm).astype("float32").tolist()
+
+    def _normalize_rows(self, rows: np.ndarray) -> np.ndarray:
+        """Bulk form of ``_normalize_vector``: each row normalised exactly as the single-row path
+        (same numpy calls per row, so the stored bits are identical)."""
+        rows = np.array(rows, dtype="float32", copy=True)
+        if not self._normalize:
+            return rows
+        for i in range(rows.shape[0]):
+            norm = np.linalg.norm(rows[i])
+            if norm != 0:
+                rows[i] = (rows[i] / norm).astype("float32")
+        return rows
+
+    def _write_index_meta(self) -> None:
+        payload = {
+            "index_type": self.index_type,
+            "metric": self.metric,
+            "dimension": self.dimension,
+            "hnsw_m": self.hnsw_m,
+            "hnsw_ef_construction": self.hnsw_ef_construction,
+            "hnsw_ef_search": self.hnsw_ef_search,
+        }
+        with open(self.meta_path, "w", encoding="utf-8") as file:
+            json.dump(payload, file, ensure_ascii=False, indent=2)
+
+    def _load_index_meta(self) -> Dict[str, Any]:
+        if not os.path.exists(self.meta_path):
+            raise ValueError("索引元信息缺失，请重新构建索引")
+        with open(self.meta_path, "r", encoding="utf-8") as file:
+            payload = json.load(file)
+        if not isinstance(payload, dict):
+            raise ValueError("索引元信息损坏，请重新构建索引")
+        return payload
+
+    def _validate_loaded_index(self, payload: Dict[str, Any], loaded: "faiss_format.FaissFile") -> None:
+        # utils/vector_store.py:125-140; an HNSW config accepts a flat or an HNSW file (both are
+        # served exactly), the metric of the payload must match the configured metric.
+        index_type = str(payload.get("index_type") or "").strip().lower()
+        metric = str(payload.get("metric") or "").strip().lower()
+        if index_type != self.index_type:
+            raise ValueError("索引类型与配置不一致，请重新构建索引")
+        if metric != self.metric:
+            raise ValueError("索引度量与配置不一致，请重新构建索引")
+        if self.index_type == "flat" and loaded.kind != "flat":
+            raise ValueError("索引结构与配置不一致，请重新构建索引")
+        want = METRIC_INNER_PRODUCT if self.metric == "cosine" else METRIC_L2
+        if loaded.metric_type != want:
+            raise ValueError("索引度量与配置不一致，请重新构建索引")
+
+    # ------------------------------------------------------------------ reference API
+    # 内部接口：仅允许indexer模块调用，禁止直接暴露给前端
+    def add_item(self, embedding: List[float], metadata: Dict) -> None:
+        """写入向量与元数据 (utils/vector_store.py:143-169)."""
+        if embedding is None:
+            raise ValueError("向量不能为空")
+        if self.index is None:
+            self.dimension = len(embedding)
+            self.index = self._create_index(self.dimension)
+        if len(embedding) != self.dimension:
+            raise ValueError(f"向量维度不匹配: {len(embedding)} != {self.dimension}")
+
+        normalized = self._normalize_vector(embedding)
+        vector = np.array([normalized], dtype="float32")
+        self.index.add(vector)
+        self.metadata.append(metadata)
+        self._embeddings[len(self.metadata) - 1] = normalized
+        photo_path = metadata.get("photo_path")
+        if isinstance(photo_path, str) and photo_path:
+            self._path_to_index[photo_path] = len(self.metadata) - 1
+
+    # 内部接口：仅允许searcher模块调用，禁止前端直接访问向量数据库
+    def search(self, query_embedding: List[float], top_k: int) -> List[Dict]:
+        """相似度检索 (utils/vector_store.py:172-198)."""
+        if self.index is None or self.index.ntotal == 0:
+            return []
+        if len(query_embedding) != self.dimension:
+            raise ValueError(f"向量维度不匹配: {len(query_embedding)} != {self.dimension}")
+
+        k = min(top_k, self.index.ntotal)
+        normalized = self._normalize_vector(query_embedding)
+        vector = np.array([normalized], dtype="float32")
+        distances, indices = self.index.search(vector, k)
+
+        results: List[Dict] = []
+        for distance, index in zip(distances[0].tolist(), indices[0].tolist()):
+            if index == -1:
+                continue
+            results.append({"metadata": self.metadata[index], "distance": float(distance)})
+        return results
+
+    def get_embedding_by_photo_path(self, photo_path: str) -> Optional[List[float]]:
+        index = self._path_to_index.get(photo_path)
+        if index is None:
+            return None
+        if index < len(self.metadata) and self.index is not None and index < self.index.ntotal:
+            cached = self._embeddings.get(index)
+            if cached is None:
+                vector = self.index.reconstruct(index)
+                cached = vector.astype("float32").tolist()
+                self._embeddings[index] = cached
+            if cached is not None:
+                return list(cached)
+        return None
+
+    def has_photo_path(self, photo_path: str) -> bool:
+        return photo_path in self._path_to_index
+
+    def save(self) -> None:
+        """索引持久化 (utils/vector_store.py:217-237)."""
+        if self.index is None:
+            raise ValueError("索引未初始化")
+
+        index_dir = os.path.dirname(self.index_path)
+        metadata_dir = os.path.dirname(self.metadata_path)
+        if index_dir:
+            os.makedirs(index_dir, exist_ok=True)
+        if metadata_dir:
+            os.makedirs(metadata_dir, exist_ok=True)
+
+        vectors = self.index.reconstruct_n(0, self.index.ntotal)
+        faiss_format.write_flat(self.index_path, vectors, self.index.metric_type)
+        self._write_index_meta()
+        with open(self.metadata_path, "w", encoding="utf-8") as file:
+            json.dump(self.metadata, file, ensure_ascii=False, indent=2)
+
+    def load(self) -> bool:
+        """加载索引与元数据 (utils/vector_store.py:239-260)."""
+        if not os.path.exists(self.index_path) or not os.path.exists(self.metadata_path):
+            return False
+
+        loaded = faiss_format.read_index(self.index_path)
+        index = self._create_index_with_metric(loaded.d, loaded.metric_type)
+        if loaded.ntotal:
+            index.add(loaded.vectors)
+        self.index = index
+        payload = self._load_index_meta()
+        self._validate_loaded_index(payload, loaded)
+
+        with open(self.metadata_path, "r", encoding="utf-8") as file:
+            self.metadata = json.load(file)
+        if self.index.ntotal != len(self.metadata):
+            raise ValueError("索引与元数据数量不一致，请重新构建索引")
+        self.dimension = self.index.d
+        self._embeddings = {}
+        self._rebuild_path_index()
+        return True
+
+    def _create_index_with_metric(self, dimension: int, metric_type: int):
+        metric = "cosine" if metric_type == METRIC_INNER_PRODUCT else "l2"
+        return _index_factory(int(dimension), metric)
+
+    def get_total_items(self) -> int:
+        """获取当前向量数量."""
+        if self.index is None:
+            return 0
+        return int(self.index.ntotal)
+
+    def clear(self) -> None:
+        """清空索引与元数据."""
+        self.index = self._create_index(self.dimension) if self.dimension else None
+        self.metadata = []
+        self._embeddings = {}
+        self._path_to_index = {}
+
+    # ------------------------------------------------------------------ batched additions
+    def add(self, embeddings: np.ndarray, metadatas: Sequence[Dict]) -> None:
+        """Bulk ``add_item``: n x d rows + n metadata dicts in one device transfer."""
+        rows = np.asarray(embeddings, dtype="float32")
+        if rows.ndim != 2:
+            raise ValueError("embeddings must be an (n, d) array")
+        if len(metadatas) != rows.shape[0]:
+            raise ValueError("metadatas must have one entry per row")
+        if rows.shape[0] == 0:
+            return
+        if self.index is None:
+            self.dimension = rows.shape[1]
+            self.index = self._create_index(self.dimension)
+        if rows.shape[1] != self.dimension:
+            raise ValueError(f"向量维度不匹配: {rows.shape[1]} != {self.dimension}")
+        self.index.add(self._normalize_rows(rows))
+        base = len(self.metadata)
+        self.metadata.extend(metadatas)
+        for i, md in enumerate(metadatas):
+            photo_path = md.get("photo_path") if isinstance(md, dict) else None
+            if isinstance(photo_path, str) and photo_path:
+                self._path_to_index[photo_path] = base + i
+
+    def search_batch(self, queries: np.ndarray, top_k: int) -> Tuple[np.ndarray, np.ndarray]:
+        """Batched search in faiss layout: (D nq x k float32, I nq x k int64), rows normalised
+        exactly like ``search``; k is clamped to ntotal as ``search`` does."""
+        q = np.asarray(queries, dtype="float32")
+        if q.ndim != 2:
+            raise ValueError("queries must be an (nq, d) array")
+        if self.index is None or self.index.ntotal == 0:
+            return np.zeros((q.shape[0], 0), dtype=np.float32), np.zeros((q.shape[0], 0), dtype=np.int64)
+        if q.shape[1] != self.dimension:
+            raise ValueError(f"向量维度不匹配: {q.shape[1]} != {self.dimension}")
+        k = min(top_k, self.index.ntotal)
+        return self.index.search(self._normalize_rows(q), k)

@@ -1,0 +1,49 @@
+"""TEST INFRASTRUCTURE: a checker-backed stand-in with FlatIndex's surface.
+
+Used only by CPU tests to exercise the host logic of ``VectorStore`` (validation, files, result
+layout) without a GPU.  Its search is the oracle's exact canonical search -- the same definition
+the HIP path is held to bit-for-bit in the GPU tests.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from oracle import oracle as O
+
+
+class OracleFlatIndex:
+    def __init__(self, d: int, metric: str = "ip") -> None:
+        self.d = int(d)
+        self.metric_type = 0 if metric in ("ip", "cosine") else 1
+        self._x = np.zeros((0, self.d), dtype=np.float32)
+
+    @property
+    def ntotal(self) -> int:
+        return int(self._x.shape[0])
+
+    def add(self, x) -> None:
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        assert x.ndim == 2 and x.shape[1] == self.d
+        self._x = np.concatenate([self._x, x], axis=0)
+
+    def search(self, q, k: int):
+        q = np.ascontiguousarray(q, dtype=np.float32)
+        if k <= 0:
+            raise RuntimeError("k must be > 0")
+        S, I = O.knn_exact(self._x, q, int(k), "ip" if self.metric_type == 0 else "l2")
+        D = S.astype(np.float32)
+        D[I < 0] = -3.4028235e38 if self.metric_type == 0 else 3.4028235e38
+        return D, I
+
+    def reconstruct(self, i: int) -> np.ndarray:
+        return self._x[int(i)].copy()
+
+    def reconstruct_n(self, i0: int, n: int) -> np.ndarray:
+        return self._x[int(i0):int(i0) + int(n)].copy()
+
+    def reset(self) -> None:
+        self._x = np.zeros((0, self.d), dtype=np.float32)
+
+
+def oracle_factory(dimension: int, metric: str):
+    return OracleFlatIndex(dimension, "ip" if metric == "cosine" else "l2")

@@ -1,0 +1,167 @@
+"""Parity of the HIP path (libvs.so through the C ABI) against the CPU oracle (MI355X only).
+
+Bar: returned ids bit-exact and distances bit-exact (D = fp32 rounding of the canonical fp64
+score, oracle/vs_oracle.c) against ``oracle.knn_exact`` on the SAME stored values (rows read back
+through vs_reconstruct_n, i.e. after the dtype rounding the index applies), and within 1e-5 of
+the faiss fp32 restatement.  Shapes cover both screen kernels (GEMV: nq <= 8 or f32 storage;
+MFMA: bf16/f16 with nq > 8), both metrics, padding of d and N, k > ntotal, exact duplicates
+(ties -> lower id), zero vectors, multi-block query batches, and the synthetic generator.
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def FlatIndex():
+    from photo_search_engine_amd.index import FlatIndex as FI
+    return FI
+
+
+def _check_exact(ix, q, k, metric):
+    x = ix.reconstruct_n(0, ix.ntotal)
+    D, I = ix.search(q, k)
+    S, Ie = O.knn_exact(x, q, k, metric)
+    np.testing.assert_array_equal(I, Ie)
+    Dexp = np.where(Ie < 0, 0.0, S).astype(np.float32)
+    Dexp[Ie < 0] = -3.4028235e38 if metric == "ip" else 3.4028235e38
+    np.testing.assert_array_equal(D, Dexp)
+    Df, _ = O.knn_faiss_fp32(x, q, min(k, x.shape[0]), metric)
+    assert np.max(np.abs(D[:, :Df.shape[1]].astype(np.float64) - Df)) <= 1e-5
+    return D, I
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16"])
+def test_synthetic_generator_bit_identical(FlatIndex, dtype):
+    ix = FlatIndex(200, "ip", dtype)
+    ix.add_synthetic(O.SEED_CORPUS, 1000, 777, True)
+    got = ix.reconstruct_n(0, 777)
+    want = O.synth_rows(O.SEED_CORPUS, 1000, 777, 200, True, dtype)
+    np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16"])
+def test_add_roundtrip_rounding(FlatIndex, dtype):
+    rng = np.random.default_rng(3)
+    x = rng.standard_normal((300, 70)).astype(np.float32)
+    ix = FlatIndex(70, "ip", dtype)
+    ix.add(x[:100])
+    ix.add(x[100:])
+    np.testing.assert_array_equal(ix.reconstruct_n(0, 300), O.round_dtype(x, dtype))
+    np.testing.assert_array_equal(ix.reconstruct(123), O.round_dtype(x[123], dtype))
+
+
+@pytest.mark.parametrize("metric", ["ip", "l2"])
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16"])
+@pytest.mark.parametrize("nq,k", [(1, 10), (3, 5), (8, 37)])
+def test_gemv_path_exact(FlatIndex, metric, dtype, nq, k):
+    d, N = 96, 5000
+    ix = FlatIndex(d, metric, dtype)
+    ix.add_synthetic(O.SEED_CORPUS, 0, N, True)
+    q = O.synth_rows(O.SEED_QUERIES, 0, nq, d, True, "f32")
+    _check_exact(ix, q, k, metric)
+
+
+@pytest.mark.parametrize("metric", ["ip", "l2"])
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+@pytest.mark.parametrize("nq,k,N,d", [(40, 10, 9000, 128), (256, 100, 20000, 192), (300, 7, 3001, 72)])
+def test_mfma_path_exact(FlatIndex, metric, dtype, nq, k, N, d):
+    ix = FlatIndex(d, metric, dtype)
+    ix.add_synthetic(O.SEED_CORPUS, 0, N, True)
+    q = O.synth_rows(O.SEED_QUERIES, 0, nq, d, True, dtype)  # queries in the corpus dtype (cfg3)
+    _check_exact(ix, q, k, metric)
+
+
+def test_mfma_fp32_queries_over_bf16_corpus(FlatIndex):
+    # queries NOT representable in bf16: screen uses rounded queries, refine uses the exact ones
+    ix = FlatIndex(256, "ip", "bf16")
+    ix.add_synthetic(O.SEED_CORPUS, 0, 30000, True)
+    q = O.synth_rows(O.SEED_QUERIES, 0, 64, 256, True, "f32")
+    _check_exact(ix, q, 50, "ip")
+
+
+def test_f32_batch_over_gemv_blocks(FlatIndex):
+    ix = FlatIndex(1536, "ip", "f32")
+    ix.add_synthetic(O.SEED_CORPUS, 0, 12000, True)
+    q = O.synth_rows(O.SEED_QUERIES, 0, 21, 1536, True, "f32")
+    _check_exact(ix, q, 10, "ip")
+
+
+def test_edge_small_and_k_beyond_ntotal(FlatIndex):
+    for metric in ("ip", "l2"):
+        ix = FlatIndex(8, metric, "f32")
+        x = np.array([[1.0] * 8, [0.5] * 8, [0.0] * 8], np.float32)
+        ix.add(x)
+        D, I = ix.search(x[:1], 5)
+        assert list(I[0, 3:]) == [-1, -1]
+        _check_exact(ix, x, 5, metric)
+
+
+def test_edge_duplicates_ties_lower_id(FlatIndex):
+    rng = np.random.default_rng(4)
+    base = rng.standard_normal((50, 64)).astype(np.float32)
+    x = np.concatenate([base, np.repeat(base[7:8], 300, axis=0), base], axis=0)  # 300 exact copies
+    for dtype in ("f32", "bf16"):
+        ix = FlatIndex(64, "ip", dtype)
+        ix.add(x)
+        q = np.repeat(base[7:8], 20, axis=0) if dtype == "bf16" else base[7:8]
+        D, I = _check_exact(ix, q, 40, "ip")
+        assert I[0, 0] == 7  # the earliest copy wins the tie
+
+
+def test_edge_zero_vectors_and_constant_rows(FlatIndex):
+    x = np.zeros((600, 40), np.float32)
+    x[::3] = 1.0 / np.sqrt(40)
+    ix = FlatIndex(40, "ip", "f32")
+    ix.add(x)
+    q = np.full((2, 40), 1.0 / np.sqrt(40), np.float32)
+    _check_exact(ix, q, 250, "ip")
+
+
+def test_large_k(FlatIndex):
+    ix = FlatIndex(64, "ip", "f32")
+    ix.add_synthetic(O.SEED_CORPUS, 0, 50000, True)
+    q = O.synth_rows(O.SEED_QUERIES, 0, 2, 64, True, "f32")
+    _check_exact(ix, q, 1500, "ip")
+
+
+def test_device_api_and_uncertified_counter(FlatIndex):
+    import torch
+    ix = FlatIndex(128, "ip", "bf16")
+    ix.add_synthetic(O.SEED_CORPUS, 0, 40000, True)
+    q = O.synth_rows(O.SEED_QUERIES, 0, 100, 128, True, "bf16")
+    qd = torch.from_numpy(q).cuda()
+    D = torch.empty((100, 10), dtype=torch.float32, device="cuda")
+    I = torch.empty((100, 10), dtype=torch.int64, device="cuda")
+    S = torch.empty((100, 10), dtype=torch.float64, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    ix.search_device(qd.data_ptr(), 100, 10, D.data_ptr(), I.data_ptr(), S.data_ptr(), 5, st)
+    torch.cuda.synchronize()
+    x = ix.reconstruct_n(0, ix.ntotal)
+    Se, Ie = O.knn_exact(x, q, 10, "ip")
+    np.testing.assert_array_equal(I.cpu().numpy(), Ie + 5)
+    np.testing.assert_array_equal(S.cpu().numpy(), Se)
+    assert ix.uncertified_count() == 0
+
+
+def test_reset_and_reuse(FlatIndex):
+    ix = FlatIndex(32, "l2", "f32")
+    ix.add_synthetic(O.SEED_CORPUS, 0, 1000, True)
+    ix.reset()
+    assert ix.ntotal == 0
+    x = O.synth_rows(7, 0, 500, 32, True, "f32")
+    ix.add(x)
+    _check_exact(ix, x[:4], 9, "l2")
+
+
+def test_real_reference_index_self_queries(FlatIndex):
+    import os
+    from photo_search_engine_amd import faiss_format
+    ff = faiss_format.read_index(os.path.join(os.path.dirname(__file__), "golden", "ref_photo_search.index"))
+    ix = FlatIndex(ff.d, "ip", "f32")
+    ix.add(np.ascontiguousarray(ff.vectors))
+    D, I = _check_exact(ix, np.ascontiguousarray(ff.vectors), 10, "ip")
+    np.testing.assert_array_equal(I[:, 0], np.arange(77))
