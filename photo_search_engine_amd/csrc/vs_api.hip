@@ -81,10 +81,10 @@ struct DevBuf {
 // per-call execution context: stream + workspace (pooled; one per concurrent search)
 struct Ctx {
     hipStream_t stream = nullptr;
-    DevBuf qdev, qtile, qinfo, qpad, cand, part, merge_a, merge_b, outD, outI, outS, cert;
+    DevBuf qdev, qtile, qinfo, qpad, cand, part, merge_a, merge_b, outD, outI, outS, cert, thr0;
     std::vector<int> cert_host;
     ~Ctx() {
-        for (DevBuf* b : {&qdev, &qtile, &qinfo, &qpad, &cand, &part, &merge_a, &merge_b, &outD, &outI, &outS, &cert})
+        for (DevBuf* b : {&qdev, &qtile, &qinfo, &qpad, &cand, &part, &merge_a, &merge_b, &outD, &outI, &outS, &cert, &thr0})
             b->release();
         if (stream) hipStreamDestroy(stream);
     }
@@ -197,6 +197,10 @@ int screen_depth(int k) {
     return std::min(kp, KP_MAX);
 }
 
+// optimistic seed: the 16th best key of the strided row sample (expected ~16 * N / sample rows
+// corpus rows above it, far more than Kp; any query left short is caught by the certificate)
+constexpr int kOptimisticSeedRank = 16;
+
 float gamma_of(int d) {
     const double u = 5.9604644775390625e-08;  // 2^-24
     const double n = (double)d + 64.0;
@@ -204,8 +208,9 @@ float gamma_of(int d) {
 }
 
 // Enqueue one query block through screen -> merge -> refine.  q: device fp32 [nqb][d].
+// seed_rank: 0 = proven (safe) seed, > 0 = optimistic seed at that sample rank (see k_seed_thr)
 void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, float* D, int64_t* I, double* S64,
-                  int* cert, int64_t id_offset, hipStream_t st) {
+                  int* cert, int64_t id_offset, hipStream_t st, int seed_rank) {
     const int64_t tiles = (ix->ntotal + TR - 1) / TR;
     const bool use_mfma = ix->dtype != DT_F32 && nqb > GEMV_NQ_MAX && Kp <= MFMA_KP_MAX;
     ScreenArgs a{};
@@ -238,6 +243,49 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
     a.cand = c->cand.as<u64>();
     a.part = c->part.as<u64>();
 
+    // merge partial lists [nseg][qstride][Kp] down to one list per query; returns it
+    auto merge_all = [&](const u64* src, int nseg, int qstride) -> const u64* {
+        const int spb = (256 * 16) / Kp;  // k_merge: 4096 keys per block
+        const size_t mbytes = (size_t)std::max(1, (nseg + spb - 1) / spb) * nqb * Kp * sizeof(u64);
+        c->merge_a.ensure(mbytes);
+        c->merge_b.ensure(mbytes);
+        u64* bufs[2] = {c->merge_a.as<u64>(), c->merge_b.as<u64>()};
+        int which = 0;
+        while (nseg > 1) {
+            int nout = 0;
+            HIP_CHECK(launch_merge(src, nseg, qstride, nqb, Kp, bufs[which], &nout, st));
+            src = bufs[which];
+            which ^= 1;
+            nseg = nout;
+            qstride = nqb;
+        }
+        return src;
+    };
+
+    // threshold seeding (MFMA path): screen one tile per workgroup, strided over the shard, and
+    // start every workgroup of the main pass at the sample's Kp-th best key per query
+    a.tile_stride = 0;
+    a.thr0 = nullptr;
+    bool optimistic = false;
+    if (use_mfma && tiles >= 4 * (int64_t)a.G) {
+        // sample = 2 tiles per CU (one per workgroup, 2 x num_cu workgroups), evenly strided
+        ScreenArgs sa = a;
+        sa.G = 2 * a.G;
+        sa.tile_stride = (int)(tiles / sa.G);
+        c->part.ensure((size_t)sa.G * QB * Kp * sizeof(u64));
+        c->cand.ensure((size_t)sa.G * QB * a.cap * sizeof(u64));
+        sa.part = c->part.as<u64>();
+        sa.cand = c->cand.as<u64>();
+        a.part = sa.part;
+        a.cand = sa.cand;
+        HIP_CHECK(launch_screen_mfma(ix->dtype, sa, c->qtile.as<uint8_t>(), nqb, st));
+        const u64* sample = merge_all(sa.part, sa.G, QB);
+        c->thr0.ensure(sizeof(u64) * MFMA_QB);
+        HIP_CHECK(launch_seed_thr(sample, Kp, nqb, c->thr0.as<u64>(), seed_rank, st));
+        a.thr0 = c->thr0.as<u64>();
+        optimistic = seed_rank > 0;
+    }
+
     const bool timing = ix->timing.load();
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (timing) {
@@ -245,32 +293,31 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
         HIP_CHECK(hipEventCreate(&e1));
         HIP_CHECK(hipEventRecord(e0, st));
     }
+    static const bool dbg_stats = getenv("VS_MF_STATS") != nullptr;
+    unsigned* dbg = nullptr;
+    if (dbg_stats && use_mfma) {
+        HIP_CHECK(hipMalloc(&dbg, 16 * sizeof(unsigned)));
+        HIP_CHECK(hipMemsetAsync(dbg, 0, 16 * sizeof(unsigned), st));
+        a.dbg = dbg;
+    }
     if (use_mfma) HIP_CHECK(launch_screen_mfma(ix->dtype, a, c->qtile.as<uint8_t>(), nqb, st));
     else HIP_CHECK(launch_screen_gemv(ix->dtype, a, c->qpad.as<float>(), nqb, QB, st));
+    if (dbg) {
+        unsigned h[16];
+        HIP_CHECK(hipMemcpyAsync(h, dbg, sizeof(h), hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+        fprintf(stderr, "[vs stats] inserts=%u slowpath_lanes=%u compactions=%u pool_overflow=%u G=%d seeded=%d\n",
+                h[0], h[1], h[2], h[3], a.G, a.thr0 != nullptr);
+        hipFree(dbg);
+        a.dbg = nullptr;
+    }
     if (timing) {
         HIP_CHECK(hipEventRecord(e1, st));
         std::lock_guard<std::mutex> g(ix->tmtx);
         ix->tev.emplace_back(e0, e1);
         ix->last_kernel_kind = use_mfma ? 1 : 2;
     }
-
-    // merge partial lists [G][QB][Kp] down to one list per query
-    const u64* cur = a.part;
-    int nseg = a.G, qstride = QB;
-    const int spb = (256 * 16) / Kp;  // k_merge: 4096 keys per block
-    const size_t mbytes = (size_t)std::max(1, (a.G + spb - 1) / spb) * nqb * Kp * sizeof(u64);
-    c->merge_a.ensure(mbytes);
-    c->merge_b.ensure(mbytes);
-    u64* bufs[2] = {c->merge_a.as<u64>(), c->merge_b.as<u64>()};
-    int which = 0;
-    while (nseg > 1) {
-        int nout = 0;
-        HIP_CHECK(launch_merge(cur, nseg, qstride, nqb, Kp, bufs[which], &nout, st));
-        cur = bufs[which];
-        which ^= 1;
-        nseg = nout;
-        qstride = nqb;
-    }
+    const u64* cur = merge_all(a.part, a.G, QB);
     // refine expects cand[q*Kp + j] (qstride == nqb) or part[0][q][Kp] (qstride QB, same row offset)
     RefineArgs r{};
     r.cand = cur;
@@ -292,12 +339,13 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
     r.S64 = S64;
     r.cert = cert;
     r.uncert = ix->d_uncert;
+    r.optimistic = optimistic ? 1 : 0;
     HIP_CHECK(launch_refine(r, nqb, st));
 }
 
 // Full search of nq device queries; outputs device [nq][k].
 void search_all(vs_index* ix, Ctx* c, const float* q, int64_t nq, int k, int Kp, float* D, int64_t* I, double* S64,
-                int* cert, int64_t id_offset, hipStream_t st) {
+                int* cert, int64_t id_offset, hipStream_t st, int seed_rank) {
     const int64_t tiles = (ix->ntotal + TR - 1) / TR;
     (void)tiles;
     const bool mfma_ok = ix->dtype != DT_F32 && Kp <= MFMA_KP_MAX;
@@ -308,7 +356,7 @@ void search_all(vs_index* ix, Ctx* c, const float* q, int64_t nq, int k, int Kp,
         if (mfma_ok && rem > GEMV_NQ_MAX) nqb = (int)std::min<int64_t>(rem, MFMA_QB);
         else nqb = (int)std::min<int64_t>(rem, GEMV_NQ_MAX);
         search_block(ix, c, q + done * ix->d, nqb, k, Kp, D ? D + done * k : nullptr, I + done * k,
-                     S64 ? S64 + done * k : nullptr, cert ? cert + done : nullptr, id_offset, st);
+                     S64 ? S64 + done * k : nullptr, cert ? cert + done : nullptr, id_offset, st, seed_rank);
         done += nqb;
     }
 }
@@ -480,7 +528,8 @@ int vs_search_device(vs_index* ix, const float* q_dev, int64_t nq, int32_t k, fl
         hipStream_t st = stream ? (hipStream_t)stream : ix->own;
         if (ix->ntotal == 0) throw VsError(VS_ERR_ARG, "index is empty");
         CtxLease L(ix);
-        search_all(ix, L.c, q_dev, nq, k, screen_depth(k), D_dev, I_dev, S64_dev, nullptr, id_offset, st);
+        search_all(ix, L.c, q_dev, nq, k, screen_depth(k), D_dev, I_dev, S64_dev, nullptr, id_offset, st,
+                   kOptimisticSeedRank);
     });
 }
 
@@ -517,7 +566,7 @@ int vs_search(vs_index* ix, const float* q, int64_t nq, int32_t k, float* D, int
         std::vector<int64_t> Ik((size_t)nq * kk);
         c->cert_host.resize((size_t)nq);
         search_all(ix, c, c->qdev.as<float>(), nq, kk, Kp, c->outD.as<float>(), c->outI.as<int64_t>(), nullptr,
-                   c->cert.as<int>(), 0, st);
+                   c->cert.as<int>(), 0, st, kOptimisticSeedRank);
         HIP_CHECK(hipMemcpyAsync(Dk.data(), c->outD.p, Dk.size() * sizeof(float), hipMemcpyDeviceToHost, st));
         HIP_CHECK(hipMemcpyAsync(Ik.data(), c->outI.p, Ik.size() * sizeof(int64_t), hipMemcpyDeviceToHost, st));
         HIP_CHECK(hipMemcpyAsync(c->cert_host.data(), c->cert.p, (size_t)nq * sizeof(int), hipMemcpyDeviceToHost, st));
@@ -531,7 +580,7 @@ int vs_search(vs_index* ix, const float* q, int64_t nq, int32_t k, float* D, int
                     throw VsError(VS_ERR_UNCERTIFIED, "exactness certificate failed at maximum screening depth");
                 Kr = (int)std::min<int64_t>(std::min<int64_t>((int64_t)Kr * 4, KP_MAX), round_up(ix->ntotal, 16));
                 search_all(ix, c, c->qdev.as<float>() + qi * ix->d, 1, kk, Kr, c->outD.as<float>(),
-                           c->outI.as<int64_t>(), nullptr, c->cert.as<int>(), 0, st);
+                           c->outI.as<int64_t>(), nullptr, c->cert.as<int>(), 0, st, /*safe seed*/ 0);
                 HIP_CHECK(hipMemcpyAsync(Dk.data() + qi * kk, c->outD.p, kk * sizeof(float), hipMemcpyDeviceToHost, st));
                 HIP_CHECK(hipMemcpyAsync(Ik.data() + qi * kk, c->outI.p, kk * sizeof(int64_t), hipMemcpyDeviceToHost, st));
                 HIP_CHECK(hipMemcpyAsync(&c->cert_host[qi], c->cert.p, sizeof(int), hipMemcpyDeviceToHost, st));

@@ -1,13 +1,13 @@
 // vs_internal.h -- shared constants, HBM layout and kernel launchers of libvs (gfx950 only).
 //
 // HBM layout of a corpus shard ("row tiles"):
-//   rows are grouped in tiles of TR = 256; d is padded to dpad = roundup(d, 64);
-//   inside a tile the matrix is stored chunk-major: [chunk c = i / 64][row r in tile][64 elements]
-//   so element (r, i) of a tile lives at  c*(TR*CB) + (r % TR)*CB + (i % 64)*es,
-//   CB = 64*es bytes (128 B bf16/f16, 256 B f32).
-// One K-step of the MFMA screen (256 rows x 64 elements) is therefore one contiguous 32 KiB
-// (bf16) block, every global load is a full 16 B/lane coalesced piece, and a row's 64-element
-// chunk is one 128 B line for the exact-rescoring gather.
+//   rows are grouped in tiles of TR = 256; d is padded to dpad = roundup(d, 32);
+//   inside a tile the matrix is stored chunk-major: [chunk c = i / 32][row r in tile][32 elements]
+//   so element (r, i) of a tile lives at  c*(TR*CB) + (r % TR)*CB + (i % 32)*es,
+//   CB = 32*es bytes (64 B bf16/f16, 128 B f32).
+// One K-step of the MFMA screen (256 rows x 32 elements) is therefore one contiguous 16 KiB
+// (bf16) block, every global load is a full 16 B/lane coalesced piece, and a row's chunk is a
+// 64 B / 128 B contiguous piece for the exact-rescoring gather.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -15,7 +15,7 @@
 namespace vs {
 
 constexpr int TR = 256;        // rows per tile
-constexpr int CH = 64;         // elements per chunk (= one MFMA K-step)
+constexpr int CH = 32;         // elements per chunk (= one MFMA K-step)
 constexpr int DT_F32 = 0, DT_BF16 = 1, DT_F16 = 2;
 constexpr int METRIC_IP = 0, METRIC_L2 = 1;
 
@@ -45,6 +45,9 @@ struct ScreenArgs {
     u64* cand;               // [G][QB][cap]
     u64* part;               // [G][QB][Kp]
     int G;                   // workgroups
+    int tile_stride;         // > 0: workgroup b screens only tile b*tile_stride (threshold seeding)
+    const u64* thr0;         // [QB] initial per-query key threshold (keys > thr0 kept), or null
+    unsigned* dbg;           // debug counters (VS_MF_STATS): inserts, slow paths, compactions, overflows
 };
 
 // ---- launchers (vs_kernels.hip) -------------------------------------------------------------
@@ -59,7 +62,7 @@ hipError_t launch_unpack_rows(int dt, const uint8_t* data, int64_t lrow0, int64_
 hipError_t launch_gather_rows(int dt, const uint8_t* data, const int64_t* ids, int64_t n, int d, int dpad,
                               float* out, hipStream_t st);
 
-// queries: MFMA tile (dtype, [nks][256][64]) or fp32 padded [NQ][dpad]; qinfo[q*2] = ||q_hat||,
+// queries: MFMA tile (dtype, [nks][256][32]) or fp32 padded [NQ][dpad]; qinfo[q*2] = ||q_hat||,
 // qinfo[q*2+1] = ||q_hat - q|| (upper bounds, fp32)
 hipError_t launch_pack_qtile(int dt, const float* q, int nqb, int d, int dpad, uint8_t* qt, float* qinfo,
                              hipStream_t st);
@@ -90,8 +93,14 @@ struct RefineArgs {
     double* S64;           // [nq][k] (may be null)
     int* cert;             // [nq] 1 = certified exact (may be null)
     unsigned* uncert;      // device counter (may be null)
+    int optimistic;        // screened with an optimistic seed: fewer than Kp candidates = uncertified
 };
 hipError_t launch_refine(const RefineArgs& a, int nq, hipStream_t st);
+// thr0[q] = (list q holds Kp keys) ? min key - 1 : 0   -- a valid lower bound for the final
+// Kp-th key, because the list is the exact top-Kp of a SUBSET of the rows
+// rank > 0: OPTIMISTIC seed = the rank-th best sample key (not a proven bound; the refine kernel's
+// certificate then rejects any query left with fewer than Kp candidates)
+hipError_t launch_seed_thr(const u64* list, int Kp, int nq, u64* thr0, int rank, hipStream_t st);
 
 hipError_t launch_merge_shards(int metric, const double* S_in, const int64_t* I_in, int G, int64_t nq, int k,
                                double* S_out, int64_t* I_out, float* D_out, hipStream_t st);

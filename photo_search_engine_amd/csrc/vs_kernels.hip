@@ -15,6 +15,7 @@
 #include "vs_internal.h"
 
 #include <math.h>
+#include <stdlib.h>
 
 namespace vs {
 
@@ -281,8 +282,8 @@ __device__ __forceinline__ int block_compact_mem(const u64* src, u64* dst, int n
 // ingest: pack host/device fp32 rows into the tiled layout; synthetic rows; unpack
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ int64_t tiled_off(int64_t row, int i, int dpad, int es) {
-    return (row / TR) * (int64_t)TR * dpad * es + (int64_t)(i >> 6) * TR * 64 * es + (row % TR) * 64 * es +
-           (int64_t)(i & 63) * es;
+    return (row / TR) * (int64_t)TR * dpad * es + (int64_t)(i >> 5) * TR * CH * es + (row % TR) * CH * es +
+           (int64_t)(i & 31) * es;
 }
 
 // one wave per row; element i handled by lane i & 63 (the canonical fp32 order for sqn)
@@ -395,7 +396,7 @@ __global__ void __launch_bounds__(256) k_gather_rows(const uint8_t* __restrict__
 // ------------------------------------------------------------------------------------------------
 // query packing
 // ------------------------------------------------------------------------------------------------
-// MFMA query tile [nks][256][64] in the corpus dtype; qinfo = (||q_hat||, ||q_hat - q||) in fp64,
+// MFMA query tile [nks][256][32] in the corpus dtype; qinfo = (||q_hat||, ||q_hat - q||) in fp64,
 // rounded up to fp32.
 template <int DT>
 __global__ void __launch_bounds__(256) k_pack_qtile(const float* __restrict__ q, int nqb, int d, int dpad,
@@ -406,7 +407,7 @@ __global__ void __launch_bounds__(256) k_pack_qtile(const float* __restrict__ q,
     double n2 = 0.0, e2 = 0.0;
     for (int i = lane; i < dpad; i += 64) {
         float v = (r < nqb && i < d) ? q[(int64_t)r * d + i] : 0.0f;
-        float st = round_store<DT>(v, qt + (int64_t)(i >> 6) * MFMA_QB * 128 + (int64_t)r * 128 + (i & 63) * 2);
+        float st = round_store<DT>(v, qt + (int64_t)(i >> 5) * MFMA_QB * 64 + (int64_t)r * 64 + (i & 31) * 2);
         n2 += (double)st * st;
         double df = (double)st - (double)v;
         e2 += df * df;
@@ -445,43 +446,104 @@ __global__ void __launch_bounds__(256) k_pack_qf32(const float* __restrict__ q, 
 // ------------------------------------------------------------------------------------------------
 // K1: MFMA screen (bf16 / f16 corpus, up to 256 queries per launch)
 // ------------------------------------------------------------------------------------------------
-// Workgroup = 512 threads = 8 waves, one per CU (132 KiB LDS), persistent over a contiguous range
-// of row tiles.  Output tile per K-step pass: 256 corpus rows (M) x 256 queries (N), K = dpad.
+// Workgroup = 512 threads = 8 waves (2 per SIMD), one per CU, persistent over a contiguous range
+// of row tiles.  Output tile per tile pass: 256 corpus rows (M) x 256 queries (N), K = dpad.
 // Waves 4(M) x 2(N): each wave 64 rows x 128 queries = 4 x 8 MFMA 16x16x32 tiles, 128 acc VGPRs.
-// Staging: both operands are contiguous 32 KiB blocks per K-step (tiled layout), copied by
-// global_load_lds (16 B/lane) into a lane-linear LDS image whose 16 B pieces are XOR-swizzled
-// on the SOURCE address (piece p of row r holds chunk p ^ ((r >> 1) & 7)), so every ds_read_b128
-// fragment read is bank-conflict free.  Two LDS stages: the next K-step streams in while the
-// current one is multiplied.
-constexpr int MF_STAGE = 65536;  // A (corpus) 32 KiB + B (queries) 32 KiB
-constexpr int MF_LDS = 2 * MF_STAGE + 256 * 8 + 256 * 4 + 256 * 4;
+//
+// K-step = 32 elements; its operands are two contiguous 16 KiB blocks (the tile's corpus rows,
+// the query tile) copied by LDS-DMA (global_load_lds_dwordx4, inline asm) into a 4-slot LDS ring
+// MF_DEPTH = 3 K-steps ahead of the MFMAs.  Each K-step waits only for its own stage (counted
+// s_waitcnt vmcnt, raw s_barrier), so three stages (48 KiB of corpus per CU) stay in flight
+// across barriers.  The lane-linear LDS image is XOR-swizzled on the SOURCE address (64 B rows:
+// 16 B piece p of row r holds chunk p ^ perm[(r >> 2) & 3]) so every ds_read_b128 fragment read
+// is bank-conflict free.
+constexpr int MF_SLOT = 32768;  // 16 KiB corpus + 16 KiB queries
+constexpr int MF_SLOTS = 4;
+constexpr int MF_DEPTH = MF_SLOTS - 1;
+constexpr int MF_THREADS = 512;
+constexpr int MF_POOL = 512;  // LDS insert pool of the loader waves (flushed by the writer waves)
+constexpr int MF_LDS = MF_SLOTS * MF_SLOT + 256 * 8 + 256 * 4 + 256 * 4 + 16 + MF_POOL * 8 + MF_POOL * 4;
 
 typedef __attribute__((address_space(3))) uint8_t* lds_u8_t;
 
-// LDS-DMA of 16 B per lane: LDS[m0 + lane*16] <- global[gptr].  Issued as inline asm so the
-// compiler does not fence every later ds_read with vmcnt(0) (it cannot tell which LDS bytes a
-// builtin DMA writes); the kernel waits for these with its own s_waitcnt vmcnt before the barrier
-// that publishes the stage.
+// LDS-DMA of 16 B per lane: LDS[m0 + lane*16] <- global[gptr].  Inline asm, so the compiler
+// neither fences later ds_reads with vmcnt(0) (it cannot tell which LDS bytes a builtin DMA
+// writes) nor drains it at barriers; the kernel counts these loads in its own s_waitcnt.
 __device__ __forceinline__ void glds16(const void* gptr, uint32_t lds_base) {
     asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gptr), "s"(lds_base)
                  : "memory", "m0");
 }
-__device__ __forceinline__ uint32_t lds_addr(const uint8_t* p) {
-    return (uint32_t)(uintptr_t)(lds_u8_t)(p);
+__device__ __forceinline__ uint32_t lds_addr(const uint8_t* p) { return (uint32_t)(uintptr_t)(lds_u8_t)(p); }
+
+// swizzle: piece position of 16 B chunk c of LDS row r (64 B rows) = c ^ mf_swz(r)
+__device__ __forceinline__ int mf_swz(int r) { return (0x78 >> (2 * ((r >> 2) & 3))) & 3; }
+
+__device__ __forceinline__ void glds16_nt(const void* gptr, uint32_t lds_base) {
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off nt" ::"v"(gptr), "s"(lds_base)
+                 : "memory", "m0");
 }
 
-__device__ __forceinline__ void mf_stage(const uint8_t* __restrict__ gA, const uint8_t* __restrict__ gB, uint8_t* lds,
-                                         int tid) {
+// issue one K-step stage: waves 0-3 (the loader waves) issue 8 LDS-DMA instructions per thread
+// (4 corpus + 4 query); waves 4-7 issue none.  Loader waves never store to global memory and the
+// writer waves never load, so each wave's in-order vmcnt holds one kind of traffic: counted waits
+// on the stage ring are never held up behind candidate stores.
+template <bool QLOAD = true, bool NT = false>
+__device__ __forceinline__ void mf_stage(const uint8_t* __restrict__ gA, const uint8_t* __restrict__ gB,
+                                         uint32_t slot_base, int tid) {
     const int w = tid >> 6, lane = tid & 63;
-    const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(lds) + (uint32_t)(w * 64 * 16));
+    if (w >= 4) return;
+    const uint32_t base = __builtin_amdgcn_readfirstlane(slot_base + (uint32_t)(w * 64 * 16));
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
-        const int g = it * 512 + w * 64 + lane;  // LDS piece written by this lane
-        const int row = g >> 3, pos = g & 7;
-        const int src = (row << 3) + (pos ^ ((row >> 1) & 7));
-        glds16(gA + (size_t)src * 16, base + it * 512 * 16);
-        glds16(gB + (size_t)src * 16, base + it * 512 * 16 + 32768);
+        const int g = it * 256 + w * 64 + lane;
+        const int row = g >> 2, pos = g & 3;
+        const int src = (row << 2) + (pos ^ mf_swz(row));
+        if constexpr (NT) glds16_nt(gA + (size_t)src * 16, base + it * 256 * 16);
+        else glds16(gA + (size_t)src * 16, base + it * 256 * 16);
     }
+    if constexpr (QLOAD) {
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+            const int g = it * 256 + w * 64 + lane;
+            const int row = g >> 2, pos = g & 3;
+            const int src = (row << 2) + (pos ^ mf_swz(row));
+            glds16(gB + (size_t)src * 16, base + it * 256 * 16 + 16384);
+        }
+    }
+}
+
+// piece g (0..3) of a stage for loader waves: 1 corpus + 1 query LDS-DMA instruction
+template <bool NT = false>
+__device__ __forceinline__ void mf_stage_piece(const uint8_t* __restrict__ gA, const uint8_t* __restrict__ gB,
+                                               uint32_t base, int g4, int w, int lane) {
+    const int g = g4 * 256 + w * 64 + lane;
+    const int row = g >> 2, pos = g & 3;
+    const int src = (row << 2) + (pos ^ mf_swz(row));
+    if constexpr (NT) glds16_nt(gA + (size_t)src * 16, base + g4 * 256 * 16);
+    else glds16(gA + (size_t)src * 16, base + g4 * 256 * 16);
+    glds16(gB + (size_t)src * 16, base + g4 * 256 * 16 + 16384);
+}
+
+// wait until at most `ahead` younger stages (4 LDS-DMA each) are in flight, then barrier
+template <bool BAR, bool HALF = false>
+__device__ __forceinline__ void mf_wait_barrier(int ahead, bool loader) {
+    if constexpr (BAR) {
+        if (!loader) {
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        } else if constexpr (HALF) {
+            if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        } else {
+            if (ahead >= 2) asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            else if (ahead == 1) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+    }
+}
+__device__ __forceinline__ void mf_barrier_lgkm() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+__device__ __forceinline__ void mf_barrier_drain() {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 template <int DT>
@@ -494,33 +556,78 @@ __device__ __forceinline__ floatx4 mfma16(const uint4 a, const uint4 b, floatx4 
                                                       0, 0);
 }
 
-template <int DT>
-__device__ __forceinline__ void mf_compute(const uint8_t* buf, floatx4 (&acc)[4][8], int wm, int wn, int lane) {
+// one K-step: 4 A (corpus) + 8 B (query) fragments by ds_read_b128 at ONE per-lane offset plus
+// immediates ((row >> 2) & 3 of every fragment row equals that of lane & 15), then 32 MFMAs.
+// One K-step with the next stage's LDS-DMA issue interleaved between its MFMA groups: the loader
+// waves' DMA issue then overlaps MFMA execution instead of delaying it.  sched_barrier pins the
+// order (hipcc would otherwise hoist the register-only MFMAs across the asm).
+template <int DT, bool NT>
+__device__ __forceinline__ void mf_compute_il(const uint8_t* buf, floatx4 (&acc)[4][8], int wm, int wn, int lane_off,
+                                              bool issue, const uint8_t* gA, const uint8_t* gB, uint32_t slot_base,
+                                              int w, int lane) {
+    uint4 af[4], bfr[8];
+    const uint8_t* pa = buf + wm * 4096 + lane_off;
+    const uint8_t* pb = buf + 16384 + wn * 8192 + lane_off;
 #pragma unroll
-    for (int kh = 0; kh < 2; ++kh) {
-        const int c = kh * 4 + (lane >> 4);
-        uint4 af[4], bfr[8];
+    for (int ni = 0; ni < 8; ++ni) bfr[ni] = *(const uint4*)(pb + ni * 1024);
 #pragma unroll
-        for (int mi = 0; mi < 4; ++mi) {
-            const int row = wm * 64 + mi * 16 + (lane & 15);
-            af[mi] = *(const uint4*)(buf + row * 128 + ((c ^ ((row >> 1) & 7)) << 4));
-        }
+    for (int mi = 0; mi < 4; ++mi) af[mi] = *(const uint4*)(pa + mi * 1024);
+    const uint32_t base = __builtin_amdgcn_readfirstlane(slot_base + (uint32_t)(w * 64 * 16));
 #pragma unroll
-        for (int ni = 0; ni < 8; ++ni) {
-            const int row = wn * 128 + ni * 16 + (lane & 15);
-            bfr[ni] = *(const uint4*)(buf + 32768 + row * 128 + ((c ^ ((row >> 1) & 7)) << 4));
-        }
+    for (int mi = 0; mi < 4; ++mi) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (issue) mf_stage_piece<NT>(gA, gB, base, mi, w, lane);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-            for (int ni = 0; ni < 8; ++ni) acc[mi][ni] = mfma16<DT>(af[mi], bfr[ni], acc[mi][ni]);
+        for (int ni = 0; ni < 8; ++ni) acc[mi][ni] = mfma16<DT>(af[mi], bfr[ni], acc[mi][ni]);
     }
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int DT, bool READS>
+__device__ __forceinline__ void mf_compute(const uint8_t* buf, floatx4 (&acc)[4][8], int wm, int wn, int lane_off) {
+    uint4 af[4], bfr[8];
+    if constexpr (READS) {
+        const uint8_t* pa = buf + wm * 4096 + lane_off;
+        const uint8_t* pb = buf + 16384 + wn * 8192 + lane_off;
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) af[mi] = *(const uint4*)(pa + mi * 1024);
+#pragma unroll
+        for (int ni = 0; ni < 8; ++ni) bfr[ni] = *(const uint4*)(pb + ni * 1024);
+    } else {
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) af[mi] = make_uint4(lane_off + mi, 1u, 2u, 3u);
+#pragma unroll
+        for (int ni = 0; ni < 8; ++ni) bfr[ni] = make_uint4(lane_off + ni, 5u, 6u, 7u);
+    }
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 8; ++ni) acc[mi][ni] = mfma16<DT>(af[mi], bfr[ni], acc[mi][ni]);
+}
+
+// fragment reads and MFMA groups as separate pieces (for the ping-pong schedule)
+__device__ __forceinline__ void mf_read(const uint8_t* buf, uint4 (&af)[4], uint4 (&bfr)[8], int wm, int wn,
+                                        int lane_off) {
+    const uint8_t* pa = buf + wm * 4096 + lane_off;
+    const uint8_t* pb = buf + 16384 + wn * 8192 + lane_off;
+#pragma unroll
+    for (int ni = 0; ni < 8; ++ni) bfr[ni] = *(const uint4*)(pb + ni * 1024);
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) af[mi] = *(const uint4*)(pa + mi * 1024);
+}
+template <int DT, int M0, int M1>
+__device__ __forceinline__ void mf_mfma(const uint4 (&af)[4], const uint4 (&bfr)[8], floatx4 (&acc)[4][8]) {
+#pragma unroll
+    for (int mi = M0; mi < M1; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 8; ++ni) acc[mi][ni] = mfma16<DT>(af[mi], bfr[ni], acc[mi][ni]);
 }
 
 // compact one (workgroup, query) candidate buffer to its best K keys (one wave)
 template <int E>
 __device__ __forceinline__ void mf_wave_compact(u64* __restrict__ buf, int n, int K, u64* thr_key, float* thr_f,
-                                             int lane) {
+                                                int lane) {
     u64 keys[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
@@ -543,29 +650,63 @@ __device__ __forceinline__ void mf_wave_compact(u64* __restrict__ buf, int n, in
     }
 }
 
-template <int DT>
+// MODE (profiling ablations, VS_MF_ABLATE; results of modes != 0 are meaningless):
+//   0 production | 1 no LDS-DMA stream | 2 no LDS reads + MFMAs | 3 = 1 + no top-k epilogue
+//   4 = 3 + no per-K-step barrier | 5 = 4 + no LDS reads (MFMAs on register operands)
+//   6 loads only (no math, no epilogue) | 7 = 6 without the query stream | 8 = 6 with nt corpus loads
+//   9 loads + math, no epilogue (burst DMA issue) | 10 = 9 with the DMA issue interleaved (as 0)
+//   11 = 9 with the ping-pong schedule (waves 4-7 half a K-step behind)
+template <int DT, int METRIC, int MODE>
 __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
+    constexpr bool LOADS = (MODE != 1 && MODE < 3) || MODE >= 6;  // 0, 2, 6..11
+    constexpr bool MATH = (MODE != 2 && MODE < 6) || MODE == 9 || MODE == 10;
+    constexpr bool PP = MODE == 11;  // ping-pong: waves 4-7 half a K-step behind waves 0-3
+    constexpr bool EPI = MODE < 3;
+    constexpr bool BAR = MODE < 4 || MODE >= 6;
+    constexpr bool READS = MODE < 5 || MODE == 9 || MODE == 10;
+    constexpr bool QLOAD = MODE != 7;
+    constexpr bool NT = MODE == 8 || MODE == 0 || MODE >= 9;
+    constexpr bool IL = MODE == 10;  // DMA issue interleaved with the MFMAs (ablation: slower)
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    u64* thr_key = (u64*)(smem + 2 * MF_STAGE);
-    float* thr_f = (float*)(smem + 2 * MF_STAGE + 256 * 8);
-    int* cnt = (int*)(smem + 2 * MF_STAGE + 256 * 12);
+    u64* thr_key = (u64*)(smem + MF_SLOTS * MF_SLOT);
+    float* thr_f = (float*)(smem + MF_SLOTS * MF_SLOT + 256 * 8);
+    int* cnt = (int*)(smem + MF_SLOTS * MF_SLOT + 256 * 12);
+    int* flag = (int*)(smem + MF_SLOTS * MF_SLOT + 256 * 16);  // [0] spare, [1] pool count
+    u64* pool_key = (u64*)(smem + MF_SLOTS * MF_SLOT + 256 * 16 + 16);
+    int* pool_q = (int*)(smem + MF_SLOTS * MF_SLOT + 256 * 16 + 16 + MF_POOL * 8);
 
+    // The LDS ring is written only by the inline-asm DMA: let the array escape into an asm with a
+    // memory clobber, so the compiler must assume every later memory-clobbering asm (DMA issue,
+    // barriers) may write it and can never fold the fragment reads away.
+    asm volatile("; lds ring escapes: %0" ::"v"(smem) : "memory");
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid & 3, wn = wid >> 2;
     const int blk = blockIdx.x;
-    const int t0 = (int)((int64_t)a.tiles * blk / a.G);
-    const int t1 = (int)((int64_t)a.tiles * (blk + 1) / a.G);
+    int t0 = (int)((int64_t)a.tiles * blk / a.G);
+    int t1 = (int)((int64_t)a.tiles * (blk + 1) / a.G);
+    if (a.tile_stride > 0) {
+        t0 = blk * a.tile_stride;
+        t1 = t0 + 1 <= a.tiles ? t0 + 1 : a.tiles;
+    }
     if (tid < 256) {
         const bool real = tid < nqb;
-        thr_key[tid] = real ? 0ull : ~0ull;
-        thr_f[tid] = real ? -INFINITY : INFINITY;
+        const u64 k0 = real ? (a.thr0 ? a.thr0[tid] : 0ull) : ~0ull;
+        thr_key[tid] = k0;
+        thr_f[tid] = !real ? INFINITY : (k0 == 0ull ? -INFINITY : key_score(k0));
         cnt[tid] = 0;
     }
-    const int nks = a.dpad / 64;
+    if (tid == 0) {
+        flag[0] = 0;
+        flag[1] = 0;
+    }
+    const int nks = a.dpad / CH;
     const int64_t tbytes = (int64_t)TR * a.dpad * 2;
     const int S = (t1 - t0) * nks;
     u64* cand = a.cand + (size_t)blk * MFMA_QB * a.cap;
     const int trigger = a.cap - TR;
+    const uint32_t ring = lds_addr(smem);
+    const int r16 = lane & 15;
+    const int lane_off = r16 * 64 + (((lane >> 4) ^ mf_swz(r16)) << 4);
 
     floatx4 acc[4][8];
 #pragma unroll
@@ -573,74 +714,229 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
 #pragma unroll
         for (int ni = 0; ni < 8; ++ni) acc[mi][ni] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-    if (S > 0) mf_stage(a.corpus + (int64_t)t0 * tbytes, qt, smem, tid);
+    // prologue: stages 0 .. DEPTH-1
+    int iti = t0, iks = 0;  // (tile, k-step) of the next stage to issue
+    for (int j = 0; j < MF_DEPTH && j < S; ++j) {
+        if constexpr (LOADS)
+            mf_stage<QLOAD, NT>(a.corpus + (int64_t)iti * tbytes + (int64_t)iks * 16384, qt + (int64_t)iks * 16384,
+                                ring + (uint32_t)(j * MF_SLOT), tid);
+        if (++iks == nks) { iks = 0; ++iti; }
+    }
+    if constexpr (!BAR) mf_barrier_drain();
     int ti = t0, ks = 0;
+    float sink = 0.0f;
+    bool check_pending = false;
+    uint4 pf_a[4], pf_b[8];
     for (int s = 0; s < S; ++s) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        {
-            int ks1 = ks + 1, ti1 = ti;
-            if (ks1 == nks) { ks1 = 0; ++ti1; }
-            if (s + 1 < S)
-                mf_stage(a.corpus + (int64_t)ti1 * tbytes + (int64_t)ks1 * 32768, qt + (int64_t)ks1 * 32768,
-                         smem + ((s + 1) & 1) * MF_STAGE, tid);
+        const int left = S - 1 - s;
+        mf_wait_barrier<BAR, !QLOAD>(left < MF_DEPTH - 1 ? left : MF_DEPTH - 1, wid < 4);
+        const bool do_issue = s + MF_DEPTH < S;
+        const uint8_t* nA = a.corpus + (int64_t)iti * tbytes + (int64_t)iks * 16384;
+        const uint8_t* nB = qt + (int64_t)iks * 16384;
+        const uint32_t nslot = ring + (uint32_t)(((s + MF_DEPTH) % MF_SLOTS) * MF_SLOT);
+        if (do_issue) {
+            if (++iks == nks) { iks = 0; ++iti; }
         }
-        mf_compute<DT>(smem + (s & 1) * MF_STAGE, acc, wm, wn, lane);
+        if constexpr (PP) {
+            if (wid < 4) {
+                if (do_issue) mf_stage<true, NT>(nA, nB, nslot, tid);
+                mf_read(smem + (s % MF_SLOTS) * MF_SLOT, pf_a, pf_b, wm, wn, lane_off);
+                mf_mfma<DT, 0, 4>(pf_a, pf_b, acc);
+            } else {
+                if (s > 0) mf_mfma<DT, 2, 4>(pf_a, pf_b, acc);
+                __builtin_amdgcn_sched_barrier(0);
+                mf_read(smem + (s % MF_SLOTS) * MF_SLOT, pf_a, pf_b, wm, wn, lane_off);
+                mf_mfma<DT, 0, 2>(pf_a, pf_b, acc);
+            }
+        } else if constexpr (IL) {
+            mf_compute_il<DT, NT>(smem + (s % MF_SLOTS) * MF_SLOT, acc, wm, wn, lane_off, do_issue && wid < 4, nA, nB,
+                                  nslot, wid, lane);
+        } else {
+            if (do_issue) {
+                if constexpr (LOADS) mf_stage<QLOAD, NT>(nA, nB, nslot, tid);
+            }
+            if constexpr (MATH) mf_compute<DT, READS>(smem + (s % MF_SLOTS) * MF_SLOT, acc, wm, wn, lane_off);
+        }
         if (ks == nks - 1) {
+            if constexpr (!EPI) {
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                    for (int ni = 0; ni < 8; ++ni) {
+                        sink += acc[mi][ni][0] + acc[mi][ni][3];
+                        acc[mi][ni] = floatx4{0.f, 0.f, 0.f, 0.f};
+                    }
+            } else {
             // ---- fused top-k epilogue: threshold filter, rare inserts ----
+            // Lane-derived indices come from an asm-opaque copy of the lane id, so the compiler
+            // cannot hoist them out of the K loop (they would pin VGPRs the MFMA loop needs).
+            int olane;
+            asm volatile("v_mov_b32 %0, %1" : "=v"(olane) : "v"(lane));
             const int64_t rowbase = (int64_t)ti * TR;
             const bool full = rowbase + TR <= a.n_valid;
+            const int rid0 = wm * 64 + (olane >> 4) * 4;       // + mi*16 + r
+            const int q0 = wn * 128 + (olane & 15);             // + ni*16
             float sq[4][4];
-            if (a.metric == METRIC_L2) {
+            if constexpr (METRIC == METRIC_L2) {
 #pragma unroll
                 for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        const int64_t gr = rowbase + wm * 64 + mi * 16 + (lane >> 4) * 4 + r;
+                        const int64_t gr = rowbase + rid0 + mi * 16 + r;
                         sq[mi][r] = gr < a.n_valid ? a.sqn[gr] : 0.0f;
                     }
             }
+            if (!full) {  // last tile of the shard: padding rows never qualify
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (rowbase + rid0 + mi * 16 + r >= a.n_valid)
+#pragma unroll
+                            for (int ni = 0; ni < 8; ++ni) acc[mi][ni][r] = -INFINITY;
+            }
 #pragma unroll
             for (int ni = 0; ni < 8; ++ni) {
-                const int q = wn * 128 + ni * 16 + (lane & 15);
-                const float tf = thr_f[q];
+                const int q = q0 + ni * 16;
+                float v[4][4];
+                float mx = -INFINITY;
 #pragma unroll
                 for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        const int rit = wm * 64 + mi * 16 + (lane >> 4) * 4 + r;
                         float sc = acc[mi][ni][r];
-                        if (a.metric == METRIC_L2) sc = 2.0f * sc - sq[mi][r];
-                        const bool valid = full || (rowbase + rit < a.n_valid);
-                        if (valid && sc >= tf) {
-                            const u64 key = mk_key(sc, (uint32_t)(rowbase + rit));
-                            if (key > thr_key[q]) {
-                                const int slot = atomicAdd(&cnt[q], 1);
-                                if (slot < a.cap) cand[(size_t)q * a.cap + slot] = key;
+                        if constexpr (METRIC == METRIC_L2) sc = 2.0f * sc - sq[mi][r];
+                        v[mi][r] = sc;
+                        mx = fmaxf(mx, sc);
+                    }
+                // one compare per query column; the insert path runs only where something passes,
+                // and then costs one LDS atomic per lane plus predicated stores
+                const float tf = thr_f[q];
+                if (mx >= tf) {
+                    const u64 tk = thr_key[q];
+                    uint32_t m = 0;
+#pragma unroll
+                    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const float x = v[mi][r];
+                            const bool p = x > tf ||
+                                           (x == tf && mk_key(x, (uint32_t)(rowbase + rid0 + mi * 16 + r)) > tk);
+                            m |= (p ? 1u : 0u) << (mi * 4 + r);
+                        }
+                    const int c = __popc(m);
+                    if (a.dbg) {
+                        atomicAdd(&a.dbg[0], (unsigned)c);
+                        if (lane == __builtin_amdgcn_readfirstlane(lane)) atomicAdd(&a.dbg[1], 1u);
+                    }
+                    // loader waves park their inserts in the LDS pool (no global store in their
+                    // vmcnt); writer waves, or a loader wave whose pool share overflows, store
+                    int pbase = MF_POOL;
+                    if (wid < 4 && c) pbase = atomicAdd(&flag[1], c);
+                    const bool to_pool = wid < 4 && pbase + c <= MF_POOL;
+                    int base = 0;
+                    if (c && !to_pool) base = atomicAdd(&cnt[q], c);
+#pragma unroll
+                    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int bit = mi * 4 + r;
+                            if ((m >> bit) & 1u) {
+                                const int off = __popc(m & ((1u << bit) - 1u));
+                                const u64 key = mk_key(v[mi][r], (uint32_t)(rowbase + rid0 + mi * 16 + r));
+                                if (to_pool) {
+                                    pool_key[pbase + off] = key;
+                                    pool_q[pbase + off] = q;
+                                } else {
+                                    // a reservation that straddles the pool end: void its in-pool part
+                                    if (wid < 4 && pbase + off < MF_POOL) pool_q[pbase + off] = -1;
+                                    if (a.dbg && wid < 4) atomicAdd(&a.dbg[3], 1u);
+                                    if (base + off < a.cap) cand[(size_t)q * a.cap + base + off] = key;
+                                }
                             }
                         }
-                    }
+                }
             }
 #pragma unroll
             for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
                 for (int ni = 0; ni < 8; ++ni) acc[mi][ni] = floatx4{0.f, 0.f, 0.f, 0.f};
-            __syncthreads();
-            for (int q = wid; q < nqb; q += 8) {
-                const int n = cnt[q];
-                if (n > trigger) {
-                    mf_wave_compact<MFMA_CAP / 64>(cand + (size_t)q * a.cap, n, a.Kp, &thr_key[q], &thr_f[q], lane);
-                    if (lane == 0) cnt[q] = a.Kp;
+            check_pending = true;
+            }
+        }
+        // Deferred compaction check, after the NEXT K-step's barrier: by then every wave's
+        // insert atomics of the finished tile are complete, and every wave reads all 256 LDS
+        // counters, so the (rare) decision to compact is uniform without extra barriers.
+        // (no check after the shard's last tile: the flush below compacts; capacity holds by the
+        // invariant cnt <= cap - TR after every check, and one tile adds at most TR per query)
+        if (check_pending && ks != nks - 1) {
+            check_pending = false;
+            // writer waves flush the loader waves' LDS pool into the global candidate buffers
+            {
+                int np = flag[1];
+                np = np < MF_POOL ? np : MF_POOL;
+                if (wid >= 4) {
+                    for (int j = (wid - 4) * 64 + lane; j < np; j += 256) {
+                        const int q = pool_q[j];
+                        if (q < 0) continue;
+                        const int slot = atomicAdd(&cnt[q], 1);
+                        if (slot < a.cap) cand[(size_t)q * a.cap + slot] = pool_key[j];
+                    }
                 }
+                mf_barrier_lgkm();
+                if (tid == 0) flag[1] = 0;
+            }
+            int need = 0;
+#pragma unroll
+            for (int i = 0; i < 256 / 64; ++i) {
+                const int q = lane + 64 * i;
+                need |= (q < nqb && cnt[q] > trigger) ? 1 : 0;
+            }
+            if (__any(need)) {
+                mf_barrier_drain();  // all candidate stores of all waves complete
+                for (int q = wid; q < nqb; q += 8) {
+                    const int n = cnt[q];
+                    if (n > trigger) {
+                        mf_wave_compact<MFMA_CAP / 64>(cand + (size_t)q * a.cap, n < a.cap ? n : a.cap, a.Kp,
+                                                       &thr_key[q], &thr_f[q], lane);
+                        if (lane == 0) cnt[q] = a.Kp;
+                        if (a.dbg && lane == 0) atomicAdd(&a.dbg[2], 1u);
+                    }
+                }
+                mf_barrier_drain();  // counters / thresholds / compacted buffers published
             }
         }
         if (++ks == nks) { ks = 0; ++ti; }
     }
-    // ---- flush: best Kp per query -> part[blk][q][Kp] ----
-    __syncthreads();
+    if constexpr (PP) {
+        if (wid >= 4 && S > 0) mf_mfma<DT, 2, 4>(pf_a, pf_b, acc);
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 8; ++ni) sink += acc[mi][ni][0] + acc[mi][ni][3];
+    }
+    if constexpr (!EPI) {
+        if (sink == 12345.678f) cnt[0] = 1;  // keep the ablated MFMAs alive
+    }
+    // ---- flush: pool -> buffers, then best Kp per query -> part[blk][q][Kp] ----
+    mf_barrier_drain();
+    {
+        int np = flag[1];
+        np = np < MF_POOL ? np : MF_POOL;
+        if (wid >= 4) {
+            for (int j = (wid - 4) * 64 + lane; j < np; j += 256) {
+                const int q = pool_q[j];
+                if (q < 0) continue;
+                const int slot = atomicAdd(&cnt[q], 1);
+                if (slot < a.cap) cand[(size_t)q * a.cap + slot] = pool_key[j];
+            }
+        }
+    }
+    mf_barrier_drain();
     for (int q = wid; q < MFMA_QB; q += 8) {
         u64* pq = a.part + ((size_t)blk * MFMA_QB + q) * a.Kp;
         int n = q < nqb ? cnt[q] : 0;
+        if (n > a.cap) n = a.cap;
         if (n > a.Kp) {
             mf_wave_compact<MFMA_CAP / 64>(cand + (size_t)q * a.cap, n, a.Kp, &thr_key[q], &thr_f[q], lane);
             n = a.Kp;
@@ -652,17 +948,18 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
 // ------------------------------------------------------------------------------------------------
 // K2: GEMV screen (any dtype, up to 8 queries per launch) -- HBM streaming, fp32 FMA
 // ------------------------------------------------------------------------------------------------
-// 256 threads, persistent over a contiguous tile range.  A row's 64-element chunk is LPR 16 B
+// 256 threads, persistent over a contiguous tile range.  A row's 32-element chunk is LPR 16 B
 // units, read by LPR consecutive lanes, so every wave-instruction is a contiguous 1 KiB piece.
 template <int DT, int NQ>
 __global__ void __launch_bounds__(256) k_screen_gemv(ScreenArgs a, const float* __restrict__ qp, int nqb) {
     constexpr int ES = DT == DT_F32 ? 4 : 2;
-    constexpr int CB = 64 * ES;
+    constexpr int CB = CH * ES;
     constexpr int LPR = CB / 16;
     constexpr int RPI = 64 / LPR;
     constexpr int EPU = 16 / ES;
     constexpr int RG = 64 / RPI;
-    constexpr int RB = (NQ <= 2) ? 8 : 4;  // rows per pass (register budget)
+    constexpr int RB0 = (NQ <= 2) ? 8 : 4;  // rows per pass (register budget)
+    constexpr int RB = RB0 < RG ? RB0 : RG;
     static_assert(RG % RB == 0, "row groups");
 
     __shared__ u64 thr_key[NQ];
@@ -682,7 +979,7 @@ __global__ void __launch_bounds__(256) k_screen_gemv(ScreenArgs a, const float* 
         cnt[tid] = 0;
     }
     __syncthreads();
-    const int nch = a.dpad / 64;
+    const int nch = a.dpad / CH;
     const int64_t tbytes = (int64_t)TR * a.dpad * ES;
     u64* cand = a.cand + (size_t)blk * NQ * a.cap;
     const int trigger = a.cap - TR;
@@ -701,7 +998,7 @@ __global__ void __launch_bounds__(256) k_screen_gemv(ScreenArgs a, const float* 
                 float qv[NQ][EPU];
 #pragma unroll
                 for (int qi = 0; qi < NQ; ++qi) {
-                    const float4* qs = (const float4*)(qp + (int64_t)qi * a.dpad + c * 64 + unit * EPU);
+                    const float4* qs = (const float4*)(qp + (int64_t)qi * a.dpad + c * CH + unit * EPU);
 #pragma unroll
                     for (int h = 0; h < EPU / 4; ++h) {
                         float4 t = qs[h];
@@ -832,11 +1129,11 @@ __device__ __forceinline__ double exact_score(const uint8_t* __restrict__ corpus
                                               const float* __restrict__ q, int d, int dpad, int metric, int lane) {
 #pragma clang fp contract(off)
     constexpr int ES = DT == DT_F32 ? 4 : 2;
-    const uint8_t* rb = corpus + (row / TR) * (int64_t)TR * dpad * ES + (row % TR) * (64 * ES);
+    const uint8_t* rb = corpus + (row / TR) * (int64_t)TR * dpad * ES + (row % TR) * (CH * ES);
     double acc = 0.0;
     for (int g = lane; 8 * g < d; g += 64) {
         const int e0 = 8 * g;
-        const uint8_t* p = rb + (int64_t)(e0 >> 6) * TR * 64 * ES + (e0 & 63) * ES;
+        const uint8_t* p = rb + (int64_t)(e0 >> 5) * TR * CH * ES + (e0 & 31) * ES;
         float xv[8];
         if constexpr (DT == DT_F32) {
             unpack16<DT>(*(const uint4*)p, xv);
@@ -954,7 +1251,8 @@ __global__ void __launch_bounds__(256) k_refine(RefineArgs a, int KP2) {
     // exactness certificate: every non-candidate row has exact transformed score <= smin + eps
     if (tid == 0) {
         int cert = 1;
-        if (nv >= a.Kp && a.k <= nv) {
+        if (a.optimistic && nv < a.Kp) cert = 0;  // an optimistic seed may have cut real candidates
+        else if (nv >= a.Kp && a.k <= nv) {
             const double smin = (double)key_score(minkey_s);
             const double qh = (double)a.qinfo[2 * q], dq = (double)a.qinfo[2 * q + 1];
             const double xm = (double)a.xmax;
@@ -982,6 +1280,35 @@ __global__ void __launch_bounds__(256) k_refine(RefineArgs a, int KP2) {
             if (a.S64) a.S64[o] = a.metric == METRIC_IP ? -1.7976931348623157e308 : 1.7976931348623157e308;
         }
     }
+}
+
+// per-query seed threshold from the top-Kp list of a row sample (one wave per query):
+//   rank == 0: min key - 1 of a full list (a proven lower bound of the final Kp-th key)
+//   rank  > 0: (rank-th best key) - 1, optimistic (see launch_seed_thr)
+__global__ void __launch_bounds__(256) k_seed_thr(const u64* __restrict__ list, int Kp, int nq, u64* __restrict__ thr0,
+                                                   int rank) {
+    const int lane = threadIdx.x & 63;
+    const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= nq) return;
+    u64 keys[KP_MAX / 64];
+    int c = 0;
+    u64 mn = ~0ull;
+#pragma unroll
+    for (int e = 0; e < KP_MAX / 64; ++e) {
+        const int j = lane + 64 * e;
+        const u64 k = j < Kp ? list[(size_t)q * Kp + j] : 0ull;
+        keys[e] = k;
+        if (k != 0ull) {
+            ++c;
+            mn = k < mn ? k : mn;
+        }
+    }
+    c = wave_sum_i(c);
+    mn = wave_min_u64(mn);
+    u64 t;
+    if (rank > 0 && c >= rank) t = wave_kth<KP_MAX / 64>(keys, rank) - 1ull;
+    else t = (c == Kp) ? mn - 1ull : 0ull;
+    if (lane == 0) thr0[q] = t;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1105,20 +1432,44 @@ hipError_t launch_pack_qf32(const float* q, int nqb, int nqpad, int d, int dpad,
     return hipGetLastError();
 }
 
+template <int DT, int METRIC, int MODE>
+static void launch_mfma_one(const ScreenArgs& a, const uint8_t* qt, int nqb, hipStream_t st) {
+    static bool attr_set = false;  // benign race: idempotent attribute
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)k_screen_mfma<DT, METRIC, MODE>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, MF_LDS);
+        attr_set = true;
+    }
+    hipLaunchKernelGGL((k_screen_mfma<DT, METRIC, MODE>), dim3(a.G), dim3(MF_THREADS), MF_LDS, st, a, qt, nqb);
+}
+template <int DT, int METRIC>
+static void launch_mfma_mode(const ScreenArgs& a, const uint8_t* qt, int nqb, hipStream_t st) {
+    static const int mode = [] {
+        const char* e = getenv("VS_MF_ABLATE");
+        return e ? atoi(e) : 0;
+    }();
+    switch (mode) {
+        case 1: launch_mfma_one<DT, METRIC, 1>(a, qt, nqb, st); break;
+        case 2: launch_mfma_one<DT, METRIC, 2>(a, qt, nqb, st); break;
+        case 3: launch_mfma_one<DT, METRIC, 3>(a, qt, nqb, st); break;
+        case 4: launch_mfma_one<DT, METRIC, 4>(a, qt, nqb, st); break;
+        case 5: launch_mfma_one<DT, METRIC, 5>(a, qt, nqb, st); break;
+        case 6: launch_mfma_one<DT, METRIC, 6>(a, qt, nqb, st); break;
+        case 7: launch_mfma_one<DT, METRIC, 7>(a, qt, nqb, st); break;
+        case 8: launch_mfma_one<DT, METRIC, 8>(a, qt, nqb, st); break;
+        case 9: launch_mfma_one<DT, METRIC, 9>(a, qt, nqb, st); break;
+        case 10: launch_mfma_one<DT, METRIC, 10>(a, qt, nqb, st); break;
+        case 11: launch_mfma_one<DT, METRIC, 11>(a, qt, nqb, st); break;
+        default: launch_mfma_one<DT, METRIC, 0>(a, qt, nqb, st); break;
+    }
+}
 hipError_t launch_screen_mfma(int dt, const ScreenArgs& a, const uint8_t* qt, int nqb, hipStream_t st) {
-    static bool attr_set[3] = {false, false, false};
     if (dt == DT_BF16) {
-        if (!attr_set[1]) {
-            hipFuncSetAttribute((const void*)k_screen_mfma<DT_BF16>, hipFuncAttributeMaxDynamicSharedMemorySize, MF_LDS);
-            attr_set[1] = true;
-        }
-        hipLaunchKernelGGL(k_screen_mfma<DT_BF16>, dim3(a.G), dim3(512), MF_LDS, st, a, qt, nqb);
+        if (a.metric == METRIC_IP) launch_mfma_mode<DT_BF16, METRIC_IP>(a, qt, nqb, st);
+        else launch_mfma_mode<DT_BF16, METRIC_L2>(a, qt, nqb, st);
     } else {
-        if (!attr_set[2]) {
-            hipFuncSetAttribute((const void*)k_screen_mfma<DT_F16>, hipFuncAttributeMaxDynamicSharedMemorySize, MF_LDS);
-            attr_set[2] = true;
-        }
-        hipLaunchKernelGGL(k_screen_mfma<DT_F16>, dim3(a.G), dim3(512), MF_LDS, st, a, qt, nqb);
+        if (a.metric == METRIC_IP) launch_mfma_mode<DT_F16, METRIC_IP>(a, qt, nqb, st);
+        else launch_mfma_mode<DT_F16, METRIC_L2>(a, qt, nqb, st);
     }
     return hipGetLastError();
 }
@@ -1158,6 +1509,11 @@ hipError_t launch_refine(const RefineArgs& a, int nq, hipStream_t st) {
         attr = true;
     }
     hipLaunchKernelGGL(k_refine<0>, dim3(nq), dim3(256), lds, st, a, KP2);
+    return hipGetLastError();
+}
+
+hipError_t launch_seed_thr(const u64* list, int Kp, int nq, u64* thr0, int rank, hipStream_t st) {
+    hipLaunchKernelGGL(k_seed_thr, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, st, list, Kp, nq, thr0, rank);
     return hipGetLastError();
 }
 

@@ -121,5 +121,6 @@ def write_flat(path: str, vectors: np.ndarray, metric_type: int) -> None:
     tmp = f"{path}.tmp-{os.getpid()}"
     with open(tmp, "wb") as f:
         f.write(flat_bytes_header(v.shape[1], v.shape[0], metric_type))
-        f.write(memoryview(v).cast("B"))
+        if v.size:
+            f.write(memoryview(v).cast("B"))
     os.replace(tmp, path)

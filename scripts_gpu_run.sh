@@ -12,6 +12,16 @@ for s in "$@"; do
     bench) timeout -k 10 600 python bench.py > gpurun_out/bench.log 2>&1 ;;
     bench_cfg2) timeout -k 10 600 python bench.py --workload cfg2 --steps 50 --no-cpu-baseline > gpurun_out/bench_cfg2.log 2>&1 ;;
     prof) timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/prof.log 2>&1 ;;
+    ablate) for m in ${MODES:-0 1 2 0}; do VS_MF_ABLATE=$m timeout -k 10 300 python bench.py --no-cpu-baseline --steps 10 > gpurun_out/ablate_$m.log 2>&1 || exit 1; tail -1 gpurun_out/ablate_$m.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('mode $m', d['roofline']['kernel_ms'])" >> gpurun_out/ablate.txt; done ;;
+    stats) VS_MF_STATS=1 timeout -k 10 300 python bench.py --no-cpu-baseline --steps 2 --warmup 1 > gpurun_out/stats.log 2>&1 ;;
+    pmcab) for m in ${MODES:-0 9}; do
+        VS_MF_ABLATE=$m timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS GRBM_GUI_ACTIVE -d gpurun_out/pmcab$m -o p --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/pmcab$m.log 2>&1 || exit 1
+        VS_MF_ABLATE=$m timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_SMEM SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_BRANCH SQ_WAIT_INST_LDS SQ_INSTS_MFMA SQ_BUSY_CYCLES SQ_INST_CYCLES_SALU -d gpurun_out/pmcbb$m -o p --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/pmcbb$m.log 2>&1 || exit 1
+      done ;;
+    pmcclk) for m in ${MODES:-0 9}; do
+        VS_MF_ABLATE=$m timeout -k 10 300 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES -d gpurun_out/pmcclk$m -o p --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/pmcclk$m.log 2>&1 || exit 1
+        VS_MF_ABLATE=$m timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_WAIT_ANY SQ_WAIT_INST_ANY -d gpurun_out/pmclds$m -o p --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/pmclds$m.log 2>&1 || exit 1
+      done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
   rc=$?

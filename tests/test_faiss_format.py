@@ -1,0 +1,65 @@
+"""faiss flat/HNSW file format against the reference's own fixture files."""
+import os
+import struct
+
+import numpy as np
+import pytest
+
+from photo_search_engine_amd import faiss_format as F
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def test_build_smoke_idx_roundtrip_byte_identical(tmp_path):
+    src = os.path.join(GOLDEN, "ref_build_smoke.idx")
+    ff = F.read_index(src)
+    assert (ff.kind, ff.fourcc, ff.d, ff.ntotal, ff.metric_type) == ("flat", b"IxFI", 8, 1, 0)
+    out = tmp_path / "idx"
+    F.write_flat(str(out), ff.vectors, 0)
+    assert out.read_bytes() == open(src, "rb").read()
+
+
+def test_reference_hnsw_index_storage():
+    ff = F.read_index(os.path.join(GOLDEN, "ref_photo_search.index"))
+    assert (ff.kind, ff.d, ff.ntotal, ff.metric_type) == ("hnsw", 4096, 77, 0)
+    assert ff.hnsw_params["efConstruction"] == 320 and ff.hnsw_params["efSearch"] == 192
+    n = np.linalg.norm(ff.vectors.astype(np.float64), axis=1)
+    assert np.all(np.abs(n - 1) < 1e-5)
+    # payload starts at the byte offset decoded in SURVEY.md §1 (IxFI storage at 30865)
+    raw = open(os.path.join(GOLDEN, "ref_photo_search.index"), "rb").read()
+    assert raw[30865:30869] == b"IxFI"
+    first = np.frombuffer(raw, dtype="<f4", count=4, offset=30865 + 37 + 8)
+    assert np.array_equal(first, ff.vectors[0, :4])
+
+
+@pytest.mark.parametrize("metric", [0, 1])
+def test_roundtrip_both_metrics(tmp_path, metric):
+    rng = np.random.default_rng(0)
+    x = rng.standard_normal((123, 17)).astype(np.float32)
+    p = str(tmp_path / "i.bin")
+    F.write_flat(p, x, metric)
+    raw = open(p, "rb").read()
+    assert raw[:4] == (b"IxFI" if metric == 0 else b"IxF2")
+    assert len(raw) == 37 + 8 + x.size * 4
+    ff = F.read_index(p)
+    assert ff.metric_type == metric and np.array_equal(ff.vectors, x)
+
+
+def test_empty_index_roundtrip(tmp_path):
+    p = str(tmp_path / "e.bin")
+    F.write_flat(p, np.zeros((0, 9), np.float32), 0)
+    ff = F.read_index(p)
+    assert ff.ntotal == 0 and ff.d == 9 and ff.vectors.shape == (0, 9)
+
+
+def test_corrupt_files_raise(tmp_path):
+    p = tmp_path / "bad.bin"
+    p.write_bytes(b"IxFI" + b"\0" * 5)
+    with pytest.raises(F.FaissFormatError):
+        F.read_index(str(p))
+    p.write_bytes(b"ABCD" + struct.pack("<iqqqBi", 4, 1, 1 << 20, 1 << 20, 1, 0) + struct.pack("<Q", 4) + b"\0" * 16)
+    with pytest.raises(F.FaissFormatError):
+        F.read_index(str(p))
+    p.write_bytes(b"IxFI" + struct.pack("<iqqqBi", 4, 2, 1 << 20, 1 << 20, 1, 0) + struct.pack("<Q", 8) + b"\0" * 16)
+    with pytest.raises(F.FaissFormatError):
+        F.read_index(str(p))
