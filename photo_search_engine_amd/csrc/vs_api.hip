@@ -81,10 +81,11 @@ struct DevBuf {
 // per-call execution context: stream + workspace (pooled; one per concurrent search)
 struct Ctx {
     hipStream_t stream = nullptr;
-    DevBuf qdev, qtile, qinfo, qpad, cand, part, merge_a, merge_b, outD, outI, outS, cert, thr0;
+    DevBuf qdev, qtile, qinfo, qpad, cand, part, merge_a, merge_b, outD, outI, outS, cert, thr0, seedmax;
     std::vector<int> cert_host;
     ~Ctx() {
-        for (DevBuf* b : {&qdev, &qtile, &qinfo, &qpad, &cand, &part, &merge_a, &merge_b, &outD, &outI, &outS, &cert, &thr0})
+        for (DevBuf* b : {&qdev, &qtile, &qinfo, &qpad, &cand, &part, &merge_a, &merge_b, &outD, &outI, &outS, &cert, &thr0,
+                          &seedmax})
             b->release();
         if (stream) hipStreamDestroy(stream);
     }
@@ -197,9 +198,11 @@ int screen_depth(int k) {
     return std::min(kp, KP_MAX);
 }
 
-// optimistic seed: the 16th best key of the strided row sample (expected ~16 * N / sample rows
-// corpus rows above it, far more than Kp; any query left short is caught by the certificate)
-constexpr int kOptimisticSeedRank = 16;
+// optimistic seed: a 16-row-group maximum of the strided tile sample, at the rank that leaves
+// ~kOptimisticPassFactor * Kp corpus rows above it in expectation (the proven seed is rank Kp); a
+// query left short is caught by the certificate and searched again with the proven seed
+constexpr int kOptimisticSeedRank = 1;  // seed_rank argument: > 0 selects the optimistic rank
+constexpr double kOptimisticPassFactor = 8.0;
 
 float gamma_of(int d) {
     const double u = 5.9604644775390625e-08;  // 2^-24
@@ -208,7 +211,7 @@ float gamma_of(int d) {
 }
 
 // Enqueue one query block through screen -> merge -> refine.  q: device fp32 [nqb][d].
-// seed_rank: 0 = proven (safe) seed, > 0 = optimistic seed at that sample rank (see k_seed_thr)
+// seed_rank: 0 = proven (safe) seed, > 0 = optimistic seed at that sample rank (see k_seed_select)
 void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, float* D, int64_t* I, double* S64,
                   int* cert, int64_t id_offset, hipStream_t st, int seed_rank) {
     const int64_t tiles = (ix->ntotal + TR - 1) / TR;
@@ -262,28 +265,30 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
         return src;
     };
 
-    // threshold seeding (MFMA path): screen one tile per workgroup, strided over the shard, and
-    // start every workgroup of the main pass at the sample's Kp-th best key per query
+    // threshold seeding (MFMA path): screen one tile per CU, strided over the shard, keep only the
+    // per-query maxima of 16-row groups, and start every workgroup of the main pass at the
+    // rank-th largest of them (rank = Kp: proven lower bound; kOptimisticSeedRank: optimistic)
     a.tile_stride = 0;
     a.thr0 = nullptr;
     bool optimistic = false;
     if (use_mfma && tiles >= 4 * (int64_t)a.G) {
-        // sample = 2 tiles per CU (one per workgroup, 2 x num_cu workgroups), evenly strided
         ScreenArgs sa = a;
-        sa.G = 2 * a.G;
         sa.tile_stride = (int)(tiles / sa.G);
-        c->part.ensure((size_t)sa.G * QB * Kp * sizeof(u64));
-        c->cand.ensure((size_t)sa.G * QB * a.cap * sizeof(u64));
-        sa.part = c->part.as<u64>();
-        sa.cand = c->cand.as<u64>();
-        a.part = sa.part;
-        a.cand = sa.cand;
-        HIP_CHECK(launch_screen_mfma(ix->dtype, sa, c->qtile.as<uint8_t>(), nqb, st));
-        const u64* sample = merge_all(sa.part, sa.G, QB);
+        const int M = sa.G * 16;
+        c->seedmax.ensure(sizeof(float) * MFMA_QB * M);
+        sa.seedmax = c->seedmax.as<float>();
+        HIP_CHECK(launch_seed_mfma(ix->dtype, sa, c->qtile.as<uint8_t>(), nqb, st));
         c->thr0.ensure(sizeof(u64) * MFMA_QB);
-        HIP_CHECK(launch_seed_thr(sample, Kp, nqb, c->thr0.as<u64>(), seed_rank, st));
+        // optimistic rank: expected rows above the seed ~ rank * rows / sampled rows ~ 8 Kp
+        int rank = Kp;
+        if (seed_rank > 0) {
+            const double sampled = (double)sa.G * TR;
+            const double r = std::ceil(kOptimisticPassFactor * Kp * sampled / (double)ix->ntotal);
+            rank = (int)std::min<double>(std::max<double>(r, 1.0), (double)Kp);
+        }
+        HIP_CHECK(launch_seed_select(sa.seedmax, M, nqb, rank, c->thr0.as<u64>(), st));
         a.thr0 = c->thr0.as<u64>();
-        optimistic = seed_rank > 0;
+        optimistic = rank < Kp;
     }
 
     const bool timing = ix->timing.load();
@@ -390,7 +395,9 @@ int vs_create(int d, int metric, int dtype, int device, vs_index** out) {
             throw VsError(VS_ERR_DEVICE, std::string("libvs is built for gfx950, device is ") + prop.gcnArchName);
         vs_index* ix = new vs_index();
         ix->d = d;
-        ix->dpad = (int)round_up(d, CH);
+        // >= 2 K-steps per tile: the MFMA screen's deferred compaction check runs on the K-step
+        // after a tile's epilogue, so a one-step tile would never compact its candidate buffers
+        ix->dpad = (int)std::max<int64_t>(round_up(d, CH), 2 * CH);
         ix->metric = metric;
         ix->dtype = dtype;
         ix->device = device;

@@ -48,6 +48,7 @@ struct ScreenArgs {
     int tile_stride;         // > 0: workgroup b screens only tile b*tile_stride (threshold seeding)
     const u64* thr0;         // [QB] initial per-query key threshold (keys > thr0 kept), or null
     unsigned* dbg;           // debug counters (VS_MF_STATS): inserts, slow paths, compactions, overflows
+    float* seedmax;          // seed pass only: [QB][G*16] maxima of disjoint 16-row groups per query
 };
 
 // ---- launchers (vs_kernels.hip) -------------------------------------------------------------
@@ -100,7 +101,10 @@ hipError_t launch_refine(const RefineArgs& a, int nq, hipStream_t st);
 // Kp-th key, because the list is the exact top-Kp of a SUBSET of the rows
 // rank > 0: OPTIMISTIC seed = the rank-th best sample key (not a proven bound; the refine kernel's
 // certificate then rejects any query left with fewer than Kp candidates)
-hipError_t launch_seed_thr(const u64* list, int Kp, int nq, u64* thr0, int rank, hipStream_t st);
+// seed pass: screen one tile per workgroup (tile_stride) and write per-query 16-row-group maxima
+hipError_t launch_seed_mfma(int dt, const ScreenArgs& a, const uint8_t* qt, int nqb, hipStream_t st);
+// thr0[q] = key just below the rank-th largest of the M group maxima of query q (0 if none)
+hipError_t launch_seed_select(const float* seedmax, int M, int nq, int rank, u64* thr0, hipStream_t st);
 
 hipError_t launch_merge_shards(int metric, const double* S_in, const int64_t* I_in, int G, int64_t nq, int k,
                                double* S_out, int64_t* I_out, float* D_out, hipStream_t st);

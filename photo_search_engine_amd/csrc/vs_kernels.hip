@@ -462,7 +462,10 @@ constexpr int MF_SLOTS = 4;
 constexpr int MF_DEPTH = MF_SLOTS - 1;
 constexpr int MF_THREADS = 512;
 constexpr int MF_POOL = 512;  // LDS insert pool of the loader waves (flushed by the writer waves)
-constexpr int MF_LDS = MF_SLOTS * MF_SLOT + 256 * 8 + 256 * 4 + 256 * 4 + 16 + MF_POOL * 8 + MF_POOL * 4;
+constexpr int MF_SEED_MODE = 20;  // k_screen_mfma MODE of the threshold-seed pass
+constexpr int MF_SX = 8 * 64 * 8 * 4;  // per-wave insert staging: 64 lanes x 8 fp32 (slow path only)
+constexpr int MF_LDS = MF_SLOTS * MF_SLOT + 256 * 8 + 256 * 4 + 256 * 4 + 16 + MF_POOL * 8 + MF_POOL * 4 + MF_SX;
+static_assert(MF_LDS <= 160 * 1024, "LDS budget");
 
 typedef __attribute__((address_space(3))) uint8_t* lds_u8_t;
 
@@ -655,15 +658,20 @@ __device__ __forceinline__ void mf_wave_compact(u64* __restrict__ buf, int n, in
 //   4 = 3 + no per-K-step barrier | 5 = 4 + no LDS reads (MFMAs on register operands)
 //   6 loads only (no math, no epilogue) | 7 = 6 without the query stream | 8 = 6 with nt corpus loads
 //   9 loads + math, no epilogue (burst DMA issue) | 10 = 9 with the DMA issue interleaved (as 0)
-//   11 = 9 with the ping-pong schedule (waves 4-7 half a K-step behind)
+//   11 = 9 with the ping-pong schedule (waves 4-7 half a K-step behind) | 12 = 11 without loads
+//   13 = 0 with compare-only epilogue (no inserts, no check) | 14 = 0 without the deferred check/pool flush
 template <int DT, int METRIC, int MODE>
 __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
-    constexpr bool LOADS = (MODE != 1 && MODE < 3) || MODE >= 6;  // 0, 2, 6..11
-    constexpr bool MATH = (MODE != 2 && MODE < 6) || MODE == 9 || MODE == 10;
-    constexpr bool PP = MODE == 11;  // ping-pong: waves 4-7 half a K-step behind waves 0-3
-    constexpr bool EPI = MODE < 3;
+    constexpr bool LOADS = (MODE != 1 && MODE < 3) || (MODE >= 6 && MODE != 12);  // (incl. the seed mode)
+    constexpr bool MATH = (MODE != 2 && MODE < 6) || MODE == 9 || MODE == 10 || MODE == 13 || MODE == 14 ||
+                          MODE == MF_SEED_MODE;
+    constexpr bool PP = MODE == 11 || MODE == 12;  // ping-pong: waves 4-7 half a K-step behind waves 0-3
+    constexpr bool SEED = MODE == MF_SEED_MODE;  // threshold-seed pass: group maxima only
+    constexpr bool EPI = MODE < 3 || MODE == 13 || MODE == 14 || SEED;
+    constexpr bool INS = MODE != 13;   // threshold passes insert candidates
+    constexpr bool CHECK = MODE != 13 && MODE != 14;  // deferred compaction check + pool flush
     constexpr bool BAR = MODE < 4 || MODE >= 6;
-    constexpr bool READS = MODE < 5 || MODE == 9 || MODE == 10;
+    constexpr bool READS = MODE < 5 || MODE == 9 || MODE == 10 || MODE == 13 || MODE == 14 || MODE == MF_SEED_MODE;
     constexpr bool QLOAD = MODE != 7;
     constexpr bool NT = MODE == 8 || MODE == 0 || MODE >= 9;
     constexpr bool IL = MODE == 10;  // DMA issue interleaved with the MFMAs (ablation: slower)
@@ -671,9 +679,11 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
     u64* thr_key = (u64*)(smem + MF_SLOTS * MF_SLOT);
     float* thr_f = (float*)(smem + MF_SLOTS * MF_SLOT + 256 * 8);
     int* cnt = (int*)(smem + MF_SLOTS * MF_SLOT + 256 * 12);
-    int* flag = (int*)(smem + MF_SLOTS * MF_SLOT + 256 * 16);  // [0] spare, [1] pool count
+    int* flag = (int*)(smem + MF_SLOTS * MF_SLOT + 256 * 16);  // [1] pool count, [2 + tile parity] inserted
     u64* pool_key = (u64*)(smem + MF_SLOTS * MF_SLOT + 256 * 16 + 16);
     int* pool_q = (int*)(smem + MF_SLOTS * MF_SLOT + 256 * 16 + 16 + MF_POOL * 8);
+    float* sx = (float*)(smem + MF_SLOTS * MF_SLOT + 256 * 16 + 16 + MF_POOL * 12) + (threadIdx.x >> 6) * 512 +
+                (threadIdx.x & 63) * 8;
 
     // The LDS ring is written only by the inline-asm DMA: let the array escape into an asm with a
     // memory clobber, so the compiler must assume every later memory-clobbering asm (DMA issue,
@@ -698,6 +708,8 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
     if (tid == 0) {
         flag[0] = 0;
         flag[1] = 0;
+        flag[2] = 0;
+        flag[3] = 0;
     }
     const int nks = a.dpad / CH;
     const int64_t tbytes = (int64_t)TR * a.dpad * 2;
@@ -739,7 +751,7 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
         }
         if constexpr (PP) {
             if (wid < 4) {
-                if (do_issue) mf_stage<true, NT>(nA, nB, nslot, tid);
+                if constexpr (LOADS) if (do_issue) mf_stage<true, NT>(nA, nB, nslot, tid);
                 mf_read(smem + (s % MF_SLOTS) * MF_SLOT, pf_a, pf_b, wm, wn, lane_off);
                 mf_mfma<DT, 0, 4>(pf_a, pf_b, acc);
             } else {
@@ -811,7 +823,15 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
                     }
                 // one compare per query column; the insert path runs only where something passes,
                 // and then costs one LDS atomic per lane plus predicated stores
+                if constexpr (SEED) {  // group g = wm*4 + lane/16 of the tile: 16 distinct rows
+                    a.seedmax[(size_t)q * (a.G * 16) + blk * 16 + wm * 4 + (olane >> 4)] = mx;
+                    continue;
+                }
                 const float tf = thr_f[q];
+                if constexpr (!INS) {
+                    sink += mx >= tf ? 1.0f : 0.0f;
+                    continue;
+                }
                 if (mx >= tf) {
                     const u64 tk = thr_key[q];
                     uint32_t m = 0;
@@ -819,49 +839,52 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
                     for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
-                            const float x = v[mi][r];
-                            const bool p = x > tf ||
-                                           (x == tf && mk_key(x, (uint32_t)(rowbase + rid0 + mi * 16 + r)) > tk);
-                            m |= (p ? 1u : 0u) << (mi * 4 + r);
+                            m |= (v[mi][r] >= tf ? 1u : 0u) << (mi * 4 + r);  // exact ties resolved below
                         }
-                    const int c = __popc(m);
+                    if (m) flag[2 + (ti & 1)] = 1;
                     if (a.dbg) {
-                        atomicAdd(&a.dbg[0], (unsigned)c);
+                        atomicAdd(&a.dbg[0], (unsigned)__popc(m));
                         if (lane == __builtin_amdgcn_readfirstlane(lane)) atomicAdd(&a.dbg[1], 1u);
                     }
-                    // loader waves park their inserts in the LDS pool (no global store in their
-                    // vmcnt); writer waves, or a loader wave whose pool share overflows, store
-                    int pbase = MF_POOL;
-                    if (wid < 4 && c) pbase = atomicAdd(&flag[1], c);
-                    const bool to_pool = wid < 4 && pbase + c <= MF_POOL;
-                    int base = 0;
-                    if (c && !to_pool) base = atomicAdd(&cnt[q], c);
+                    // Compact insert loop (not unrolled: an unrolled insert path for 8 columns x 16
+                    // values costs more in instruction fetch than the rare inserts themselves).  The
+                    // lane's values go through its LDS staging row, 8 at a time, so the loop can
+                    // index them.  Loader waves park keys in the LDS pool; writer waves store them to
+                    // the global candidate buffer.  (A younger VMEM op in a loader wave -- a pool
+                    // overflow store -- only makes its counted ring waits stricter, never looser.)
 #pragma unroll
-                    for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            const int bit = mi * 4 + r;
-                            if ((m >> bit) & 1u) {
-                                const int off = __popc(m & ((1u << bit) - 1u));
-                                const u64 key = mk_key(v[mi][r], (uint32_t)(rowbase + rid0 + mi * 16 + r));
-                                if (to_pool) {
-                                    pool_key[pbase + off] = key;
-                                    pool_q[pbase + off] = q;
-                                } else {
-                                    // a reservation that straddles the pool end: void its in-pool part
-                                    if (wid < 4 && pbase + off < MF_POOL) pool_q[pbase + off] = -1;
-                                    if (a.dbg && wid < 4) atomicAdd(&a.dbg[3], 1u);
-                                    if (base + off < a.cap) cand[(size_t)q * a.cap + base + off] = key;
+                    for (int h = 0; h < 2; ++h) {
+                        uint32_t mh = (m >> (8 * h)) & 0xFFu;
+                        if (!mh) continue;
+                        *(float4*)(sx) = make_float4(v[2 * h][0], v[2 * h][1], v[2 * h][2], v[2 * h][3]);
+                        *(float4*)(sx + 4) = make_float4(v[2 * h + 1][0], v[2 * h + 1][1], v[2 * h + 1][2],
+                                                         v[2 * h + 1][3]);
+                        while (mh) {
+                            const int j = __builtin_ctz(mh);
+                            mh &= mh - 1u;
+                            const int bit = 8 * h + j;
+                            const u64 key = mk_key(sx[j], (uint32_t)(rowbase + rid0 + (bit >> 2) * 16 + (bit & 3)));
+                            if (key <= tk) continue;  // score == threshold and not ahead of it by id
+                            if (wid < 4) {
+                                const int slot = atomicAdd(&flag[1], 1);
+                                if (slot < MF_POOL) {
+                                    pool_key[slot] = key;
+                                    pool_q[slot] = q;
+                                    continue;
                                 }
+                                if (a.dbg) atomicAdd(&a.dbg[3], 1u);
                             }
+                            const int slot = atomicAdd(&cnt[q], 1);
+                            if (slot < a.cap) cand[(size_t)q * a.cap + slot] = key;
                         }
+                    }
                 }
             }
 #pragma unroll
             for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
                 for (int ni = 0; ni < 8; ++ni) acc[mi][ni] = floatx4{0.f, 0.f, 0.f, 0.f};
-            check_pending = true;
+            check_pending = CHECK && !SEED;
             }
         }
         // Deferred compaction check, after the NEXT K-step's barrier: by then every wave's
@@ -869,6 +892,9 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
         // counters, so the (rare) decision to compact is uniform without extra barriers.
         // (no check after the shard's last tile: the flush below compacts; capacity holds by the
         // invariant cnt <= cap - TR after every check, and one tile adds at most TR per query)
+        // skipped when the finished tile inserted nothing anywhere in the workgroup (the common case
+        // once the threshold is seeded): its parity flag was set before this step's barrier
+        if (check_pending && ks != nks - 1 && flag[2 + ((ti - 1) & 1)] == 0) check_pending = false;
         if (check_pending && ks != nks - 1) {
             check_pending = false;
             // writer waves flush the loader waves' LDS pool into the global candidate buffers
@@ -883,8 +909,11 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
                         if (slot < a.cap) cand[(size_t)q * a.cap + slot] = pool_key[j];
                     }
                 }
-                mf_barrier_lgkm();
-                if (tid == 0) flag[1] = 0;
+                mf_barrier_lgkm();  // every wave has read the tile's insert flag and the pool
+                if (tid == 0) {
+                    flag[1] = 0;
+                    flag[2 + ((ti - 1) & 1)] = 0;
+                }
             }
             int need = 0;
 #pragma unroll
@@ -915,9 +944,10 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
 #pragma unroll
             for (int ni = 0; ni < 8; ++ni) sink += acc[mi][ni][0] + acc[mi][ni][3];
     }
-    if constexpr (!EPI) {
+    if constexpr (!EPI || !INS) {
         if (sink == 12345.678f) cnt[0] = 1;  // keep the ablated MFMAs alive
     }
+    if constexpr (SEED) return;  // no candidates (no DMA is in flight after the last K-step)
     // ---- flush: pool -> buffers, then best Kp per query -> part[blk][q][Kp] ----
     mf_barrier_drain();
     {
@@ -1282,33 +1312,41 @@ __global__ void __launch_bounds__(256) k_refine(RefineArgs a, int KP2) {
     }
 }
 
-// per-query seed threshold from the top-Kp list of a row sample (one wave per query):
-//   rank == 0: min key - 1 of a full list (a proven lower bound of the final Kp-th key)
-//   rank  > 0: (rank-th best key) - 1, optimistic (see launch_seed_thr)
-__global__ void __launch_bounds__(256) k_seed_thr(const u64* __restrict__ list, int Kp, int nq, u64* __restrict__ thr0,
-                                                   int rank) {
-    const int lane = threadIdx.x & 63;
-    const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (q >= nq) return;
-    u64 keys[KP_MAX / 64];
-    int c = 0;
-    u64 mn = ~0ull;
+// seed threshold from 16-row group maxima (one block per query): the rank-th largest maximum T
+// has `rank` DISTINCT rows scoring >= T, so T never exceeds the true rank-th best screen score and
+// the key just below every score >= T, (ord(T) << 32) | 0, is a valid starting threshold
+// (rank = Kp: proven; rank < Kp: optimistic, checked by the refine certificate).
+constexpr int SEED_VPT = 32;  // values per thread: up to 256 * 32 = 8192 maxima per query
+__global__ void __launch_bounds__(256) k_seed_select(const float* __restrict__ seedmax, int M, int rank,
+                                                     u64* __restrict__ thr0) {
+    __shared__ int part[4];
+    const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    uint32_t v[SEED_VPT];
 #pragma unroll
-    for (int e = 0; e < KP_MAX / 64; ++e) {
-        const int j = lane + 64 * e;
-        const u64 k = j < Kp ? list[(size_t)q * Kp + j] : 0ull;
-        keys[e] = k;
-        if (k != 0ull) {
-            ++c;
-            mn = k < mn ? k : mn;
-        }
+    for (int e = 0; e < SEED_VPT; ++e) {
+        const int j = tid + 256 * e;
+        v[e] = j < M ? ord_f32(seedmax[(size_t)q * M + j]) : 0u;
     }
-    c = wave_sum_i(c);
-    mn = wave_min_u64(mn);
-    u64 t;
-    if (rank > 0 && c >= rank) t = wave_kth<KP_MAX / 64>(keys, rank) - 1ull;
-    else t = (c == Kp) ? mn - 1ull : 0ull;
-    if (lane == 0) thr0[q] = t;
+    // largest t with count(v >= t) >= rank (bisection on the orderable bits)
+    uint32_t lo = 0u, hi = 0xFFFFFFFFu;
+    while (lo < hi) {
+        const uint32_t mid = lo + (uint32_t)(((uint64_t)hi - lo + 1) >> 1);
+        int c = 0;
+#pragma unroll
+        for (int e = 0; e < SEED_VPT; ++e) c += v[e] >= mid ? 1 : 0;
+        c = wave_sum_i(c);
+        __syncthreads();
+        if (lane == 0) part[wid] = c;
+        __syncthreads();
+        const int tot = part[0] + part[1] + part[2] + part[3];
+        if (tot >= rank) lo = mid;
+        else hi = mid - 1u;
+    }
+    if (tid == 0) {
+        const float T = unord_f32(lo);
+        // lo == 0: fewer than `rank` values; -inf: only padding rows -> no threshold
+        thr0[q] = (lo == 0u || T == -INFINITY) ? 0ull : ((u64)lo << 32);
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1460,6 +1498,9 @@ static void launch_mfma_mode(const ScreenArgs& a, const uint8_t* qt, int nqb, hi
         case 9: launch_mfma_one<DT, METRIC, 9>(a, qt, nqb, st); break;
         case 10: launch_mfma_one<DT, METRIC, 10>(a, qt, nqb, st); break;
         case 11: launch_mfma_one<DT, METRIC, 11>(a, qt, nqb, st); break;
+        case 12: launch_mfma_one<DT, METRIC, 12>(a, qt, nqb, st); break;
+        case 13: launch_mfma_one<DT, METRIC, 13>(a, qt, nqb, st); break;
+        case 14: launch_mfma_one<DT, METRIC, 14>(a, qt, nqb, st); break;
         default: launch_mfma_one<DT, METRIC, 0>(a, qt, nqb, st); break;
     }
 }
@@ -1512,8 +1553,23 @@ hipError_t launch_refine(const RefineArgs& a, int nq, hipStream_t st) {
     return hipGetLastError();
 }
 
-hipError_t launch_seed_thr(const u64* list, int Kp, int nq, u64* thr0, int rank, hipStream_t st) {
-    hipLaunchKernelGGL(k_seed_thr, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, st, list, Kp, nq, thr0, rank);
+hipError_t launch_seed_mfma(int dt, const ScreenArgs& a, const uint8_t* qt, int nqb, hipStream_t st) {
+    if (nqb > MFMA_QB || a.tile_stride <= 0 || !a.seedmax) return hipErrorInvalidValue;
+    if (dt == DT_BF16) {
+        if (a.metric == METRIC_IP) launch_mfma_one<DT_BF16, METRIC_IP, MF_SEED_MODE>(a, qt, nqb, st);
+        else launch_mfma_one<DT_BF16, METRIC_L2, MF_SEED_MODE>(a, qt, nqb, st);
+    } else if (dt == DT_F16) {
+        if (a.metric == METRIC_IP) launch_mfma_one<DT_F16, METRIC_IP, MF_SEED_MODE>(a, qt, nqb, st);
+        else launch_mfma_one<DT_F16, METRIC_L2, MF_SEED_MODE>(a, qt, nqb, st);
+    } else {
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_seed_select(const float* seedmax, int M, int nq, int rank, u64* thr0, hipStream_t st) {
+    if (M > 256 * SEED_VPT || rank <= 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_seed_select, dim3((unsigned)nq), dim3(256), 0, st, seedmax, M, rank, thr0);
     return hipGetLastError();
 }
 

@@ -165,3 +165,54 @@ def test_real_reference_index_self_queries(FlatIndex):
     ix.add(np.ascontiguousarray(ff.vectors))
     D, I = _check_exact(ix, np.ascontiguousarray(ff.vectors), 10, "ip")
     np.testing.assert_array_equal(I[:, 0], np.arange(77))
+
+
+@pytest.mark.parametrize("d", [16, 32])
+def test_mfma_tiny_dim_many_tiles_per_workgroup(FlatIndex, d):
+    # d <= 32 is one 32-element chunk; the layout pads it to two K-steps so the screen's
+    # per-tile compaction check runs.  ~3.8 tiles per workgroup, unseeded threshold: without
+    # compaction a workgroup's candidate buffer (768 keys per query) would overflow.
+    ix = FlatIndex(d, "ip", "bf16")
+    ix.add_synthetic(O.SEED_CORPUS, 0, 250_000, False)
+    q = O.synth_rows(O.SEED_QUERIES, 0, 40, d, False, "bf16")
+    _check_exact(ix, q, 100, "ip")
+
+
+def _num_cu():
+    import torch
+    return torch.cuda.get_device_properties(0).multi_processor_count
+
+
+@pytest.mark.parametrize("metric", ["ip", "l2"])
+@pytest.mark.parametrize("k", [10, 100])
+def test_seeded_threshold_search_exact(FlatIndex, metric, k):
+    # >= 4 tiles per CU: the MFMA path seeds every workgroup's threshold from a strided tile
+    # sample (optimistic rank), so this covers the seed pass + certificate on real sizes
+    N = 256 * 4 * _num_cu() + 777
+    ix = FlatIndex(64, metric, "bf16")
+    ix.add_synthetic(O.SEED_CORPUS, 0, N, True)
+    q = O.synth_rows(O.SEED_QUERIES, 0, 48, 64, True, "bf16")
+    _check_exact(ix, q, k, metric)
+    assert ix.uncertified_count() == 0
+
+
+def test_optimistic_seed_failure_falls_back_exactly(FlatIndex):
+    # Adversarial corpus: one near-copy of the query in every SAMPLED tile (tile j * stride) and
+    # nowhere else, so the optimistic seed threshold (16th best sample maximum) lets fewer than Kp
+    # rows through; the certificate must reject it and vs_search must re-search exactly.
+    # 32 tiles per CU: the optimistic rank is ceil(8 * Kp / 32) = 8 < the 16 planted rows/query
+    d, k = 64, 10
+    cu = _num_cu()
+    tiles = 32 * cu + 3
+    N = tiles * 256
+    x = O.synth_rows(O.SEED_CORPUS, 0, N, d, True, "f32")
+    q = O.synth_rows(O.SEED_QUERIES, 0, 16, d, True, "f32")
+    stride = tiles // cu
+    rng = np.random.default_rng(11)
+    for j in range(cu):
+        r = j * stride * 256 + 5
+        x[r] = q[j % 16] + 0.01 * rng.standard_normal(d).astype(np.float32)
+    ix = FlatIndex(d, "ip", "bf16")
+    ix.add(x)
+    _check_exact(ix, O.round_dtype(q, "bf16"), k, "ip")
+    assert ix.uncertified_count() > 0  # the optimistic pass was rejected (and then redone exactly)
