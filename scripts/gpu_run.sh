@@ -1,5 +1,5 @@
 #!/bin/bash
-# usage: bash scripts_gpu_run.sh <step>...   steps: smoke tests bench_small bench prof
+# usage: bash scripts/gpu_run.sh <step>...   steps: smoke tests bench_small bench bench_cfg2 prof ablate stats pmcclk
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp

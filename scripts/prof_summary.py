@@ -1,0 +1,106 @@
+#!/usr/bin/env python3
+"""Summarise one scripts/gpu_prof.sh run into profiles/<tag>_*.{csv,json,md}.
+
+HBM bytes per launch follow MI355X_MICROARCH.md (HBM section): FETCH_SIZE is in KiB and on gfx950
+reports half the bytes of wide coalesced streaming reads, so traffic = 2 * 1024 * FETCH_SIZE;
+WRITE_SIZE (KiB) is taken as is.  Effective clock = GRBM_GUI_ACTIVE / 8 XCDs / kernel duration.
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+
+def short(name):
+    return name.split("(")[0].replace("void ", "")
+
+
+def per_dispatch(d):
+    kt = {r["Dispatch_Id"]: r for r in csv.DictReader(open(os.path.join(d, "p_kernel_trace.csv")))}
+    out = collections.defaultdict(dict)
+    for r in csv.DictReader(open(os.path.join(d, "p_counter_collection.csv"))):
+        did = r["Dispatch_Id"]
+        out[did]["name"] = short(r["Kernel_Name"])
+        out[did]["grid"] = int(r["Grid_Size"])
+        out[did][r["Counter_Name"]] = out[did].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        k = kt.get(did)
+        if k:
+            out[did]["dur_s"] = (int(k["End_Timestamp"]) - int(k["Start_Timestamp"])) * 1e-9
+    return out
+
+
+def group(disp):
+    g = collections.defaultdict(list)
+    for v in disp.values():
+        g[(v["name"], v["grid"])].append(v)
+    return g
+
+
+def main():
+    src, tag = sys.argv[1], sys.argv[2]
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    prof = os.path.join(repo, "profiles")
+    os.makedirs(prof, exist_ok=True)
+    shutil.copy(os.path.join(src, "kt", "kt_kernel_stats.csv"), os.path.join(prof, f"{tag}_kernel_stats.csv"))
+    bench_line = None
+    for line in open(os.path.join(src, "kt.log")):
+        if line.startswith("{"):
+            bench_line = json.loads(line)
+    summary = {"tag": tag, "bench_args_line": bench_line and {k: bench_line.get(k) for k in
+                                                              ("value", "ms_per_step", "config")},
+               "kernels": {}}
+    passes = {p: group(per_dispatch(os.path.join(src, p))) for p in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_lds")
+              if os.path.exists(os.path.join(src, p, "p_counter_collection.csv"))}
+    keys = set()
+    for g in passes.values():
+        keys |= set(g)
+    for key in sorted(keys):
+        name, grid = key
+        ent = {}
+        for p, g in passes.items():
+            ds = g.get(key, [])
+            if not ds:
+                continue
+            ds = ds[len(ds) // 2:]  # steady state: drop the first half (warmup)
+            for c in ds[0]:
+                if c in ("name", "grid"):
+                    continue
+                ent.setdefault(c + "_by_pass", {})[p] = sum(x.get(c, 0.0) for x in ds) / len(ds)
+        if not ent:
+            continue
+        flat = {}
+        for c, byp in ent.items():
+            base = c[: -len("_by_pass")]
+            flat[base] = byp.get("pmc_sq", next(iter(byp.values())))
+        if "FETCH_SIZE" in flat:
+            flat["hbm_read_bytes_corrected"] = flat["FETCH_SIZE"] * 1024 * 2
+        if "WRITE_SIZE" in flat:
+            flat["hbm_write_bytes"] = flat["WRITE_SIZE"] * 1024
+        if "GRBM_GUI_ACTIVE" in flat and flat.get("dur_s"):
+            flat["clock_ghz"] = flat["GRBM_GUI_ACTIVE"] / 8 / flat["dur_s"] / 1e9
+        summary["kernels"][f"{name} grid={grid}"] = flat
+    # the dominant screen launch (largest mean duration among k_screen_*)
+    screens = {k: v for k, v in summary["kernels"].items() if "k_screen" in k and v.get("dur_s")}
+    if screens and bench_line:
+        top = max(screens, key=lambda k: screens[k]["dur_s"])
+        t = screens[top]
+        cfg = bench_line["config"]
+        rd = t.get("hbm_read_bytes_corrected")
+        wr = t.get("hbm_write_bytes", 0.0)
+        traffic = {"workload": cfg["workload"], "n_local": cfg["n_local"], "kernel": top,
+                   "hbm_bytes_per_launch": None if rd is None else rd + wr,
+                   "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
+                   "profiled_kernel_ms": t["dur_s"] * 1e3, "clock_ghz": t.get("clock_ghz"),
+                   "source": f"profiles/{tag}_pmc.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes)"}
+        with open(os.path.join(prof, f"traffic_{cfg['workload']}.json"), "w") as f:
+            json.dump(traffic, f, indent=1)
+        summary["dominant"] = traffic
+    with open(os.path.join(prof, f"{tag}_pmc.json"), "w") as f:
+        json.dump(summary, f, indent=1)
+    print(json.dumps(summary.get("dominant"), indent=1))
+
+
+if __name__ == "__main__":
+    main()
