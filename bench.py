@@ -9,7 +9,7 @@ One process per GPU (torchrun for N > 1).  The corpus is row-sharded: rank r hol
 oracle/vs_oracle.c); every rank holds the same synthetic query batch.  One step = the hot path on
 one batch: per-shard exact search (pack -> MFMA screen with fused top-k -> merge -> exact
 refine) and, for N > 1, an RCCL all-gather of the per-shard (fp64 score, id) lists + the on-device
-merge.  Prints ONE JSON line on rank 0 with `roofline` (dominant kernel, HIP events on its own
+merge (photo_search_engine_amd/distributed.py, the product's multi-GPU layer).  Prints ONE JSON line on rank 0 with `roofline` (dominant kernel, HIP events on its own
 stream) and `cpu_baseline` (faiss fp32 restatement on this host, bounded sample).
 """
 from __future__ import annotations
@@ -56,7 +56,8 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from photo_search_engine_amd.index import FlatIndex, merge_shards_device, synthesize_device
+    from photo_search_engine_amd.distributed import ShardedFlatIndex, shard_range
+    from photo_search_engine_amd.index import synthesize_device
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -73,34 +74,22 @@ def main():
     if args.rows:
         N = args.rows
     G = world
-    row0 = N * rank // G
-    n_local = N * (rank + 1) // G - row0
+    row0, n_local = shard_range(N, rank, G)
 
     t_build = time.time()
-    ix = FlatIndex(d, "ip", dtype, device=local)
-    ix.add_synthetic(SEED_CORPUS, row0, n_local, True)
+    # the product's multi-GPU layer: one row shard per rank, all-gather + device merge (G > 1)
+    sh = ShardedFlatIndex(d, "ip", dtype, device=local)
+    sh.add_synthetic(SEED_CORPUS, N, True)
+    ix = sh.index
     q = torch.empty((nq, d), dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev)
     synthesize_device(local, SEED_QUERIES, 0, nq, d, q.data_ptr(), True, dtype, stream.cuda_stream)
-    D = torch.empty((nq, k), dtype=torch.float32, device=dev)
-    I = torch.empty((nq, k), dtype=torch.int64, device=dev)
-    S = torch.empty((nq, k), dtype=torch.float64, device=dev)
-    if G > 1:
-        Sg = torch.empty((G, nq, k), dtype=torch.float64, device=dev)
-        Ig = torch.empty((G, nq, k), dtype=torch.int64, device=dev)
-        Sf = torch.empty((nq, k), dtype=torch.float64, device=dev)
-        If = torch.empty((nq, k), dtype=torch.int64, device=dev)
-        Df = torch.empty((nq, k), dtype=torch.float32, device=dev)
     torch.cuda.synchronize()
     t_build = time.time() - t_build
+    result = {}
 
     def step():
-        ix.search_device(q.data_ptr(), nq, k, D.data_ptr(), I.data_ptr(), S.data_ptr(), row0, stream.cuda_stream)
-        if G > 1:
-            dist.all_gather_into_tensor(Sg, S)
-            dist.all_gather_into_tensor(Ig, I)
-            merge_shards_device(0, Sg.data_ptr(), Ig.data_ptr(), G, nq, k, Sf.data_ptr(), If.data_ptr(),
-                                Df.data_ptr(), stream.cuda_stream)
+        result["D"], result["I"], result["S"] = sh.search(q, k)
 
     for _ in range(args.warmup):
         step()
@@ -176,9 +165,10 @@ def main():
         }
     if rank == 0 and G == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"], out["recall@10"], out["parity"] = cpu_baseline_and_recall(
-            args, N, d, dtype, nq, k, local, torch, (D.cpu().numpy(), I.cpu().numpy()))
+            args, N, d, dtype, nq, k, local, torch, (result["D"].cpu().numpy(), result["I"].cpu().numpy()))
     if rank == 0:
         print(json.dumps(out), flush=True)
+    sh.close()
     if G > 1:
         dist.destroy_process_group()
 

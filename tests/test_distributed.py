@@ -1,0 +1,102 @@
+"""Multi-process (gloo, world_size 2, CPU) tests of the row-sharded search layer
+(photo_search_engine_amd/distributed.py): shard ranges, the all-gather, query broadcast, empty
+shards and k beyond a shard's rows.  The per-shard search and the merge are the CPU oracle here
+(checker only); on GPUs they are the HIP library (same ShardedFlatIndex code)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import oracle as O
+from photo_search_engine_amd.distributed import ShardedFlatIndex, shard_range
+from tests.oracle_index import OracleFlatIndex
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _oracle_local_search(index, q, k, row0):
+    metric = "ip" if index.metric_type == 0 else "l2"
+    S, I = O.knn_exact(index._x, q.numpy(), k, metric)
+    worst = -1.7976931348623157e308 if metric == "ip" else 1.7976931348623157e308
+    S = np.where(I >= 0, S, worst)
+    D = S.astype(np.float32)
+    D[I < 0] = -3.4028235e38 if metric == "ip" else 3.4028235e38
+    I = np.where(I >= 0, I + row0, -1)
+    return torch.from_numpy(S), torch.from_numpy(I), torch.from_numpy(D)
+
+
+def _oracle_merge(metric, Sg, Ig, k):
+    S, I = O.merge_topk(Sg.numpy(), Ig.numpy(), k, "ip" if metric == 0 else "l2")
+    D = S.astype(np.float32)
+    D[I < 0] = -3.4028235e38 if metric == 0 else 3.4028235e38
+    return torch.from_numpy(S), torch.from_numpy(I), torch.from_numpy(D)
+
+
+def _worker(rank, world, port, N, d, nq, k, metric, use_broadcast, outdir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        x = O.synth_rows(O.SEED_CORPUS, 0, N, d, True, "f32")
+        sh = ShardedFlatIndex(d, metric, index=OracleFlatIndex(d, metric),
+                              local_search=_oracle_local_search, merge=_oracle_merge)
+        row0, n = shard_range(N, rank, world)
+        sh.add_shard(x[row0:row0 + n], row0, N)
+        q = torch.from_numpy(O.synth_rows(O.SEED_QUERIES, 0, nq, d, True, "f32"))
+        if use_broadcast and rank != 0:
+            q = torch.zeros_like(q)  # rank 0's batch must arrive by broadcast
+        D, I, S = sh.search(q, k, src=0 if use_broadcast else None)
+        np.savez(os.path.join(outdir, f"r{rank}.npz"), D=D.numpy(), I=I.numpy(), S=S.numpy(), n=n)
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(tmp_path, N, d, nq, k, metric="ip", use_broadcast=False, world=2):
+    mp.spawn(_worker, args=(world, _free_port(), N, d, nq, k, metric, use_broadcast, str(tmp_path)), nprocs=world,
+             join=True)
+    outs = [np.load(tmp_path / f"r{r}.npz") for r in range(world)]
+    x = O.synth_rows(O.SEED_CORPUS, 0, N, d, True, "f32")
+    q = O.synth_rows(O.SEED_QUERIES, 0, nq, d, True, "f32")
+    Se, Ie = O.knn_exact(x, q, k, metric)
+    for o in outs:  # every rank holds the same, globally exact answer
+        np.testing.assert_array_equal(o["I"], Ie)
+        valid = Ie >= 0
+        np.testing.assert_array_equal(o["S"][valid], Se[valid])
+        np.testing.assert_array_equal(o["D"][valid], Se[valid].astype(np.float32))
+    return outs
+
+
+def test_shard_range_partitions_rows():
+    for N in (0, 1, 7, 1000, 10_000_001):
+        for world in (1, 2, 3, 8):
+            spans = [shard_range(N, r, world) for r in range(world)]
+            assert spans[0][0] == 0
+            assert sum(n for _, n in spans) == N
+            for (a0, an), (b0, _) in zip(spans, spans[1:]):
+                assert a0 + an == b0
+            assert max(n for _, n in spans) - min(n for _, n in spans) <= 1
+
+
+@pytest.mark.parametrize("metric", ["ip", "l2"])
+def test_two_rank_search_matches_single_index(tmp_path, metric):
+    outs = _run(tmp_path, N=1001, d=24, nq=5, k=12, metric=metric)
+    assert int(outs[0]["n"]) + int(outs[1]["n"]) == 1001
+
+
+def test_two_rank_query_broadcast(tmp_path):
+    _run(tmp_path, N=300, d=16, nq=3, k=7, use_broadcast=True)
+
+
+def test_two_rank_empty_shard_and_k_beyond_rows(tmp_path):
+    # N = 1: rank 0 owns no rows, rank 1 one row; k = 4 pads with id -1
+    outs = _run(tmp_path, N=1, d=8, nq=2, k=4)
+    assert (outs[0]["I"][:, 1:] == -1).all()
+    assert (outs[1]["I"][:, 0] == 0).all()

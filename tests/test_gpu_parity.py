@@ -216,3 +216,54 @@ def test_optimistic_seed_failure_falls_back_exactly(FlatIndex):
     ix.add(x)
     _check_exact(ix, O.round_dtype(q, "bf16"), k, "ip")
     assert ix.uncertified_count() > 0  # the optimistic pass was rejected (and then redone exactly)
+
+
+def test_device_shard_merge_matches_oracle(FlatIndex):
+    # 4 row shards searched separately (one shorter than k -> id -1 padding), merged on the device
+    import torch
+    from photo_search_engine_amd.index import merge_shards_device
+    d, k, nq = 48, 17, 33
+    bounds = [0, 5000, 5010, 9000, 12000]
+    x = O.synth_rows(O.SEED_CORPUS, 0, bounds[-1], d, True, "f32")
+    q = O.synth_rows(O.SEED_QUERIES, 0, nq, d, True, "f32")
+    Sg = np.empty((4, nq, k), dtype=np.float64)
+    Ig = np.empty((4, nq, k), dtype=np.int64)
+    for g in range(4):
+        ix = FlatIndex(d, "ip", "f32")
+        ix.add(x[bounds[g]:bounds[g + 1]])
+        Sd = torch.empty((nq, k), dtype=torch.float64, device="cuda")
+        Id = torch.empty((nq, k), dtype=torch.int64, device="cuda")
+        qd = torch.from_numpy(q).cuda()
+        ix.search_device(qd.data_ptr(), nq, k, None, Id.data_ptr(), Sd.data_ptr(), bounds[g],
+                         torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        Sg[g], Ig[g] = Sd.cpu().numpy(), Id.cpu().numpy()
+        ix.close()
+    assert (Ig[1][:, 10:] == -1).all()  # the 10-row shard pads
+    St, It = torch.from_numpy(Sg).cuda(), torch.from_numpy(Ig).cuda()
+    S = torch.empty((nq, k), dtype=torch.float64, device="cuda")
+    I = torch.empty((nq, k), dtype=torch.int64, device="cuda")
+    D = torch.empty((nq, k), dtype=torch.float32, device="cuda")
+    merge_shards_device(0, St.data_ptr(), It.data_ptr(), 4, nq, k, S.data_ptr(), I.data_ptr(), D.data_ptr(),
+                        torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    Sm, Im = O.merge_topk(Sg, Ig, k, "ip")
+    np.testing.assert_array_equal(I.cpu().numpy(), Im)
+    np.testing.assert_array_equal(S.cpu().numpy(), Sm)
+    Se, Ie = O.knn_exact(x, q, k, "ip")  # = one index over all rows
+    np.testing.assert_array_equal(I.cpu().numpy(), Ie)
+    np.testing.assert_array_equal(D.cpu().numpy(), Se.astype(np.float32))
+
+
+def test_sharded_index_single_process_matches_oracle():
+    import torch
+    from photo_search_engine_amd.distributed import ShardedFlatIndex
+    sh = ShardedFlatIndex(96, "l2", "bf16", device=0)
+    sh.add_synthetic(O.SEED_CORPUS, 30000, True)
+    q = torch.from_numpy(O.synth_rows(O.SEED_QUERIES, 0, 20, 96, True, "bf16")).cuda()
+    D, I, S = sh.search(q, 25)
+    x = sh.index.reconstruct_n(0, 30000)
+    Se, Ie = O.knn_exact(x, q.cpu().numpy(), 25, "l2")
+    np.testing.assert_array_equal(I.cpu().numpy(), Ie)
+    np.testing.assert_array_equal(S.cpu().numpy(), Se)
+    sh.close()
