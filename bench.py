@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--cpu-sample-rows", type=int, default=0,
                     help="rows of the corpus the CPU baseline scans (default: the whole corpus if host memory allows)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--zero-corpus", action="store_true",
+                    help="diagnostic only: all-zero corpus rows (DVFS/power test with VS_MF_ABLATE=9; results meaningless)")
     ap.add_argument("--traffic-file", default=os.path.join(REPO, "profiles", "traffic_cfg3.json"))
     return ap.parse_args()
 
@@ -79,7 +81,15 @@ def main():
     t_build = time.time()
     # the product's multi-GPU layer: one row shard per rank, all-gather + device merge (G > 1)
     sh = ShardedFlatIndex(d, "ip", dtype, device=local)
-    sh.add_synthetic(SEED_CORPUS, N, True)
+    if args.zero_corpus:
+        zeros = torch.zeros((1 << 20, d), dtype=torch.float32, device=dev)
+        sh.row0, sh.n_total = row0, N
+        for r in range(0, n_local, zeros.shape[0]):
+            m = min(zeros.shape[0], n_local - r)
+            sh.index.add_device(zeros.data_ptr(), m, torch.cuda.current_stream(dev).cuda_stream)
+        del zeros
+    else:
+        sh.add_synthetic(SEED_CORPUS, N, True)
     ix = sh.index
     q = torch.empty((nq, d), dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev)
@@ -188,9 +198,11 @@ def cpu_baseline_and_recall(args, N, d, dtype, nq, k, local, torch, gpu_full):
     from photo_search_engine_amd.index import FlatIndex
 
     ns = args.cpu_sample_rows or N
-    mem = _host_mem_bytes()
-    if mem and ns * d * 4 > 0.4 * mem:  # keep the fp32 copy well inside host memory
-        ns = int(0.4 * mem // (d * 4))
+    # keep the fp32 copy well inside host memory: 40% of the machine, and never above 96 GiB (the
+    # GPU box caps a command's host memory well below the machine's total)
+    budget = min(0.4 * (_host_mem_bytes() or 1 << 40), 96 * (1 << 30))
+    if ns * d * 4 > budget:
+        ns = int(budget // (d * 4))
     ns = min(ns, N)
     cores = len(os.sched_getaffinity(0))
     threads = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores) or cores))

@@ -81,11 +81,11 @@ struct DevBuf {
 // per-call execution context: stream + workspace (pooled; one per concurrent search)
 struct Ctx {
     hipStream_t stream = nullptr;
-    DevBuf qdev, qtile, qinfo, qpad, cand, part, merge_a, merge_b, outD, outI, outS, cert, thr0, seedmax;
+    DevBuf qdev, qtile, qinfo, qpad, cand, part, merge_a, merge_b, outD, outI, outS, cert, thr0, seedmax, gcnt;
     std::vector<int> cert_host;
     ~Ctx() {
         for (DevBuf* b : {&qdev, &qtile, &qinfo, &qpad, &cand, &part, &merge_a, &merge_b, &outD, &outI, &outS, &cert, &thr0,
-                          &seedmax})
+                          &seedmax, &gcnt})
             b->release();
         if (stream) hipStreamDestroy(stream);
     }
@@ -232,7 +232,9 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
         a.cap = MFMA_CAP;
         a.G = (int)std::min<int64_t>(tiles, ix->num_cu);
         c->qtile.ensure((size_t)MFMA_QB * ix->dpad * 2);
-        HIP_CHECK(launch_pack_qtile(ix->dtype, q, nqb, ix->d, ix->dpad, c->qtile.as<uint8_t>(), c->qinfo.as<float>(), st));
+        c->gcnt.ensure(sizeof(int) * MFMA_QB);
+        HIP_CHECK(launch_pack_qtile(ix->dtype, q, nqb, ix->d, ix->dpad, c->qtile.as<uint8_t>(), c->qinfo.as<float>(),
+                                    c->gcnt.as<int>(), st));
     } else {
         QB = nqb <= 1 ? 1 : nqb <= 2 ? 2 : nqb <= 4 ? 4 : 8;
         a.cap = (int)round_up(Kp + 2 * TR, 256);
@@ -242,9 +244,14 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
     }
     a.G = std::max(a.G, 1);
     c->cand.ensure((size_t)a.G * QB * a.cap * sizeof(u64));
-    c->part.ensure((size_t)a.G * QB * Kp * sizeof(u64));
+    c->part.ensure((size_t)a.G * QB * Kp * sizeof(u64));  // GEMV: [G][QB][Kp]; MFMA: [QB][G*Kp] survivor lists
     a.cand = c->cand.as<u64>();
     a.part = c->part.as<u64>();
+    if (use_mfma) {
+        a.glist = c->part.as<u64>();
+        a.gcnt = c->gcnt.as<int>();
+        a.lcap = a.G * Kp;
+    }
 
     // merge partial lists [nseg][qstride][Kp] down to one list per query; returns it
     auto merge_all = [&](const u64* src, int nseg, int qstride) -> const u64* {
@@ -273,6 +280,7 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
     bool optimistic = false;
     if (use_mfma && tiles >= 4 * (int64_t)a.G) {
         ScreenArgs sa = a;
+        sa.G = std::min(sa.G, 512);  // k_seed_select holds up to 8192 maxima per query
         sa.tile_stride = (int)(tiles / sa.G);
         const int M = sa.G * 16;
         c->seedmax.ensure(sizeof(float) * MFMA_QB * M);
@@ -305,6 +313,15 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
         HIP_CHECK(hipMemsetAsync(dbg, 0, 16 * sizeof(unsigned), st));
         a.dbg = dbg;
     }
+    // diagnostic: VS_MF_STAMPS=1 runs the stamped build of the main screen (VS_MF_ABLATE=15) and
+    // prints per-phase cycles per K-step for loader (0-3) and writer (4-7) waves
+    static const bool stamps_on = getenv("VS_MF_STAMPS") != nullptr;
+    unsigned long long* stamps = nullptr;
+    if (stamps_on && use_mfma) {
+        HIP_CHECK(hipMalloc(&stamps, sizeof(unsigned long long) * a.G * 8 * 6));
+        HIP_CHECK(hipMemsetAsync(stamps, 0, sizeof(unsigned long long) * a.G * 8 * 6, st));
+        a.stamps = stamps;
+    }
     if (use_mfma) HIP_CHECK(launch_screen_mfma(ix->dtype, a, c->qtile.as<uint8_t>(), nqb, st));
     else HIP_CHECK(launch_screen_gemv(ix->dtype, a, c->qpad.as<float>(), nqb, QB, st));
     if (dbg) {
@@ -316,16 +333,42 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
         hipFree(dbg);
         a.dbg = nullptr;
     }
+    if (stamps) {
+        std::vector<unsigned long long> h((size_t)a.G * 8 * 6);
+        HIP_CHECK(hipMemcpyAsync(h.data(), stamps, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+        const double steps = (double)((tiles + a.G - 1) / a.G) * (ix->dpad / CH);
+        const double tiles_per_wg = (double)((tiles + a.G - 1) / a.G);
+        double acc[2][6] = {};
+        for (int b = 0; b < a.G; ++b)
+            for (int w = 0; w < 8; ++w)
+                for (int i = 0; i < 6; ++i) acc[w >= 4][i] += (double)h[((size_t)b * 8 + w) * 6 + i];
+        for (int r = 0; r < 2; ++r) {
+            const double n = 4.0 * a.G;
+            fprintf(stderr, "[vs stamps] %s waves, cycles per K-step: barrier %.0f dma %.0f reads+mfma %.0f tail %.0f "
+                    "| per tile-end step: tail %.0f | total loop per K-step %.0f\n", r ? "writer" : "loader",
+                    acc[r][0] / n / steps, acc[r][1] / n / steps, acc[r][2] / n / steps,
+                    acc[r][5] / n / (steps - tiles_per_wg), acc[r][3] / n / tiles_per_wg, acc[r][4] / n / steps);
+        }
+        hipFree(stamps);
+        a.stamps = nullptr;
+    }
     if (timing) {
         HIP_CHECK(hipEventRecord(e1, st));
         std::lock_guard<std::mutex> g(ix->tmtx);
         ix->tev.emplace_back(e0, e1);
         ix->last_kernel_kind = use_mfma ? 1 : 2;
     }
-    const u64* cur = merge_all(a.part, a.G, QB);
-    // refine expects cand[q*Kp + j] (qstride == nqb) or part[0][q][Kp] (qstride QB, same row offset)
     RefineArgs r{};
-    r.cand = cur;
+    if (use_mfma) {  // the refine selects the best Kp of each query's survivor list itself
+        r.cand = a.glist;
+        r.cand_n = a.gcnt;
+        r.lcap = a.lcap;
+    } else {  // GEMV: merge the per-block lists down to [q][Kp] (qstride nqb, or part[0] with QB)
+        r.cand = merge_all(a.part, a.G, QB);
+        r.cand_n = nullptr;
+        r.lcap = Kp;
+    }
     r.Kp = Kp;
     r.q = q;
     r.d = ix->d;

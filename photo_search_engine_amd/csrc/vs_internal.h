@@ -49,6 +49,10 @@ struct ScreenArgs {
     const u64* thr0;         // [QB] initial per-query key threshold (keys > thr0 kept), or null
     unsigned* dbg;           // debug counters (VS_MF_STATS): inserts, slow paths, compactions, overflows
     float* seedmax;          // seed pass only: [QB][G*16] maxima of disjoint 16-row groups per query
+    u64* glist;              // MFMA path output: per-query compact survivor list [QB][lcap] ...
+    int* gcnt;               // ... with its length per query (zeroed by k_pack_qtile)
+    int lcap;                // = G * Kp
+    unsigned long long* stamps;  // diagnostic build only (VS_MF_STAMPS): [G][8 waves][5] phase cycles
 };
 
 // ---- launchers (vs_kernels.hip) -------------------------------------------------------------
@@ -65,7 +69,7 @@ hipError_t launch_gather_rows(int dt, const uint8_t* data, const int64_t* ids, i
 
 // queries: MFMA tile (dtype, [nks][256][32]) or fp32 padded [NQ][dpad]; qinfo[q*2] = ||q_hat||,
 // qinfo[q*2+1] = ||q_hat - q|| (upper bounds, fp32)
-hipError_t launch_pack_qtile(int dt, const float* q, int nqb, int d, int dpad, uint8_t* qt, float* qinfo,
+hipError_t launch_pack_qtile(int dt, const float* q, int nqb, int d, int dpad, uint8_t* qt, float* qinfo, int* gcnt,
                              hipStream_t st);
 hipError_t launch_pack_qf32(const float* q, int nqb, int nqpad, int d, int dpad, float* qp, float* qinfo,
                             hipStream_t st);
@@ -78,7 +82,9 @@ hipError_t launch_merge(const u64* in, int nseg, int qstride, int nq, int Kp, u6
                         hipStream_t st);
 
 struct RefineArgs {
-    const u64* cand;       // [nq][Kp] (qstride = nq)
+    const u64* cand;       // [nq][lcap] candidate keys: the first cand_n[q] (or, if cand_n is null,
+    const int* cand_n;     //  the first Kp, zero = empty) of each row; the refine keeps the best Kp
+    int lcap;
     int Kp;
     const float* q;        // [nq][d] fp32 (original queries)
     int d, dpad, dt, metric;
@@ -97,10 +103,6 @@ struct RefineArgs {
     int optimistic;        // screened with an optimistic seed: fewer than Kp candidates = uncertified
 };
 hipError_t launch_refine(const RefineArgs& a, int nq, hipStream_t st);
-// thr0[q] = (list q holds Kp keys) ? min key - 1 : 0   -- a valid lower bound for the final
-// Kp-th key, because the list is the exact top-Kp of a SUBSET of the rows
-// rank > 0: OPTIMISTIC seed = the rank-th best sample key (not a proven bound; the refine kernel's
-// certificate then rejects any query left with fewer than Kp candidates)
 // seed pass: screen one tile per workgroup (tile_stride) and write per-query 16-row-group maxima
 hipError_t launch_seed_mfma(int dt, const ScreenArgs& a, const uint8_t* qt, int nqb, hipStream_t st);
 // thr0[q] = key just below the rank-th largest of the M group maxima of query q (0 if none)

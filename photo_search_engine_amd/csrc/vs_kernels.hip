@@ -400,10 +400,12 @@ __global__ void __launch_bounds__(256) k_gather_rows(const uint8_t* __restrict__
 // rounded up to fp32.
 template <int DT>
 __global__ void __launch_bounds__(256) k_pack_qtile(const float* __restrict__ q, int nqb, int d, int dpad,
-                                                     uint8_t* __restrict__ qt, float* __restrict__ qinfo) {
+                                                     uint8_t* __restrict__ qt, float* __restrict__ qinfo,
+                                                     int* __restrict__ gcnt) {
     const int lane = threadIdx.x & 63;
     const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= MFMA_QB) return;
+    if (gcnt && lane == 0) gcnt[r] = 0;  // survivor-list lengths of the screen that follows
     double n2 = 0.0, e2 = 0.0;
     for (int i = lane; i < dpad; i += 64) {
         float v = (r < nqb && i < d) ? q[(int64_t)r * d + i] : 0.0f;
@@ -462,7 +464,8 @@ constexpr int MF_SLOTS = 4;
 constexpr int MF_DEPTH = MF_SLOTS - 1;
 constexpr int MF_THREADS = 512;
 constexpr int MF_POOL = 512;  // LDS insert pool of the loader waves (flushed by the writer waves)
-constexpr int MF_SEED_MODE = 20;  // k_screen_mfma MODE of the threshold-seed pass
+constexpr int MF_SEED_MODE = 20;   // k_screen_mfma MODE of the threshold-seed pass
+constexpr int MF_STAMP_MODE = 15;  // diagnostic: production + per-phase cycle stamps (VS_MF_STAMPS)
 constexpr int MF_SX = 8 * 64 * 8 * 4;  // per-wave insert staging: 64 lanes x 8 fp32 (slow path only)
 constexpr int MF_LDS = MF_SLOTS * MF_SLOT + 256 * 8 + 256 * 4 + 256 * 4 + 16 + MF_POOL * 8 + MF_POOL * 4 + MF_SX;
 static_assert(MF_LDS <= 160 * 1024, "LDS budget");
@@ -515,6 +518,25 @@ __device__ __forceinline__ void mf_stage(const uint8_t* __restrict__ gA, const u
     }
 }
 
+// balanced stage issue: waves 0-3 the 4 corpus pieces, waves 4-7 the 4 query pieces (4 LDS-DMA
+// instructions per wave per stage; counted waits use 4 per stage on every wave)
+template <bool NT>
+__device__ __forceinline__ void mf_stage_bal(const uint8_t* __restrict__ gA, const uint8_t* __restrict__ gB,
+                                             uint32_t slot_base, int tid) {
+    const int w = tid >> 6, lane = tid & 63;
+    const int wq = w & 3;
+    const uint32_t base = __builtin_amdgcn_readfirstlane(slot_base + (uint32_t)(wq * 64 * 16) + (w >= 4 ? 16384u : 0u));
+    const uint8_t* src0 = w >= 4 ? gB : gA;
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+        const int g = it * 256 + wq * 64 + lane;
+        const int row = g >> 2, pos = g & 3;
+        const int src = (row << 2) + (pos ^ mf_swz(row));
+        if (NT && w < 4) glds16_nt(src0 + (size_t)src * 16, base + it * 256 * 16);
+        else glds16(src0 + (size_t)src * 16, base + it * 256 * 16);
+    }
+}
+
 // piece g (0..3) of a stage for loader waves: 1 corpus + 1 query LDS-DMA instruction
 template <bool NT = false>
 __device__ __forceinline__ void mf_stage_piece(const uint8_t* __restrict__ gA, const uint8_t* __restrict__ gB,
@@ -531,7 +553,7 @@ __device__ __forceinline__ void mf_stage_piece(const uint8_t* __restrict__ gA, c
 template <bool BAR, bool HALF = false>
 __device__ __forceinline__ void mf_wait_barrier(int ahead, bool loader) {
     if constexpr (BAR) {
-        if (!loader) {
+        if (!loader && !HALF) {
             asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         } else if constexpr (HALF) {
             if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -662,19 +684,24 @@ __device__ __forceinline__ void mf_wave_compact(u64* __restrict__ buf, int n, in
 //   13 = 0 with compare-only epilogue (no inserts, no check) | 14 = 0 without the deferred check/pool flush
 template <int DT, int METRIC, int MODE>
 __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
-    constexpr bool LOADS = (MODE != 1 && MODE < 3) || (MODE >= 6 && MODE != 12);  // (incl. the seed mode)
+    constexpr bool LOADS = (MODE != 1 && MODE < 3) || (MODE >= 6 && MODE != 12);  // (incl. seed, stamps)
     constexpr bool MATH = (MODE != 2 && MODE < 6) || MODE == 9 || MODE == 10 || MODE == 13 || MODE == 14 ||
-                          MODE == MF_SEED_MODE;
+                          MODE == MF_SEED_MODE || MODE == MF_STAMP_MODE || MODE == 16 || MODE == 17;
     constexpr bool PP = MODE == 11 || MODE == 12;  // ping-pong: waves 4-7 half a K-step behind waves 0-3
     constexpr bool SEED = MODE == MF_SEED_MODE;  // threshold-seed pass: group maxima only
-    constexpr bool EPI = MODE < 3 || MODE == 13 || MODE == 14 || SEED;
+    constexpr bool EPI = MODE < 3 || MODE == 13 || MODE == 14 || SEED || MODE == MF_STAMP_MODE || MODE == 16 ||
+                         MODE == 17;
     constexpr bool INS = MODE != 13;   // threshold passes insert candidates
     constexpr bool CHECK = MODE != 13 && MODE != 14;  // deferred compaction check + pool flush
-    constexpr bool BAR = MODE < 4 || MODE >= 6;
-    constexpr bool READS = MODE < 5 || MODE == 9 || MODE == 10 || MODE == 13 || MODE == 14 || MODE == MF_SEED_MODE;
+    constexpr bool BAR = MODE < 4 || MODE >= 6;  // (incl. seed, stamps)
+    constexpr bool READS = MODE < 5 || MODE == 9 || MODE == 10 || MODE == 13 || MODE == 14 || MODE == MF_SEED_MODE ||
+                           MODE == MF_STAMP_MODE || MODE == 16 || MODE == 17;
     constexpr bool QLOAD = MODE != 7;
     constexpr bool NT = MODE == 8 || MODE == 0 || MODE >= 9;
     constexpr bool IL = MODE == 10;  // DMA issue interleaved with the MFMAs (ablation: slower)
+    constexpr bool STAMP = MODE == MF_STAMP_MODE;  // = production + per-phase s_memtime stamps
+    constexpr bool BAL = MODE == 16;               // balanced DMA issue (4 per wave on all 8 waves)
+    constexpr bool PAIR = MODE == 17;              // one barrier per 2 K-steps (needs an even K-step count)
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     u64* thr_key = (u64*)(smem + MF_SLOTS * MF_SLOT);
     float* thr_f = (float*)(smem + MF_SLOTS * MF_SLOT + 256 * 8);
@@ -728,20 +755,43 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
 
     // prologue: stages 0 .. DEPTH-1
     int iti = t0, iks = 0;  // (tile, k-step) of the next stage to issue
-    for (int j = 0; j < MF_DEPTH && j < S; ++j) {
-        if constexpr (LOADS)
+    for (int j = 0; j < (PAIR ? 2 : MF_DEPTH) && j < S; ++j) {
+        if constexpr (BAL)
+            mf_stage_bal<NT>(a.corpus + (int64_t)iti * tbytes + (int64_t)iks * 16384, qt + (int64_t)iks * 16384,
+                             ring + (uint32_t)(j * MF_SLOT), tid);
+        else if constexpr (LOADS)
             mf_stage<QLOAD, NT>(a.corpus + (int64_t)iti * tbytes + (int64_t)iks * 16384, qt + (int64_t)iks * 16384,
                                 ring + (uint32_t)(j * MF_SLOT), tid);
         if (++iks == nks) { iks = 0; ++iti; }
     }
     if constexpr (!BAR) mf_barrier_drain();
+    int pti = iti, pks = iks;  // PAIR mode: next stage to issue
     int ti = t0, ks = 0;
     float sink = 0.0f;
     bool check_pending = false;
     uint4 pf_a[4], pf_b[8];
+    // stamps: barrier, DMA issue, reads+MFMA, tail of tile-end steps, total, tail of other steps
+    uint64_t ph[6] = {0, 0, 0, 0, 0, 0}, tl = 0;
+    bool tile_end = false;
+    if constexpr (STAMP) tl = __builtin_amdgcn_s_memtime();
     for (int s = 0; s < S; ++s) {
         const int left = S - 1 - s;
-        mf_wait_barrier<BAR, !QLOAD>(left < MF_DEPTH - 1 ? left : MF_DEPTH - 1, wid < 4);
+        uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+        if constexpr (STAMP) {
+            __builtin_amdgcn_sched_barrier(0);
+            t0 = __builtin_amdgcn_s_memtime();
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (PAIR) {
+            if ((s & 1) == 0) mf_barrier_drain();  // this pair's two stages landed, previous pair read
+        } else {
+            mf_wait_barrier<BAR, !QLOAD || BAL>(left < MF_DEPTH - 1 ? left : MF_DEPTH - 1, wid < 4 || BAL);
+        }
+        if constexpr (STAMP) {
+            __builtin_amdgcn_sched_barrier(0);
+            t1 = __builtin_amdgcn_s_memtime();
+            __builtin_amdgcn_sched_barrier(0);
+        }
         const bool do_issue = s + MF_DEPTH < S;
         const uint8_t* nA = a.corpus + (int64_t)iti * tbytes + (int64_t)iks * 16384;
         const uint8_t* nB = qt + (int64_t)iks * 16384;
@@ -763,12 +813,36 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
         } else if constexpr (IL) {
             mf_compute_il<DT, NT>(smem + (s % MF_SLOTS) * MF_SLOT, acc, wm, wn, lane_off, do_issue && wid < 4, nA, nB,
                                   nslot, wid, lane);
+        } else if constexpr (PAIR) {
+            if ((s & 1) == 0) {  // the next pair's two stages, into the slots the previous pair used
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                    if (s + 2 + h < S) {
+                        mf_stage<true, NT>(a.corpus + (int64_t)pti * tbytes + (int64_t)pks * 16384,
+                                           qt + (int64_t)pks * 16384,
+                                           ring + (uint32_t)(((s + 2 + h) % MF_SLOTS) * MF_SLOT), tid);
+                        if (++pks == nks) { pks = 0; ++pti; }
+                    }
+            }
+            mf_compute<DT, true>(smem + (s % MF_SLOTS) * MF_SLOT, acc, wm, wn, lane_off);
         } else {
             if (do_issue) {
-                if constexpr (LOADS) mf_stage<QLOAD, NT>(nA, nB, nslot, tid);
+                if constexpr (BAL) mf_stage_bal<NT>(nA, nB, nslot, tid);
+                else if constexpr (LOADS) mf_stage<QLOAD, NT>(nA, nB, nslot, tid);
+            }
+            if constexpr (STAMP) {
+                __builtin_amdgcn_sched_barrier(0);
+                t2 = __builtin_amdgcn_s_memtime();
+                __builtin_amdgcn_sched_barrier(0);
             }
             if constexpr (MATH) mf_compute<DT, READS>(smem + (s % MF_SLOTS) * MF_SLOT, acc, wm, wn, lane_off);
+            if constexpr (STAMP) {
+                __builtin_amdgcn_sched_barrier(0);
+                t3 = __builtin_amdgcn_s_memtime();
+                __builtin_amdgcn_sched_barrier(0);
+            }
         }
+        if constexpr (STAMP) tile_end = ks == nks - 1;
         if (ks == nks - 1) {
             if constexpr (!EPI) {
 #pragma unroll
@@ -936,6 +1010,20 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
             }
         }
         if (++ks == nks) { ks = 0; ++ti; }
+        if constexpr (STAMP) {
+            __builtin_amdgcn_sched_barrier(0);
+            const uint64_t t4 = __builtin_amdgcn_s_memtime();
+            __builtin_amdgcn_sched_barrier(0);
+            ph[0] += t1 - t0;
+            ph[1] += t2 - t1;
+            ph[2] += t3 - t2;
+            ph[tile_end ? 3 : 5] += t4 - t3;
+        }
+    }
+    if constexpr (STAMP) {
+        ph[4] = __builtin_amdgcn_s_memtime() - tl;
+        if (lane == 0 && a.stamps)
+            for (int i = 0; i < 6; ++i) a.stamps[((size_t)blk * 8 + wid) * 6 + i] = ph[i];
     }
     if constexpr (PP) {
         if (wid >= 4 && S > 0) mf_mfma<DT, 2, 4>(pf_a, pf_b, acc);
@@ -963,15 +1051,20 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
         }
     }
     mf_barrier_drain();
-    for (int q = wid; q < MFMA_QB; q += 8) {
-        u64* pq = a.part + ((size_t)blk * MFMA_QB + q) * a.Kp;
-        int n = q < nqb ? cnt[q] : 0;
+    // survivors (the workgroup's best <= Kp per query) appended to the query's compact list
+    for (int q = wid; q < nqb; q += 8) {
+        int n = cnt[q];
         if (n > a.cap) n = a.cap;
         if (n > a.Kp) {
             mf_wave_compact<MFMA_CAP / 64>(cand + (size_t)q * a.cap, n, a.Kp, &thr_key[q], &thr_f[q], lane);
             n = a.Kp;
         }
-        for (int j = lane; j < a.Kp; j += 64) pq[j] = j < n ? cand[(size_t)q * a.cap + j] : 0ull;
+        if (n == 0) continue;
+        int off = 0;
+        if (lane == 0) off = atomicAdd(&a.gcnt[q], n);
+        off = __shfl(off, 0, 64);
+        u64* dst = a.glist + (size_t)q * a.lcap + off;
+        for (int j = lane; j < n; j += 64) dst[j] = cand[(size_t)q * a.cap + j];
     }
 }
 
@@ -1154,36 +1247,60 @@ __global__ void __launch_bounds__(256) k_merge(const u64* __restrict__ in, int n
 // ------------------------------------------------------------------------------------------------
 // K5: exact refine -- canonical fp64 rescoring, sort, certificate, faiss-layout output
 // ------------------------------------------------------------------------------------------------
-template <int DT>
-__device__ __forceinline__ double exact_score(const uint8_t* __restrict__ corpus, int64_t row,
-                                              const float* __restrict__ q, int d, int dpad, int metric, int lane) {
+__device__ __forceinline__ bool better_exact(double sa, uint32_t ia, double sb, uint32_t ib, int metric) {
+    if (sa != sb) return metric == METRIC_IP ? (sa > sb) : (sa < sb);
+    return ia < ib;
+}
+
+// Exact canonical fp64 score of one stored row, query staged in LDS as fp64 (QLDS) or read from
+// global fp32.  Lane l owns 8-element groups g = l, l+64, ... in ascending order and accumulates
+// them sequentially; RU groups are loaded before any is consumed (independent gathers in flight).
+// The expression tree is the oracle's orc_canon_scores (oracle/vs_oracle.c), so scores are equal.
+template <int DT, int METRIC, bool QLDS>
+__device__ __forceinline__ double exact_score_q(const uint8_t* __restrict__ corpus, int64_t row,
+                                                const double* __restrict__ qs, const float* __restrict__ qg, int d,
+                                                int dpad, int lane) {
 #pragma clang fp contract(off)
     constexpr int ES = DT == DT_F32 ? 4 : 2;
+    constexpr int NV = DT == DT_F32 ? 2 : 1;  // 16 B vectors per 8-element group
+    constexpr int RU = 4;
     const uint8_t* rb = corpus + (row / TR) * (int64_t)TR * dpad * ES + (row % TR) * (CH * ES);
+    const int ng = (d + 7) >> 3;
     double acc = 0.0;
-    for (int g = lane; 8 * g < d; g += 64) {
-        const int e0 = 8 * g;
-        const uint8_t* p = rb + (int64_t)(e0 >> 5) * TR * CH * ES + (e0 & 31) * ES;
-        float xv[8];
-        if constexpr (DT == DT_F32) {
-            unpack16<DT>(*(const uint4*)p, xv);
-            unpack16<DT>(*(const uint4*)(p + 16), xv + 4);
-        } else {
-            unpack16<DT>(*(const uint4*)p, xv);
+    for (int g0 = lane; g0 < ng; g0 += 64 * RU) {
+        uint4 raw[RU][NV];
+#pragma unroll
+        for (int u = 0; u < RU; ++u) {
+            const int g = g0 + 64 * u;
+            if (g < ng) {
+                const int e0 = 8 * g;
+                const uint8_t* p = rb + (int64_t)(e0 >> 5) * TR * CH * ES + (e0 & 31) * ES;
+#pragma unroll
+                for (int v = 0; v < NV; ++v) raw[u][v] = *(const uint4*)(p + 16 * v);
+            }
         }
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const int i = e0 + e;
-            if (i < d) {
-                const double x = (double)xv[e];
-                const double qq = (double)q[i];
-                if (metric == METRIC_IP) {
-                    const double pr = x * qq;
-                    acc = acc + pr;
-                } else {
-                    const double dl = x - qq;
-                    const double pr = dl * dl;
-                    acc = acc + pr;
+        for (int u = 0; u < RU; ++u) {
+            const int g = g0 + 64 * u;
+            if (g < ng) {
+                float xv[8];
+#pragma unroll
+                for (int v = 0; v < NV; ++v) unpack16<DT>(raw[u][v], xv + 4 * v);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const int i = 8 * g + e;
+                    if (i < d) {
+                        const double x = (double)xv[e];
+                        const double qq = QLDS ? qs[i] : (double)qg[i];
+                        if constexpr (METRIC == METRIC_IP) {
+                            const double pr = x * qq;
+                            acc = acc + pr;
+                        } else {
+                            const double dl = x - qq;
+                            const double pr = dl * dl;
+                            acc = acc + pr;
+                        }
+                    }
                 }
             }
         }
@@ -1196,36 +1313,53 @@ __device__ __forceinline__ double exact_score(const uint8_t* __restrict__ corpus
     return acc;
 }
 
-__device__ __forceinline__ bool better_exact(double sa, uint32_t ia, double sb, uint32_t ib, int metric) {
-    if (sa != sb) return metric == METRIC_IP ? (sa > sb) : (sa < sb);
-    return ia < ib;
-}
+constexpr int RF_THREADS = 1024;  // 16 waves per query: Kp / 16 candidates per wave
+constexpr int RF_E = 16;          // candidate keys per thread held in registers for the selection
 
-template <int DT>
-__global__ void __launch_bounds__(256) k_refine(RefineArgs a, int KP2) {
+template <int DT, int METRIC, bool QLDS>
+__global__ void __launch_bounds__(RF_THREADS) k_refine(RefineArgs a, int KP2) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     double* sc = (double*)smem;
     uint32_t* ids = (uint32_t*)(smem + (size_t)KP2 * 8);
+    double* qs = (double*)(smem + (((size_t)KP2 * 12 + 7) & ~(size_t)7));  // 8-B aligned
     __shared__ int nv_s;
     __shared__ u64 minkey_s;
     __shared__ double qq_s;
+    __shared__ int red[RF_THREADS / 64];
     const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const u64* cq = a.cand + (size_t)q * a.Kp;
+    constexpr int NW = RF_THREADS / 64;
+    // the best Kp keys of the candidate list, compacted into LDS (cq)
+    u64* cq = (u64*)(smem + (((size_t)KP2 * 12 + 7) & ~(size_t)7) + (QLDS ? (size_t)a.d * 8 : 0));
+    const u64* src = a.cand + (size_t)q * a.lcap;
+    const int n = a.cand_n ? min(a.cand_n[q], a.lcap) : a.Kp;
     const float* qv = a.q + (int64_t)q * a.d;
     if (tid == 0) {
         nv_s = 0;
         minkey_s = ~0ull;
     }
+    if constexpr (QLDS)
+        for (int i = tid; i < a.d; i += RF_THREADS) qs[i] = (double)qv[i];
+    int nkept;
+    if (n <= RF_THREADS * RF_E) {
+        u64 keys[RF_E];
+#pragma unroll
+        for (int e = 0; e < RF_E; ++e) {
+            const int j = tid + RF_THREADS * e;
+            keys[e] = j < n ? src[j] : 0ull;
+        }
+        const u64 t = n > a.Kp ? block_kth<RF_E>(keys, a.Kp, red) : 1ull;
+        nkept = block_write_kept<RF_E>(keys, t, cq, red);
+    } else {  // very long lists (unseeded screens of many workgroups): selection from memory
+        const u64 t = block_kth_mem(src, n, a.Kp, red);
+        nkept = block_compact_mem(src, cq, n, t, red);
+    }
     __syncthreads();
-    // candidates are compacted (non-empty first)
     int myv = 0;
     u64 mymin = ~0ull;
-    for (int j = tid; j < a.Kp; j += 256) {
+    for (int j = tid; j < nkept; j += RF_THREADS) {
         const u64 k = cq[j];
-        if (k != 0ull) {
-            ++myv;
-            mymin = k < mymin ? k : mymin;
-        }
+        ++myv;
+        mymin = k < mymin ? k : mymin;
     }
     myv = wave_sum_i(myv);
     mymin = wave_min_u64(mymin);
@@ -1242,19 +1376,16 @@ __global__ void __launch_bounds__(256) k_refine(RefineArgs a, int KP2) {
     }
     __syncthreads();
     const int nv = nv_s;
-    for (int j = wid; j < nv; j += 4) {
+    for (int j = wid; j < nv; j += NW) {
         const uint32_t id = key_id(cq[j]);
-        double s;
-        if (a.dt == DT_F32) s = exact_score<DT_F32>(a.corpus, id, qv, a.d, a.dpad, a.metric, lane);
-        else if (a.dt == DT_BF16) s = exact_score<DT_BF16>(a.corpus, id, qv, a.d, a.dpad, a.metric, lane);
-        else s = exact_score<DT_F16>(a.corpus, id, qv, a.d, a.dpad, a.metric, lane);
+        const double s = exact_score_q<DT, METRIC, QLDS>(a.corpus, id, qs, qv, a.d, a.dpad, lane);
         if (lane == 0) {
             sc[j] = s;
             ids[j] = id;
         }
     }
-    const double worst = a.metric == METRIC_IP ? -INFINITY : INFINITY;
-    for (int j = nv + tid; j < KP2; j += 256) {
+    const double worst = METRIC == METRIC_IP ? -INFINITY : INFINITY;
+    for (int j = nv + tid; j < KP2; j += RF_THREADS) {
         sc[j] = worst;
         ids[j] = 0xFFFFFFFFu;
     }
@@ -1262,13 +1393,13 @@ __global__ void __launch_bounds__(256) k_refine(RefineArgs a, int KP2) {
     // bitonic sort, best first
     for (int size = 2; size <= KP2; size <<= 1) {
         for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int i = tid; i < KP2; i += 256) {
+            for (int i = tid; i < KP2; i += RF_THREADS) {
                 const int j = i ^ stride;
                 if (j > i) {
                     const bool up = (i & size) == 0;
                     const double si = sc[i], sj = sc[j];
                     const uint32_t ii = ids[i], ij = ids[j];
-                    const bool jb = better_exact(sj, ij, si, ii, a.metric);
+                    const bool jb = better_exact(sj, ij, si, ii, METRIC);
                     if (up ? jb : !jb) {
                         sc[i] = sj; sc[j] = si;
                         ids[i] = ij; ids[j] = ii;
@@ -1298,7 +1429,7 @@ __global__ void __launch_bounds__(256) k_refine(RefineArgs a, int KP2) {
         if (a.cert) a.cert[q] = cert;
         if (!cert && a.uncert) atomicAdd(a.uncert, 1u);
     }
-    for (int j = tid; j < a.k; j += 256) {
+    for (int j = tid; j < a.k; j += RF_THREADS) {
         const size_t o = (size_t)q * a.k + j;
         if (j < nv) {
             if (a.D) a.D[o] = (float)sc[j];
@@ -1316,36 +1447,72 @@ __global__ void __launch_bounds__(256) k_refine(RefineArgs a, int KP2) {
 // has `rank` DISTINCT rows scoring >= T, so T never exceeds the true rank-th best screen score and
 // the key just below every score >= T, (ord(T) << 32) | 0, is a valid starting threshold
 // (rank = Kp: proven; rank < Kp: optimistic, checked by the refine certificate).
-constexpr int SEED_VPT = 32;  // values per thread: up to 256 * 32 = 8192 maxima per query
-__global__ void __launch_bounds__(256) k_seed_select(const float* __restrict__ seedmax, int M, int rank,
+// 8-bit radix select, one 256-thread block per query, maxima held in registers (VPT per thread):
+// four rounds of (LDS histogram of the next digit among values matching the prefix so far, one
+// wave scans the 256 bins from the top) give the exact rank-th largest orderable value.
+constexpr int SEED_VPT = 16;  // up to 256 * 16 = 4096 maxima per query (2x / 4x variants below)
+template <int VPT>
+__global__ void __launch_bounds__(256) k_seed_select(const float* __restrict__ seedmax, int M, int nq, int rank,
                                                      u64* __restrict__ thr0) {
-    __shared__ int part[4];
-    const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    uint32_t v[SEED_VPT];
+    __shared__ unsigned hist[256];
+    __shared__ unsigned s_digit;
+    __shared__ int s_rank;
+    const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    uint32_t v[VPT];
 #pragma unroll
-    for (int e = 0; e < SEED_VPT; ++e) {
+    for (int e = 0; e < VPT; ++e) {
         const int j = tid + 256 * e;
-        v[e] = j < M ? ord_f32(seedmax[(size_t)q * M + j]) : 0u;
+        v[e] = j < M ? ord_f32(seedmax[(size_t)q * M + j]) : 0u;  // 0 = padding (below every value)
     }
-    // largest t with count(v >= t) >= rank (bisection on the orderable bits)
-    uint32_t lo = 0u, hi = 0xFFFFFFFFu;
-    while (lo < hi) {
-        const uint32_t mid = lo + (uint32_t)(((uint64_t)hi - lo + 1) >> 1);
-        int c = 0;
+    uint32_t prefix = 0u, mask = 0u;
+    int r = rank;
+    for (int shift = 24; shift >= 0; shift -= 8) {
+        hist[tid] = 0u;
+        __syncthreads();
 #pragma unroll
-        for (int e = 0; e < SEED_VPT; ++e) c += v[e] >= mid ? 1 : 0;
-        c = wave_sum_i(c);
+        for (int e = 0; e < VPT; ++e)
+            if ((v[e] & mask) == prefix) atomicAdd(&hist[(v[e] >> shift) & 255u], 1u);
         __syncthreads();
-        if (lane == 0) part[wid] = c;
+        if (tid < 64) {  // lane l holds bins 255-4l .. 252-4l (descending)
+            unsigned c[4], sum = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                c[i] = hist[255 - 4 * lane - i];
+                sum += c[i];
+            }
+            unsigned incl = sum;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const unsigned t = __shfl_up(incl, o, 64);
+                if (lane >= o) incl += t;
+            }
+            const unsigned excl = incl - sum;
+            const bool here = excl < (unsigned)r && incl >= (unsigned)r;
+            if (here) {
+                unsigned cum = excl;
+                int i = 0;
+                while (cum + c[i] < (unsigned)r) cum += c[i++];
+                s_digit = 255u - 4u * lane - (unsigned)i;
+                s_rank = r - (int)cum;
+            }
+            if (__ballot(here) == 0ull && lane == 0) {  // fewer than `rank` values in total
+                s_digit = 0u;
+                s_rank = 0;
+            }
+        }
         __syncthreads();
-        const int tot = part[0] + part[1] + part[2] + part[3];
-        if (tot >= rank) lo = mid;
-        else hi = mid - 1u;
+        if (s_rank == 0) {  // not enough values: no threshold
+            prefix = 0u;
+            break;
+        }
+        prefix |= s_digit << shift;
+        mask |= 255u << shift;
+        r = s_rank;
+        __syncthreads();
     }
     if (tid == 0) {
-        const float T = unord_f32(lo);
-        // lo == 0: fewer than `rank` values; -inf: only padding rows -> no threshold
-        thr0[q] = (lo == 0u || T == -INFINITY) ? 0ull : ((u64)lo << 32);
+        const float T = unord_f32(prefix);
+        thr0[q] = (prefix == 0u || T == -INFINITY) ? 0ull : ((u64)prefix << 32);
     }
 }
 
@@ -1455,12 +1622,14 @@ hipError_t launch_gather_rows(int dt, const uint8_t* data, const int64_t* ids, i
     return hipGetLastError();
 }
 
-hipError_t launch_pack_qtile(int dt, const float* q, int nqb, int d, int dpad, uint8_t* qt, float* qinfo,
+hipError_t launch_pack_qtile(int dt, const float* q, int nqb, int d, int dpad, uint8_t* qt, float* qinfo, int* gcnt,
                              hipStream_t st) {
     if (dt == DT_BF16)
-        hipLaunchKernelGGL(k_pack_qtile<DT_BF16>, dim3(MFMA_QB / 4), dim3(256), 0, st, q, nqb, d, dpad, qt, qinfo);
+        hipLaunchKernelGGL(k_pack_qtile<DT_BF16>, dim3(MFMA_QB / 4), dim3(256), 0, st, q, nqb, d, dpad, qt, qinfo,
+                           gcnt);
     else
-        hipLaunchKernelGGL(k_pack_qtile<DT_F16>, dim3(MFMA_QB / 4), dim3(256), 0, st, q, nqb, d, dpad, qt, qinfo);
+        hipLaunchKernelGGL(k_pack_qtile<DT_F16>, dim3(MFMA_QB / 4), dim3(256), 0, st, q, nqb, d, dpad, qt, qinfo,
+                           gcnt);
     return hipGetLastError();
 }
 
@@ -1483,6 +1652,7 @@ static void launch_mfma_one(const ScreenArgs& a, const uint8_t* qt, int nqb, hip
 template <int DT, int METRIC>
 static void launch_mfma_mode(const ScreenArgs& a, const uint8_t* qt, int nqb, hipStream_t st) {
     static const int mode = [] {
+        if (getenv("VS_MF_STAMPS")) return MF_STAMP_MODE;
         const char* e = getenv("VS_MF_ABLATE");
         return e ? atoi(e) : 0;
     }();
@@ -1501,6 +1671,9 @@ static void launch_mfma_mode(const ScreenArgs& a, const uint8_t* qt, int nqb, hi
         case 12: launch_mfma_one<DT, METRIC, 12>(a, qt, nqb, st); break;
         case 13: launch_mfma_one<DT, METRIC, 13>(a, qt, nqb, st); break;
         case 14: launch_mfma_one<DT, METRIC, 14>(a, qt, nqb, st); break;
+        case MF_STAMP_MODE: launch_mfma_one<DT, METRIC, MF_STAMP_MODE>(a, qt, nqb, st); break;
+        case 16: launch_mfma_one<DT, METRIC, 16>(a, qt, nqb, st); break;
+        case 17: launch_mfma_one<DT, METRIC, 17>(a, qt, nqb, st); break;
         default: launch_mfma_one<DT, METRIC, 0>(a, qt, nqb, st); break;
     }
 }
@@ -1540,16 +1713,38 @@ hipError_t launch_merge(const u64* in, int nseg, int qstride, int nq, int Kp, u6
     return hipGetLastError();
 }
 
+template <int DT, int METRIC, bool QLDS>
+static void launch_refine_one(const RefineArgs& a, int nq, int KP2, size_t lds, hipStream_t st) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_refine<DT, METRIC, QLDS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  152 * 1024);
+        (void)hipGetLastError();  // an attribute failure must not surface as the launch's error
+        attr = true;
+    }
+    hipLaunchKernelGGL((k_refine<DT, METRIC, QLDS>), dim3(nq), dim3(RF_THREADS), lds, st, a, KP2);
+}
+
+template <int DT>
+static void launch_refine_dt(const RefineArgs& a, int nq, int KP2, size_t lds, bool qlds, hipStream_t st) {
+    if (a.metric == METRIC_IP) {
+        if (qlds) launch_refine_one<DT, METRIC_IP, true>(a, nq, KP2, lds, st);
+        else launch_refine_one<DT, METRIC_IP, false>(a, nq, KP2, lds, st);
+    } else {
+        if (qlds) launch_refine_one<DT, METRIC_L2, true>(a, nq, KP2, lds, st);
+        else launch_refine_one<DT, METRIC_L2, false>(a, nq, KP2, lds, st);
+    }
+}
+
 hipError_t launch_refine(const RefineArgs& a, int nq, hipStream_t st) {
     int KP2 = 1;
     while (KP2 < a.Kp) KP2 <<= 1;
-    const size_t lds = (size_t)KP2 * 12;
-    static bool attr = false;
-    if (!attr) {
-        hipFuncSetAttribute((const void*)k_refine<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
-        attr = true;
-    }
-    hipLaunchKernelGGL(k_refine<0>, dim3(nq), dim3(256), lds, st, a, KP2);
+    const size_t base = (size_t)KP2 * 12 + 8 + (size_t)KP2 * 8;  // scores, ids, (query), kept keys
+    const bool qlds = base + (size_t)a.d * 8 <= 148 * 1024;  // query as fp64 in LDS when it fits
+    const size_t lds = qlds ? base + (size_t)a.d * 8 : base;
+    if (a.dt == DT_F32) launch_refine_dt<DT_F32>(a, nq, KP2, lds, qlds, st);
+    else if (a.dt == DT_BF16) launch_refine_dt<DT_BF16>(a, nq, KP2, lds, qlds, st);
+    else launch_refine_dt<DT_F16>(a, nq, KP2, lds, qlds, st);
     return hipGetLastError();
 }
 
@@ -1568,8 +1763,14 @@ hipError_t launch_seed_mfma(int dt, const ScreenArgs& a, const uint8_t* qt, int 
 }
 
 hipError_t launch_seed_select(const float* seedmax, int M, int nq, int rank, u64* thr0, hipStream_t st) {
-    if (M > 256 * SEED_VPT || rank <= 0) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_seed_select, dim3((unsigned)nq), dim3(256), 0, st, seedmax, M, rank, thr0);
+    if (rank <= 0) return hipErrorInvalidValue;
+    const dim3 grid((unsigned)nq);
+    if (M <= 256 * SEED_VPT)
+        hipLaunchKernelGGL(k_seed_select<SEED_VPT>, grid, dim3(256), 0, st, seedmax, M, nq, rank, thr0);
+    else if (M <= 256 * 2 * SEED_VPT)
+        hipLaunchKernelGGL(k_seed_select<2 * SEED_VPT>, grid, dim3(256), 0, st, seedmax, M, nq, rank, thr0);
+    else
+        return hipErrorInvalidValue;
     return hipGetLastError();
 }
 
