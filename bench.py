@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--cpu-sample-rows", type=int, default=0,
                     help="rows of the corpus the CPU baseline scans (default: the whole corpus if host memory allows)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="rehearsal only: every rank on cuda:0 (with --dist-backend gloo on a 1-GPU box)")
     ap.add_argument("--zero-corpus", action="store_true",
                     help="diagnostic only: all-zero corpus rows (DVFS/power test with VS_MF_ABLATE=9; results meaningless)")
     ap.add_argument("--traffic-file", default=os.path.join(REPO, "profiles", "traffic_cfg3.json"))
@@ -64,10 +67,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.same_device:
+        local = 0
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.dist_backend)
     else:
         torch.cuda.set_device(local)
     dev = torch.device("cuda", local)

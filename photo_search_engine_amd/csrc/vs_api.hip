@@ -388,7 +388,25 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
     r.cert = cert;
     r.uncert = ix->d_uncert;
     r.optimistic = optimistic ? 1 : 0;
+    static const bool rf_stamps = getenv("VS_RF_STAMPS") != nullptr;
+    if (rf_stamps) HIP_CHECK(hipMalloc(&r.stamps, sizeof(unsigned long long) * 6 * nqb));
     HIP_CHECK(launch_refine(r, nqb, st));
+    if (rf_stamps) {
+        std::vector<unsigned long long> h((size_t)6 * nqb);
+        HIP_CHECK(hipMemcpyAsync(h.data(), r.stamps, h.size() * 8, hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+        double ph[5] = {};
+        for (int qi = 0; qi < nqb; ++qi) {
+            const unsigned long long* t = &h[(size_t)qi * 6];
+            ph[0] += (double)(t[0] - t[5]);  // start -> selection start (query + keys loads, setup)
+            ph[1] += (double)(t[1] - t[0]);  // selection, compaction, count
+            ph[2] += (double)(t[2] - t[1]);  // exact scoring
+            ph[3] += (double)(t[3] - t[2]);  // sort
+        }
+        fprintf(stderr, "[vs rf stamps] cycles per query block: setup %.0f select %.0f score %.0f sort %.0f\n",
+                ph[0] / nqb, ph[1] / nqb, ph[2] / nqb, ph[3] / nqb);
+        hipFree(r.stamps);
+    }
 }
 
 // Full search of nq device queries; outputs device [nq][k].

@@ -101,6 +101,7 @@ struct RefineArgs {
     int* cert;             // [nq] 1 = certified exact (may be null)
     unsigned* uncert;      // device counter (may be null)
     int optimistic;        // screened with an optimistic seed: fewer than Kp candidates = uncertified
+    unsigned long long* stamps;  // diagnostic (VS_RF_STAMPS): [nq][6] phase cycles of block 0's thread 0
 };
 hipError_t launch_refine(const RefineArgs& a, int nq, hipStream_t st);
 // seed pass: screen one tile per workgroup (tile_stride) and write per-query 16-row-group maxima

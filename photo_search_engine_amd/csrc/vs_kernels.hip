@@ -407,6 +407,7 @@ __global__ void __launch_bounds__(256) k_pack_qtile(const float* __restrict__ q,
     if (r >= MFMA_QB) return;
     if (gcnt && lane == 0) gcnt[r] = 0;  // survivor-list lengths of the screen that follows
     double n2 = 0.0, e2 = 0.0;
+#pragma unroll 8
     for (int i = lane; i < dpad; i += 64) {
         float v = (r < nqb && i < d) ? q[(int64_t)r * d + i] : 0.0f;
         float st = round_store<DT>(v, qt + (int64_t)(i >> 5) * MFMA_QB * 64 + (int64_t)r * 64 + (i & 31) * 2);
@@ -1252,53 +1253,75 @@ __device__ __forceinline__ bool better_exact(double sa, uint32_t ia, double sb, 
     return ia < ib;
 }
 
-// Exact canonical fp64 score of one stored row, query staged in LDS as fp64 (QLDS) or read from
+// Exact canonical fp64 scores of stored rows, query staged in LDS as fp64 (QLDS) or read from
 // global fp32.  Lane l owns 8-element groups g = l, l+64, ... in ascending order and accumulates
-// them sequentially; RU groups are loaded before any is consumed (independent gathers in flight).
-// The expression tree is the oracle's orc_canon_scores (oracle/vs_oracle.c), so scores are equal.
+// them sequentially, then an xor-butterfly 32..1 -- the expression tree of the oracle's
+// orc_canon_scores (oracle/vs_oracle.c), so scores are bit-identical.
+// Two rows at once (row1 < 0: only row0): both rows' gathers are issued before either is
+// consumed, halving the serialized HBM latency per wave.  Same expression tree per row.
 template <int DT, int METRIC, bool QLDS>
-__device__ __forceinline__ double exact_score_q(const uint8_t* __restrict__ corpus, int64_t row,
-                                                const double* __restrict__ qs, const float* __restrict__ qg, int d,
-                                                int dpad, int lane) {
+__device__ __forceinline__ void exact_score_q2(const uint8_t* __restrict__ corpus, int64_t row0, int64_t row1,
+                                               const double* __restrict__ qs, const float* __restrict__ qg, int d,
+                                               int dpad, int lane, double& s0, double& s1) {
 #pragma clang fp contract(off)
     constexpr int ES = DT == DT_F32 ? 4 : 2;
-    constexpr int NV = DT == DT_F32 ? 2 : 1;  // 16 B vectors per 8-element group
-    constexpr int RU = 4;
-    const uint8_t* rb = corpus + (row / TR) * (int64_t)TR * dpad * ES + (row % TR) * (CH * ES);
+    constexpr int NV = DT == DT_F32 ? 2 : 1;
+    constexpr int RU = 3;
+    const bool two = row1 >= 0;
+    const uint8_t* rb0 = corpus + (row0 / TR) * (int64_t)TR * dpad * ES + (row0 % TR) * (CH * ES);
+    const int64_t r1 = two ? row1 : row0;
+    const uint8_t* rb1 = corpus + (r1 / TR) * (int64_t)TR * dpad * ES + (r1 % TR) * (CH * ES);
     const int ng = (d + 7) >> 3;
-    double acc = 0.0;
+    double acc0 = 0.0, acc1 = 0.0;
     for (int g0 = lane; g0 < ng; g0 += 64 * RU) {
-        uint4 raw[RU][NV];
+        uint4 raw0[RU][NV], raw1[RU][NV];
 #pragma unroll
         for (int u = 0; u < RU; ++u) {
             const int g = g0 + 64 * u;
             if (g < ng) {
                 const int e0 = 8 * g;
-                const uint8_t* p = rb + (int64_t)(e0 >> 5) * TR * CH * ES + (e0 & 31) * ES;
+                const int64_t off = (int64_t)(e0 >> 5) * TR * CH * ES + (e0 & 31) * ES;
 #pragma unroll
-                for (int v = 0; v < NV; ++v) raw[u][v] = *(const uint4*)(p + 16 * v);
+                for (int v = 0; v < NV; ++v) {
+                    raw0[u][v] = *(const uint4*)(rb0 + off + 16 * v);
+                    if (two) raw1[u][v] = *(const uint4*)(rb1 + off + 16 * v);
+                }
             }
         }
 #pragma unroll
         for (int u = 0; u < RU; ++u) {
             const int g = g0 + 64 * u;
             if (g < ng) {
-                float xv[8];
+                float x0[8], x1[8];
 #pragma unroll
-                for (int v = 0; v < NV; ++v) unpack16<DT>(raw[u][v], xv + 4 * v);
+                for (int v = 0; v < NV; ++v) {
+                    unpack16<DT>(raw0[u][v], x0 + 4 * v);
+                    if (two) unpack16<DT>(raw1[u][v], x1 + 4 * v);
+                }
 #pragma unroll
                 for (int e = 0; e < 8; ++e) {
                     const int i = 8 * g + e;
                     if (i < d) {
-                        const double x = (double)xv[e];
                         const double qq = QLDS ? qs[i] : (double)qg[i];
+                        const double xa = (double)x0[e];
                         if constexpr (METRIC == METRIC_IP) {
-                            const double pr = x * qq;
-                            acc = acc + pr;
+                            const double pa = xa * qq;
+                            acc0 = acc0 + pa;
                         } else {
-                            const double dl = x - qq;
-                            const double pr = dl * dl;
-                            acc = acc + pr;
+                            const double da = xa - qq;
+                            const double pa = da * da;
+                            acc0 = acc0 + pa;
+                        }
+                        if (two) {
+                            const double xb = (double)x1[e];
+                            if constexpr (METRIC == METRIC_IP) {
+                                const double pb = xb * qq;
+                                acc1 = acc1 + pb;
+                            } else {
+                                const double db = xb - qq;
+                                const double pb = db * db;
+                                acc1 = acc1 + pb;
+                            }
                         }
                     }
                 }
@@ -1306,15 +1329,19 @@ __device__ __forceinline__ double exact_score_q(const uint8_t* __restrict__ corp
         }
     }
 #pragma unroll
-    for (int s = 32; s > 0; s >>= 1) {
-        const double o = __shfl_xor(acc, s, 64);
-        acc = acc + o;
+    for (int sft = 32; sft > 0; sft >>= 1) {
+        const double o0 = __shfl_xor(acc0, sft, 64);
+        const double o1 = __shfl_xor(acc1, sft, 64);
+        acc0 = acc0 + o0;
+        acc1 = acc1 + o1;
     }
-    return acc;
+    s0 = acc0;
+    s1 = acc1;
 }
 
 constexpr int RF_THREADS = 1024;  // 16 waves per query: Kp / 16 candidates per wave
 constexpr int RF_E = 16;          // candidate keys per thread held in registers for the selection
+constexpr int RF_WE = 32;         // lists up to 64 * RF_WE keys: threshold found by one wave
 
 template <int DT, int METRIC, bool QLDS>
 __global__ void __launch_bounds__(RF_THREADS) k_refine(RefineArgs a, int KP2) {
@@ -1323,13 +1350,14 @@ __global__ void __launch_bounds__(RF_THREADS) k_refine(RefineArgs a, int KP2) {
     uint32_t* ids = (uint32_t*)(smem + (size_t)KP2 * 8);
     double* qs = (double*)(smem + (((size_t)KP2 * 12 + 7) & ~(size_t)7));  // 8-B aligned
     __shared__ int nv_s;
-    __shared__ u64 minkey_s;
+    __shared__ u64 minkey_s, thr_s;
     __shared__ double qq_s;
     __shared__ int red[RF_THREADS / 64];
     const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     constexpr int NW = RF_THREADS / 64;
     // the best Kp keys of the candidate list, compacted into LDS (cq)
     u64* cq = (u64*)(smem + (((size_t)KP2 * 12 + 7) & ~(size_t)7) + (QLDS ? (size_t)a.d * 8 : 0));
+    if (a.stamps && tid == 0) a.stamps[(size_t)q * 6 + 5] = __builtin_amdgcn_s_memtime();
     const u64* src = a.cand + (size_t)q * a.lcap;
     const int n = a.cand_n ? min(a.cand_n[q], a.lcap) : a.Kp;
     const float* qv = a.q + (int64_t)q * a.d;
@@ -1339,6 +1367,11 @@ __global__ void __launch_bounds__(RF_THREADS) k_refine(RefineArgs a, int KP2) {
     }
     if constexpr (QLDS)
         for (int i = tid; i < a.d; i += RF_THREADS) qs[i] = (double)qv[i];
+    if (a.stamps && tid == 0) {
+        __builtin_amdgcn_sched_barrier(0);
+        a.stamps[(size_t)q * 6 + 0] = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_sched_barrier(0);
+    }
     int nkept;
     if (n <= RF_THREADS * RF_E) {
         u64 keys[RF_E];
@@ -1347,7 +1380,25 @@ __global__ void __launch_bounds__(RF_THREADS) k_refine(RefineArgs a, int KP2) {
             const int j = tid + RF_THREADS * e;
             keys[e] = j < n ? src[j] : 0ull;
         }
-        const u64 t = n > a.Kp ? block_kth<RF_E>(keys, a.Kp, red) : 1ull;
+        u64 t = 1ull;
+        if (n > a.Kp) {
+            if (n <= 64 * RF_WE) {  // typical seeded list: one wave finds the threshold, no block barriers
+                if (wid == 0) {
+                    u64 wk[RF_WE];
+#pragma unroll
+                    for (int e = 0; e < RF_WE; ++e) {
+                        const int j = lane + 64 * e;
+                        wk[e] = j < n ? src[j] : 0ull;
+                    }
+                    const u64 tw = wave_kth<RF_WE>(wk, a.Kp);
+                    if (lane == 0) thr_s = tw;
+                }
+                __syncthreads();
+                t = thr_s;
+            } else {
+                t = block_kth<RF_E>(keys, a.Kp, red);
+            }
+        }
         nkept = block_write_kept<RF_E>(keys, t, cq, red);
     } else {  // very long lists (unseeded screens of many workgroups): selection from memory
         const u64 t = block_kth_mem(src, n, a.Kp, red);
@@ -1367,21 +1418,36 @@ __global__ void __launch_bounds__(RF_THREADS) k_refine(RefineArgs a, int KP2) {
         atomicAdd(&nv_s, myv);
         atomicMin(&minkey_s, mymin);
     }
-    if (wid == 0) {
+    if (wid == 1 && METRIC == METRIC_L2) {  // ||q||^2 for the L2 margin (staged query when in LDS)
         double s2 = 0.0;
-        for (int i = lane; i < a.d; i += 64) s2 += (double)qv[i] * (double)qv[i];
+        for (int i = lane; i < a.d; i += 64) {
+            const double v = QLDS ? qs[i] : (double)qv[i];
+            s2 += v * v;
+        }
 #pragma unroll
         for (int s = 32; s > 0; s >>= 1) s2 += __shfl_xor(s2, s, 64);
         if (lane == 0) qq_s = s2;
     }
     __syncthreads();
+    if (a.stamps && tid == 0) {
+        __builtin_amdgcn_sched_barrier(0);
+        a.stamps[(size_t)q * 6 + 1] = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_sched_barrier(0);
+    }
     const int nv = nv_s;
-    for (int j = wid; j < nv; j += NW) {
-        const uint32_t id = key_id(cq[j]);
-        const double s = exact_score_q<DT, METRIC, QLDS>(a.corpus, id, qs, qv, a.d, a.dpad, lane);
+    for (int j = wid; j < nv; j += 2 * NW) {
+        const int j2 = j + NW;
+        const uint32_t id0 = key_id(cq[j]);
+        const uint32_t id1 = j2 < nv ? key_id(cq[j2]) : 0u;
+        double s0, s1;
+        exact_score_q2<DT, METRIC, QLDS>(a.corpus, id0, j2 < nv ? (int64_t)id1 : -1, qs, qv, a.d, a.dpad, lane, s0, s1);
         if (lane == 0) {
-            sc[j] = s;
-            ids[j] = id;
+            sc[j] = s0;
+            ids[j] = id0;
+            if (j2 < nv) {
+                sc[j2] = s1;
+                ids[j2] = id1;
+            }
         }
     }
     const double worst = METRIC == METRIC_IP ? -INFINITY : INFINITY;
@@ -1390,6 +1456,11 @@ __global__ void __launch_bounds__(RF_THREADS) k_refine(RefineArgs a, int KP2) {
         ids[j] = 0xFFFFFFFFu;
     }
     __syncthreads();
+    if (a.stamps && tid == 0) {
+        __builtin_amdgcn_sched_barrier(0);
+        a.stamps[(size_t)q * 6 + 2] = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_sched_barrier(0);
+    }
     // bitonic sort, best first
     for (int size = 2; size <= KP2; size <<= 1) {
         for (int stride = size >> 1; stride > 0; stride >>= 1) {
@@ -1408,6 +1479,11 @@ __global__ void __launch_bounds__(RF_THREADS) k_refine(RefineArgs a, int KP2) {
             }
             __syncthreads();
         }
+    }
+    if (a.stamps && tid == 0) {
+        __builtin_amdgcn_sched_barrier(0);
+        a.stamps[(size_t)q * 6 + 3] = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_sched_barrier(0);
     }
     // exactness certificate: every non-candidate row has exact transformed score <= smin + eps
     if (tid == 0) {
@@ -1519,38 +1595,70 @@ __global__ void __launch_bounds__(256) k_seed_select(const float* __restrict__ s
 // ------------------------------------------------------------------------------------------------
 // merge of per-shard sorted results (after the RCCL all-gather)
 // ------------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(64) k_merge_shards(int metric, const double* __restrict__ S_in,
-                                                     const int64_t* __restrict__ I_in, int G, int64_t nq, int k,
-                                                     double* __restrict__ S_out, int64_t* __restrict__ I_out,
-                                                     float* __restrict__ D_out) {
-    const int64_t q = (int64_t)blockIdx.x * 64 + threadIdx.x;
+// one wave per query: lane g < G holds the head of shard list g; each of the k rounds picks the
+// best head by a wave butterfly on (score, id) -- score desc (IP) / asc (L2), ties -> lower id --
+// and the winning lane advances.  Lists end at their first id -1.
+__global__ void __launch_bounds__(256) k_merge_shards(int metric, const double* __restrict__ S_in,
+                                                      const int64_t* __restrict__ I_in, int G, int64_t nq, int k,
+                                                      double* __restrict__ S_out, int64_t* __restrict__ I_out,
+                                                      float* __restrict__ D_out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (q >= nq) return;
-    int pos[64];
-    for (int g = 0; g < G; ++g) pos[g] = 0;
-    for (int j = 0; j < k; ++j) {
-        int bg = -1;
-        double bs = 0.0;
-        int64_t bi = 0;
-        for (int g = 0; g < G; ++g) {
-            if (pos[g] >= k) continue;
-            const size_t o = ((size_t)g * nq + q) * k + pos[g];
+    const double worst = metric == METRIC_IP ? -INFINITY : INFINITY;
+    int pos = 0;
+    double hs = worst;
+    int64_t hi = -1;
+    auto load_head = [&]() {
+        hs = worst;
+        hi = -1;
+        if (lane < G && pos < k) {
+            const size_t o = ((size_t)lane * nq + q) * k + pos;
             const int64_t id = I_in[o];
-            if (id < 0) continue;
-            const double s = S_in[o];
-            bool take = bg < 0;
-            if (!take) take = (s != bs) ? (metric == METRIC_IP ? s > bs : s < bs) : id < bi;
-            if (take) { bg = g; bs = s; bi = id; }
+            if (id >= 0) {
+                hs = S_in[o];
+                hi = id;
+            }
+        }
+    };
+    load_head();
+    for (int j = 0; j < k; ++j) {
+        double bs = hs;
+        int64_t bi = hi;
+        int bl = hi >= 0 ? lane : 64;
+#pragma unroll
+        for (int sft = 32; sft > 0; sft >>= 1) {
+            const double os = __shfl_xor(bs, sft, 64);
+            const int64_t oi = __shfl_xor(bi, sft, 64);
+            const int ol = __shfl_xor(bl, sft, 64);
+            bool take;
+            if (ol == 64) take = false;
+            else if (bl == 64) take = true;
+            else if (os != bs) take = metric == METRIC_IP ? os > bs : os < bs;
+            else take = oi < bi;
+            if (take) {
+                bs = os;
+                bi = oi;
+                bl = ol;
+            }
         }
         const size_t oo = (size_t)q * k + j;
-        if (bg < 0) {
-            S_out[oo] = metric == METRIC_IP ? -1.7976931348623157e308 : 1.7976931348623157e308;
-            I_out[oo] = -1;
-            if (D_out) D_out[oo] = metric == METRIC_IP ? -3.402823466e+38f : 3.402823466e+38f;
-        } else {
+        if (bl == 64) {  // every list exhausted: padding
+            if (lane == 0) {
+                S_out[oo] = metric == METRIC_IP ? -1.7976931348623157e308 : 1.7976931348623157e308;
+                I_out[oo] = -1;
+                if (D_out) D_out[oo] = metric == METRIC_IP ? -3.402823466e+38f : 3.402823466e+38f;
+            }
+            continue;
+        }
+        if (lane == 0) {
             S_out[oo] = bs;
             I_out[oo] = bi;
             if (D_out) D_out[oo] = (float)bs;
-            pos[bg]++;
+        }
+        if (lane == bl) {
+            ++pos;
+            load_head();
         }
     }
 }
@@ -1777,8 +1885,8 @@ hipError_t launch_seed_select(const float* seedmax, int M, int nq, int rank, u64
 hipError_t launch_merge_shards(int metric, const double* S_in, const int64_t* I_in, int G, int64_t nq, int k,
                                double* S_out, int64_t* I_out, float* D_out, hipStream_t st) {
     if (G > 64) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_merge_shards, dim3((unsigned)((nq + 63) / 64)), dim3(64), 0, st, metric, S_in, I_in, G, nq,
-                       k, S_out, I_out, D_out);
+    hipLaunchKernelGGL(k_merge_shards, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, st, metric, S_in, I_in, G, nq, k,
+                       S_out, I_out, D_out);
     return hipGetLastError();
 }
 

@@ -1,0 +1,58 @@
+"""The multi-rank search path on a real GPU: two ranks (gloo, both on cuda:0 -- the box has one
+GPU; the driver's 8-GPU runs use nccl/RCCL with one GPU per rank) run the product's
+ShardedFlatIndex with its default HIP local search and HIP device merge, and every rank's merged
+answer must equal the oracle's exact answer over the whole corpus (ids and fp64 scores)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, N, d, dtype, nq, k, metric, outdir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from photo_search_engine_amd.distributed import ShardedFlatIndex
+        sh = ShardedFlatIndex(d, metric, dtype, device=0)
+        sh.add_synthetic(O.SEED_CORPUS, N, True)
+        q = torch.from_numpy(O.synth_rows(O.SEED_QUERIES, 0, nq, d, True, dtype)).cuda()
+        if rank != 0:
+            q.zero_()  # rank 0's batch arrives by broadcast
+        D, I, S = sh.search(q, k, src=0)
+        torch.cuda.synchronize()
+        np.savez(os.path.join(outdir, f"r{rank}.npz"), D=D.cpu().numpy(), I=I.cpu().numpy(), S=S.cpu().numpy(),
+                 row0=sh.row0, n=sh.n_local)
+        sh.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("metric,dtype,nq,k", [("ip", "bf16", 40, 25), ("l2", "f32", 3, 10)])
+def test_two_ranks_one_gpu_match_oracle(tmp_path, metric, dtype, nq, k):
+    N, d = 20011, 64
+    mp.spawn(_worker, args=(2, _free_port(), N, d, dtype, nq, k, metric, str(tmp_path)), nprocs=2, join=True)
+    outs = [np.load(tmp_path / f"r{r}.npz") for r in range(2)]
+    assert int(outs[0]["row0"]) == 0 and int(outs[1]["row0"]) == int(outs[0]["n"])
+    x = O.synth_rows(O.SEED_CORPUS, 0, N, d, True, dtype)
+    q = O.synth_rows(O.SEED_QUERIES, 0, nq, d, True, dtype)
+    Se, Ie = O.knn_exact(x, q, k, metric)
+    for o in outs:
+        np.testing.assert_array_equal(o["I"], Ie)
+        np.testing.assert_array_equal(o["S"], Se)
+        np.testing.assert_array_equal(o["D"], Se.astype(np.float32))
