@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 for s in "$@"; do
   case $s in
     smoke) timeout -k 10 300 python __graft_entry__.py --smoke > gpurun_out/smoke.log 2>&1 ;;
-    tests) timeout -k 10 900 python -m pytest tests -x -q -m gpu > gpurun_out/pytest_gpu.log 2>&1 ;;
+    tests) timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 ;;
     bench_small) timeout -k 10 300 python bench.py --rows 1000000 --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/bench_small.log 2>&1 ;;
     bench) timeout -k 10 600 python bench.py > gpurun_out/bench.log 2>&1 ;;
     bench_cfg2) timeout -k 10 600 python bench.py --workload cfg2 --steps 50 --no-cpu-baseline > gpurun_out/bench_cfg2.log 2>&1 ;;
