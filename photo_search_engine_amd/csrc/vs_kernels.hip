@@ -685,19 +685,23 @@ __device__ __forceinline__ void mf_wave_compact(u64* __restrict__ buf, int n, in
 //   13 = 0 with compare-only epilogue (no inserts, no check) | 14 = 0 without the deferred check/pool flush
 template <int DT, int METRIC, int MODE>
 __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
+    // 21 = 0 without the query stream (stale query tile) | 22 = 0 with B fragments re-read every other
+    // K-step only | 23 = 0 with A fragments re-read every other K-step only  (energy ablations)
+    constexpr bool XP = MODE == 21 || MODE == 22 || MODE == 23;
     constexpr bool LOADS = (MODE != 1 && MODE < 3) || (MODE >= 6 && MODE != 12);  // (incl. seed, stamps)
     constexpr bool MATH = (MODE != 2 && MODE < 6) || MODE == 9 || MODE == 10 || MODE == 13 || MODE == 14 ||
-                          MODE == MF_SEED_MODE || MODE == MF_STAMP_MODE || MODE == 16 || MODE == 17;
+                          MODE == MF_SEED_MODE || MODE == MF_STAMP_MODE || MODE == 16 || MODE == 17 || XP;
     constexpr bool PP = MODE == 11 || MODE == 12;  // ping-pong: waves 4-7 half a K-step behind waves 0-3
     constexpr bool SEED = MODE == MF_SEED_MODE;  // threshold-seed pass: group maxima only
     constexpr bool EPI = MODE < 3 || MODE == 13 || MODE == 14 || SEED || MODE == MF_STAMP_MODE || MODE == 16 ||
-                         MODE == 17;
+                         MODE == 17 || XP;
     constexpr bool INS = MODE != 13;   // threshold passes insert candidates
     constexpr bool CHECK = MODE != 13 && MODE != 14;  // deferred compaction check + pool flush
     constexpr bool BAR = MODE < 4 || MODE >= 6;  // (incl. seed, stamps)
     constexpr bool READS = MODE < 5 || MODE == 9 || MODE == 10 || MODE == 13 || MODE == 14 || MODE == MF_SEED_MODE ||
-                           MODE == MF_STAMP_MODE || MODE == 16 || MODE == 17;
+                           MODE == MF_STAMP_MODE || MODE == 16 || MODE == 17 || XP;
     constexpr bool QLOAD = MODE != 7;
+    constexpr int64_t QSTEP = MODE == 21 ? 0 : 16384;  // 21: every stage re-reads query block 0 (L1-resident)
     constexpr bool NT = MODE == 8 || MODE == 0 || MODE >= 9;
     constexpr bool IL = MODE == 10;  // DMA issue interleaved with the MFMAs (ablation: slower)
     constexpr bool STAMP = MODE == MF_STAMP_MODE;  // = production + per-phase s_memtime stamps
@@ -761,7 +765,7 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
             mf_stage_bal<NT>(a.corpus + (int64_t)iti * tbytes + (int64_t)iks * 16384, qt + (int64_t)iks * 16384,
                              ring + (uint32_t)(j * MF_SLOT), tid);
         else if constexpr (LOADS)
-            mf_stage<QLOAD, NT>(a.corpus + (int64_t)iti * tbytes + (int64_t)iks * 16384, qt + (int64_t)iks * 16384,
+            mf_stage<QLOAD, NT>(a.corpus + (int64_t)iti * tbytes + (int64_t)iks * 16384, qt + (int64_t)iks * QSTEP,
                                 ring + (uint32_t)(j * MF_SLOT), tid);
         if (++iks == nks) { iks = 0; ++iti; }
     }
@@ -795,7 +799,7 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
         }
         const bool do_issue = s + MF_DEPTH < S;
         const uint8_t* nA = a.corpus + (int64_t)iti * tbytes + (int64_t)iks * 16384;
-        const uint8_t* nB = qt + (int64_t)iks * 16384;
+        const uint8_t* nB = qt + (int64_t)iks * QSTEP;
         const uint32_t nslot = ring + (uint32_t)(((s + MF_DEPTH) % MF_SLOTS) * MF_SLOT);
         if (do_issue) {
             if (++iks == nks) { iks = 0; ++iti; }
@@ -836,7 +840,17 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
                 t2 = __builtin_amdgcn_s_memtime();
                 __builtin_amdgcn_sched_barrier(0);
             }
-            if constexpr (MATH) mf_compute<DT, READS>(smem + (s % MF_SLOTS) * MF_SLOT, acc, wm, wn, lane_off);
+            if constexpr (MODE == 22 || MODE == 23) {
+                const uint8_t* buf = smem + (s % MF_SLOTS) * MF_SLOT;
+                if (MODE == 23 || (s & 1) == 0)
+#pragma unroll
+                    for (int ni = 0; ni < 8; ++ni)
+                        pf_b[ni] = *(const uint4*)(buf + 16384 + wn * 8192 + lane_off + ni * 1024);
+                if (MODE == 22 || (s & 1) == 0)
+#pragma unroll
+                    for (int mi = 0; mi < 4; ++mi) pf_a[mi] = *(const uint4*)(buf + wm * 4096 + lane_off + mi * 1024);
+                mf_mfma<DT, 0, 4>(pf_a, pf_b, acc);
+            } else if constexpr (MATH) mf_compute<DT, READS>(smem + (s % MF_SLOTS) * MF_SLOT, acc, wm, wn, lane_off);
             if constexpr (STAMP) {
                 __builtin_amdgcn_sched_barrier(0);
                 t3 = __builtin_amdgcn_s_memtime();
@@ -1782,6 +1796,9 @@ static void launch_mfma_mode(const ScreenArgs& a, const uint8_t* qt, int nqb, hi
         case MF_STAMP_MODE: launch_mfma_one<DT, METRIC, MF_STAMP_MODE>(a, qt, nqb, st); break;
         case 16: launch_mfma_one<DT, METRIC, 16>(a, qt, nqb, st); break;
         case 17: launch_mfma_one<DT, METRIC, 17>(a, qt, nqb, st); break;
+        case 21: launch_mfma_one<DT, METRIC, 21>(a, qt, nqb, st); break;
+        case 22: launch_mfma_one<DT, METRIC, 22>(a, qt, nqb, st); break;
+        case 23: launch_mfma_one<DT, METRIC, 23>(a, qt, nqb, st); break;
         default: launch_mfma_one<DT, METRIC, 0>(a, qt, nqb, st); break;
     }
 }
