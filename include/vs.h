@@ -102,6 +102,41 @@ int vs_set_timing(vs_index* index, int enable);
 int vs_timing_fetch(vs_index* index, float* ms, int cap, int* kernel_kind);
 int64_t vs_uncertified_count(vs_index* index);   /* synchronises the device counter */
 
+/* ==== IVF-Flat (BASELINE cfg5) ===========================================
+ * Not a reference call site: the reference's VectorStore offers flat and HNSW only
+ * (utils/vector_store.py:51-53, 72-81).  This is the faiss IndexIVFFlat surface (faiss-cpu,
+ * requirements.txt:5): IndexIVFFlat(quantizer, d, nlist, metric) -> vs_ivf_create,
+ * .train -> vs_ivf_set_centroids (k-means runs in the Python layer over vs_ivf_assign),
+ * .add -> vs_ivf_add, .search with .nprobe -> vs_ivf_search, .reconstruct -> vs_ivf_reconstruct.
+ * Semantics (made exact, oracle/ivf_oracle.py): rows go to their exact best centroid (ties ->
+ * lower list id); a query probes its exact top-nprobe centroids and gets the exact top-k of the
+ * rows of those lists (canonical fp64 score, ties -> lower id; -1 / worst-score padding).
+ * Ids are insertion order 0..ntotal-1, as for the flat index.  Searches on one handle are
+ * serialised; add/reset take an exclusive lock. */
+typedef struct vs_ivf vs_ivf;
+
+int vs_ivf_create(int d, int nlist, int metric, int dtype, int device, vs_ivf** out);
+void vs_ivf_destroy(vs_ivf* ivf);
+int vs_ivf_set_centroids(vs_ivf* ivf, const float* c);        /* host nlist x d; only while empty */
+int vs_ivf_get_centroids(vs_ivf* ivf, float* out);            /* host nlist x d, values as stored */
+int vs_ivf_is_trained(const vs_ivf* ivf);
+int vs_ivf_assign(vs_ivf* ivf, const float* x, int64_t n, int64_t* lists); /* host in / out */
+int vs_ivf_add(vs_ivf* ivf, const float* x, int64_t n);       /* host fp32 n x d */
+int vs_ivf_add_synthetic(vs_ivf* ivf, uint64_t seed, int64_t global_row0, int64_t n, int normalize);
+int vs_ivf_search(vs_ivf* ivf, const float* q, int64_t nq, int32_t k, int32_t nprobe, float* D, int64_t* I);
+/* device q/D/I/S64 (D, S64 may be NULL); host-synchronising (the probe -> work-item step). */
+int vs_ivf_search_device(vs_ivf* ivf, const float* q_dev, int64_t nq, int32_t k, int32_t nprobe, float* D_dev,
+                         int64_t* I_dev, double* S64_dev, void* stream);
+int vs_ivf_reconstruct(vs_ivf* ivf, int64_t id, float* out);
+int vs_ivf_list_sizes(vs_ivf* ivf, int64_t* out);             /* nlist entries */
+int vs_ivf_reset(vs_ivf* ivf);                                /* drop rows, keep centroids */
+int64_t vs_ivf_ntotal(const vs_ivf* ivf);
+int vs_ivf_nlist(const vs_ivf* ivf);
+/* bench: HIP events around the list-scan kernels of each search (same contract as vs_timing_fetch);
+ * bytes_scanned (may be NULL) receives the algorithmic bytes those scans read, per search. */
+int vs_ivf_set_timing(vs_ivf* ivf, int enable);
+int vs_ivf_timing_fetch(vs_ivf* ivf, float* ms, double* bytes_scanned, int cap);
+
 #ifdef __cplusplus
 }
 #endif

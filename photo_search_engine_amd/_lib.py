@@ -71,6 +71,25 @@ _SIGS = {
     "vs_set_timing": (ctypes.c_int, [_vp, ctypes.c_int]),
     "vs_timing_fetch": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
     "vs_uncertified_count": (_c_i64, [_vp]),
+    # IVF-Flat
+    "vs_ivf_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     ctypes.POINTER(_vp)]),
+    "vs_ivf_destroy": (None, [_vp]),
+    "vs_ivf_set_centroids": (ctypes.c_int, [_vp, _vp]),
+    "vs_ivf_get_centroids": (ctypes.c_int, [_vp, _vp]),
+    "vs_ivf_is_trained": (ctypes.c_int, [_vp]),
+    "vs_ivf_assign": (ctypes.c_int, [_vp, _vp, _c_i64, _vp]),
+    "vs_ivf_add": (ctypes.c_int, [_vp, _vp, _c_i64]),
+    "vs_ivf_add_synthetic": (ctypes.c_int, [_vp, ctypes.c_uint64, _c_i64, _c_i64, ctypes.c_int]),
+    "vs_ivf_search": (ctypes.c_int, [_vp, _vp, _c_i64, ctypes.c_int32, ctypes.c_int32, _vp, _vp]),
+    "vs_ivf_search_device": (ctypes.c_int, [_vp, _vp, _c_i64, ctypes.c_int32, ctypes.c_int32, _vp, _vp, _vp, _vp]),
+    "vs_ivf_reconstruct": (ctypes.c_int, [_vp, _c_i64, _vp]),
+    "vs_ivf_list_sizes": (ctypes.c_int, [_vp, _vp]),
+    "vs_ivf_reset": (ctypes.c_int, [_vp]),
+    "vs_ivf_ntotal": (_c_i64, [_vp]),
+    "vs_ivf_nlist": (ctypes.c_int, [_vp]),
+    "vs_ivf_set_timing": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "vs_ivf_timing_fetch": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int]),
 }
 
 

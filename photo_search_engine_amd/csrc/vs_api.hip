@@ -25,59 +25,6 @@ namespace {
 
 thread_local std::string g_err;
 
-struct VsError : std::runtime_error {
-    int code;
-    VsError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
-};
-
-#define HIP_CHECK(expr)                                                                                    \
-    do {                                                                                                   \
-        hipError_t _e = (expr);                                                                            \
-        if (_e != hipSuccess)                                                                              \
-            throw VsError(_e == hipErrorOutOfMemory ? VS_ERR_OOM : VS_ERR_DEVICE,                          \
-                          std::string(#expr) + ": " + hipGetErrorString(_e));                              \
-    } while (0)
-
-template <typename F>
-int guarded(F&& f) {
-    try {
-        f();
-        return VS_OK;
-    } catch (const VsError& e) {
-        g_err = e.what();
-        return e.code;
-    } catch (const std::exception& e) {
-        g_err = e.what();
-        return VS_ERR_INTERNAL;
-    } catch (...) {
-        g_err = "unknown error";
-        return VS_ERR_INTERNAL;
-    }
-}
-
-inline int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
-
-// device buffer that only grows
-struct DevBuf {
-    void* p = nullptr;
-    size_t bytes = 0;
-    void ensure(size_t want) {
-        if (want <= bytes) return;
-        if (p) hipFree(p);
-        p = nullptr;
-        bytes = 0;
-        HIP_CHECK(hipMalloc(&p, want));
-        bytes = want;
-    }
-    template <typename T>
-    T* as() const { return (T*)p; }
-    void release() {
-        if (p) hipFree(p);
-        p = nullptr;
-        bytes = 0;
-    }
-};
-
 // per-call execution context: stream + workspace (pooled; one per concurrent search)
 struct Ctx {
     hipStream_t stream = nullptr;
@@ -92,6 +39,8 @@ struct Ctx {
 };
 
 }  // namespace
+
+void vs::set_last_error(const std::string& msg) { g_err = msg; }
 
 struct vs_index {
     int d = 0, dpad = 0, metric = 0, dtype = 0, device = 0, es = 4;
@@ -116,19 +65,6 @@ struct vs_index {
 };
 
 namespace {
-
-struct DeviceGuard {
-    int prev = -1;
-    explicit DeviceGuard(int dev) {
-        hipGetDevice(&prev);
-        if (prev != dev) HIP_CHECK(hipSetDevice(dev));
-    }
-    ~DeviceGuard() {
-        int cur = -1;
-        hipGetDevice(&cur);
-        if (prev >= 0 && cur != prev) hipSetDevice(prev);
-    }
-};
 
 Ctx* acquire_ctx(vs_index* ix) {
     std::lock_guard<std::mutex> g(ix->pool_mtx);
@@ -191,24 +127,11 @@ void refresh_maxsq(vs_index* ix) {
     ix->maxsq = f;
 }
 
-// screening depth: k plus a margin that certifies exactness for all but pathological inputs
-int screen_depth(int k) {
-    int kp = k + std::max(16, k / 4);
-    kp = (int)round_up(kp, 16);
-    return std::min(kp, KP_MAX);
-}
-
 // optimistic seed: a 16-row-group maximum of the strided tile sample, at the rank that leaves
 // ~kOptimisticPassFactor * Kp corpus rows above it in expectation (the proven seed is rank Kp); a
 // query left short is caught by the certificate and searched again with the proven seed
 constexpr int kOptimisticSeedRank = 1;  // seed_rank argument: > 0 selects the optimistic rank
 constexpr double kOptimisticPassFactor = 8.0;
-
-float gamma_of(int d) {
-    const double u = 5.9604644775390625e-08;  // 2^-24
-    const double n = (double)d + 64.0;
-    return (float)(n * u / (1.0 - n * u));
-}
 
 // Enqueue one query block through screen -> merge -> refine.  q: device fp32 [nqb][d].
 // seed_rank: 0 = proven (safe) seed, > 0 = optimistic seed at that sample rank (see k_seed_select)
@@ -432,6 +355,39 @@ void check_index(const vs_index* ix) {
 }
 
 }  // namespace
+
+// exact device search for in-library callers (the IVF coarse quantizer): like vs_search_device,
+// but certificate failures are re-searched with deeper screens, as vs_search does
+void vs::search_exact_device(vs_index* ix, const float* q_dev, int64_t nq, int k, int64_t* I_dev, double* S64_dev,
+                             hipStream_t st) {
+    check_index(ix);
+    if (nq <= 0) return;
+    std::shared_lock<std::shared_mutex> lk(ix->rw);
+    DeviceGuard dg(ix->device);
+    if (k <= 0 || k > ix->ntotal) throw VsError(VS_ERR_ARG, "k must be in [1, ntotal]");
+    CtxLease L(ix);
+    Ctx* c = L.c;
+    c->outD.ensure((size_t)nq * k * sizeof(float));
+    c->cert.ensure((size_t)nq * sizeof(int));
+    const int Kp = screen_depth(k);
+    search_all(ix, c, q_dev, nq, k, Kp, c->outD.as<float>(), I_dev, S64_dev, c->cert.as<int>(), 0, st,
+               kOptimisticSeedRank);
+    c->cert_host.resize((size_t)nq);
+    HIP_CHECK(hipMemcpyAsync(c->cert_host.data(), c->cert.p, (size_t)nq * sizeof(int), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    for (int64_t qi = 0; qi < nq; ++qi) {
+        int Kr = Kp;
+        while (!c->cert_host[qi]) {
+            if (Kr >= KP_MAX || Kr >= ix->ntotal)
+                throw VsError(VS_ERR_UNCERTIFIED, "exactness certificate failed at maximum screening depth");
+            Kr = (int)std::min<int64_t>(std::min<int64_t>((int64_t)Kr * 4, KP_MAX), round_up(ix->ntotal, 16));
+            search_all(ix, c, q_dev + qi * ix->d, 1, k, Kr, c->outD.as<float>(), I_dev + qi * k,
+                       S64_dev ? S64_dev + qi * k : nullptr, c->cert.as<int>(), 0, st, /*safe seed*/ 0);
+            HIP_CHECK(hipMemcpyAsync(&c->cert_host[qi], c->cert.p, sizeof(int), hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipStreamSynchronize(st));
+        }
+    }
+}
 
 extern "C" {
 

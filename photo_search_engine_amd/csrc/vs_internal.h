@@ -12,6 +12,12 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+#include <stdexcept>
+#include <string>
+
+#include "../../include/vs.h"
+
 namespace vs {
 
 constexpr int TR = 256;        // rows per tile
@@ -28,6 +34,87 @@ constexpr int SELECT_E = 16;   // keys per thread in block selection (256 thread
 
 inline int es_of(int dt) { return dt == DT_F32 ? 4 : 2; }
 inline int64_t tile_bytes(int dpad, int dt) { return (int64_t)TR * dpad * es_of(dt); }
+inline int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
+
+// screening depth: k plus a margin that certifies exactness for all but pathological inputs
+inline int screen_depth(int k) {
+    int kp = k + std::max(16, k / 4);
+    kp = (int)round_up(kp, 16);
+    return std::min(kp, KP_MAX);
+}
+
+// fp32 accumulation error factor of a d-term dot product (chains of <= d + 64 roundings)
+inline float gamma_of(int d) {
+    const double u = 5.9604644775390625e-08;  // 2^-24
+    const double n = (double)d + 64.0;
+    return (float)(n * u / (1.0 - n * u));
+}
+
+// ---- errors: C++ exceptions inside the library, int codes + vs_last_error() at the ABI --------
+struct VsError : std::runtime_error {
+    int code;
+    VsError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+void set_last_error(const std::string& msg);  // thread-local message read by vs_last_error()
+
+#define HIP_CHECK(expr)                                                                                    \
+    do {                                                                                                   \
+        hipError_t _e = (expr);                                                                            \
+        if (_e != hipSuccess)                                                                              \
+            throw ::vs::VsError(_e == hipErrorOutOfMemory ? VS_ERR_OOM : VS_ERR_DEVICE,                    \
+                                std::string(#expr) + ": " + hipGetErrorString(_e));                        \
+    } while (0)
+
+template <typename F>
+int guarded(F&& f) {
+    try {
+        f();
+        return VS_OK;
+    } catch (const VsError& e) {
+        set_last_error(e.what());
+        return e.code;
+    } catch (const std::exception& e) {
+        set_last_error(e.what());
+        return VS_ERR_INTERNAL;
+    } catch (...) {
+        set_last_error("unknown error");
+        return VS_ERR_INTERNAL;
+    }
+}
+
+// device buffer that only grows
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    void ensure(size_t want) {
+        if (want <= bytes) return;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        HIP_CHECK(hipMalloc(&p, want));
+        bytes = want;
+    }
+    template <typename T>
+    T* as() const { return (T*)p; }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+};
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        (void)hipGetDevice(&prev);
+        if (prev != dev) HIP_CHECK(hipSetDevice(dev));
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        (void)hipGetDevice(&cur);
+        if (prev >= 0 && cur != prev) (void)hipSetDevice(prev);
+    }
+};
 
 // candidate key: (orderable score << 32) | (0xFFFFFFFF - local id); larger key = better,
 // equal scores -> lower id first; key 0 = empty slot.
@@ -102,8 +189,45 @@ struct RefineArgs {
     unsigned* uncert;      // device counter (may be null)
     int optimistic;        // screened with an optimistic seed: fewer than Kp candidates = uncertified
     unsigned long long* stamps;  // diagnostic (VS_RF_STAMPS): [nq][6] phase cycles of block 0's thread 0
+    const uint32_t* idmap; // IVF: user id of every storage slot (keys carry slots); null = identity
 };
 hipError_t launch_refine(const RefineArgs& a, int nq, hipStream_t st);
+
+// ---- IVF-Flat (vs_ivf.hip) ---------------------------------------------------------------------
+// Inverted lists are chains of pages: a page is one row tile (TR rows, the flat layout above) of
+// a shared page pool; storage slot = page * TR + row.  A scan work item is (list, page range,
+// up to IVF_QG queries probing that list).
+constexpr int IVF_QG = 8;                       // queries per scan item
+constexpr int IVF_ITEM_INTS = 4 + IVF_QG;       // list, page_begin, page_end, nq_item, query ids
+struct IvfScanArgs {
+    const uint8_t* data;       // page pool
+    const float* sqn;          // ||x||^2 per slot (L2 screening)
+    const float* qp;           // [nq][dpad] fp32 queries (k_pack_qf32)
+    const int* items;          // [n_items][IVF_ITEM_INTS]
+    int n_items;
+    const int* list_pages;     // page table: pages of list l at list_pages[page_off[l] ...]
+    const int* page_off;       // [nlist + 1]
+    const int64_t* list_n;     // rows per list
+    int dpad, metric, Kp, cap;
+    u64* cand;                 // [gridDim][nq_item][cap] workspace
+    u64* glist;                // per-query candidate lists [nq][lcap] (refine input) ...
+    int* gcnt;                 // ... with their lengths (zeroed before the scan)
+    int lcap;
+};
+hipError_t launch_ivf_scan(int dt, int nq_class, const IvfScanArgs& a, int grid, hipStream_t st);
+// pack fp32 rows into the slots slots[r] (slot_id[slot] = id0 + r); sqn / maxsq as k_pack_rows
+hipError_t launch_pack_rows_map(int dt, const float* src, int64_t n, int d, int dpad, uint8_t* data,
+                                const int64_t* slots, float* sqn, unsigned* maxsq, uint32_t* slot_id, int64_t id0,
+                                hipStream_t st);
+
+}  // namespace vs
+
+struct vs_index;
+namespace vs {
+// Exact top-k of device queries over a flat index, certificate failures re-searched (host-
+// synchronising).  I_dev [nq][k] (k <= ntotal), S64_dev optional.
+void search_exact_device(vs_index* ix, const float* q_dev, int64_t nq, int k, int64_t* I_dev, double* S64_dev,
+                         hipStream_t st);
 // seed pass: screen one tile per workgroup (tile_stride) and write per-query 16-row-group maxima
 hipError_t launch_seed_mfma(int dt, const ScreenArgs& a, const uint8_t* qt, int nqb, hipStream_t st);
 // thr0[q] = key just below the rank-th largest of the M group maxima of query q (0 if none)

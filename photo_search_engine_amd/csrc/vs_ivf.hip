@@ -1,0 +1,625 @@
+// vs_ivf.hip -- IVF-Flat index of libvs (include/vs.h, "IVF-Flat"; SURVEY.md §8 f2, BASELINE cfg5).
+//
+// The reference has flat and HNSW indexes only (/root/reference/utils/vector_store.py:51-53,72-81);
+// this is the faiss IndexIVFFlat design rebuilt for one MI355X:
+//   * coarse quantizer: an exact flat libvs index over the nlist centroids (vs_index, MFMA/GEMV
+//     screen + exact refine), used for row assignment (k=1) and query probing (k=nprobe);
+//   * inverted lists: chains of pages in ONE HBM page pool; a page is one row tile of the flat
+//     layout (TR rows, chunk-major), so every scan read is a full coalesced 1 KiB wave piece.
+//     slot = page * TR + row; slot_id[slot] = user id (insertion order);
+//   * search: exact probe -> host inversion into (list, page range, <= IVF_QG queries) work items
+//     -> k_ivf_scan (GEMV screen, fused threshold top-Kp) -> k_refine (exact fp64 rescoring, slot ->
+//     id map, certificate) -> uncertified queries re-searched with a 4x deeper screen.
+// Results equal oracle/ivf_oracle.py bit for bit (ids and fp64 scores).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstring>
+#include <mutex>
+#include <shared_mutex>
+#include <vector>
+
+#include "../../include/vs.h"
+#include "vs_internal.h"
+
+using namespace vs;
+
+struct vs_ivf {
+    int d = 0, dpad = 0, nlist = 0, metric = 0, dtype = 0, device = 0, es = 4, num_cu = 256;
+    vs_index* coarse = nullptr;
+    bool trained = false;
+    // page pool
+    uint8_t* data = nullptr;
+    float* sqn = nullptr;
+    uint32_t* slot_id = nullptr;
+    int64_t cap_pages = 0, used_pages = 0;
+    unsigned* d_flags = nullptr;  // [0] max ||x||^2 bits, [1] uncertified-query counter
+    float maxsq = 0.0f;
+    std::vector<std::vector<int>> pages;  // page chain of every list
+    std::vector<int64_t> list_n;          // rows of every list
+    std::vector<int64_t> id_slot;         // storage slot of every id
+    int64_t ntotal = 0;
+    // device copy of the page tables (CSR), refreshed lazily after adds
+    DevBuf d_page_off, d_list_pages, d_list_n;
+    bool csr_dirty = true;
+    // workspaces (add: exclusive lock; search / reconstruct: search_mtx)
+    DevBuf tmp_rows, slots, assign_ids;
+    DevBuf qdev, probes, items, qp, qinfo, cand, glist, gcnt, cert, outD, outI, rec;
+    std::vector<int64_t> probes_h;
+    std::vector<int> cert_h;
+    hipStream_t own = nullptr;
+    std::shared_mutex rw;
+    std::mutex search_mtx;
+    std::atomic<bool> timing{false};
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> tev;
+    std::vector<double> tbytes;
+};
+
+namespace {
+
+constexpr int kPagesPerItem = 16;  // scan work item: up to 16 pages (4096 rows) of one list
+
+void check_ivf(const vs_ivf* ix) {
+    if (!ix) throw VsError(VS_ERR_ARG, "null IVF index");
+}
+
+int64_t rows_per_chunk(int d) { return std::max<int64_t>(1, (int64_t)(256 << 20) / ((int64_t)d * 4)); }
+
+void ensure_pages(vs_ivf* ix, int64_t need) {
+    if (need <= ix->cap_pages) return;
+    const int64_t ncap = std::max(need, ix->cap_pages + ix->cap_pages / 4);
+    const int64_t tb = tile_bytes(ix->dpad, ix->dtype);
+    uint8_t* nd = nullptr;
+    float* ns = nullptr;
+    uint32_t* ni = nullptr;
+    HIP_CHECK(hipMalloc(&nd, (size_t)ncap * tb));
+    hipError_t e = hipMalloc(&ns, (size_t)ncap * TR * sizeof(float));
+    if (e == hipSuccess) e = hipMalloc(&ni, (size_t)ncap * TR * sizeof(uint32_t));
+    if (e != hipSuccess) {
+        (void)hipFree(nd);
+        if (ns) (void)hipFree(ns);
+        HIP_CHECK(e);
+    }
+    HIP_CHECK(hipMemsetAsync(nd, 0, (size_t)ncap * tb, ix->own));
+    HIP_CHECK(hipMemsetAsync(ns, 0, (size_t)ncap * TR * sizeof(float), ix->own));
+    HIP_CHECK(hipMemsetAsync(ni, 0xFF, (size_t)ncap * TR * sizeof(uint32_t), ix->own));
+    if (ix->used_pages > 0) {
+        HIP_CHECK(hipMemcpyAsync(nd, ix->data, (size_t)ix->used_pages * tb, hipMemcpyDeviceToDevice, ix->own));
+        HIP_CHECK(hipMemcpyAsync(ns, ix->sqn, (size_t)ix->used_pages * TR * sizeof(float), hipMemcpyDeviceToDevice,
+                                 ix->own));
+        HIP_CHECK(hipMemcpyAsync(ni, ix->slot_id, (size_t)ix->used_pages * TR * sizeof(uint32_t),
+                                 hipMemcpyDeviceToDevice, ix->own));
+    }
+    HIP_CHECK(hipStreamSynchronize(ix->own));
+    if (ix->data) (void)hipFree(ix->data);
+    if (ix->sqn) (void)hipFree(ix->sqn);
+    if (ix->slot_id) (void)hipFree(ix->slot_id);
+    ix->data = nd;
+    ix->sqn = ns;
+    ix->slot_id = ni;
+    ix->cap_pages = ncap;
+}
+
+void refresh_maxsq(vs_ivf* ix) {
+    unsigned bits = 0;
+    HIP_CHECK(hipMemcpyAsync(&bits, ix->d_flags, sizeof(unsigned), hipMemcpyDeviceToHost, ix->own));
+    HIP_CHECK(hipStreamSynchronize(ix->own));
+    std::memcpy(&ix->maxsq, &bits, 4);
+}
+
+void upload_csr(vs_ivf* ix, hipStream_t st) {
+    if (!ix->csr_dirty) return;
+    std::vector<int> off(ix->nlist + 1, 0), flat;
+    for (int l = 0; l < ix->nlist; ++l) {
+        off[l + 1] = off[l] + (int)ix->pages[l].size();
+        flat.insert(flat.end(), ix->pages[l].begin(), ix->pages[l].end());
+    }
+    if (flat.empty()) flat.push_back(0);
+    ix->d_page_off.ensure(off.size() * sizeof(int));
+    ix->d_list_pages.ensure(flat.size() * sizeof(int));
+    ix->d_list_n.ensure((size_t)ix->nlist * sizeof(int64_t));
+    HIP_CHECK(hipMemcpyAsync(ix->d_page_off.p, off.data(), off.size() * sizeof(int), hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipMemcpyAsync(ix->d_list_pages.p, flat.data(), flat.size() * sizeof(int), hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipMemcpyAsync(ix->d_list_n.p, ix->list_n.data(), (size_t)ix->nlist * sizeof(int64_t),
+                             hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipStreamSynchronize(st));  // host vectors above are temporaries
+    ix->csr_dirty = false;
+}
+
+// list id of every row: exact best centroid (fill(r0, m, dst) writes rows r0.. as device fp32)
+template <typename Fill>
+void assign_rows(vs_ivf* ix, int64_t n, Fill&& fill, int64_t* lists_host) {
+    const int64_t rpc = rows_per_chunk(ix->d);
+    ix->tmp_rows.ensure((size_t)std::min(n, rpc) * ix->d * sizeof(float));
+    ix->assign_ids.ensure((size_t)std::min(n, rpc) * sizeof(int64_t));
+    for (int64_t r0 = 0; r0 < n; r0 += rpc) {
+        const int64_t m = std::min(rpc, n - r0);
+        fill(r0, m, ix->tmp_rows.as<float>());
+        search_exact_device(ix->coarse, ix->tmp_rows.as<float>(), m, 1, ix->assign_ids.as<int64_t>(), nullptr, ix->own);
+        HIP_CHECK(hipMemcpyAsync(lists_host + r0, ix->assign_ids.p, (size_t)m * sizeof(int64_t),
+                                 hipMemcpyDeviceToHost, ix->own));
+        HIP_CHECK(hipStreamSynchronize(ix->own));
+    }
+}
+
+template <typename Fill>
+void add_rows(vs_ivf* ix, int64_t n, Fill&& fill) {
+    if (!ix->trained) throw VsError(VS_ERR_ARG, "IVF index is not trained (set its centroids first)");
+    if (ix->ntotal + n > (int64_t)0xFFFFFFF0LL) throw VsError(VS_ERR_ARG, "IVF index exceeds 2^32 rows");
+    std::vector<int64_t> lists((size_t)n);
+    assign_rows(ix, n, fill, lists.data());
+    // destinations: append to each list's last page, new pages from the pool (committed at the end)
+    std::vector<std::vector<int>> pages = ix->pages;
+    std::vector<int64_t> list_n = ix->list_n;
+    int64_t used = ix->used_pages;
+    std::vector<int64_t> slot((size_t)n);
+    for (int64_t r = 0; r < n; ++r) {
+        const int64_t l = lists[r];
+        if (l < 0 || l >= ix->nlist) throw VsError(VS_ERR_INTERNAL, "coarse assignment out of range");
+        if (list_n[l] % TR == 0) {
+            if (used >= (int64_t)1 << 31) throw VsError(VS_ERR_ARG, "IVF page pool exceeds 2^31 pages");
+            pages[l].push_back((int)used++);
+        }
+        slot[r] = (int64_t)pages[l].back() * TR + list_n[l] % TR;
+        ++list_n[l];
+    }
+    ensure_pages(ix, used);
+    const int64_t rpc = rows_per_chunk(ix->d);
+    ix->slots.ensure((size_t)std::min(n, rpc) * sizeof(int64_t));
+    for (int64_t r0 = 0; r0 < n; r0 += rpc) {
+        const int64_t m = std::min(rpc, n - r0);
+        fill(r0, m, ix->tmp_rows.as<float>());
+        HIP_CHECK(hipMemcpyAsync(ix->slots.p, slot.data() + r0, (size_t)m * sizeof(int64_t), hipMemcpyHostToDevice,
+                                 ix->own));
+        HIP_CHECK(launch_pack_rows_map(ix->dtype, ix->tmp_rows.as<float>(), m, ix->d, ix->dpad, ix->data,
+                                       ix->slots.as<int64_t>(), ix->sqn, ix->d_flags, ix->slot_id, ix->ntotal + r0,
+                                       ix->own));
+        HIP_CHECK(hipStreamSynchronize(ix->own));  // slot staging reuse
+    }
+    ix->pages.swap(pages);
+    ix->list_n.swap(list_n);
+    ix->used_pages = used;
+    ix->id_slot.insert(ix->id_slot.end(), slot.begin(), slot.end());
+    ix->ntotal += n;
+    ix->csr_dirty = true;
+    refresh_maxsq(ix);
+}
+
+// one search pass at screening depth Kp; outputs device [nq][k]; cert_dev [nq]
+void search_core(vs_ivf* ix, const float* q_dev, int64_t nq, int k, int nprobe, int Kp, float* D, int64_t* I,
+                 double* S64, int* cert_dev, hipStream_t st) {
+    // 1. probes: exact top-nprobe centroids of every query
+    ix->probes.ensure((size_t)nq * nprobe * sizeof(int64_t));
+    search_exact_device(ix->coarse, q_dev, nq, nprobe, ix->probes.as<int64_t>(), nullptr, st);
+    ix->probes_h.resize((size_t)nq * nprobe);
+    HIP_CHECK(hipMemcpyAsync(ix->probes_h.data(), ix->probes.p, ix->probes_h.size() * sizeof(int64_t),
+                             hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    // 2. work items (list, page range, <= IVF_QG queries), grouped by query-count class
+    std::vector<std::vector<int>> lq((size_t)ix->nlist);
+    for (int64_t q = 0; q < nq; ++q)
+        for (int p = 0; p < nprobe; ++p) {
+            const int64_t l = ix->probes_h[(size_t)q * nprobe + p];
+            if (l < 0 || l >= ix->nlist) throw VsError(VS_ERR_INTERNAL, "probe out of range");
+            lq[l].push_back((int)q);
+        }
+    const int classes[4] = {1, 2, 4, IVF_QG};
+    std::vector<int> cls_items[4];
+    std::vector<int> per_q((size_t)nq, 0);
+    double bytes = 0.0;
+    for (int l = 0; l < ix->nlist; ++l) {
+        const int nql = (int)lq[l].size();
+        const int np = (int)ix->pages[l].size();
+        if (nql == 0 || np == 0) continue;
+        for (int g0 = 0; g0 < nql; g0 += IVF_QG) {
+            const int gq = std::min(IVF_QG, nql - g0);
+            const int c = gq <= 1 ? 0 : gq <= 2 ? 1 : gq <= 4 ? 2 : 3;
+            for (int pb = 0; pb < np; pb += kPagesPerItem) {
+                const int pe = std::min(np, pb + kPagesPerItem);
+                std::vector<int>& v = cls_items[c];
+                v.push_back(l);
+                v.push_back(pb);
+                v.push_back(pe);
+                v.push_back(gq);
+                for (int j = 0; j < IVF_QG; ++j) v.push_back(j < gq ? lq[l][g0 + j] : -1);
+                for (int j = 0; j < gq; ++j) ++per_q[lq[l][g0 + j]];
+                const int64_t rows = std::min<int64_t>(ix->list_n[l] - (int64_t)pb * TR, (int64_t)(pe - pb) * TR);
+                bytes += (double)rows * ix->d * ix->es;
+            }
+        }
+    }
+    int max_items = 1;
+    for (int v : per_q) max_items = std::max(max_items, v);
+    const int lcap = max_items * Kp;
+    size_t total_ints = 0;
+    for (auto& v : cls_items) total_ints += v.size();
+    ix->items.ensure(std::max<size_t>(total_ints, 1) * sizeof(int));
+    {
+        std::vector<int> all;
+        all.reserve(total_ints);
+        for (auto& v : cls_items) all.insert(all.end(), v.begin(), v.end());
+        if (!all.empty())
+            HIP_CHECK(hipMemcpyAsync(ix->items.p, all.data(), all.size() * sizeof(int), hipMemcpyHostToDevice, st));
+        upload_csr(ix, st);  // synchronises the stream, so `all` may go out of scope
+    }
+    // 3. queries fp32 padded, ||q|| for the certificate
+    ix->qp.ensure((size_t)nq * ix->dpad * sizeof(float));
+    ix->qinfo.ensure((size_t)nq * 2 * sizeof(float));
+    HIP_CHECK(launch_pack_qf32(q_dev, (int)nq, (int)nq, ix->d, ix->dpad, ix->qp.as<float>(), ix->qinfo.as<float>(), st));
+    // 4. list scans
+    ix->glist.ensure((size_t)nq * lcap * sizeof(u64));
+    ix->gcnt.ensure((size_t)nq * sizeof(int));
+    HIP_CHECK(hipMemsetAsync(ix->gcnt.p, 0, (size_t)nq * sizeof(int), st));
+    IvfScanArgs a{};
+    a.data = ix->data;
+    a.sqn = ix->sqn;
+    a.qp = ix->qp.as<float>();
+    a.list_pages = ix->d_list_pages.as<int>();
+    a.page_off = ix->d_page_off.as<int>();
+    a.list_n = ix->d_list_n.as<int64_t>();
+    a.dpad = ix->dpad;
+    a.metric = ix->metric;
+    a.Kp = Kp;
+    a.cap = (int)round_up(Kp + 2 * TR, 256);
+    a.glist = ix->glist.as<u64>();
+    a.gcnt = ix->gcnt.as<int>();
+    a.lcap = lcap;
+    const int max_grid = ix->num_cu * 4;
+    ix->cand.ensure((size_t)max_grid * IVF_QG * a.cap * sizeof(u64));
+    a.cand = ix->cand.as<u64>();
+    const bool timing = ix->timing.load();
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (timing) {
+        HIP_CHECK(hipEventCreate(&e0));
+        HIP_CHECK(hipEventCreate(&e1));
+        HIP_CHECK(hipEventRecord(e0, st));
+    }
+    size_t off = 0;
+    for (int c = 0; c < 4; ++c) {
+        const int n_items = (int)(cls_items[c].size() / IVF_ITEM_INTS);
+        a.items = ix->items.as<int>() + off;
+        a.n_items = n_items;
+        off += cls_items[c].size();
+        if (n_items == 0) continue;
+        HIP_CHECK(launch_ivf_scan(ix->dtype, classes[c], a, std::min(n_items, max_grid), st));
+    }
+    if (timing) {
+        HIP_CHECK(hipEventRecord(e1, st));
+        ix->tev.emplace_back(e0, e1);
+        ix->tbytes.push_back(bytes);
+    }
+    // 5. exact refine over each query's candidate list (slots -> user ids)
+    RefineArgs r{};
+    r.cand = ix->glist.as<u64>();
+    r.cand_n = ix->gcnt.as<int>();
+    r.lcap = lcap;
+    r.Kp = Kp;
+    r.q = q_dev;
+    r.d = ix->d;
+    r.dpad = ix->dpad;
+    r.dt = ix->dtype;
+    r.metric = ix->metric;
+    r.corpus = ix->data;
+    r.qinfo = ix->qinfo.as<float>();
+    r.xmax = (float)(std::sqrt((double)ix->maxsq) * (1.0 + 1e-5)) + 1e-30f;
+    r.gamma = gamma_of(ix->d);
+    r.k = k;
+    r.n_valid = ix->ntotal;
+    r.id_offset = 0;
+    r.D = D;
+    r.I = I;
+    r.S64 = S64;
+    r.cert = cert_dev;
+    r.uncert = ix->d_flags + 1;
+    r.optimistic = 0;
+    r.idmap = ix->slot_id;
+    HIP_CHECK(launch_refine(r, (int)nq, st));
+}
+
+void fill_padding(vs_ivf* ix, int64_t nq, int k, float* D, int64_t* I, double* S64, hipStream_t st) {
+    const size_t n = (size_t)nq * k;
+    std::vector<int64_t> hi(n, -1);
+    HIP_CHECK(hipMemcpyAsync(I, hi.data(), n * sizeof(int64_t), hipMemcpyHostToDevice, st));
+    if (D) {
+        std::vector<float> hd(n, ix->metric == VS_METRIC_IP ? -3.402823466e+38f : 3.402823466e+38f);
+        HIP_CHECK(hipMemcpyAsync(D, hd.data(), n * sizeof(float), hipMemcpyHostToDevice, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+    }
+    if (S64) {
+        std::vector<double> hs(n, ix->metric == VS_METRIC_IP ? -1.7976931348623157e308 : 1.7976931348623157e308);
+        HIP_CHECK(hipMemcpyAsync(S64, hs.data(), n * sizeof(double), hipMemcpyHostToDevice, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+    }
+    HIP_CHECK(hipStreamSynchronize(st));
+}
+
+// full search with certificate retries (caller holds the locks)
+void search_locked(vs_ivf* ix, const float* q_dev, int64_t nq, int k, int nprobe, float* D, int64_t* I, double* S64,
+                   hipStream_t st) {
+    if (ix->ntotal == 0) {
+        fill_padding(ix, nq, k, D, I, S64, st);
+        return;
+    }
+    nprobe = std::min(nprobe, ix->nlist);
+    const int Kp = screen_depth(k);
+    ix->cert.ensure((size_t)nq * sizeof(int));
+    search_core(ix, q_dev, nq, k, nprobe, Kp, D, I, S64, ix->cert.as<int>(), st);
+    ix->cert_h.resize((size_t)nq);
+    HIP_CHECK(hipMemcpyAsync(ix->cert_h.data(), ix->cert.p, (size_t)nq * sizeof(int), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    std::vector<int> cert = ix->cert_h;
+    for (int64_t qi = 0; qi < nq; ++qi) {
+        int Kr = Kp;
+        while (!cert[qi]) {
+            if (Kr >= KP_MAX) throw VsError(VS_ERR_UNCERTIFIED, "exactness certificate failed at maximum screening depth");
+            Kr = std::min(Kr * 4, KP_MAX);
+            search_core(ix, q_dev + qi * ix->d, 1, k, nprobe, Kr, D ? D + qi * k : nullptr, I + qi * k,
+                        S64 ? S64 + qi * k : nullptr, ix->cert.as<int>(), st);
+            HIP_CHECK(hipMemcpyAsync(&cert[qi], ix->cert.p, sizeof(int), hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipStreamSynchronize(st));
+        }
+    }
+}
+
+void check_search_args(const vs_ivf* ix, int64_t nq, int32_t k, int32_t nprobe) {
+    check_ivf(ix);
+    if (nq < 0) throw VsError(VS_ERR_ARG, "nq must be >= 0");
+    if (k <= 0) throw VsError(VS_ERR_ARG, "k must be > 0");
+    if (screen_depth(k) < k || k > KP_MAX * 4 / 5)
+        throw VsError(VS_ERR_ARG, "k too large (max " + std::to_string(KP_MAX * 4 / 5) + ")");
+    if (nprobe <= 0) throw VsError(VS_ERR_ARG, "nprobe must be > 0");
+    if (!ix->trained) throw VsError(VS_ERR_ARG, "IVF index is not trained (set its centroids first)");
+}
+
+}  // namespace
+
+extern "C" {
+
+int vs_ivf_create(int d, int nlist, int metric, int dtype, int device, vs_ivf** out) {
+    return guarded([&] {
+        if (!out) throw VsError(VS_ERR_ARG, "out is null");
+        *out = nullptr;
+        if (d <= 0) throw VsError(VS_ERR_ARG, "dimension must be > 0");
+        if (nlist <= 0) throw VsError(VS_ERR_ARG, "nlist must be > 0");
+        if (metric != VS_METRIC_IP && metric != VS_METRIC_L2) throw VsError(VS_ERR_ARG, "metric must be IP(0) or L2(1)");
+        if (dtype < VS_DTYPE_F32 || dtype > VS_DTYPE_F16) throw VsError(VS_ERR_ARG, "dtype must be 0 (f32), 1 (bf16), 2 (f16)");
+        vs_index* coarse = nullptr;
+        int rc = vs_create(d, metric, dtype, device, &coarse);
+        if (rc != VS_OK) throw VsError(rc, std::string("coarse quantizer: ") + vs_last_error());
+        vs_ivf* ix = new vs_ivf();
+        ix->coarse = coarse;
+        ix->d = d;
+        ix->dpad = (int)std::max<int64_t>(round_up(d, CH), 2 * CH);
+        ix->nlist = nlist;
+        ix->metric = metric;
+        ix->dtype = dtype;
+        ix->device = device;
+        ix->es = es_of(dtype);
+        ix->pages.resize((size_t)nlist);
+        ix->list_n.assign((size_t)nlist, 0);
+        try {
+            DeviceGuard dg(device);
+            hipDeviceProp_t prop;
+            HIP_CHECK(hipGetDeviceProperties(&prop, device));
+            ix->num_cu = prop.multiProcessorCount;
+            HIP_CHECK(hipStreamCreateWithFlags(&ix->own, hipStreamNonBlocking));
+            HIP_CHECK(hipMalloc(&ix->d_flags, sizeof(unsigned) * 2));
+            HIP_CHECK(hipMemset(ix->d_flags, 0, sizeof(unsigned) * 2));
+        } catch (...) {
+            vs_ivf_destroy(ix);
+            throw;
+        }
+        *out = ix;
+    });
+}
+
+void vs_ivf_destroy(vs_ivf* ix) {
+    if (!ix) return;
+    {
+        DeviceGuard dg(ix->device);
+        (void)hipDeviceSynchronize();
+        for (DevBuf* b : {&ix->d_page_off, &ix->d_list_pages, &ix->d_list_n, &ix->tmp_rows, &ix->slots, &ix->assign_ids,
+                          &ix->qdev, &ix->probes, &ix->items, &ix->qp, &ix->qinfo, &ix->cand, &ix->glist, &ix->gcnt,
+                          &ix->cert, &ix->outD, &ix->outI, &ix->rec})
+            b->release();
+        for (auto& pr : ix->tev) {
+            (void)hipEventDestroy(pr.first);
+            (void)hipEventDestroy(pr.second);
+        }
+        if (ix->data) (void)hipFree(ix->data);
+        if (ix->sqn) (void)hipFree(ix->sqn);
+        if (ix->slot_id) (void)hipFree(ix->slot_id);
+        if (ix->d_flags) (void)hipFree(ix->d_flags);
+        if (ix->own) (void)hipStreamDestroy(ix->own);
+    }
+    vs_destroy(ix->coarse);
+    delete ix;
+}
+
+int vs_ivf_set_centroids(vs_ivf* ix, const float* c) {
+    return guarded([&] {
+        check_ivf(ix);
+        if (!c) throw VsError(VS_ERR_ARG, "centroids are null");
+        std::unique_lock<std::shared_mutex> lk(ix->rw);
+        if (ix->ntotal > 0) throw VsError(VS_ERR_ARG, "IVF index is not empty: reset() before setting centroids");
+        int rc = vs_reset(ix->coarse);
+        if (rc == VS_OK) rc = vs_add(ix->coarse, c, ix->nlist);
+        if (rc != VS_OK) throw VsError(rc, std::string("coarse quantizer: ") + vs_last_error());
+        ix->trained = true;
+    });
+}
+
+int vs_ivf_get_centroids(vs_ivf* ix, float* out) {
+    return guarded([&] {
+        check_ivf(ix);
+        if (!out) throw VsError(VS_ERR_ARG, "out is null");
+        if (!ix->trained) throw VsError(VS_ERR_ARG, "IVF index is not trained (set its centroids first)");
+        const int rc = vs_reconstruct_n(ix->coarse, 0, ix->nlist, out);
+        if (rc != VS_OK) throw VsError(rc, vs_last_error());
+    });
+}
+
+int vs_ivf_is_trained(const vs_ivf* ix) { return ix ? (ix->trained ? 1 : 0) : -1; }
+
+int vs_ivf_assign(vs_ivf* ix, const float* x, int64_t n, int64_t* lists) {
+    return guarded([&] {
+        check_ivf(ix);
+        if (n < 0) throw VsError(VS_ERR_ARG, "n must be >= 0");
+        if (n == 0) return;
+        if (!x || !lists) throw VsError(VS_ERR_ARG, "null host buffer");
+        if (!ix->trained) throw VsError(VS_ERR_ARG, "IVF index is not trained (set its centroids first)");
+        std::unique_lock<std::shared_mutex> lk(ix->rw);  // shares the add workspaces
+        DeviceGuard dg(ix->device);
+        const int d = ix->d;
+        assign_rows(ix, n,
+                    [&](int64_t r0, int64_t m, float* dst) {
+                        HIP_CHECK(hipMemcpyAsync(dst, x + r0 * d, (size_t)m * d * sizeof(float), hipMemcpyHostToDevice,
+                                                 ix->own));
+                    },
+                    lists);
+    });
+}
+
+int vs_ivf_add(vs_ivf* ix, const float* x, int64_t n) {
+    return guarded([&] {
+        check_ivf(ix);
+        if (n < 0) throw VsError(VS_ERR_ARG, "n must be >= 0");
+        if (n == 0) return;
+        if (!x) throw VsError(VS_ERR_ARG, "x is null");
+        std::unique_lock<std::shared_mutex> lk(ix->rw);
+        DeviceGuard dg(ix->device);
+        const int d = ix->d;
+        add_rows(ix, n, [&](int64_t r0, int64_t m, float* dst) {
+            HIP_CHECK(hipMemcpyAsync(dst, x + r0 * d, (size_t)m * d * sizeof(float), hipMemcpyHostToDevice, ix->own));
+        });
+    });
+}
+
+int vs_ivf_add_synthetic(vs_ivf* ix, uint64_t seed, int64_t global_row0, int64_t n, int normalize) {
+    return guarded([&] {
+        check_ivf(ix);
+        if (n < 0 || global_row0 < 0) throw VsError(VS_ERR_ARG, "bad synthetic range");
+        if (n == 0) return;
+        std::unique_lock<std::shared_mutex> lk(ix->rw);
+        DeviceGuard dg(ix->device);
+        add_rows(ix, n, [&](int64_t r0, int64_t m, float* dst) {
+            // unrounded fp32 rows; k_pack_rows_map rounds to the index dtype exactly as k_synth_rows does
+            HIP_CHECK(launch_synth_f32(DT_F32, seed, global_row0 + r0, m, ix->d, normalize, dst, ix->own));
+        });
+    });
+}
+
+int vs_ivf_search_device(vs_ivf* ix, const float* q_dev, int64_t nq, int32_t k, int32_t nprobe, float* D_dev,
+                         int64_t* I_dev, double* S64_dev, void* stream) {
+    return guarded([&] {
+        check_search_args(ix, nq, k, nprobe);
+        if (nq == 0) return;
+        if (!q_dev || !I_dev) throw VsError(VS_ERR_ARG, "null device buffer");
+        std::shared_lock<std::shared_mutex> lk(ix->rw);
+        std::lock_guard<std::mutex> sg(ix->search_mtx);
+        DeviceGuard dg(ix->device);
+        search_locked(ix, q_dev, nq, k, nprobe, D_dev, I_dev, S64_dev, stream ? (hipStream_t)stream : ix->own);
+    });
+}
+
+int vs_ivf_search(vs_ivf* ix, const float* q, int64_t nq, int32_t k, int32_t nprobe, float* D, int64_t* I) {
+    return guarded([&] {
+        check_search_args(ix, nq, k, nprobe);
+        if (nq == 0) return;
+        if (!q || !D || !I) throw VsError(VS_ERR_ARG, "null host buffer");
+        std::shared_lock<std::shared_mutex> lk(ix->rw);
+        std::lock_guard<std::mutex> sg(ix->search_mtx);
+        DeviceGuard dg(ix->device);
+        hipStream_t st = ix->own;
+        ix->qdev.ensure((size_t)nq * ix->d * sizeof(float));
+        ix->outD.ensure((size_t)nq * k * sizeof(float));
+        ix->outI.ensure((size_t)nq * k * sizeof(int64_t));
+        HIP_CHECK(hipMemcpyAsync(ix->qdev.p, q, (size_t)nq * ix->d * sizeof(float), hipMemcpyHostToDevice, st));
+        search_locked(ix, ix->qdev.as<float>(), nq, k, nprobe, ix->outD.as<float>(), ix->outI.as<int64_t>(), nullptr,
+                      st);
+        HIP_CHECK(hipMemcpyAsync(D, ix->outD.p, (size_t)nq * k * sizeof(float), hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipMemcpyAsync(I, ix->outI.p, (size_t)nq * k * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+    });
+}
+
+int vs_ivf_reconstruct(vs_ivf* ix, int64_t id, float* out) {
+    return guarded([&] {
+        check_ivf(ix);
+        if (!out) throw VsError(VS_ERR_ARG, "out is null");
+        std::shared_lock<std::shared_mutex> lk(ix->rw);
+        if (id < 0 || id >= ix->ntotal) throw VsError(VS_ERR_ARG, "reconstruct id out of bounds");
+        std::lock_guard<std::mutex> sg(ix->search_mtx);
+        DeviceGuard dg(ix->device);
+        ix->rec.ensure((size_t)ix->d * sizeof(float));
+        HIP_CHECK(launch_unpack_rows(ix->dtype, ix->data, ix->id_slot[(size_t)id], 1, ix->d, ix->dpad,
+                                     ix->rec.as<float>(), ix->own));
+        HIP_CHECK(hipMemcpyAsync(out, ix->rec.p, (size_t)ix->d * sizeof(float), hipMemcpyDeviceToHost, ix->own));
+        HIP_CHECK(hipStreamSynchronize(ix->own));
+    });
+}
+
+int vs_ivf_list_sizes(vs_ivf* ix, int64_t* out) {
+    return guarded([&] {
+        check_ivf(ix);
+        if (!out) throw VsError(VS_ERR_ARG, "out is null");
+        std::shared_lock<std::shared_mutex> lk(ix->rw);
+        std::copy(ix->list_n.begin(), ix->list_n.end(), out);
+    });
+}
+
+int vs_ivf_reset(vs_ivf* ix) {
+    return guarded([&] {
+        check_ivf(ix);
+        std::unique_lock<std::shared_mutex> lk(ix->rw);
+        DeviceGuard dg(ix->device);
+        for (auto& p : ix->pages) p.clear();
+        std::fill(ix->list_n.begin(), ix->list_n.end(), 0);
+        ix->id_slot.clear();
+        ix->used_pages = 0;
+        ix->ntotal = 0;
+        ix->maxsq = 0.0f;
+        ix->csr_dirty = true;
+        HIP_CHECK(hipMemsetAsync(ix->d_flags, 0, sizeof(unsigned), ix->own));
+        HIP_CHECK(hipStreamSynchronize(ix->own));
+    });
+}
+
+int64_t vs_ivf_ntotal(const vs_ivf* ix) { return ix ? ix->ntotal : -1; }
+int vs_ivf_nlist(const vs_ivf* ix) { return ix ? ix->nlist : -1; }
+
+int vs_ivf_set_timing(vs_ivf* ix, int enable) {
+    return guarded([&] {
+        check_ivf(ix);
+        ix->timing.store(enable != 0);
+    });
+}
+
+int vs_ivf_timing_fetch(vs_ivf* ix, float* ms, double* bytes_scanned, int cap) {
+    int count = 0;
+    int rc = guarded([&] {
+        check_ivf(ix);
+        std::lock_guard<std::mutex> sg(ix->search_mtx);
+        DeviceGuard dg(ix->device);
+        for (size_t i = 0; i < ix->tev.size(); ++i) {
+            auto& pr = ix->tev[i];
+            HIP_CHECK(hipEventSynchronize(pr.second));
+            float t = 0.0f;
+            HIP_CHECK(hipEventElapsedTime(&t, pr.first, pr.second));
+            if (count < cap) {
+                if (ms) ms[count] = t;
+                if (bytes_scanned) bytes_scanned[count] = ix->tbytes[i];
+            }
+            ++count;
+            (void)hipEventDestroy(pr.first);
+            (void)hipEventDestroy(pr.second);
+        }
+        ix->tev.clear();
+        ix->tbytes.clear();
+    });
+    return rc == VS_OK ? std::min(count, cap) : rc;
+}
+
+}  // extern "C"

@@ -310,6 +310,33 @@ __global__ void __launch_bounds__(256) k_pack_rows(const float* __restrict__ src
     }
 }
 
+// IVF ingest: the same packing into an arbitrary storage slot per row (list pages), recording
+// the row's user id in slot_id
+template <int DT>
+__global__ void __launch_bounds__(256) k_pack_rows_map(const float* __restrict__ src, int64_t n, int d, int dpad,
+                                                        uint8_t* __restrict__ data, const int64_t* __restrict__ slots,
+                                                        float* __restrict__ sqn, unsigned* __restrict__ maxsq,
+                                                        uint32_t* __restrict__ slot_id, int64_t id0) {
+    constexpr int ES = DT == DT_F32 ? 4 : 2;
+    const int lane = threadIdx.x & 63;
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= n) return;
+    const float* s = src + r * (int64_t)d;
+    const int64_t row = slots[r];
+    float ss = 0.0f;
+    for (int i = lane; i < dpad; i += 64) {
+        float v = i < d ? s[i] : 0.0f;
+        float st = round_store<DT>(v, data + tiled_off(row, i, dpad, ES));
+        ss = fmaf(st, st, ss);
+    }
+    ss = wave_sum_fp32_canon(ss);
+    if (lane == 0) {
+        sqn[row] = ss;
+        slot_id[row] = (uint32_t)(id0 + r);
+        atomicMax(maxsq, __float_as_uint(ss));
+    }
+}
+
 template <int DT>
 __global__ void __launch_bounds__(256) k_synth_rows(uint64_t base, int64_t grow0, int64_t n, int d, int dpad,
                                                      uint8_t* __restrict__ data, int64_t lrow0, int normalize,
@@ -1224,6 +1251,158 @@ __global__ void __launch_bounds__(256) k_screen_gemv(ScreenArgs a, const float* 
 }
 
 // ------------------------------------------------------------------------------------------------
+// K6: IVF list scan -- the GEMV screen over the pages of one inverted list for the (few) queries
+// that probe it.  At batch 256 / nprobe 32 / nlist 4096 a list is probed by ~2 queries, so each
+// corpus byte feeds ~2 query dot products: HBM streaming, fp32 FMA, no MFMA.  256 threads,
+// persistent over work items (list, page range, <= NQ queries); per (item, query) the best Kp
+// keys (screen score, storage slot) are appended to the query's candidate list for k_refine.
+// ------------------------------------------------------------------------------------------------
+template <int DT, int NQ>
+__global__ void __launch_bounds__(256) k_ivf_scan(IvfScanArgs a) {
+    constexpr int ES = DT == DT_F32 ? 4 : 2;
+    constexpr int CB = CH * ES;
+    constexpr int LPR = CB / 16;
+    constexpr int RPI = 64 / LPR;
+    constexpr int EPU = 16 / ES;
+    constexpr int RG = 64 / RPI;
+    constexpr int RB0 = (NQ <= 2) ? 8 : 4;
+    constexpr int RB = RB0 < RG ? RB0 : RG;
+    static_assert(RG % RB == 0, "row groups");
+
+    __shared__ u64 thr_key[NQ];
+    __shared__ float thr_f[NQ];
+    __shared__ int cnt[NQ];
+    __shared__ int qid[NQ];
+    __shared__ int red[8];
+    __shared__ int off_s;
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int unit = lane % LPR, rsub = lane / LPR;
+    const int nch = a.dpad / CH;
+    const int64_t tbytes = (int64_t)TR * a.dpad * ES;
+    u64* cand = a.cand + (size_t)blockIdx.x * NQ * a.cap;
+    const int trigger = a.cap - TR;
+
+    for (int it = blockIdx.x; it < a.n_items; it += gridDim.x) {
+        const int* itm = a.items + (size_t)it * IVF_ITEM_INTS;
+        const int l = itm[0], p0 = itm[1], p1 = itm[2], nqi = itm[3];
+        __syncthreads();  // the previous item's buffers are flushed
+        if (tid < NQ) {
+            const bool real = tid < nqi;
+            thr_key[tid] = real ? 0ull : ~0ull;
+            thr_f[tid] = real ? -INFINITY : INFINITY;
+            cnt[tid] = 0;
+            qid[tid] = real ? itm[4 + tid] : itm[4];
+        }
+        __syncthreads();
+        const int64_t ln = a.list_n[l];
+        const int pbase = a.page_off[l];
+        for (int p = p0; p < p1; ++p) {
+            const int64_t page = a.list_pages[pbase + p];
+            const int nvalid = (int)(ln - (int64_t)p * TR < TR ? ln - (int64_t)p * TR : TR);
+            const uint8_t* tb = a.data + page * tbytes;
+            const int64_t slot0 = page * TR;
+            for (int gb = 0; gb < RG / RB; ++gb) {
+                float acc[RB][NQ];
+#pragma unroll
+                for (int r = 0; r < RB; ++r)
+#pragma unroll
+                    for (int qi = 0; qi < NQ; ++qi) acc[r][qi] = 0.0f;
+#pragma unroll 2
+                for (int c = 0; c < nch; ++c) {
+                    float qv[NQ][EPU];
+#pragma unroll
+                    for (int qi = 0; qi < NQ; ++qi) {
+                        const float4* qs = (const float4*)(a.qp + (int64_t)qid[qi] * a.dpad + c * CH + unit * EPU);
+#pragma unroll
+                        for (int h = 0; h < EPU / 4; ++h) {
+                            float4 t = qs[h];
+                            qv[qi][4 * h + 0] = t.x; qv[qi][4 * h + 1] = t.y;
+                            qv[qi][4 * h + 2] = t.z; qv[qi][4 * h + 3] = t.w;
+                        }
+                    }
+                    uint4 raw[RB];
+#pragma unroll
+                    for (int r = 0; r < RB; ++r) {
+                        const int rit = wid * 64 + (gb * RB + r) * RPI + rsub;
+                        raw[r] = *(const uint4*)(tb + (int64_t)c * TR * CB + rit * CB + unit * 16);
+                    }
+#pragma unroll
+                    for (int r = 0; r < RB; ++r) {
+                        float xv[EPU];
+                        unpack16<DT>(raw[r], xv);
+#pragma unroll
+                        for (int qi = 0; qi < NQ; ++qi)
+#pragma unroll
+                            for (int e = 0; e < EPU; ++e) acc[r][qi] = fmaf(xv[e], qv[qi][e], acc[r][qi]);
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < RB; ++r)
+#pragma unroll
+                    for (int qi = 0; qi < NQ; ++qi) {
+                        float v = acc[r][qi];
+#pragma unroll
+                        for (int s = 1; s < LPR; s <<= 1) v += __shfl_xor(v, s, 64);
+                        acc[r][qi] = v;
+                    }
+                if (unit == 0) {
+#pragma unroll
+                    for (int r = 0; r < RB; ++r) {
+                        const int rit = wid * 64 + (gb * RB + r) * RPI + rsub;
+                        if (rit >= nvalid) continue;  // page padding of the list's last page
+                        const int64_t slot = slot0 + rit;
+                        const float sq = a.metric == METRIC_L2 ? a.sqn[slot] : 0.0f;
+#pragma unroll
+                        for (int qi = 0; qi < NQ; ++qi) {
+                            float sc = acc[r][qi];
+                            if (a.metric == METRIC_L2) sc = 2.0f * sc - sq;
+                            if (sc >= thr_f[qi]) {
+                                const u64 key = mk_key(sc, (uint32_t)slot);
+                                if (key > thr_key[qi]) {
+                                    const int s = atomicAdd(&cnt[qi], 1);
+                                    if (s < a.cap) cand[(size_t)qi * a.cap + s] = key;
+                                }
+                            }
+                        }
+                    }
+                }
+            }
+            __syncthreads();
+            for (int qi = 0; qi < nqi; ++qi) {
+                const int n = cnt[qi];
+                if (n > trigger) {  // block-uniform
+                    u64* buf = cand + (size_t)qi * a.cap;
+                    const u64 t = block_kth_mem(buf, n, a.Kp, red);
+                    block_compact_mem(buf, buf, n, t, red);
+                    if (tid == 0) {
+                        thr_key[qi] = t;
+                        thr_f[qi] = key_score(t);
+                        cnt[qi] = a.Kp;
+                    }
+                    __syncthreads();
+                }
+            }
+        }
+        __syncthreads();
+        // flush: the item's best <= Kp keys per query, appended to the query's candidate list
+        for (int qi = 0; qi < nqi; ++qi) {
+            u64* buf = cand + (size_t)qi * a.cap;
+            int n = cnt[qi] < a.cap ? cnt[qi] : a.cap;
+            if (n > a.Kp) {
+                const u64 t = block_kth_mem(buf, n, a.Kp, red);
+                n = block_compact_mem(buf, buf, n, t, red);
+            }
+            if (tid == 0) off_s = n ? atomicAdd(&a.gcnt[qid[qi]], n) : 0;
+            __syncthreads();
+            u64* dst = a.glist + (size_t)qid[qi] * a.lcap + off_s;
+            for (int j = tid; j < n; j += 256) dst[j] = buf[j];
+            __syncthreads();
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // K3: merge of partial candidate lists (block-wide selection)
 // ------------------------------------------------------------------------------------------------
 constexpr int MERGE_E = 16;  // 4096 keys per block
@@ -1455,12 +1634,12 @@ __global__ void __launch_bounds__(RF_THREADS) k_refine(RefineArgs a, int KP2) {
         const uint32_t id1 = j2 < nv ? key_id(cq[j2]) : 0u;
         double s0, s1;
         exact_score_q2<DT, METRIC, QLDS>(a.corpus, id0, j2 < nv ? (int64_t)id1 : -1, qs, qv, a.d, a.dpad, lane, s0, s1);
-        if (lane == 0) {
+        if (lane == 0) {  // keys carry storage slots; IVF maps them to user ids (sort + output)
             sc[j] = s0;
-            ids[j] = id0;
+            ids[j] = a.idmap ? a.idmap[id0] : id0;
             if (j2 < nv) {
                 sc[j2] = s1;
-                ids[j2] = id1;
+                ids[j2] = a.idmap ? a.idmap[id1] : id1;
             }
         }
     }
@@ -1896,6 +2075,33 @@ hipError_t launch_seed_select(const float* seedmax, int M, int nq, int rank, u64
         hipLaunchKernelGGL(k_seed_select<2 * SEED_VPT>, grid, dim3(256), 0, st, seedmax, M, nq, rank, thr0);
     else
         return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+hipError_t launch_pack_rows_map(int dt, const float* src, int64_t n, int d, int dpad, uint8_t* data,
+                                const int64_t* slots, float* sqn, unsigned* maxsq, uint32_t* slot_id, int64_t id0,
+                                hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    VS_DISPATCH_DT(dt, k_pack_rows_map, dim3(blocks4(n)), dim3(256), 0, st, src, n, d, dpad, data, slots, sqn, maxsq,
+                   slot_id, id0);
+    return hipGetLastError();
+}
+
+template <int DT>
+static void launch_ivf_scan_dt(int nq_class, const IvfScanArgs& a, int grid, hipStream_t st) {
+    switch (nq_class) {
+        case 1: hipLaunchKernelGGL((k_ivf_scan<DT, 1>), dim3(grid), dim3(256), 0, st, a); break;
+        case 2: hipLaunchKernelGGL((k_ivf_scan<DT, 2>), dim3(grid), dim3(256), 0, st, a); break;
+        case 4: hipLaunchKernelGGL((k_ivf_scan<DT, 4>), dim3(grid), dim3(256), 0, st, a); break;
+        default: hipLaunchKernelGGL((k_ivf_scan<DT, IVF_QG>), dim3(grid), dim3(256), 0, st, a); break;
+    }
+}
+hipError_t launch_ivf_scan(int dt, int nq_class, const IvfScanArgs& a, int grid, hipStream_t st) {
+    if (a.n_items <= 0 || grid <= 0) return hipSuccess;
+    if (nq_class != 1 && nq_class != 2 && nq_class != 4 && nq_class != IVF_QG) return hipErrorInvalidValue;
+    if (dt == DT_F32) launch_ivf_scan_dt<DT_F32>(nq_class, a, grid, st);
+    else if (dt == DT_BF16) launch_ivf_scan_dt<DT_BF16>(nq_class, a, grid, st);
+    else launch_ivf_scan_dt<DT_F16>(nq_class, a, grid, st);
     return hipGetLastError();
 }
 
