@@ -109,7 +109,7 @@ int64_t vs_uncertified_count(vs_index* index);   /* synchronises the device coun
  * .train -> vs_ivf_set_centroids (k-means runs in the Python layer over vs_ivf_assign),
  * .add -> vs_ivf_add, .search with .nprobe -> vs_ivf_search, .reconstruct -> vs_ivf_reconstruct.
  * Semantics (made exact, oracle/ivf_oracle.py): rows go to their exact best centroid (ties ->
- * lower list id); a query probes its exact top-nprobe centroids and gets the exact top-k of the
+ * lower list id) by its stored (dtype-rounded) values; a query probes its exact top-nprobe centroids and gets the exact top-k of the
  * rows of those lists (canonical fp64 score, ties -> lower id; -1 / worst-score padding).
  * Ids are insertion order 0..ntotal-1, as for the flat index.  Searches on one handle are
  * serialised; add/reset take an exclusive lock. */
@@ -120,7 +120,7 @@ void vs_ivf_destroy(vs_ivf* ivf);
 int vs_ivf_set_centroids(vs_ivf* ivf, const float* c);        /* host nlist x d; only while empty */
 int vs_ivf_get_centroids(vs_ivf* ivf, float* out);            /* host nlist x d, values as stored */
 int vs_ivf_is_trained(const vs_ivf* ivf);
-int vs_ivf_assign(vs_ivf* ivf, const float* x, int64_t n, int64_t* lists); /* host in / out */
+int vs_ivf_assign(vs_ivf* ivf, const float* x, int64_t n, int64_t* lists); /* host; by the rows' dtype-rounded values */
 int vs_ivf_add(vs_ivf* ivf, const float* x, int64_t n);       /* host fp32 n x d */
 int vs_ivf_add_synthetic(vs_ivf* ivf, uint64_t seed, int64_t global_row0, int64_t n, int normalize);
 int vs_ivf_search(vs_ivf* ivf, const float* q, int64_t nq, int32_t k, int32_t nprobe, float* D, int64_t* I);

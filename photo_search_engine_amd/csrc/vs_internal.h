@@ -215,6 +215,7 @@ struct IvfScanArgs {
     int lcap;
 };
 hipError_t launch_ivf_scan(int dt, int nq_class, const IvfScanArgs& a, int grid, hipStream_t st);
+hipError_t launch_round_f32(int dt, float* x, int64_t n, hipStream_t st);  // in place, to the dtype's values
 // pack fp32 rows into the slots slots[r] (slot_id[slot] = id0 + r); sqn / maxsq as k_pack_rows
 hipError_t launch_pack_rows_map(int dt, const float* src, int64_t n, int d, int dpad, uint8_t* data,
                                 const int64_t* slots, float* sqn, unsigned* maxsq, uint32_t* slot_id, int64_t id0,

@@ -128,7 +128,8 @@ void upload_csr(vs_ivf* ix, hipStream_t st) {
     ix->csr_dirty = false;
 }
 
-// list id of every row: exact best centroid (fill(r0, m, dst) writes rows r0.. as device fp32)
+// list id of every row: exact best centroid of its stored (dtype-rounded) values
+// (fill(r0, m, dst) writes rows r0.. as device fp32)
 template <typename Fill>
 void assign_rows(vs_ivf* ix, int64_t n, Fill&& fill, int64_t* lists_host) {
     const int64_t rpc = rows_per_chunk(ix->d);
@@ -137,6 +138,8 @@ void assign_rows(vs_ivf* ix, int64_t n, Fill&& fill, int64_t* lists_host) {
     for (int64_t r0 = 0; r0 < n; r0 += rpc) {
         const int64_t m = std::min(rpc, n - r0);
         fill(r0, m, ix->tmp_rows.as<float>());
+        // a row goes to the best centroid of its STORED values (the dtype-rounded row)
+        HIP_CHECK(launch_round_f32(ix->dtype, ix->tmp_rows.as<float>(), m * ix->d, ix->own));
         search_exact_device(ix->coarse, ix->tmp_rows.as<float>(), m, 1, ix->assign_ids.as<int64_t>(), nullptr, ix->own);
         HIP_CHECK(hipMemcpyAsync(lists_host + r0, ix->assign_ids.p, (size_t)m * sizeof(int64_t),
                                  hipMemcpyDeviceToHost, ix->own));

@@ -337,6 +337,13 @@ __global__ void __launch_bounds__(256) k_pack_rows_map(const float* __restrict__
     }
 }
 
+// round fp32 values to the storage dtype in place (IVF: rows are assigned by their stored values)
+template <int DT>
+__global__ void __launch_bounds__(256) k_round_f32(float* __restrict__ x, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) x[i] = round_only<DT>(x[i]);
+}
+
 template <int DT>
 __global__ void __launch_bounds__(256) k_synth_rows(uint64_t base, int64_t grow0, int64_t n, int d, int dpad,
                                                      uint8_t* __restrict__ data, int64_t lrow0, int normalize,
@@ -915,13 +922,16 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
                     }
             }
             if (!full) {  // last tile of the shard: padding rows never qualify
+                // NaN, not -inf: fmaxf skips it and every `>= threshold` test fails, even against
+                // the unseeded threshold -inf (a -inf padding key would enter the candidates and
+                // be rescored exactly as 0, beating a query's all-negative real scores)
 #pragma unroll
                 for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
                         if (rowbase + rid0 + mi * 16 + r >= a.n_valid)
 #pragma unroll
-                            for (int ni = 0; ni < 8; ++ni) acc[mi][ni][r] = -INFINITY;
+                            for (int ni = 0; ni < 8; ++ni) acc[mi][ni][r] = __builtin_nanf("");
             }
 #pragma unroll
             for (int ni = 0; ni < 8; ++ni) {
@@ -2084,6 +2094,14 @@ hipError_t launch_pack_rows_map(int dt, const float* src, int64_t n, int d, int 
     if (n <= 0) return hipSuccess;
     VS_DISPATCH_DT(dt, k_pack_rows_map, dim3(blocks4(n)), dim3(256), 0, st, src, n, d, dpad, data, slots, sqn, maxsq,
                    slot_id, id0);
+    return hipGetLastError();
+}
+
+hipError_t launch_round_f32(int dt, float* x, int64_t n, hipStream_t st) {
+    if (n <= 0 || dt == DT_F32) return hipSuccess;
+    const unsigned blocks = (unsigned)((n + 255) / 256);
+    if (dt == DT_BF16) hipLaunchKernelGGL(k_round_f32<DT_BF16>, dim3(blocks), dim3(256), 0, st, x, n);
+    else hipLaunchKernelGGL(k_round_f32<DT_F16>, dim3(blocks), dim3(256), 0, st, x, n);
     return hipGetLastError();
 }
 

@@ -77,7 +77,8 @@ class IVFFlatIndex:
         return out
 
     def assign(self, x) -> np.ndarray:
-        """Exact list id of every row (the coarse quantizer's top-1, ties -> lower list id)."""
+        """Exact list id of every row (the coarse quantizer's top-1 for the row rounded to the index
+        dtype, i.e. as it would be stored; ties -> lower list id)."""
         x = self._rows(x, "assign")
         out = np.empty((x.shape[0],), dtype=np.int64)
         if x.shape[0]:

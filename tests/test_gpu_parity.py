@@ -121,6 +121,20 @@ def test_edge_zero_vectors_and_constant_rows(FlatIndex):
     _check_exact(ix, q, 250, "ip")
 
 
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+def test_mfma_partial_tile_all_negative_scores(FlatIndex, dtype):
+    # a corpus smaller than one tile whose scores are all negative for every query: the zero
+    # padding rows of the tile (exact score 0) must never become candidates (regression: they
+    # did on the MFMA path with an unseeded threshold)
+    rng = np.random.default_rng(8)
+    x = np.abs(rng.standard_normal((8, 48))).astype(np.float32)
+    q = -np.abs(rng.standard_normal((40, 48))).astype(np.float32)
+    ix = FlatIndex(48, "ip", dtype)
+    ix.add(x)
+    D, I = _check_exact(ix, O.round_dtype(q, dtype), 5, "ip")
+    assert (D < 0).all() and (I < 8).all()
+
+
 def test_large_k(FlatIndex):
     ix = FlatIndex(64, "ip", "f32")
     ix.add_synthetic(O.SEED_CORPUS, 0, 50000, True)
