@@ -228,10 +228,11 @@ void search_core(vs_ivf* ix, const float* q_dev, int64_t nq, int k, int nprobe, 
                 v.push_back(gq);
                 for (int j = 0; j < IVF_QG; ++j) v.push_back(j < gq ? lq[l][g0 + j] : -1);
                 for (int j = 0; j < gq; ++j) ++per_q[lq[l][g0 + j]];
-                const int64_t rows = std::min<int64_t>(ix->list_n[l] - (int64_t)pb * TR, (int64_t)(pe - pb) * TR);
-                bytes += (double)rows * ix->d * ix->es;
             }
         }
+        // algorithmic bytes: every probed list read once (a list probed by more than IVF_QG
+        // queries is re-read per query group; that extra traffic is not algorithmic)
+        bytes += (double)ix->list_n[l] * ix->d * ix->es;
     }
     int max_items = 1;
     for (int v : per_q) max_items = std::max(max_items, v);
