@@ -252,6 +252,34 @@ def cpu_baseline_and_recall(args, N, d, dtype, nq, k, local, torch, gpu_full):
     return cpu, round(rec10, 6), parity
 
 
+def _progress(msg: str) -> None:
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+class _heartbeat:
+    """Print a progress line every 30 s while a long native call runs (ctypes releases the GIL)."""
+
+    def __init__(self, msg: str) -> None:
+        import threading
+        self.msg, self.stop = msg, threading.Event()
+        self.t = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self) -> None:
+        t0 = time.time()
+        while not self.stop.wait(30.0):
+            _progress(f"{self.msg} ... {time.time() - t0:.0f} s")
+
+    def __enter__(self):
+        _progress(self.msg)
+        self.t.start()
+        return self
+
+    def __exit__(self, *exc):
+        self.stop.set()
+        self.t.join()
+        _progress(f"{self.msg}: done")
+
+
 def run_ivf(args):
     """BASELINE cfg5: IVF-Flat (photo_search_engine_amd.ivf) on one GPU.  One step = one batch:
     exact coarse probe -> list scans (k_ivf_scan) -> exact refine.  Centroids are 4096 synthetic
@@ -278,7 +306,10 @@ def run_ivf(args):
     synthesize_device(0, SEED_CENTROIDS, 0, nlist, d, c.data_ptr(), True, dtype, stream)
     torch.cuda.synchronize()
     ix.set_centroids(c.cpu().numpy())
-    ix.add_synthetic(SEED_CORPUS, 0, N, True)
+    # one add call: the page pool is sized once (chunked adds would grow it by device copy, and
+    # old + new pools of a 154 GB corpus do not fit together); a heartbeat shows progress
+    with _heartbeat(f"cfg5 build: assigning and packing {N} rows"):
+        ix.add_synthetic(SEED_CORPUS, 0, N, True)
     q = torch.empty((nq, d), dtype=torch.float32, device=dev)
     synthesize_device(0, SEED_QUERIES, 0, nq, d, q.data_ptr(), True, dtype, stream)
     D = torch.empty((nq, k), dtype=torch.float32, device=dev)
@@ -334,6 +365,7 @@ def run_ivf(args):
         for i in np.unique(Ih):
             lists_of[int(i)] = fx.reconstruct(int(i) - r0)
         fx.close()
+        _progress(f"cfg5 ground truth: rows {r0}..{r0 + n} searched")
     Sall = np.concatenate(parts_S, axis=1)
     Iall = np.concatenate(parts_I, axis=1)
     Itrue = np.empty((nq, k), dtype=np.int64)

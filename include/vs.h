@@ -86,6 +86,16 @@ int vs_merge_shards_device(int metric, const double* S_in, const int64_t* I_in, 
 int vs_reconstruct(vs_index* index, int64_t id, float* out);
 int vs_reconstruct_n(vs_index* index, int64_t i0, int64_t n, float* out); /* host n x d */
 
+/* ---- persistence (faiss.read_index / faiss.write_index payloads, utils/vector_store.py:249, :234;
+ * SURVEY.md §8 f3).  The host layer parses / writes the 45-byte IxFI/IxF2 header; these move the
+ * row-major fp32 payload between the file and HBM through pinned double buffers (file reads and
+ * writes overlap the PCIe copies and the pack / unpack kernels).
+ * vs_add_from_file appends rows [0, n) of the payload at byte_offset (== index.add of them).
+ * vs_write_rows_to_file writes stored rows [i0, i0+n) at byte_offset of `path` (created if absent,
+ * never truncated): a full rewrite, or an append of the rows added since the last save. */
+int vs_add_from_file(vs_index* index, const char* path, int64_t byte_offset, int64_t n);
+int vs_write_rows_to_file(vs_index* index, const char* path, int64_t byte_offset, int64_t i0, int64_t n);
+
 /* ---- introspection */
 int64_t vs_ntotal(const vs_index* index);
 int vs_dim(const vs_index* index);

@@ -59,6 +59,8 @@ _SIGS = {
     "vs_search_device": (ctypes.c_int, [_vp, _vp, _c_i64, ctypes.c_int32, _vp, _vp, _vp, _c_i64, _vp]),
     "vs_merge_shards_device": (ctypes.c_int, [ctypes.c_int, _vp, _vp, ctypes.c_int, _c_i64, ctypes.c_int32, _vp,
                                               _vp, _vp, _vp]),
+    "vs_add_from_file": (ctypes.c_int, [_vp, ctypes.c_char_p, _c_i64, _c_i64]),
+    "vs_write_rows_to_file": (ctypes.c_int, [_vp, ctypes.c_char_p, _c_i64, _c_i64, _c_i64]),
     "vs_reconstruct": (ctypes.c_int, [_vp, _c_i64, _vp]),
     "vs_reconstruct_n": (ctypes.c_int, [_vp, _c_i64, _c_i64, _vp]),
     "vs_ntotal": (_c_i64, [_vp]),

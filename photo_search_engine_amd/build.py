@@ -11,7 +11,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libvs.so")
-SOURCES = ["vs_api.hip", "vs_ivf.hip", "vs_kernels.hip"]
+SOURCES = ["vs_api.hip", "vs_io.hip", "vs_ivf.hip", "vs_kernels.hip"]
 ARCH = os.environ.get("VS_OFFLOAD_ARCH", "gfx950")
 
 
@@ -30,24 +30,38 @@ def needs_build() -> bool:
     return any(os.path.getmtime(p) > t for p in deps if os.path.exists(p))
 
 
+OBJ_DIR = os.path.join(HERE, "_obj")  # per-source objects, kept between builds (not shipped)
+
+
+def _stale(target: str, deps) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(p) > t for p in deps if os.path.exists(p))
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not needs_build():
         return LIB
+    os.makedirs(OBJ_DIR, exist_ok=True)
+    headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    headers.append(os.path.join(HERE, "..", "include", "vs.h"))
     objs = []
     for src in SOURCES:
-        obj = os.path.join(CSRC, src.replace(".hip", ".o"))
-        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-result", "-Wno-unused-value", "-Wno-inline-asm",
-               "-c", os.path.join(CSRC, src), "-o", obj]
-        if verbose:
-            print(" ".join(cmd), file=sys.stderr)
-        subprocess.run(cmd, check=True)
+        spath = os.path.join(CSRC, src)
+        obj = os.path.join(OBJ_DIR, src.replace(".hip", ".o"))
+        if force or _stale(obj, [spath] + headers):
+            cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-result",
+                   "-Wno-unused-value", "-Wno-inline-asm", "-c", spath, "-o", obj + ".tmp.o"]
+            if verbose:
+                print(" ".join(cmd), file=sys.stderr)
+            subprocess.run(cmd, check=True)
+            os.replace(obj + ".tmp.o", obj)
         objs.append(obj)
     tmp = os.path.join(HERE, "libvs.tmp.so")  # a .so suffix keeps hipcc from emitting bundle side files
     cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
     subprocess.run(cmd, check=True)
     os.replace(tmp, LIB)
-    for o in objs:
-        os.remove(o)
     return LIB
 
 

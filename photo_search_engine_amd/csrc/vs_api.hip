@@ -29,11 +29,14 @@ thread_local std::string g_err;
 struct Ctx {
     hipStream_t stream = nullptr;
     DevBuf qdev, qtile, qinfo, qpad, cand, part, merge_a, merge_b, outD, outI, outS, cert, thr0, seedmax, gcnt;
+    DevBuf rows[2];  // read_rows_host: unpacked fp32 chunks
+    PinnedPair pin;  // read_rows_host: pinned landing chunks
     std::vector<int> cert_host;
     ~Ctx() {
         for (DevBuf* b : {&qdev, &qtile, &qinfo, &qpad, &cand, &part, &merge_a, &merge_b, &outD, &outI, &outS, &cert, &thr0,
-                          &seedmax, &gcnt})
+                          &seedmax, &gcnt, &rows[0], &rows[1]})
             b->release();
+        pin.release();
         if (stream) hipStreamDestroy(stream);
     }
 };
@@ -52,7 +55,8 @@ struct vs_index {
     unsigned* d_uncert = nullptr;
     float maxsq = 0.0f;
     hipStream_t own = nullptr;  // ingest stream
-    DevBuf stage;               // host->device staging for vs_add
+    DevBuf stage[2];            // add_rows_host: fp32 chunks on the device ...
+    PinnedPair pin;             // ... and their pinned host sources
     std::shared_mutex rw;       // shared: search; exclusive: add/reset
     std::mutex pool_mtx;
     std::vector<Ctx*> pool_free;
@@ -389,6 +393,84 @@ void vs::search_exact_device(vs_index* ix, const float* q_dev, int64_t nq, int k
     }
 }
 
+int64_t vs::stream_chunk_rows(int d) { return std::max<int64_t>(1, (int64_t)(32 << 20) / ((int64_t)d * 4)); }
+
+// Double-buffered host -> HBM ingest: chunk c is filled on the host (memcpy, file read) into pinned
+// buffer c&1 while the copy engine and k_pack_rows still work on chunk c-1.  A pinned buffer is
+// refilled only after the event recorded behind its previous pack has fired.
+void vs::add_rows_host(vs_index* ix, int64_t n, const std::function<void(int64_t, int64_t, float*)>& fill) {
+    check_index(ix);
+    std::unique_lock<std::shared_mutex> lk(ix->rw);
+    DeviceGuard dg(ix->device);
+    if (ix->ntotal + n > (int64_t)0xFFFFFFF0LL) throw VsError(VS_ERR_ARG, "shard exceeds 2^32 rows");
+    ensure_capacity(ix, ix->ntotal + n);
+    const int64_t rpc = stream_chunk_rows(ix->d);
+    const size_t cbytes = (size_t)std::min(n, rpc) * ix->d * sizeof(float);
+    ix->pin.ensure(cbytes);
+    ix->stage[0].ensure(cbytes);
+    ix->stage[1].ensure(cbytes);
+    try {
+        for (int64_t c = 0, r0 = 0; r0 < n; ++c, r0 += rpc) {
+            const int b = (int)(c & 1);
+            const int64_t m = std::min(rpc, n - r0);
+            if (c >= 2) HIP_CHECK(hipEventSynchronize(ix->pin.done[b]));
+            fill(r0, m, ix->pin.host[b]);
+            HIP_CHECK(hipMemcpyAsync(ix->stage[b].p, ix->pin.host[b], (size_t)m * ix->d * sizeof(float),
+                                     hipMemcpyHostToDevice, ix->own));
+            HIP_CHECK(launch_pack_rows(ix->dtype, ix->stage[b].as<float>(), m, ix->d, ix->dpad, ix->data,
+                                       ix->ntotal + r0, ix->sqn, ix->d_maxsq, ix->own));
+            HIP_CHECK(hipEventRecord(ix->pin.done[b], ix->own));
+        }
+        HIP_CHECK(hipStreamSynchronize(ix->own));
+    } catch (...) {
+        (void)hipStreamSynchronize(ix->own);  // the pinned chunks may still be in flight
+        throw;                                // ntotal unchanged: the packed rows stay invisible
+    }
+    ix->ntotal += n;
+    refresh_maxsq(ix);
+}
+
+// Double-buffered HBM -> host export: chunk c is unpacked and copied into pinned buffer c&1 while
+// the host consumes chunk c-1 (memcpy out, file write).
+void vs::read_rows_host(vs_index* ix, int64_t i0, int64_t n,
+                        const std::function<void(int64_t, int64_t, const float*)>& sink) {
+    check_index(ix);
+    std::shared_lock<std::shared_mutex> lk(ix->rw);
+    if (i0 < 0 || n < 0 || i0 + n > ix->ntotal) throw VsError(VS_ERR_ARG, "reconstruct range out of bounds");
+    if (n == 0) return;
+    DeviceGuard dg(ix->device);
+    CtxLease L(ix);
+    Ctx* c = L.c;
+    const int64_t rpc = stream_chunk_rows(ix->d);
+    const size_t cbytes = (size_t)std::min(n, rpc) * ix->d * sizeof(float);
+    c->pin.ensure(cbytes);
+    c->rows[0].ensure(cbytes);
+    c->rows[1].ensure(cbytes);
+    const int64_t nchunks = (n + rpc - 1) / rpc;
+    auto enqueue = [&](int64_t ci) {
+        const int b = (int)(ci & 1);
+        const int64_t r0 = ci * rpc, m = std::min(rpc, n - r0);
+        HIP_CHECK(launch_unpack_rows(ix->dtype, ix->data, i0 + r0, m, ix->d, ix->dpad, c->rows[b].as<float>(),
+                                     c->stream));
+        HIP_CHECK(hipMemcpyAsync(c->pin.host[b], c->rows[b].p, (size_t)m * ix->d * sizeof(float),
+                                 hipMemcpyDeviceToHost, c->stream));
+        HIP_CHECK(hipEventRecord(c->pin.done[b], c->stream));
+    };
+    try {
+        enqueue(0);
+        for (int64_t ci = 0; ci < nchunks; ++ci) {
+            if (ci + 1 < nchunks) enqueue(ci + 1);  // pinned buffer (ci+1)&1 was drained at ci-1
+            const int b = (int)(ci & 1);
+            HIP_CHECK(hipEventSynchronize(c->pin.done[b]));
+            const int64_t r0 = ci * rpc;
+            sink(r0, std::min(rpc, n - r0), c->pin.host[b]);
+        }
+    } catch (...) {
+        (void)hipStreamSynchronize(c->stream);
+        throw;
+    }
+}
+
 extern "C" {
 
 const char* vs_last_error(void) { return g_err.c_str(); }
@@ -443,7 +525,9 @@ void vs_destroy(vs_index* ix) {
             hipEventDestroy(pr.first);
             hipEventDestroy(pr.second);
         }
-        ix->stage.release();
+        ix->stage[0].release();
+        ix->stage[1].release();
+        ix->pin.release();
         if (ix->data) hipFree(ix->data);
         if (ix->sqn) hipFree(ix->sqn);
         if (ix->d_maxsq) hipFree(ix->d_maxsq);
@@ -470,22 +554,10 @@ int vs_add(vs_index* ix, const float* x, int64_t n) {
         if (n < 0) throw VsError(VS_ERR_ARG, "n must be >= 0");
         if (n == 0) return;
         if (!x) throw VsError(VS_ERR_ARG, "x is null");
-        std::unique_lock<std::shared_mutex> lk(ix->rw);
-        DeviceGuard dg(ix->device);
-        if (ix->ntotal + n > (int64_t)0xFFFFFFF0LL) throw VsError(VS_ERR_ARG, "shard exceeds 2^32 rows");
-        ensure_capacity(ix, ix->ntotal + n);
-        const int64_t rows_per_chunk = std::max<int64_t>(1, (int64_t)(64 << 20) / ((int64_t)ix->d * 4));
-        ix->stage.ensure((size_t)std::min(n, rows_per_chunk) * ix->d * sizeof(float));
-        for (int64_t r0 = 0; r0 < n; r0 += rows_per_chunk) {
-            const int64_t m = std::min(rows_per_chunk, n - r0);
-            HIP_CHECK(hipMemcpyAsync(ix->stage.p, x + r0 * ix->d, (size_t)m * ix->d * sizeof(float),
-                                     hipMemcpyHostToDevice, ix->own));
-            HIP_CHECK(launch_pack_rows(ix->dtype, ix->stage.as<float>(), m, ix->d, ix->dpad, ix->data,
-                                       ix->ntotal + r0, ix->sqn, ix->d_maxsq, ix->own));
-            HIP_CHECK(hipStreamSynchronize(ix->own));  // staging buffer reuse
-        }
-        ix->ntotal += n;
-        refresh_maxsq(ix);
+        const int64_t d = ix->d;
+        add_rows_host(ix, n, [&](int64_t r0, int64_t m, float* dst) {
+            std::memcpy(dst, x + r0 * d, (size_t)(m * d) * sizeof(float));
+        });
     });
 }
 
@@ -639,20 +711,10 @@ int vs_reconstruct_n(vs_index* ix, int64_t i0, int64_t n, float* out) {
         check_index(ix);
         if (n == 0) return;
         if (!out) throw VsError(VS_ERR_ARG, "out is null");
-        std::shared_lock<std::shared_mutex> lk(ix->rw);
-        if (i0 < 0 || n < 0 || i0 + n > ix->ntotal) throw VsError(VS_ERR_ARG, "reconstruct range out of bounds");
-        DeviceGuard dg(ix->device);
-        CtxLease L(ix);
-        Ctx* c = L.c;
-        const int64_t rows_per_chunk = std::max<int64_t>(1, (int64_t)(64 << 20) / ((int64_t)ix->d * 4));
-        c->outD.ensure((size_t)std::min(n, rows_per_chunk) * ix->d * sizeof(float));
-        for (int64_t r0 = 0; r0 < n; r0 += rows_per_chunk) {
-            const int64_t m = std::min(rows_per_chunk, n - r0);
-            HIP_CHECK(launch_unpack_rows(ix->dtype, ix->data, i0 + r0, m, ix->d, ix->dpad, c->outD.as<float>(), c->stream));
-            HIP_CHECK(hipMemcpyAsync(out + r0 * ix->d, c->outD.p, (size_t)m * ix->d * sizeof(float),
-                                     hipMemcpyDeviceToHost, c->stream));
-            HIP_CHECK(hipStreamSynchronize(c->stream));
-        }
+        const int64_t d = ix->d;
+        read_rows_host(ix, i0, n, [&](int64_t r0, int64_t m, const float* src) {
+            std::memcpy(out + r0 * d, src, (size_t)(m * d) * sizeof(float));
+        });
     });
 }
 

@@ -103,6 +103,38 @@ struct DevBuf {
     }
 };
 
+// two pinned host chunks + their "chunk consumed" events: double buffering of host <-> HBM copies
+struct PinnedPair {
+    float* host[2] = {nullptr, nullptr};
+    hipEvent_t done[2] = {nullptr, nullptr};
+    size_t bytes = 0;
+    void ensure(size_t want) {
+        if (!done[0]) {
+            HIP_CHECK(hipEventCreateWithFlags(&done[0], hipEventDisableTiming));
+            HIP_CHECK(hipEventCreateWithFlags(&done[1], hipEventDisableTiming));
+        }
+        if (want <= bytes) return;
+        release_host();
+        HIP_CHECK(hipHostMalloc((void**)&host[0], want, hipHostMallocDefault));
+        HIP_CHECK(hipHostMalloc((void**)&host[1], want, hipHostMallocDefault));
+        bytes = want;
+    }
+    void release_host() {
+        for (float*& h : host) {
+            if (h) (void)hipHostFree(h);
+            h = nullptr;
+        }
+        bytes = 0;
+    }
+    void release() {
+        release_host();
+        for (hipEvent_t& e : done) {
+            if (e) (void)hipEventDestroy(e);
+            e = nullptr;
+        }
+    }
+};
+
 struct DeviceGuard {
     int prev = -1;
     explicit DeviceGuard(int dev) {
@@ -223,8 +255,22 @@ hipError_t launch_pack_rows_map(int dt, const float* src, int64_t n, int d, int 
 
 }  // namespace vs
 
+#include <functional>
+
 struct vs_index;
 namespace vs {
+// Host <-> HBM row streaming through two pinned host chunks (bulk add, persistence).
+// add_rows_host appends n rows: fill(r0, m, dst) writes rows r0..r0+m-1 (fp32, row-major) into a
+// pinned chunk while the copy engine and the pack kernel work on the previous one.  Takes the
+// index's exclusive lock.
+void add_rows_host(vs_index* ix, int64_t n, const std::function<void(int64_t, int64_t, float*)>& fill);
+// read_rows_host streams rows i0..i0+n-1 as stored (dtype values widened to fp32): sink(r0, m, src)
+// consumes one pinned chunk while the next is unpacked and copied.  Shared lock (concurrent with
+// searches).
+void read_rows_host(vs_index* ix, int64_t i0, int64_t n,
+                    const std::function<void(int64_t, int64_t, const float*)>& sink);
+int64_t stream_chunk_rows(int d);  // rows per pinned chunk (32 MiB of fp32)
+
 // Exact top-k of device queries over a flat index, certificate failures re-searched (host-
 // synchronising).  I_dev [nq][k] (k <= ntotal), S64_dev optional.
 void search_exact_device(vs_index* ix, const float* q_dev, int64_t nq, int k, int64_t* I_dev, double* S64_dev,

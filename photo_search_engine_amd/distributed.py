@@ -6,8 +6,9 @@ own :class:`~photo_search_engine_amd.index.FlatIndex` (HBM-resident); a search i
 
   1. local exact search on the rank's shard (MFMA/GEMV screen + exact refine), returning the
      per-shard top-k as (exact fp64 score, GLOBAL id) -- ids offset on the device;
-  2. one all-gather of those lists (``nq * k * 16`` bytes per rank; RCCL over xGMI with the
-     ``nccl`` backend) -- the only collective, and the path's only exchange step;
+  2. one all-gather of those lists as interleaved (score bits, id) pairs (``nq * k * 16`` bytes
+     per rank; RCCL over xGMI with the ``nccl`` backend) -- the only collective, and the path's
+     only exchange step;
   3. a merge of the G sorted lists on the device (``vs_merge_shards_device``) on every rank, so
      all ranks hold the same final (D, I) without a second collective.
 
@@ -139,7 +140,11 @@ class ShardedFlatIndex:
                            dtype=torch.float32, device=q.device)
         if self.world == 1:
             return D, I, S
-        S, I, D = self._merge(self.metric, self._gather(S), self._gather(I), k)
+        # ONE all-gather of interleaved (fp64 score bits, id) pairs: a second collective would add
+        # its full latency to every step (the payload is only nq * k * 16 B per rank)
+        SI = torch.stack([S.contiguous().view(torch.int64), I.contiguous()], dim=-1)
+        g = self._gather(SI)
+        S, I, D = self._merge(self.metric, g[..., 0].contiguous().view(torch.float64), g[..., 1].contiguous(), k)
         return D, I, S
 
     def close(self) -> None:

@@ -46,6 +46,7 @@ class FaissFile:
     metric_type: int
     vectors: np.ndarray  # (ntotal, d) float32 (memory-mapped for large files)
     hnsw_params: dict
+    payload_offset: int = 0  # byte offset of the row-major float32 payload in the file
 
 
 class FaissFormatError(ValueError):
@@ -81,7 +82,7 @@ def _read_at(path: str, buf: memoryview, off: int) -> FaissFile:
             vec = np.frombuffer(buf, dtype="<f4", count=nf, offset=off).reshape(ntotal, d).copy()
         mt = METRIC_INNER_PRODUCT if fourcc == FOURCC_FLAT_IP else METRIC_L2
         return FaissFile("flat", fourcc, d, ntotal, mt if metric_type in (0, 1) else metric_type,
-                         np.asarray(vec, dtype=np.float32), {})
+                         np.asarray(vec, dtype=np.float32), {}, off)
     if fourcc == FOURCC_HNSW_FLAT:
         for es in (8, 4, 4, 8, 4):  # assign_probas, cum_nneighbor_per_level, levels, offsets, neighbors
             (n,) = struct.unpack_from("<Q", buf, off)
@@ -93,7 +94,7 @@ def _read_at(path: str, buf: memoryview, off: int) -> FaissFile:
             raise FaissFormatError("HNSW storage does not match its header")
         return FaissFile("hnsw", fourcc, d, ntotal, metric_type, storage.vectors,
                          {"entry_point": entry_point, "max_level": max_level, "efConstruction": ef_c,
-                          "efSearch": ef_s})
+                          "efSearch": ef_s}, storage.payload_offset)
     raise FaissFormatError(f"unsupported faiss index type {fourcc!r}")
 
 
@@ -110,6 +111,32 @@ def flat_bytes_header(d: int, ntotal: int, metric_type: int) -> bytes:
     fourcc = FOURCC_FLAT_IP if metric_type == METRIC_INNER_PRODUCT else FOURCC_FLAT_L2
     return (fourcc + struct.pack("<iqqqBi", d, ntotal, _DUMMY, _DUMMY, 1, metric_type)
             + struct.pack("<Q", d * ntotal))
+
+
+FLAT_HEADER_BYTES = 45  # fourcc .. metric_type (37) + uint64 n_floats (8)
+
+
+def write_flat_rows(path: str, d: int, ntotal: int, metric_type: int, write_rows) -> None:
+    """Full rewrite of an IxFI / IxF2 file whose payload is produced by ``write_rows(path, offset)``
+    (the device-to-file stream of ``FlatIndex.write_rows``).  Temporary name + rename, so a crash
+    never leaves a torn index."""
+    tmp = f"{path}.tmp-{os.getpid()}"
+    with open(tmp, "wb") as f:
+        f.write(flat_bytes_header(d, ntotal, metric_type))
+    if ntotal:
+        write_rows(tmp, FLAT_HEADER_BYTES)
+    os.replace(tmp, path)
+
+
+def append_flat_rows(path: str, d: int, old_ntotal: int, new_ntotal: int, metric_type: int, write_rows) -> None:
+    """Grow an existing flat file from ``old_ntotal`` to ``new_ntotal`` rows in place: the new rows
+    go after the old payload (``write_rows(path, offset)``), then the header is rewritten in one
+    write.  The result is byte-identical to a full rewrite; until the header write lands, readers
+    see the old index (faiss and :func:`read_index` ignore trailing bytes)."""
+    if new_ntotal > old_ntotal:
+        write_rows(path, FLAT_HEADER_BYTES + old_ntotal * d * 4)
+    with open(path, "r+b") as f:
+        f.write(flat_bytes_header(d, new_ntotal, metric_type))
 
 
 def write_flat(path: str, vectors: np.ndarray, metric_type: int) -> None:

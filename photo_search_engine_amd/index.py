@@ -9,6 +9,7 @@ hand in torch tensors' ``data_ptr()`` without torch types crossing the C ABI.
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Optional, Tuple
 
 import numpy as np
@@ -85,6 +86,15 @@ class FlatIndex:
 
     def reset(self) -> None:
         check(self._L.vs_reset(self._h))
+
+    # -- persistence (faiss read_index / write_index payloads, streamed file <-> HBM) ---------------
+    def add_from_file(self, path: str, byte_offset: int, n: int) -> None:
+        """Append rows [0, n) of the row-major fp32 payload at ``byte_offset`` of ``path``."""
+        check(self._L.vs_add_from_file(self._h, os.fsencode(path), int(byte_offset), int(n)))
+
+    def write_rows(self, path: str, byte_offset: int, i0: int, n: int) -> None:
+        """Write stored rows [i0, i0+n) as fp32 at ``byte_offset`` of ``path`` (no truncation)."""
+        check(self._L.vs_write_rows_to_file(self._h, os.fsencode(path), int(byte_offset), int(i0), int(n)))
 
     # -- device-resident surface (bench / multi-GPU) -----------------------------------------
     def add_device(self, x_ptr: int, n: int, stream: Optional[int] = None) -> None:

@@ -87,6 +87,9 @@ class VectorStore:
         self._normalize = self.metric == "cosine"
         self._embeddings: Dict[int, List[float]] = {}
         self._path_to_index: Dict[str, int] = {}
+        # what the index file on disk holds, when it is known to be a prefix of this index
+        # (set by save() / load(); None after clear()): lets save() append instead of rewriting
+        self._persisted: Optional[Dict[str, Any]] = None
 
     # ------------------------------------------------------------------ internals
     def _rebuild_path_index(self) -> None:
@@ -228,8 +231,19 @@ class VectorStore:
         if metadata_dir:
             os.makedirs(metadata_dir, exist_ok=True)
 
-        vectors = self.index.reconstruct_n(0, self.index.ntotal)
-        faiss_format.write_flat(self.index_path, vectors, self.index.metric_type)
+        # The reference rewrites the whole index per indexer batch (utils/vector_store.py:234,
+        # core/indexer.py:945): O(N) per save.  Rows never change once added, so when the file on
+        # disk is the one this store last wrote or loaded, only the new rows and the header are
+        # written -- the bytes are identical to a full rewrite.  Payload bytes stream HBM -> file.
+        n, d, mt = int(self.index.ntotal), int(self.index.d), int(self.index.metric_type)
+        old = self._appendable_rows(d, mt)
+        if old is not None and old <= n:
+            faiss_format.append_flat_rows(self.index_path, d, old, n, mt,
+                                          lambda path, off: self.index.write_rows(path, off, old, n - old))
+        else:
+            faiss_format.write_flat_rows(self.index_path, d, n, mt,
+                                         lambda path, off: self.index.write_rows(path, off, 0, n))
+        self._persisted = self._file_state(n, d, mt)
         self._write_index_meta()
         with open(self.metadata_path, "w", encoding="utf-8") as file:
             json.dump(self.metadata, file, ensure_ascii=False, indent=2)
@@ -241,9 +255,11 @@ class VectorStore:
 
         loaded = faiss_format.read_index(self.index_path)
         index = self._create_index_with_metric(loaded.d, loaded.metric_type)
-        if loaded.ntotal:
-            index.add(loaded.vectors)
+        if loaded.ntotal:  # payload streamed file -> pinned chunks -> HBM (no host copy of the matrix)
+            index.add_from_file(self.index_path, loaded.payload_offset, loaded.ntotal)
         self.index = index
+        self._persisted = (self._file_state(loaded.ntotal, loaded.d, loaded.metric_type)
+                           if loaded.kind == "flat" else None)
         payload = self._load_index_meta()
         self._validate_loaded_index(payload, loaded)
 
@@ -272,6 +288,31 @@ class VectorStore:
         self.metadata = []
         self._embeddings = {}
         self._path_to_index = {}
+        self._persisted = None
+
+    # ------------------------------------------------------------------ persistence state
+    def _file_state(self, rows: int, d: int, metric_type: int) -> Optional[Dict[str, Any]]:
+        try:
+            st = os.stat(self.index_path)
+        except OSError:
+            return None
+        return {"path": os.path.abspath(self.index_path), "rows": int(rows), "d": int(d), "metric_type": int(metric_type),
+                "stat": (st.st_dev, st.st_ino, st.st_size, st.st_mtime_ns)}
+
+    def _appendable_rows(self, d: int, metric_type: int) -> Optional[int]:
+        """Rows of the index file if it is still exactly what this store last wrote or loaded."""
+        p = self._persisted
+        if not p or p["path"] != os.path.abspath(self.index_path) or p["d"] != d or p["metric_type"] != metric_type:
+            return None
+        try:
+            st = os.stat(self.index_path)
+        except OSError:
+            return None
+        if (st.st_dev, st.st_ino, st.st_size, st.st_mtime_ns) != p["stat"]:
+            return None
+        if st.st_size != faiss_format.FLAT_HEADER_BYTES + p["rows"] * d * 4:
+            return None
+        return p["rows"]
 
     # ------------------------------------------------------------------ batched additions
     def add(self, embeddings: np.ndarray, metadatas: Sequence[Dict]) -> None:

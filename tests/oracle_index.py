@@ -41,6 +41,16 @@ class OracleFlatIndex:
     def reconstruct_n(self, i0: int, n: int) -> np.ndarray:
         return self._x[int(i0):int(i0) + int(n)].copy()
 
+    def add_from_file(self, path: str, byte_offset: int, n: int) -> None:
+        x = np.fromfile(path, dtype="<f4", count=int(n) * self.d, offset=int(byte_offset))
+        assert x.size == int(n) * self.d, "file too short"
+        self.add(x.reshape(int(n), self.d))
+
+    def write_rows(self, path: str, byte_offset: int, i0: int, n: int) -> None:
+        with open(path, "r+b") as f:
+            f.seek(int(byte_offset))
+            f.write(np.ascontiguousarray(self._x[int(i0):int(i0) + int(n)], dtype="<f4").tobytes())
+
     def reset(self) -> None:
         self._x = np.zeros((0, self.d), dtype=np.float32)
 
