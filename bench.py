@@ -58,6 +58,8 @@ def parse():
                     help="rehearsal only: every rank on cuda:0 (with --dist-backend gloo on a 1-GPU box)")
     ap.add_argument("--zero-corpus", action="store_true",
                     help="diagnostic only: all-zero corpus rows (DVFS/power test with VS_MF_ABLATE=9; results meaningless)")
+    ap.add_argument("--iso-data", action="store_true",
+                    help="cfg5: isotropic rows (the flat bench's data) instead of the Gaussian mixture")
     ap.add_argument("--traffic-file", default=os.path.join(REPO, "profiles", "traffic_cfg3.json"))
     return ap.parse_args()
 
@@ -280,13 +282,31 @@ class _heartbeat:
         _progress(f"{self.msg}: done")
 
 
+def _mixture_rows(seed, r0, m, d, centroids, sigma, dev, stream):
+    """Synthetic IVF corpus / query rows: a Gaussian mixture over the coarse centroids (the data
+    model IVF exists for).  Row i = normalise(c[h(i) mod nlist] + sigma * g_i), g_i the unit
+    counter-hash Gaussian row i of `seed` (bit-identical generator of oracle/vs_oracle.c), h a
+    multiplicative hash.  Deterministic: elementwise torch ops + the row norm on the same device."""
+    import torch
+
+    from photo_search_engine_amd.index import synthesize_device
+    g = torch.empty((m, d), dtype=torch.float32, device=dev)
+    synthesize_device(dev.index, seed, r0, m, d, g.data_ptr(), True, "f32", stream)
+    rows = torch.arange(r0, r0 + m, dtype=torch.int64, device=dev)
+    cid = ((rows * 2654435761) >> 7) % centroids.shape[0]
+    x = centroids[cid] + sigma * g
+    return x / torch.linalg.vector_norm(x, dim=1, keepdim=True)
+
+
 def run_ivf(args):
     """BASELINE cfg5: IVF-Flat (photo_search_engine_amd.ivf) on one GPU.  One step = one batch:
     exact coarse probe -> list scans (k_ivf_scan) -> exact refine.  Centroids are 4096 synthetic
-    unit vectors (seed 20260419; training is not part of the metric).  recall@10 is measured
-    against the exact flat top-10 of the whole corpus (row shards through FlatIndex, merged);
-    `probed_recall@10` checks the IVF exactness contract at full size: every exact top-10 row
-    whose list was probed must be returned."""
+    unit vectors (seed 20260419; training is not part of the metric); corpus and queries are a
+    Gaussian mixture around them (sigma 1, `_mixture_rows`); `--iso-data` uses the isotropic flat-
+    bench rows instead (no cluster structure: IVF recall is then ~0.03 at nprobe 32 by nature of
+    the data, whatever the implementation).  recall@10 is measured against the exact flat top-10
+    of the whole corpus (FlatIndex row shards, merged); `probed_recall@10` checks the IVF exactness
+    contract at full size: every exact top-10 row whose list was probed must be returned."""
     import torch
 
     from photo_search_engine_amd.index import FlatIndex, synthesize_device
@@ -300,18 +320,31 @@ def run_ivf(args):
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
     stream = torch.cuda.current_stream(dev).cuda_stream
+    sigma = 1.0
+    chunk = 1 << 20
     t_build = time.time()
     ix = IVFFlatIndex(d, nlist, "ip", dtype, device=0, nprobe=nprobe)
     c = torch.empty((nlist, d), dtype=torch.float32, device=dev)
     synthesize_device(0, SEED_CENTROIDS, 0, nlist, d, c.data_ptr(), True, dtype, stream)
     torch.cuda.synchronize()
     ix.set_centroids(c.cpu().numpy())
-    # one add call: the page pool is sized once (chunked adds would grow it by device copy, and
-    # old + new pools of a 154 GB corpus do not fit together); a heartbeat shows progress
-    with _heartbeat(f"cfg5 build: assigning and packing {N} rows"):
-        ix.add_synthetic(SEED_CORPUS, 0, N, True)
-    q = torch.empty((nq, d), dtype=torch.float32, device=dev)
-    synthesize_device(0, SEED_QUERIES, 0, nq, d, q.data_ptr(), True, dtype, stream)
+
+    def corpus_chunk(r0, m):
+        return _mixture_rows(SEED_CORPUS, r0, m, d, c, sigma, dev, stream)
+
+    if args.iso_data:
+        with _heartbeat(f"cfg5 build (isotropic rows): assigning and packing {N} rows"):
+            ix.add_synthetic(SEED_CORPUS, 0, N, True)
+        q = torch.empty((nq, d), dtype=torch.float32, device=dev)
+        synthesize_device(0, SEED_QUERIES, 0, nq, d, q.data_ptr(), True, dtype, stream)
+    else:
+        ix.reserve(N)  # one page-pool allocation for the whole corpus
+        with _heartbeat(f"cfg5 build (Gaussian mixture, sigma {sigma}): assigning and packing {N} rows"):
+            for r0 in range(0, N, chunk):
+                x = corpus_chunk(r0, min(chunk, N - r0))
+                ix.add_device(x.data_ptr(), x.shape[0], stream)
+                del x
+        q = _mixture_rows(SEED_QUERIES, 0, nq, d, c, sigma, dev, stream).contiguous()
     D = torch.empty((nq, k), dtype=torch.float32, device=dev)
     I = torch.empty((nq, k), dtype=torch.int64, device=dev)
     S = torch.empty((nq, k), dtype=torch.float64, device=dev)
@@ -349,16 +382,25 @@ def run_ivf(args):
     pairs = float(sum(int(sizes[l]) for l in P.reshape(-1)))  # (row, query) dot products per batch
 
     # exact flat ground truth over the whole corpus, shard by shard (the IVF stays resident)
-    shard = 12_500_000
+    shard = 6_250_000
     parts_S, parts_I, lists_of = [], [], {}
     for r0 in range(0, N, shard):
         n = min(shard, N - r0)
         fx = FlatIndex(d, "ip", dtype, device=0)
-        fx.add_synthetic(SEED_CORPUS, r0, n, True)
+        if args.iso_data:
+            fx.add_synthetic(SEED_CORPUS, r0, n, True)
+        else:
+            for s0 in range(r0, r0 + n, chunk):
+                x = corpus_chunk(s0, min(chunk, r0 + n - s0))
+                fx.add_device(x.data_ptr(), x.shape[0], stream)
+                del x
         Sd = torch.empty((nq, k), dtype=torch.float64, device=dev)
         Id = torch.empty((nq, k), dtype=torch.int64, device=dev)
         fx.search_device(q.data_ptr(), nq, k, None, Id.data_ptr(), Sd.data_ptr(), r0, stream)
         torch.cuda.synchronize()
+        unc = fx.uncertified_count()
+        if unc:
+            raise SystemExit(f"cfg5 ground truth: {unc} uncertified flat searches")
         Ih = Id.cpu().numpy()
         parts_S.append(Sd.cpu().numpy())
         parts_I.append(Ih)
@@ -384,6 +426,21 @@ def run_ivf(args):
                 need += 1
                 got += int(i in res)
 
+    if os.environ.get("VS_IVF_DEBUG"):
+        Sg = S.cpu().numpy()
+        for a in [a for a in range(nq) if set(Ig[a, :10].tolist()) != set(Itrue[a, :10].tolist())][:3]:
+            _progress(f"q{a} ivf  {Ig[a, :10].tolist()} {np.round(Sg[a, :10], 6).tolist()}")
+            ts = [float(Sall[a][np.where(Iall[a] == i)[0][0]]) for i in Itrue[a, :10]]
+            _progress(f"q{a} flat {Itrue[a, :10].tolist()} {np.round(ts, 6).tolist()}")
+            _progress(f"q{a} lists of flat ids {[lst[i] for i in Itrue[a, :10].tolist()]} probed {sorted(P[a].tolist())}")
+            for i in Itrue[a, :4].tolist():
+                xi = lists_of[i]
+                _progress(f"   id {i}: flat row == ivf row: {np.array_equal(xi, ix.reconstruct(i))}  "
+                          f"flat-row score {float(xi.astype(np.float64) @ qh[a].astype(np.float64)):.9f}  "
+                          f"gen row[:3] {corpus_chunk(i, 1).cpu().numpy()[0, :3].tolist()} flat row[:3] {xi[:3].tolist()}")
+    data = ("synthetic isotropic (counter-hash N(0,1) rows, L2-normalised, seeds 20260417/20260418)" if args.iso_data
+            else f"synthetic Gaussian mixture: normalise(centroid[hash(i) % {nlist}] + {sigma} * unit counter-hash "
+                 "Gaussian row i), seeds 20260417 (rows) / 20260418 (queries) / 20260419 (centroids)")
     out = {
         "metric": f"kNN queries/sec + recall@10 vs exact flat, IVF-Flat nlist={nlist} nprobe={nprobe} N=50M d=1536 batch=256",
         "value": round(nq * args.steps / elapsed, 2),
@@ -396,7 +453,7 @@ def run_ivf(args):
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": dtype,
-        "data": "synthetic (counter-hash N(0,1) rows, L2-normalised, seeds 20260417/20260418; centroids seed 20260419)",
+        "data": data,
         "config": {"workload": args.workload, "desc": desc, "N": N, "d": d, "batch": nq, "k": k, "nlist": nlist,
                    "nprobe": nprobe, "list_rows_min_max": [int(sizes.min()), int(sizes.max())],
                    "parallelism": "1 GPU"},

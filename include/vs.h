@@ -58,7 +58,8 @@ int vs_reset(vs_index* index);                    /* clear(): utils/vector_store
 
 /* ---- add (index.add, utils/vector_store.py:164) */
 int vs_add(vs_index* index, const float* x, int64_t n);                 /* host fp32 n x d */
-int vs_add_device(vs_index* index, const float* x_dev, int64_t n, void* stream); /* device fp32 */
+int vs_add_device(vs_index* index, const float* x_dev, int64_t n, void* stream); /* device fp32, packed on
+                                                                                  * `stream` (NULL: legacy default) */
 /* Fill rows [ntotal, ntotal+n) with synthetic rows global_row0.. of the counter-hash generator
  * (bench / tests; bit-identical to oracle/vs_oracle.c orc_synth_rows). */
 int vs_add_synthetic(vs_index* index, uint64_t seed, int64_t global_row0, int64_t n, int normalize);
@@ -69,7 +70,8 @@ int vs_synthesize(int device, uint64_t seed, int64_t global_row0, int64_t n, int
 
 /* ---- search (index.search, utils/vector_store.py:191) */
 int vs_search(vs_index* index, const float* q, int64_t nq, int32_t k, float* D, int64_t* I);
-/* All pointers device-resident; enqueued on `stream` (NULL = the index's own stream), no host
+/* All pointers device-resident; enqueued on `stream` (NULL = the legacy default stream, which is
+ * torch's default stream: device calls are always ordered with the caller's stream), no host
  * sync.  S64 (optional, may be NULL) receives the exact fp64 scores; id_offset is added to every
  * returned id (row-sharded corpora).  Certification failures are counted on the device
  * (vs_uncertified_count) and are NOT retried on this path. */
@@ -132,7 +134,11 @@ int vs_ivf_get_centroids(vs_ivf* ivf, float* out);            /* host nlist x d,
 int vs_ivf_is_trained(const vs_ivf* ivf);
 int vs_ivf_assign(vs_ivf* ivf, const float* x, int64_t n, int64_t* lists); /* host; by the rows' dtype-rounded values */
 int vs_ivf_add(vs_ivf* ivf, const float* x, int64_t n);       /* host fp32 n x d */
+int vs_ivf_add_device(vs_ivf* ivf, const float* x_dev, int64_t n, void* stream); /* device fp32 n x d */
 int vs_ivf_add_synthetic(vs_ivf* ivf, uint64_t seed, int64_t global_row0, int64_t n, int normalize);
+/* size the HBM page pool for n more rows at once (chunked adds otherwise grow it by device copy,
+ * which needs the old and the new pool side by side) */
+int vs_ivf_reserve(vs_ivf* ivf, int64_t n);
 int vs_ivf_search(vs_ivf* ivf, const float* q, int64_t nq, int32_t k, int32_t nprobe, float* D, int64_t* I);
 /* device q/D/I/S64 (D, S64 may be NULL); host-synchronising (the probe -> work-item step). */
 int vs_ivf_search_device(vs_ivf* ivf, const float* q_dev, int64_t nq, int32_t k, int32_t nprobe, float* D_dev,

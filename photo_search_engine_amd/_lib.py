@@ -82,7 +82,9 @@ _SIGS = {
     "vs_ivf_is_trained": (ctypes.c_int, [_vp]),
     "vs_ivf_assign": (ctypes.c_int, [_vp, _vp, _c_i64, _vp]),
     "vs_ivf_add": (ctypes.c_int, [_vp, _vp, _c_i64]),
+    "vs_ivf_add_device": (ctypes.c_int, [_vp, _vp, _c_i64, _vp]),
     "vs_ivf_add_synthetic": (ctypes.c_int, [_vp, ctypes.c_uint64, _c_i64, _c_i64, ctypes.c_int]),
+    "vs_ivf_reserve": (ctypes.c_int, [_vp, _c_i64]),
     "vs_ivf_search": (ctypes.c_int, [_vp, _vp, _c_i64, ctypes.c_int32, ctypes.c_int32, _vp, _vp]),
     "vs_ivf_search_device": (ctypes.c_int, [_vp, _vp, _c_i64, ctypes.c_int32, ctypes.c_int32, _vp, _vp, _vp, _vp]),
     "vs_ivf_reconstruct": (ctypes.c_int, [_vp, _c_i64, _vp]),

@@ -571,7 +571,9 @@ int vs_add_device(vs_index* ix, const float* x_dev, int64_t n, void* stream) {
         DeviceGuard dg(ix->device);
         if (ix->ntotal + n > (int64_t)0xFFFFFFF0LL) throw VsError(VS_ERR_ARG, "shard exceeds 2^32 rows");
         ensure_capacity(ix, ix->ntotal + n);
-        hipStream_t st = stream ? (hipStream_t)stream : ix->own;
+        // NULL is the legacy default stream (torch's default stream handle is 0), never the
+        // index's private non-blocking stream: that one is unordered with the caller's producers
+        hipStream_t st = (hipStream_t)stream;
         HIP_CHECK(launch_pack_rows(ix->dtype, x_dev, n, ix->d, ix->dpad, ix->data, ix->ntotal, ix->sqn, ix->d_maxsq, st));
         HIP_CHECK(hipStreamSynchronize(st));
         ix->ntotal += n;
@@ -621,7 +623,9 @@ int vs_search_device(vs_index* ix, const float* q_dev, int64_t nq, int32_t k, fl
         if (!q_dev || !I_dev) throw VsError(VS_ERR_ARG, "null device buffer");
         std::shared_lock<std::shared_mutex> lk(ix->rw);
         DeviceGuard dg(ix->device);
-        hipStream_t st = stream ? (hipStream_t)stream : ix->own;
+        // NULL is the legacy default stream (torch's default stream handle is 0), never the
+        // index's private non-blocking stream: that one is unordered with the caller's producers
+        hipStream_t st = (hipStream_t)stream;
         if (ix->ntotal == 0) throw VsError(VS_ERR_ARG, "index is empty");
         CtxLease L(ix);
         search_all(ix, L.c, q_dev, nq, k, screen_depth(k), D_dev, I_dev, S64_dev, nullptr, id_offset, st,

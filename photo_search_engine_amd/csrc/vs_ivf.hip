@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <shared_mutex>
@@ -270,7 +271,9 @@ void search_core(vs_ivf* ix, const float* q_dev, int64_t nq, int k, int nprobe, 
     a.glist = ix->glist.as<u64>();
     a.gcnt = ix->gcnt.as<int>();
     a.lcap = lcap;
-    const int max_grid = ix->num_cu * 4;
+    // persistent scan workgroups: 8 per CU (32 waves) keep enough 16 B loads in flight per CU
+    static const int grid_per_cu = getenv("VS_IVF_GRID") ? std::max(1, atoi(getenv("VS_IVF_GRID"))) : 8;
+    const int max_grid = ix->num_cu * grid_per_cu;
     ix->cand.ensure((size_t)max_grid * IVF_QG * a.cap * sizeof(u64));
     a.cand = ix->cand.as<u64>();
     const bool timing = ix->timing.load();
@@ -501,6 +504,35 @@ int vs_ivf_add(vs_ivf* ix, const float* x, int64_t n) {
     });
 }
 
+int vs_ivf_add_device(vs_ivf* ix, const float* x_dev, int64_t n, void* stream) {
+    return guarded([&] {
+        check_ivf(ix);
+        if (n < 0) throw VsError(VS_ERR_ARG, "n must be >= 0");
+        if (n == 0) return;
+        if (!x_dev) throw VsError(VS_ERR_ARG, "x_dev is null");
+        std::unique_lock<std::shared_mutex> lk(ix->rw);
+        DeviceGuard dg(ix->device);
+        // the producer's writes land first (NULL = the legacy default stream, torch's default)
+        HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+        const int d = ix->d;
+        add_rows(ix, n, [&](int64_t r0, int64_t m, float* dst) {
+            HIP_CHECK(hipMemcpyAsync(dst, x_dev + r0 * d, (size_t)m * d * sizeof(float), hipMemcpyDeviceToDevice,
+                                     ix->own));
+        });
+    });
+}
+
+int vs_ivf_reserve(vs_ivf* ix, int64_t n) {
+    return guarded([&] {
+        check_ivf(ix);
+        if (n < 0) throw VsError(VS_ERR_ARG, "n must be >= 0");
+        std::unique_lock<std::shared_mutex> lk(ix->rw);
+        DeviceGuard dg(ix->device);
+        // n more rows need at most ceil(n / TR) new pages plus one partly filled page per list
+        ensure_pages(ix, ix->used_pages + (n + TR - 1) / TR + ix->nlist);
+    });
+}
+
 int vs_ivf_add_synthetic(vs_ivf* ix, uint64_t seed, int64_t global_row0, int64_t n, int normalize) {
     return guarded([&] {
         check_ivf(ix);
@@ -524,7 +556,7 @@ int vs_ivf_search_device(vs_ivf* ix, const float* q_dev, int64_t nq, int32_t k, 
         std::shared_lock<std::shared_mutex> lk(ix->rw);
         std::lock_guard<std::mutex> sg(ix->search_mtx);
         DeviceGuard dg(ix->device);
-        search_locked(ix, q_dev, nq, k, nprobe, D_dev, I_dev, S64_dev, stream ? (hipStream_t)stream : ix->own);
+        search_locked(ix, q_dev, nq, k, nprobe, D_dev, I_dev, S64_dev, (hipStream_t)stream);  // NULL: legacy default
     });
 }
 

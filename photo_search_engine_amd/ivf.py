@@ -114,6 +114,14 @@ class IVFFlatIndex:
         x = self._rows(x, "add")
         check(self._L.vs_ivf_add(self._h, _ptr(x), x.shape[0]))
 
+    def add_device(self, x_ptr: int, n: int, stream: Optional[int] = None) -> None:
+        """Append n fp32 rows (row-major n x d) from device memory; ``stream`` is synchronised first."""
+        check(self._L.vs_ivf_add_device(self._h, x_ptr, int(n), stream or None))
+
+    def reserve(self, n: int) -> None:
+        """Size the page pool for ``n`` more rows in one allocation."""
+        check(self._L.vs_ivf_reserve(self._h, int(n)))
+
     def add_synthetic(self, seed: int, global_row0: int, n: int, normalize: bool = True) -> None:
         check(self._L.vs_ivf_add_synthetic(self._h, int(seed), int(global_row0), int(n), int(bool(normalize))))
 

@@ -12,6 +12,8 @@ for s in "$@"; do
     bench) timeout -k 10 600 python bench.py > gpurun_out/bench.log 2>&1 ;;
     bench_cfg5_small) timeout -k 10 600 python bench.py --workload cfg5 --rows 2000000 --steps 5 --warmup 2 > gpurun_out/bench_cfg5_small.log 2>&1 ;;
     bench_cfg5) timeout -k 10 900 python bench.py --workload cfg5 --steps 10 --warmup 2 > gpurun_out/bench_cfg5.log 2>&1 ;;
+    bench_cfg5_g4) VS_IVF_GRID=4 timeout -k 10 900 python bench.py --workload cfg5 --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/bench_cfg5_g4.log 2>&1 ;;
+    bench_cfg5_g16) VS_IVF_GRID=16 timeout -k 10 900 python bench.py --workload cfg5 --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/bench_cfg5_g16.log 2>&1 ;;
     bench_cfg2) timeout -k 10 600 python bench.py --workload cfg2 --steps 50 --no-cpu-baseline > gpurun_out/bench_cfg2.log 2>&1 ;;
     prof) timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/prof.log 2>&1 ;;
     ablate) for m in ${MODES:-0 1 2 0}; do VS_MF_ABLATE=$m timeout -k 10 300 python bench.py --no-cpu-baseline --steps 10 > gpurun_out/ablate_$m.log 2>&1 || exit 1; tail -1 gpurun_out/ablate_$m.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('mode $m', d['roofline']['kernel_ms'])" >> gpurun_out/ablate.txt; done ;;
