@@ -97,6 +97,26 @@ def main():
         with open(os.path.join(prof, f"traffic_{cfg['workload']}.json"), "w") as f:
             json.dump(traffic, f, indent=1)
         summary["dominant"] = traffic
+    # IVF (cfg5): one search launches k_ivf_scan once per query-count class; traffic per search =
+    # all scan dispatches / searches run (warmup + steps; every search is the same batch)
+    ivf = {k: v for k, v in summary["kernels"].items() if "k_ivf_scan" in k}
+    if ivf and bench_line and bench_line["config"]["workload"] == "cfg5":
+        searches = bench_line["steps"] + bench_line["warmup"]
+        tot = {}
+        for p in ("pmc_fetch", "pmc_write"):
+            disp = per_dispatch(os.path.join(src, p))
+            tot[p] = sum(v.get("FETCH_SIZE" if p == "pmc_fetch" else "WRITE_SIZE", 0.0)
+                         for v in disp.values() if "k_ivf_scan" in v["name"])
+        kt = list(csv.DictReader(open(os.path.join(src, "kt", "kt_kernel_trace.csv"))))
+        scan_ns = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in kt if "k_ivf_scan" in r["Kernel_Name"])
+        rd, wr = tot["pmc_fetch"] * 1024 * 2 / searches, tot["pmc_write"] * 1024 / searches
+        traffic = {"workload": "cfg5", "n_local": bench_line["config"]["N"], "kernel": "k_ivf_scan (all class launches of one search)",
+                   "hbm_bytes_per_launch": rd + wr, "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
+                   "profiled_kernel_ms": scan_ns * 1e-6 / searches,
+                   "source": f"profiles/{tag}_pmc.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes)"}
+        with open(os.path.join(prof, "traffic_cfg5.json"), "w") as f:
+            json.dump(traffic, f, indent=1)
+        summary["dominant"] = traffic
     with open(os.path.join(prof, f"{tag}_pmc.json"), "w") as f:
         json.dump(summary, f, indent=1)
     print(json.dumps(summary.get("dominant"), indent=1))
