@@ -41,7 +41,7 @@ def group(disp):
 def main():
     src, tag = sys.argv[1], sys.argv[2]
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    prof = os.path.join(repo, "profiles")
+    prof = os.environ.get("PROF_OUT") or os.path.join(repo, "profiles")
     os.makedirs(prof, exist_ok=True)
     shutil.copy(os.path.join(src, "kt", "kt_kernel_stats.csv"), os.path.join(prof, f"{tag}_kernel_stats.csv"))
     bench_line = None
@@ -83,7 +83,7 @@ def main():
         summary["kernels"][f"{name} grid={grid}"] = flat
     # the dominant screen launch (largest mean duration among k_screen_*)
     screens = {k: v for k, v in summary["kernels"].items() if "k_screen" in k and v.get("dur_s")}
-    if screens and bench_line:
+    if screens and bench_line and bench_line["config"]["workload"] != "cfg5":
         top = max(screens, key=lambda k: screens[k]["dur_s"])
         t = screens[top]
         cfg = bench_line["config"]
