@@ -98,6 +98,18 @@ class ShardedFlatIndex:
         if len(x_local):
             self.index.add(x_local)
 
+    def add_shard_from_file(self, path: str) -> None:
+        """Load this rank's contiguous row range of a faiss flat (or HNSW-wrapped flat) index file:
+        only the shard's bytes are read, streamed file -> pinned chunks -> this rank's HBM."""
+        from . import faiss_format
+        ff = faiss_format.read_index(path)
+        if ff.d != self.d:
+            raise ValueError(f"index file dimension {ff.d} != {self.d}")
+        row0, n = shard_range(ff.ntotal, self.rank, self.world)
+        self.row0, self.n_total = row0, int(ff.ntotal)
+        if n:
+            self.index.add_from_file(path, ff.payload_offset + row0 * self.d * 4, n)
+
     def add_synthetic(self, seed: int, n_total: int, normalize: bool = True) -> None:
         """Each rank generates its own contiguous shard of the synthetic corpus in HBM."""
         row0, n = shard_range(int(n_total), self.rank, self.world)

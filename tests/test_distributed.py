@@ -40,7 +40,7 @@ def _oracle_merge(metric, Sg, Ig, k):
     return torch.from_numpy(S), torch.from_numpy(I), torch.from_numpy(D)
 
 
-def _worker(rank, world, port, N, d, nq, k, metric, use_broadcast, outdir):
+def _worker(rank, world, port, N, d, nq, k, metric, use_broadcast, outdir, from_file=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -49,7 +49,11 @@ def _worker(rank, world, port, N, d, nq, k, metric, use_broadcast, outdir):
         sh = ShardedFlatIndex(d, metric, index=OracleFlatIndex(d, metric),
                               local_search=_oracle_local_search, merge=_oracle_merge)
         row0, n = shard_range(N, rank, world)
-        sh.add_shard(x[row0:row0 + n], row0, N)
+        if from_file:  # each rank streams only its own row range of the faiss file
+            sh.add_shard_from_file(from_file)
+            assert (sh.row0, sh.n_local, sh.n_total) == (row0, n, N)
+        else:
+            sh.add_shard(x[row0:row0 + n], row0, N)
         q = torch.from_numpy(O.synth_rows(O.SEED_QUERIES, 0, nq, d, True, "f32"))
         if use_broadcast and rank != 0:
             q = torch.zeros_like(q)  # rank 0's batch must arrive by broadcast
@@ -59,9 +63,9 @@ def _worker(rank, world, port, N, d, nq, k, metric, use_broadcast, outdir):
         dist.destroy_process_group()
 
 
-def _run(tmp_path, N, d, nq, k, metric="ip", use_broadcast=False, world=2):
-    mp.spawn(_worker, args=(world, _free_port(), N, d, nq, k, metric, use_broadcast, str(tmp_path)), nprocs=world,
-             join=True)
+def _run(tmp_path, N, d, nq, k, metric="ip", use_broadcast=False, world=2, from_file=None):
+    mp.spawn(_worker, args=(world, _free_port(), N, d, nq, k, metric, use_broadcast, str(tmp_path), from_file),
+             nprocs=world, join=True)
     outs = [np.load(tmp_path / f"r{r}.npz") for r in range(world)]
     x = O.synth_rows(O.SEED_CORPUS, 0, N, d, True, "f32")
     q = O.synth_rows(O.SEED_QUERIES, 0, nq, d, True, "f32")
@@ -100,3 +104,11 @@ def test_two_rank_empty_shard_and_k_beyond_rows(tmp_path):
     outs = _run(tmp_path, N=1, d=8, nq=2, k=4)
     assert (outs[0]["I"][:, 1:] == -1).all()
     assert (outs[1]["I"][:, 0] == 0).all()
+
+
+def test_two_rank_shards_loaded_from_index_file(tmp_path):
+    from photo_search_engine_amd import faiss_format as F
+    x = O.synth_rows(O.SEED_CORPUS, 0, 777, 20, True, "f32")
+    p = str(tmp_path / "corpus.index")
+    F.write_flat(p, x, 0)
+    _run(tmp_path, N=777, d=20, nq=4, k=9, from_file=p)
