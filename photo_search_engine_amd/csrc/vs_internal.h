@@ -245,8 +245,11 @@ struct IvfScanArgs {
     u64* glist;                // per-query candidate lists [nq][lcap] (refine input) ...
     int* gcnt;                 // ... with their lengths (zeroed before the scan)
     int lcap;
+    int* next_item;            // k_ivf_scan_dyn: work-queue counter (zeroed before the launch)
 };
 hipError_t launch_ivf_scan(int dt, int nq_class, const IvfScanArgs& a, int grid, hipStream_t st);
+// every class in one launch, items fetched dynamically (nq_class of each item from its query count)
+hipError_t launch_ivf_scan_dyn(int dt, const IvfScanArgs& a, int grid, hipStream_t st);
 hipError_t launch_round_f32(int dt, float* x, int64_t n, hipStream_t st);  // in place, to the dtype's values
 // pack fp32 rows into the slots slots[r] (slot_id[slot] = id0 + r); sqn / maxsq as k_pack_rows
 hipError_t launch_pack_rows_map(int dt, const float* src, int64_t n, int d, int dpad, uint8_t* data,

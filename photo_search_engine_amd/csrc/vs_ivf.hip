@@ -47,7 +47,7 @@ struct vs_ivf {
     bool csr_dirty = true;
     // workspaces (add: exclusive lock; search / reconstruct: search_mtx)
     DevBuf tmp_rows, slots, assign_ids;
-    DevBuf qdev, probes, items, qp, qinfo, cand, glist, gcnt, cert, outD, outI, rec;
+    DevBuf qdev, probes, items, qp, qinfo, cand, glist, gcnt, cert, outD, outI, rec, next_item;
     std::vector<int64_t> probes_h;
     std::vector<int> cert_h;
     hipStream_t own = nullptr;
@@ -241,10 +241,16 @@ void search_core(vs_ivf* ix, const float* q_dev, int64_t nq, int k, int nprobe, 
     size_t total_ints = 0;
     for (auto& v : cls_items) total_ints += v.size();
     ix->items.ensure(std::max<size_t>(total_ints, 1) * sizeof(int));
+    // one dynamic launch (default) takes the items most expensive class first; VS_IVF_DYN=0 keeps
+    // one launch per class (A/B)
+    static const bool dyn = !(getenv("VS_IVF_DYN") && atoi(getenv("VS_IVF_DYN")) == 0);
     {
         std::vector<int> all;
         all.reserve(total_ints);
-        for (auto& v : cls_items) all.insert(all.end(), v.begin(), v.end());
+        if (dyn)
+            for (int c = 3; c >= 0; --c) all.insert(all.end(), cls_items[c].begin(), cls_items[c].end());
+        else
+            for (auto& v : cls_items) all.insert(all.end(), v.begin(), v.end());
         if (!all.empty())
             HIP_CHECK(hipMemcpyAsync(ix->items.p, all.data(), all.size() * sizeof(int), hipMemcpyHostToDevice, st));
         upload_csr(ix, st);  // synchronises the stream, so `all` may go out of scope
@@ -284,7 +290,15 @@ void search_core(vs_ivf* ix, const float* q_dev, int64_t nq, int k, int nprobe, 
         HIP_CHECK(hipEventRecord(e0, st));
     }
     size_t off = 0;
-    for (int c = 0; c < 4; ++c) {
+    if (dyn) {
+        ix->next_item.ensure(sizeof(int));
+        HIP_CHECK(hipMemsetAsync(ix->next_item.p, 0, sizeof(int), st));
+        a.next_item = ix->next_item.as<int>();
+        a.items = ix->items.as<int>();
+        a.n_items = (int)(total_ints / IVF_ITEM_INTS);
+        if (a.n_items > 0) HIP_CHECK(launch_ivf_scan_dyn(ix->dtype, a, std::min(a.n_items, max_grid), st));
+    }
+    for (int c = 0; c < 4 && !dyn; ++c) {
         const int n_items = (int)(cls_items[c].size() / IVF_ITEM_INTS);
         a.items = ix->items.as<int>() + off;
         a.n_items = n_items;
@@ -429,7 +443,7 @@ void vs_ivf_destroy(vs_ivf* ix) {
         (void)hipDeviceSynchronize();
         for (DevBuf* b : {&ix->d_page_off, &ix->d_list_pages, &ix->d_list_n, &ix->tmp_rows, &ix->slots, &ix->assign_ids,
                           &ix->qdev, &ix->probes, &ix->items, &ix->qp, &ix->qinfo, &ix->cand, &ix->glist, &ix->gcnt,
-                          &ix->cert, &ix->outD, &ix->outI, &ix->rec})
+                          &ix->cert, &ix->outD, &ix->outI, &ix->rec, &ix->next_item})
             b->release();
         for (auto& pr : ix->tev) {
             (void)hipEventDestroy(pr.first);

@@ -595,7 +595,8 @@ __device__ __forceinline__ void mf_wait_barrier(int ahead, bool loader) {
             else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
             else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
         } else {
-            if (ahead >= 2) asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            if (ahead >= 3) asm volatile("s_waitcnt vmcnt(24) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            else if (ahead == 2) asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)\n\ts_barrier" ::: "memory");
             else if (ahead == 1) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
             else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
         }
@@ -684,6 +685,32 @@ __device__ __forceinline__ void mf_mfma(const uint4 (&af)[4], const uint4 (&bfr)
         for (int ni = 0; ni < 8; ++ni) acc[mi][ni] = mfma16<DT>(af[mi], bfr[ni], acc[mi][ni]);
 }
 
+// Software-pipelined K-step (MODE 24): 32 MFMAs on the fragments of stage s already in registers
+// (ca, cb), with the ds_reads of stage s+1 interleaved: next A into na at the start, next B[ni]
+// into cb[ni] right after the MFMA group that last reads cb[ni] (ni-outer order), so only 16
+// extra VGPRs are live and the LDS read latency hides behind the MFMA pipe instead of idling it
+// after every barrier.  sched_barrier pins the order (hipcc would hoist every read to the top).
+template <int DT>
+__device__ __forceinline__ void mf_compute_sp(const uint8_t* nbuf, uint4 (&ca)[4], uint4 (&cb)[8],
+                                              floatx4 (&acc)[4][8], int wm, int wn, int lane_off) {
+    uint4 na[4];
+    const uint8_t* pa = nbuf + wm * 4096 + lane_off;
+    const uint8_t* pb = nbuf + 16384 + wn * 8192 + lane_off;
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) na[mi] = *(const uint4*)(pa + mi * 1024);
+#pragma unroll
+    for (int ni = 0; ni < 8; ++ni) {
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) acc[mi][ni] = mfma16<DT>(ca[mi], cb[ni], acc[mi][ni]);
+        __builtin_amdgcn_sched_barrier(0);
+        cb[ni] = *(const uint4*)(pb + ni * 1024);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) ca[mi] = na[mi];
+}
+
 // compact one (workgroup, query) candidate buffer to its best K keys (one wave)
 template <int E>
 __device__ __forceinline__ void mf_wave_compact(u64* __restrict__ buf, int n, int K, u64* thr_key, float* thr_f,
@@ -724,11 +751,11 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
     constexpr bool XP = MODE == 21 || MODE == 22 || MODE == 23;
     constexpr bool LOADS = (MODE != 1 && MODE < 3) || (MODE >= 6 && MODE != 12);  // (incl. seed, stamps)
     constexpr bool MATH = (MODE != 2 && MODE < 6) || MODE == 9 || MODE == 10 || MODE == 13 || MODE == 14 ||
-                          MODE == MF_SEED_MODE || MODE == MF_STAMP_MODE || MODE == 16 || MODE == 17 || XP;
+                          MODE == MF_SEED_MODE || MODE == MF_STAMP_MODE || MODE == 16 || MODE == 17 || MODE == 24 || XP;
     constexpr bool PP = MODE == 11 || MODE == 12;  // ping-pong: waves 4-7 half a K-step behind waves 0-3
     constexpr bool SEED = MODE == MF_SEED_MODE;  // threshold-seed pass: group maxima only
     constexpr bool EPI = MODE < 3 || MODE == 13 || MODE == 14 || SEED || MODE == MF_STAMP_MODE || MODE == 16 ||
-                         MODE == 17 || XP;
+                         MODE == 17 || MODE == 24 || XP;
     constexpr bool INS = MODE != 13;   // threshold passes insert candidates
     constexpr bool CHECK = MODE != 13 && MODE != 14;  // deferred compaction check + pool flush
     constexpr bool BAR = MODE < 4 || MODE >= 6;  // (incl. seed, stamps)
@@ -741,6 +768,7 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
     constexpr bool STAMP = MODE == MF_STAMP_MODE;  // = production + per-phase s_memtime stamps
     constexpr bool BAL = MODE == 16;               // balanced DMA issue (4 per wave on all 8 waves)
     constexpr bool PAIR = MODE == 17;              // one barrier per 2 K-steps (needs an even K-step count)
+    constexpr bool SP = MODE == 24;                // fragment reads of stage s+1 pipelined under stage s's MFMAs
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     u64* thr_key = (u64*)(smem + MF_SLOTS * MF_SLOT);
     float* thr_f = (float*)(smem + MF_SLOTS * MF_SLOT + 256 * 8);
@@ -794,7 +822,7 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
 
     // prologue: stages 0 .. DEPTH-1
     int iti = t0, iks = 0;  // (tile, k-step) of the next stage to issue
-    for (int j = 0; j < (PAIR ? 2 : MF_DEPTH) && j < S; ++j) {
+    for (int j = 0; j < (PAIR ? 2 : SP ? MF_SLOTS : MF_DEPTH) && j < S; ++j) {
         if constexpr (BAL)
             mf_stage_bal<NT>(a.corpus + (int64_t)iti * tbytes + (int64_t)iks * 16384, qt + (int64_t)iks * 16384,
                              ring + (uint32_t)(j * MF_SLOT), tid);
@@ -804,6 +832,18 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
         if (++iks == nks) { iks = 0; ++iti; }
     }
     if constexpr (!BAR) mf_barrier_drain();
+    uint4 ca[4], cb[8];  // SP: fragments of the current stage, in registers
+    if constexpr (SP) {
+        if (S > 0) {  // stage 0 landed (stages 1..3 may still fly), then its fragments
+            mf_wait_barrier<true>(S - 1 < 3 ? S - 1 : 3, wid < 4);
+            const uint8_t* pa = smem + wm * 4096 + lane_off;
+            const uint8_t* pb = smem + 16384 + wn * 8192 + lane_off;
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi) ca[mi] = *(const uint4*)(pa + mi * 1024);
+#pragma unroll
+            for (int ni = 0; ni < 8; ++ni) cb[ni] = *(const uint4*)(pb + ni * 1024);
+        }
+    }
     int pti = iti, pks = iks;  // PAIR mode: next stage to issue
     int ti = t0, ks = 0;
     float sink = 0.0f;
@@ -823,6 +863,12 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
         }
         if constexpr (PAIR) {
             if ((s & 1) == 0) mf_barrier_drain();  // this pair's two stages landed, previous pair read
+        } else if constexpr (SP) {
+            // stage s+1 landed (its fragments are read during this step); stage s's fragments are in
+            // registers (lgkmcnt(0)), so slot s % 4 is free for stage s+4
+            const int last = S - 1 < s + 3 ? S - 1 : s + 3;  // youngest stage issued so far
+            const int ahead = last - (s + 1);
+            mf_wait_barrier<true>(ahead > 0 ? ahead : 0, wid < 4);
         } else {
             mf_wait_barrier<BAR, !QLOAD || BAL>(left < MF_DEPTH - 1 ? left : MF_DEPTH - 1, wid < 4 || BAL);
         }
@@ -831,10 +877,11 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
             t1 = __builtin_amdgcn_s_memtime();
             __builtin_amdgcn_sched_barrier(0);
         }
-        const bool do_issue = s + MF_DEPTH < S;
+        constexpr int AHEAD = SP ? MF_SLOTS : MF_DEPTH;  // stage issued at step s: s + AHEAD
+        const bool do_issue = s + AHEAD < S;
         const uint8_t* nA = a.corpus + (int64_t)iti * tbytes + (int64_t)iks * 16384;
         const uint8_t* nB = qt + (int64_t)iks * QSTEP;
-        const uint32_t nslot = ring + (uint32_t)(((s + MF_DEPTH) % MF_SLOTS) * MF_SLOT);
+        const uint32_t nslot = ring + (uint32_t)(((s + AHEAD) % MF_SLOTS) * MF_SLOT);
         if (do_issue) {
             if (++iks == nks) { iks = 0; ++iti; }
         }
@@ -852,6 +899,9 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
         } else if constexpr (IL) {
             mf_compute_il<DT, NT>(smem + (s % MF_SLOTS) * MF_SLOT, acc, wm, wn, lane_off, do_issue && wid < 4, nA, nB,
                                   nslot, wid, lane);
+        } else if constexpr (SP) {
+            if (do_issue && wid < 4) mf_stage<true, NT>(nA, nB, nslot, tid);
+            mf_compute_sp<DT>(smem + ((s + 1) % MF_SLOTS) * MF_SLOT, ca, cb, acc, wm, wn, lane_off);
         } else if constexpr (PAIR) {
             if ((s & 1) == 0) {  // the next pair's two stages, into the slots the previous pair used
 #pragma unroll
@@ -1267,6 +1317,175 @@ __global__ void __launch_bounds__(256) k_screen_gemv(ScreenArgs a, const float* 
 // persistent over work items (list, page range, <= NQ queries); per (item, query) the best Kp
 // keys (screen score, storage slot) are appended to the query's candidate list for k_refine.
 // ------------------------------------------------------------------------------------------------
+// 16 B streaming load with the non-temporal hint (each list byte is read once per query group)
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld_nt16(const uint8_t* p) {
+    const u32x4_t v = __builtin_nontemporal_load((const u32x4_t*)p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// One work item (list l, pages [p0, p1), nqi <= NQ queries) of the IVF scan, by one 256-thread
+// block.  Shared state (thresholds, counts, query ids) is the caller's; the block is synchronised
+// on entry and exit.
+template <int DT, int NQ>
+__device__ __forceinline__ void ivf_scan_item(const IvfScanArgs& a, const int* itm, u64* cand, u64* thr_key,
+                                              float* thr_f, int* cnt, int* qid, int* red, int* off_s) {
+    constexpr int ES = DT == DT_F32 ? 4 : 2;
+    constexpr int CB = CH * ES;
+    constexpr int LPR = CB / 16;
+    constexpr int RPI = 64 / LPR;
+    constexpr int EPU = 16 / ES;
+    constexpr int RG = 64 / RPI;
+    constexpr int RB0 = (NQ <= 2) ? 8 : 4;  // rows per pass (register budget of the shared dyn kernel)
+    constexpr int RB = RB0 < RG ? RB0 : RG;
+    static_assert(RG % RB == 0, "row groups");
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int unit = lane % LPR, rsub = lane / LPR;
+    const int nch = a.dpad / CH;
+    const int64_t tbytes = (int64_t)TR * a.dpad * ES;
+    const int trigger = a.cap - TR;
+    const int l = itm[0], p0 = itm[1], p1 = itm[2], nqi = itm[3];
+    if (tid < NQ) {
+        const bool real = tid < nqi;
+        thr_key[tid] = real ? 0ull : ~0ull;
+        thr_f[tid] = real ? -INFINITY : INFINITY;
+        cnt[tid] = 0;
+        qid[tid] = real ? itm[4 + tid] : itm[4];
+    }
+    __syncthreads();
+    const int64_t ln = a.list_n[l];
+    const int pbase = a.page_off[l];
+    for (int p = p0; p < p1; ++p) {
+        const int64_t page = a.list_pages[pbase + p];
+        const int nvalid = (int)(ln - (int64_t)p * TR < TR ? ln - (int64_t)p * TR : TR);
+        const uint8_t* tb = a.data + page * tbytes;
+        const int64_t slot0 = page * TR;
+        for (int gb = 0; gb < RG / RB; ++gb) {
+            float acc[RB][NQ];
+#pragma unroll
+            for (int r = 0; r < RB; ++r)
+#pragma unroll
+                for (int qi = 0; qi < NQ; ++qi) acc[r][qi] = 0.0f;
+#pragma unroll 2
+            for (int c = 0; c < nch; ++c) {
+                float qv[NQ][EPU];
+#pragma unroll
+                for (int qi = 0; qi < NQ; ++qi) {
+                    const float4* qs = (const float4*)(a.qp + (int64_t)qid[qi] * a.dpad + c * CH + unit * EPU);
+#pragma unroll
+                    for (int h = 0; h < EPU / 4; ++h) {
+                        float4 t = qs[h];
+                        qv[qi][4 * h + 0] = t.x; qv[qi][4 * h + 1] = t.y;
+                        qv[qi][4 * h + 2] = t.z; qv[qi][4 * h + 3] = t.w;
+                    }
+                }
+                uint4 raw[RB];
+#pragma unroll
+                for (int r = 0; r < RB; ++r) {
+                    const int rit = wid * 64 + (gb * RB + r) * RPI + rsub;
+                    raw[r] = ld_nt16(tb + (int64_t)c * TR * CB + rit * CB + unit * 16);
+                }
+#pragma unroll
+                for (int r = 0; r < RB; ++r) {
+                    float xv[EPU];
+                    unpack16<DT>(raw[r], xv);
+#pragma unroll
+                    for (int qi = 0; qi < NQ; ++qi)
+#pragma unroll
+                        for (int e = 0; e < EPU; ++e) acc[r][qi] = fmaf(xv[e], qv[qi][e], acc[r][qi]);
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < RB; ++r)
+#pragma unroll
+                for (int qi = 0; qi < NQ; ++qi) {
+                    float v = acc[r][qi];
+#pragma unroll
+                    for (int s = 1; s < LPR; s <<= 1) v += __shfl_xor(v, s, 64);
+                    acc[r][qi] = v;
+                }
+            if (unit == 0) {
+#pragma unroll
+                for (int r = 0; r < RB; ++r) {
+                    const int rit = wid * 64 + (gb * RB + r) * RPI + rsub;
+                    if (rit >= nvalid) continue;  // page padding of the list's last page
+                    const int64_t slot = slot0 + rit;
+                    const float sq = a.metric == METRIC_L2 ? a.sqn[slot] : 0.0f;
+#pragma unroll
+                    for (int qi = 0; qi < NQ; ++qi) {
+                        float sc = acc[r][qi];
+                        if (a.metric == METRIC_L2) sc = 2.0f * sc - sq;
+                        if (sc >= thr_f[qi]) {
+                            const u64 key = mk_key(sc, (uint32_t)slot);
+                            if (key > thr_key[qi]) {
+                                const int s = atomicAdd(&cnt[qi], 1);
+                                if (s < a.cap) cand[(size_t)qi * a.cap + s] = key;
+                            }
+                        }
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        for (int qi = 0; qi < nqi; ++qi) {
+            const int n = cnt[qi];
+            if (n > trigger) {  // block-uniform
+                u64* buf = cand + (size_t)qi * a.cap;
+                const u64 t = block_kth_mem(buf, n, a.Kp, red);
+                block_compact_mem(buf, buf, n, t, red);
+                if (tid == 0) {
+                    thr_key[qi] = t;
+                    thr_f[qi] = key_score(t);
+                    cnt[qi] = a.Kp;
+                }
+                __syncthreads();
+            }
+        }
+    }
+    __syncthreads();
+    // flush: the item's best <= Kp keys per query, appended to the query's candidate list
+    for (int qi = 0; qi < nqi; ++qi) {
+        u64* buf = cand + (size_t)qi * a.cap;
+        int n = cnt[qi] < a.cap ? cnt[qi] : a.cap;
+        if (n > a.Kp) {
+            const u64 t = block_kth_mem(buf, n, a.Kp, red);
+            n = block_compact_mem(buf, buf, n, t, red);
+        }
+        if (tid == 0) *off_s = n ? atomicAdd(&a.gcnt[qid[qi]], n) : 0;
+        __syncthreads();
+        u64* dst = a.glist + (size_t)qid[qi] * a.lcap + *off_s;
+        for (int j = tid; j < n; j += 256) dst[j] = buf[j];
+        __syncthreads();
+    }
+}
+
+// All query-count classes in ONE persistent launch with dynamic item fetch (an atomic counter):
+// the host orders items most expensive class first, so no per-class launch tail idles the HBM
+// stream and no block waits on a static share of heavier items.
+template <int DT>
+__global__ void __launch_bounds__(256, 3) k_ivf_scan_dyn(IvfScanArgs a) {
+    __shared__ u64 thr_key[IVF_QG];
+    __shared__ float thr_f[IVF_QG];
+    __shared__ int cnt[IVF_QG];
+    __shared__ int qid[IVF_QG];
+    __shared__ int red[8];
+    __shared__ int off_s, item_s;
+    u64* cand = a.cand + (size_t)blockIdx.x * IVF_QG * a.cap;
+    for (;;) {
+        __syncthreads();  // the previous item is flushed, item_s is free
+        if (threadIdx.x == 0) item_s = atomicAdd(a.next_item, 1);
+        __syncthreads();
+        const int it = item_s;
+        if (it >= a.n_items) break;  // block-uniform: every wave leaves here, the queue is drained
+        const int* itm = a.items + (size_t)it * IVF_ITEM_INTS;
+        const int nqi = itm[3];
+        if (nqi <= 1) ivf_scan_item<DT, 1>(a, itm, cand, thr_key, thr_f, cnt, qid, red, &off_s);
+        else if (nqi <= 2) ivf_scan_item<DT, 2>(a, itm, cand, thr_key, thr_f, cnt, qid, red, &off_s);
+        else if (nqi <= 4) ivf_scan_item<DT, 4>(a, itm, cand, thr_key, thr_f, cnt, qid, red, &off_s);
+        else ivf_scan_item<DT, IVF_QG>(a, itm, cand, thr_key, thr_f, cnt, qid, red, &off_s);
+    }
+}
+
 template <int DT, int NQ>
 __global__ void __launch_bounds__(256) k_ivf_scan(IvfScanArgs a) {
     constexpr int ES = DT == DT_F32 ? 4 : 2;
@@ -1988,6 +2207,7 @@ static void launch_mfma_mode(const ScreenArgs& a, const uint8_t* qt, int nqb, hi
         case 21: launch_mfma_one<DT, METRIC, 21>(a, qt, nqb, st); break;
         case 22: launch_mfma_one<DT, METRIC, 22>(a, qt, nqb, st); break;
         case 23: launch_mfma_one<DT, METRIC, 23>(a, qt, nqb, st); break;
+        case 24: launch_mfma_one<DT, METRIC, 24>(a, qt, nqb, st); break;
         default: launch_mfma_one<DT, METRIC, 0>(a, qt, nqb, st); break;
     }
 }
@@ -2120,6 +2340,15 @@ hipError_t launch_ivf_scan(int dt, int nq_class, const IvfScanArgs& a, int grid,
     if (dt == DT_F32) launch_ivf_scan_dt<DT_F32>(nq_class, a, grid, st);
     else if (dt == DT_BF16) launch_ivf_scan_dt<DT_BF16>(nq_class, a, grid, st);
     else launch_ivf_scan_dt<DT_F16>(nq_class, a, grid, st);
+    return hipGetLastError();
+}
+
+hipError_t launch_ivf_scan_dyn(int dt, const IvfScanArgs& a, int grid, hipStream_t st) {
+    if (a.n_items <= 0 || grid <= 0) return hipSuccess;
+    if (!a.next_item) return hipErrorInvalidValue;
+    if (dt == DT_F32) hipLaunchKernelGGL(k_ivf_scan_dyn<DT_F32>, dim3(grid), dim3(256), 0, st, a);
+    else if (dt == DT_BF16) hipLaunchKernelGGL(k_ivf_scan_dyn<DT_BF16>, dim3(grid), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(k_ivf_scan_dyn<DT_F16>, dim3(grid), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 
