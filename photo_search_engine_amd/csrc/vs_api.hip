@@ -9,6 +9,7 @@
 #include <cmath>
 #include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <shared_mutex>
@@ -30,11 +31,12 @@ struct Ctx {
     hipStream_t stream = nullptr;
     DevBuf qdev, qtile, qinfo, qpad, cand, part, merge_a, merge_b, outD, outI, outS, cert, thr0, seedmax, gcnt;
     DevBuf rows[2];  // read_rows_host: unpacked fp32 chunks
+    DevBuf tilectr;  // GEMV screen: tile work-queue counter
     PinnedPair pin;  // read_rows_host: pinned landing chunks
     std::vector<int> cert_host;
     ~Ctx() {
         for (DevBuf* b : {&qdev, &qtile, &qinfo, &qpad, &cand, &part, &merge_a, &merge_b, &outD, &outI, &outS, &cert, &thr0,
-                          &seedmax, &gcnt, &rows[0], &rows[1]})
+                          &seedmax, &gcnt, &rows[0], &rows[1], &tilectr})
             b->release();
         pin.release();
         if (stream) hipStreamDestroy(stream);
@@ -137,6 +139,11 @@ void refresh_maxsq(vs_index* ix) {
 constexpr int kOptimisticSeedRank = 1;  // seed_rank argument: > 0 selects the optimistic rank
 constexpr double kOptimisticPassFactor = 8.0;
 
+bool gemv_dyn() {
+    static const bool on = !(getenv("VS_GEMV_DYN") && atoi(getenv("VS_GEMV_DYN")) == 0);
+    return on;
+}
+
 // Enqueue one query block through screen -> merge -> refine.  q: device fp32 [nqb][d].
 // seed_rank: 0 = proven (safe) seed, > 0 = optimistic seed at that sample rank (see k_seed_select)
 void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, float* D, int64_t* I, double* S64,
@@ -165,7 +172,8 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
     } else {
         QB = nqb <= 1 ? 1 : nqb <= 2 ? 2 : nqb <= 4 ? 4 : 8;
         a.cap = (int)round_up(Kp + 2 * TR, 256);
-        a.G = (int)std::min<int64_t>(tiles, (int64_t)ix->num_cu * 8);
+        // work-queue tiles over exactly the resident blocks (VS_GEMV_DYN=0: static ranges, 8 per CU)
+        a.G = (int)std::min<int64_t>(tiles, (int64_t)ix->num_cu * (gemv_dyn() ? gemv_blocks_per_cu(ix->dtype, QB) : 8));
         c->qpad.ensure((size_t)QB * ix->dpad * sizeof(float));
         HIP_CHECK(launch_pack_qf32(q, nqb, QB, ix->d, ix->dpad, c->qpad.as<float>(), c->qinfo.as<float>(), st));
     }
@@ -174,6 +182,11 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
     c->part.ensure((size_t)a.G * QB * Kp * sizeof(u64));  // GEMV: [G][QB][Kp]; MFMA: [QB][G*Kp] survivor lists
     a.cand = c->cand.as<u64>();
     a.part = c->part.as<u64>();
+    if (!use_mfma && gemv_dyn()) {
+        c->tilectr.ensure(sizeof(int));
+        HIP_CHECK(hipMemsetAsync(c->tilectr.p, 0, sizeof(int), st));
+        a.next_tile = c->tilectr.as<int>();
+    }
     if (use_mfma) {
         a.glist = c->part.as<u64>();
         a.gcnt = c->gcnt.as<int>();

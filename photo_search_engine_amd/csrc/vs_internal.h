@@ -172,7 +172,9 @@ struct ScreenArgs {
     int* gcnt;               // ... with its length per query (zeroed by k_pack_qtile)
     int lcap;                // = G * Kp
     unsigned long long* stamps;  // diagnostic build only (VS_MF_STAMPS): [G][8 waves][5] phase cycles
+    int* next_tile;          // GEMV: tile work-queue counter (zeroed before the launch); null = static ranges
 };
+int gemv_blocks_per_cu(int dt, int nqpad);  // resident k_screen_gemv blocks per CU (occupancy API)
 
 // ---- launchers (vs_kernels.hip) -------------------------------------------------------------
 hipError_t launch_pack_rows(int dt, const float* src, int64_t n, int d, int dpad, uint8_t* data, int64_t lrow0,

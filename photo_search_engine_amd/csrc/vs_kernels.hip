@@ -1191,6 +1191,7 @@ __global__ void __launch_bounds__(256) k_screen_gemv(ScreenArgs a, const float* 
     __shared__ float thr_f[NQ];
     __shared__ int cnt[NQ];
     __shared__ int red[8];
+    __shared__ int tile_s;
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int unit = lane % LPR, rsub = lane / LPR;
@@ -1209,7 +1210,20 @@ __global__ void __launch_bounds__(256) k_screen_gemv(ScreenArgs a, const float* 
     u64* cand = a.cand + (size_t)blk * NQ * a.cap;
     const int trigger = a.cap - TR;
 
-    for (int ti = t0; ti < t1; ++ti) {
+    // tiles: a static contiguous range, or (next_tile) one at a time from a work queue with a grid
+    // of exactly the resident blocks, so no second partial round of blocks idles the HBM stream
+    for (int it = 0;; ++it) {
+        int ti;
+        if (a.next_tile) {
+            if (tid == 0) tile_s = atomicAdd(a.next_tile, 1);
+            __syncthreads();
+            ti = tile_s;
+            __syncthreads();  // every thread has its tile before tile_s is reused
+            if (ti >= a.tiles) break;  // block-uniform
+        } else {
+            ti = t0 + it;
+            if (ti >= t1) break;
+        }
         const uint8_t* tb = a.corpus + (int64_t)ti * tbytes;
         const int64_t rowbase = (int64_t)ti * TR;
         for (int gb = 0; gb < RG / RB; ++gb) {
@@ -2220,6 +2234,26 @@ hipError_t launch_screen_mfma(int dt, const ScreenArgs& a, const uint8_t* qt, in
         else launch_mfma_mode<DT_F16, METRIC_L2>(a, qt, nqb, st);
     }
     return hipGetLastError();
+}
+
+template <int DT>
+static int gemv_occ(int nqpad) {
+    int n = 0;
+    hipError_t e = hipSuccess;
+    switch (nqpad) {
+        case 1: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_screen_gemv<DT, 1>, 256, 0); break;
+        case 2: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_screen_gemv<DT, 2>, 256, 0); break;
+        case 4: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_screen_gemv<DT, 4>, 256, 0); break;
+        default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_screen_gemv<DT, 8>, 256, 0); break;
+    }
+    return e == hipSuccess && n > 0 ? n : 4;
+}
+int gemv_blocks_per_cu(int dt, int nqpad) {
+    static int cache[3][9] = {};  // benign race: idempotent
+    const int q = nqpad <= 1 ? 1 : nqpad <= 2 ? 2 : nqpad <= 4 ? 4 : 8;
+    int& v = cache[dt][q];
+    if (!v) v = dt == DT_F32 ? gemv_occ<DT_F32>(q) : dt == DT_BF16 ? gemv_occ<DT_BF16>(q) : gemv_occ<DT_F16>(q);
+    return v;
 }
 
 template <int DT>
