@@ -61,7 +61,8 @@ def parse():
     ap.add_argument("--no-recall", action="store_true", help="cfg5: skip the exact ground truth (profiling runs)")
     ap.add_argument("--iso-data", action="store_true",
                     help="cfg5: isotropic rows (the flat bench's data) instead of the Gaussian mixture")
-    ap.add_argument("--traffic-file", default=os.path.join(REPO, "profiles", "traffic_cfg3.json"))
+    ap.add_argument("--traffic-file", default=None,
+                    help="rocprofv3 PMC summary giving HBM bytes per launch (default profiles/traffic_<workload>.json)")
     return ap.parse_args()
 
 
@@ -150,14 +151,8 @@ def main():
     alg_bytes = n_local * d * es + nq * d * es + nq * k * 12
     alg_flops = 2.0 * n_local * d * nq
     achieved_gbs = alg_bytes / (kavg * 1e-3) / 1e9
-    traffic = None
-    try:
-        with open(args.traffic_file) as f:
-            tr = json.load(f)
-        if tr.get("workload") == args.workload and tr.get("n_local") == n_local:
-            traffic = tr.get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
-        pass
+    traffic = _traffic(args.traffic_file or os.path.join(REPO, "profiles", f"traffic_{args.workload}.json"),
+                       args.workload, n_local)
 
     out = None
     if rank == 0:
