@@ -184,7 +184,8 @@ def main():
                 "mfma_tflops": round(alg_flops / (kavg * 1e-3) / 1e12, 1),
                 "mfma_frac": round(alg_flops / (kavg * 1e-3) / 1e12 / MFMA_BF16_PEAK_TF, 4),
             },
-            "uncertified_queries": uncert,
+            # first-pass certificate failures; every one was re-searched exactly (search_device_exact)
+            "uncertified_first_pass": uncert,
             "build_s": round(t_build, 2),
         }
     if rank == 0 and G == 1 and not args.no_cpu_baseline:
@@ -476,7 +477,7 @@ def run_ivf(args):
             "kernel_ms": round(kavg, 4),
             "alg_bytes_per_launch": alg_bytes,
         },
-        "uncertified_queries": None,
+        "uncertified_first_pass": None,
         "build_s": round(t_build, 2),
         "recall@10": round(hit / (nq * 10.0), 6) if parts_S else None,
         "probed_recall@10": round(got / max(need, 1), 6) if parts_S else None,

@@ -78,6 +78,12 @@ int vs_search(vs_index* index, const float* q, int64_t nq, int32_t k, float* D, 
 int vs_search_device(vs_index* index, const float* q_dev, int64_t nq, int32_t k, float* D_dev,
                      int64_t* I_dev, double* S64_dev, int64_t id_offset, void* stream);
 
+/* Same outputs, but exact for every query: the certificate flags are read back (one host sync)
+ * and uncertified queries are re-searched with deeper screens, as vs_search does.  The product's
+ * multi-GPU layer (photo_search_engine_amd/distributed.py) uses this one. */
+int vs_search_device_exact(vs_index* index, const float* q_dev, int64_t nq, int32_t k, float* D_dev,
+                           int64_t* I_dev, double* S64_dev, int64_t id_offset, void* stream);
+
 /* ---- merge of per-shard results (all-gather + K3 merge).
  * S_in/I_in: G x nq x k (device), each list sorted best-first; output nq x k best-first under
  * (score desc | asc for L2, id asc).  D_out is S_out rounded to fp32 (may be NULL). */

@@ -138,6 +138,7 @@ void refresh_maxsq(vs_index* ix) {
 // query left short is caught by the certificate and searched again with the proven seed
 constexpr int kOptimisticSeedRank = 1;  // seed_rank argument: > 0 selects the optimistic rank
 constexpr double kOptimisticPassFactor = 8.0;
+constexpr int kOptimisticMinRank = 4;
 
 bool gemv_dyn() {
     static const bool on = !(getenv("VS_GEMV_DYN") && atoi(getenv("VS_GEMV_DYN")) == 0);
@@ -232,7 +233,10 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
         if (seed_rank > 0) {
             const double sampled = (double)sa.G * TR;
             const double r = std::ceil(kOptimisticPassFactor * Kp * sampled / (double)ix->ntotal);
-            rank = (int)std::min<double>(std::max<double>(r, 1.0), (double)Kp);
+            // floor: at rank 1 a sample maximum that falls inside the true top-Kp leaves fewer than
+            // Kp survivors (probability ~Kp * sampled / N per query, ~2% at 100M rows); with >= 4
+            // sampled rows required in the top-Kp the failure odds drop to ~(that)^4 / 24
+            rank = (int)std::min<double>(std::max<double>(r, (double)kOptimisticMinRank), (double)Kp);
         }
         HIP_CHECK(launch_seed_select(sa.seedmax, M, nqb, rank, c->thr0.as<u64>(), st));
         a.thr0 = c->thr0.as<u64>();
@@ -373,10 +377,10 @@ void check_index(const vs_index* ix) {
 
 }  // namespace
 
-// exact device search for in-library callers (the IVF coarse quantizer): like vs_search_device,
+// exact device search (vs_search_device_exact; the IVF coarse quantizer): like vs_search_device,
 // but certificate failures are re-searched with deeper screens, as vs_search does
 void vs::search_exact_device(vs_index* ix, const float* q_dev, int64_t nq, int k, int64_t* I_dev, double* S64_dev,
-                             hipStream_t st) {
+                             hipStream_t st, float* D_dev, int64_t id_offset) {
     check_index(ix);
     if (nq <= 0) return;
     std::shared_lock<std::shared_mutex> lk(ix->rw);
@@ -387,8 +391,8 @@ void vs::search_exact_device(vs_index* ix, const float* q_dev, int64_t nq, int k
     c->outD.ensure((size_t)nq * k * sizeof(float));
     c->cert.ensure((size_t)nq * sizeof(int));
     const int Kp = screen_depth(k);
-    search_all(ix, c, q_dev, nq, k, Kp, c->outD.as<float>(), I_dev, S64_dev, c->cert.as<int>(), 0, st,
-               kOptimisticSeedRank);
+    search_all(ix, c, q_dev, nq, k, Kp, D_dev ? D_dev : c->outD.as<float>(), I_dev, S64_dev, c->cert.as<int>(),
+               id_offset, st, kOptimisticSeedRank);
     c->cert_host.resize((size_t)nq);
     HIP_CHECK(hipMemcpyAsync(c->cert_host.data(), c->cert.p, (size_t)nq * sizeof(int), hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));
@@ -398,8 +402,8 @@ void vs::search_exact_device(vs_index* ix, const float* q_dev, int64_t nq, int k
             if (Kr >= KP_MAX || Kr >= ix->ntotal)
                 throw VsError(VS_ERR_UNCERTIFIED, "exactness certificate failed at maximum screening depth");
             Kr = (int)std::min<int64_t>(std::min<int64_t>((int64_t)Kr * 4, KP_MAX), round_up(ix->ntotal, 16));
-            search_all(ix, c, q_dev + qi * ix->d, 1, k, Kr, c->outD.as<float>(), I_dev + qi * k,
-                       S64_dev ? S64_dev + qi * k : nullptr, c->cert.as<int>(), 0, st, /*safe seed*/ 0);
+            search_all(ix, c, q_dev + qi * ix->d, 1, k, Kr, D_dev ? D_dev + qi * k : c->outD.as<float>(), I_dev + qi * k,
+                       S64_dev ? S64_dev + qi * k : nullptr, c->cert.as<int>(), id_offset, st, /*safe seed*/ 0);
             HIP_CHECK(hipMemcpyAsync(&c->cert_host[qi], c->cert.p, sizeof(int), hipMemcpyDeviceToHost, st));
             HIP_CHECK(hipStreamSynchronize(st));
         }
@@ -643,6 +647,20 @@ int vs_search_device(vs_index* ix, const float* q_dev, int64_t nq, int32_t k, fl
         CtxLease L(ix);
         search_all(ix, L.c, q_dev, nq, k, screen_depth(k), D_dev, I_dev, S64_dev, nullptr, id_offset, st,
                    kOptimisticSeedRank);
+    });
+}
+
+int vs_search_device_exact(vs_index* ix, const float* q_dev, int64_t nq, int32_t k, float* D_dev, int64_t* I_dev,
+                           double* S64_dev, int64_t id_offset, void* stream) {
+    return guarded([&] {
+        check_index(ix);
+        if (nq < 0) throw VsError(VS_ERR_ARG, "nq must be >= 0");
+        if (k <= 0) throw VsError(VS_ERR_ARG, "k must be > 0");
+        if (screen_depth(k) < k) throw VsError(VS_ERR_ARG, "k too large (max " + std::to_string(KP_MAX * 4 / 5) + ")");
+        if (nq == 0) return;
+        if (!q_dev || !I_dev) throw VsError(VS_ERR_ARG, "null device buffer");
+        if (ix->ntotal == 0) throw VsError(VS_ERR_ARG, "index is empty");
+        search_exact_device(ix, q_dev, nq, k, I_dev, S64_dev, (hipStream_t)stream, D_dev, id_offset);
     });
 }
 

@@ -279,7 +279,7 @@ int64_t stream_chunk_rows(int d);  // rows per pinned chunk (32 MiB of fp32)
 // Exact top-k of device queries over a flat index, certificate failures re-searched (host-
 // synchronising).  I_dev [nq][k] (k <= ntotal), S64_dev optional.
 void search_exact_device(vs_index* ix, const float* q_dev, int64_t nq, int k, int64_t* I_dev, double* S64_dev,
-                         hipStream_t st);
+                         hipStream_t st, float* D_dev = nullptr, int64_t id_offset = 0);
 // seed pass: screen one tile per workgroup (tile_stride) and write per-query 16-row-group maxima
 hipError_t launch_seed_mfma(int dt, const ScreenArgs& a, const uint8_t* qt, int nqb, hipStream_t st);
 // thr0[q] = key just below the rank-th largest of the M group maxima of query q (0 if none)

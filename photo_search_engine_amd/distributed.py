@@ -60,7 +60,8 @@ def _device_local_search(index, q: torch.Tensor, k: int, row0: int):
     I = torch.empty((nq, k), dtype=torch.int64, device=q.device)
     D = torch.empty((nq, k), dtype=torch.float32, device=q.device)
     stream = torch.cuda.current_stream(q.device).cuda_stream
-    index.search_device(q.data_ptr(), nq, k, D.data_ptr(), I.data_ptr(), S.data_ptr(), row0, stream)
+    # exact for every query: uncertified screens are re-searched before the exchange
+    index.search_device_exact(q.data_ptr(), nq, k, D.data_ptr(), I.data_ptr(), S.data_ptr(), row0, stream)
     return S, I, D
 
 

@@ -108,6 +108,12 @@ class FlatIndex:
         check(self._L.vs_search_device(self._h, q_ptr, int(nq), int(k), D_ptr or None, I_ptr, S64_ptr or None,
                                        int(id_offset), stream or None))
 
+    def search_device_exact(self, q_ptr: int, nq: int, k: int, D_ptr: Optional[int], I_ptr: int,
+                            S64_ptr: Optional[int] = None, id_offset: int = 0, stream: Optional[int] = None) -> None:
+        """``search_device`` with certificate failures re-searched (one host sync per call)."""
+        check(self._L.vs_search_device_exact(self._h, q_ptr, int(nq), int(k), D_ptr or None, I_ptr, S64_ptr or None,
+                                             int(id_offset), stream or None))
+
     def set_timing(self, enable: bool) -> None:
         check(self._L.vs_set_timing(self._h, int(bool(enable))))
 

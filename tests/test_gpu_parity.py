@@ -232,6 +232,35 @@ def test_optimistic_seed_failure_falls_back_exactly(FlatIndex):
     assert ix.uncertified_count() > 0  # the optimistic pass was rejected (and then redone exactly)
 
 
+def test_device_exact_search_re_searches_uncertified_queries(FlatIndex):
+    # the adversarial corpus above through the device API used by the multi-GPU layer: the
+    # optimistic pass is rejected on the device and re-searched before the call returns
+    import torch
+    d, k = 64, 10
+    cu = _num_cu()
+    tiles = 32 * cu + 3
+    N = tiles * 256
+    x = O.synth_rows(O.SEED_CORPUS, 0, N, d, True, "f32")
+    q = O.synth_rows(O.SEED_QUERIES, 0, 16, d, True, "f32")
+    stride = tiles // cu
+    rng = np.random.default_rng(11)
+    for j in range(cu):
+        x[j * stride * 256 + 5] = q[j % 16] + 0.01 * rng.standard_normal(d).astype(np.float32)
+    ix = FlatIndex(d, "ip", "bf16")
+    ix.add(x)
+    qb = O.round_dtype(q, "bf16")
+    qd = torch.from_numpy(qb).cuda()
+    S = torch.empty((16, k), dtype=torch.float64, device="cuda")
+    I = torch.empty((16, k), dtype=torch.int64, device="cuda")
+    D = torch.empty((16, k), dtype=torch.float32, device="cuda")
+    ix.search_device_exact(qd.data_ptr(), 16, k, D.data_ptr(), I.data_ptr(), S.data_ptr(), 1000, 0)
+    Se, Ie = O.knn_exact(ix.reconstruct_n(0, N), qb, k, "ip")
+    np.testing.assert_array_equal(I.cpu().numpy(), Ie + 1000)
+    np.testing.assert_array_equal(S.cpu().numpy(), Se)
+    np.testing.assert_array_equal(D.cpu().numpy(), Se.astype(np.float32))
+    assert ix.uncertified_count() > 0
+
+
 def test_device_shard_merge_matches_oracle(FlatIndex):
     # 4 row shards searched separately (one shorter than k -> id -1 padding), merged on the device
     import torch
