@@ -20,9 +20,13 @@ def test_library_exports_every_header_symbol():
     assert sorted(_lib._SIGS) == names
 
 
-def test_library_is_gfx950_code_object():
-    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", _lib.LIB_PATH],
-                         capture_output=True, text=True)
+def test_library_is_gfx950_code_object(tmp_path):
+    # llvm-objdump --offloading extracts the bundles next to its input: work on a copy
+    import shutil
+    lib = tmp_path / "libvs.so"
+    shutil.copy(_lib.LIB_PATH, lib)
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", str(lib)],
+                         capture_output=True, text=True, cwd=tmp_path)
     text = out.stdout + out.stderr
     assert "gfx950" in text
 
