@@ -129,3 +129,56 @@ def test_device_calls_are_ordered_with_torch_default_stream():
     np.testing.assert_array_equal(np.stack([iv.reconstruct(50_000 + i) for i in (0, 777, 49_999)]),
                                   want[[0, 777, 49_999]])
     iv.close()
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_product_shapes_d4096_candidate_k(monkeypatch, tmp_path, dtype):
+    # the product's own ranges: EMBEDDING_DIMENSION 4096 (config.py:142), one query per call with
+    # candidate_k up to ~1.5k (core/searcher.py:807-817), image search k = 5 top_k (:1774-1777),
+    # and batched rounds (search_batch) with large k through the GEMV screen in blocks of 8
+    from photo_search_engine_amd import vector_store as vsmod
+    monkeypatch.setenv("VECTOR_DTYPE", dtype)
+    d, N = 4096, 12_000
+    x = O.synth_rows(O.SEED_CORPUS, 0, N, d, False, "f32")  # unnormalised: VectorStore normalises
+    store = vsmod.VectorStore(dimension=d, index_path=str(tmp_path / "i"), metadata_path=str(tmp_path / "m"))
+    store.add(x, [{"photo_path": f"/{i}"} for i in range(N)])
+    xs = store.index.reconstruct_n(0, N)
+    q = O.synth_rows(O.SEED_QUERIES, 0, 40, d, False, "f32")
+    qn = store._normalize_rows(q)
+    for k in (250, 1500):
+        res = store.search(q[0].tolist(), k)
+        S, I = O.knn_exact(xs, qn[:1], k, "ip")
+        assert [r["metadata"]["photo_path"] for r in res] == [f"/{i}" for i in I[0]]
+        assert [r["distance"] for r in res] == S[0].astype(np.float32).tolist()
+    for nq, k in ((5, 1500), (40, 300)):
+        D, I = store.search_batch(q[:nq], k)
+        S, Ie = O.knn_exact(xs, qn[:nq], k, "ip")
+        np.testing.assert_array_equal(I, Ie)
+        np.testing.assert_array_equal(D, S.astype(np.float32))
+
+
+def test_concurrent_searches_from_many_threads():
+    # Flask's threaded server can call VectorStore.search concurrently (SURVEY §5, §8 b): each
+    # call leases its own stream + workspace; the corpus is shared read-only
+    from concurrent.futures import ThreadPoolExecutor
+    from photo_search_engine_amd.index import FlatIndex
+    d, N = 256, 60_000
+    ix = FlatIndex(d, "ip", "bf16")
+    ix.add_synthetic(O.SEED_CORPUS, 0, N, True)
+    qs = [O.synth_rows(O.SEED_QUERIES, 100 * t, nq, d, True, "f32") for t, nq in enumerate([1, 3, 9, 40, 1, 8, 64, 2])]
+    ref = [ix.search(q, 20) for q in qs]
+
+    def run(t):
+        out = []
+        for _ in range(6):
+            out.append(ix.search(qs[t], 20))
+            ix.reconstruct(t * 1000)
+        return out
+
+    with ThreadPoolExecutor(8) as ex:
+        results = list(ex.map(run, range(8)))
+    for t, outs in enumerate(results):
+        for D, I in outs:
+            np.testing.assert_array_equal(I, ref[t][1])
+            np.testing.assert_array_equal(D, ref[t][0])
+    ix.close()
