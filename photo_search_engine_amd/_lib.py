@@ -12,7 +12,7 @@ import sys
 import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libvs.so")
+LIB_PATH = os.environ.get("VS_LIB_PATH") or os.path.join(HERE, "libvs.so")  # override: A/B builds
 HEADER_PATH = os.path.join(HERE, "..", "include", "vs.h")
 
 METRIC_IP = 0
