@@ -18,8 +18,9 @@ fixtures ``pytest-tmp/build-smoke/data/idx`` (IxFI, d=8, 77 bytes) and
             | storage index (IxFI / IxF2), recursively
   vec<T>  = uint64 count | T[count]
 
-Writing always produces a flat file (IxFI for inner product, IxF2 for L2): the drop-in serves
-every index exactly, so there is no graph to persist (DESIGN.md "HNSW").
+Flat files are written for flat indexes; an HNSW-configured store writes an ``IHNf`` file whose
+graph is the exact k-NN graph of the rows on one level (:func:`single_level_graph`), so the
+reference's faiss can still load it.  Searches here are exact flat searches either way.
 """
 from __future__ import annotations
 
@@ -96,6 +97,78 @@ def _read_at(path: str, buf: memoryview, off: int) -> FaissFile:
                          {"entry_point": entry_point, "max_level": max_level, "efConstruction": ef_c,
                           "efSearch": ef_s}, storage.payload_offset)
     raise FaissFormatError(f"unsupported faiss index type {fourcc!r}")
+
+
+def hnsw_default_probas(M: int):
+    """faiss ``HNSW::set_default_probas(M, 1 / log(M))``: level probabilities (computed with a
+    float level multiplier, stored as float, widened to double) and cumulative neighbour counts
+    (2M on level 0, M above).  Pinned bit for bit by the reference's HNSW fixture (M = 48)."""
+    lm = np.float32(1.0 / np.log(M))
+    probas, cum, nn, level = [], [0], 0, 0
+    while True:
+        p = np.float32(np.exp(np.float64(np.float32(-level) / lm)) * (1.0 - np.exp(np.float64(np.float32(-1) / lm))))
+        if p < 1e-9:
+            break
+        probas.append(float(p))
+        nn += 2 * M if level == 0 else M
+        cum.append(nn)
+        level += 1
+    return np.array(probas, dtype="<f8"), np.array(cum, dtype="<i4")
+
+
+def read_hnsw_graph(path: str) -> dict:
+    """The graph arrays of an ``IHNf`` file (faiss ``write_index`` of an IndexHNSWFlat)."""
+    with open(path, "rb") as f:
+        raw = f.read()
+    fourcc, d, ntotal, _trained, metric_type, off = _header(memoryview(raw), 0)
+    if fourcc != FOURCC_HNSW_FLAT:
+        raise FaissFormatError(f"not an HNSW file: {fourcc!r}")
+    g = {"d": d, "ntotal": ntotal, "metric_type": metric_type}
+    for name, dt in (("assign_probas", "<f8"), ("cum_nneighbor_per_level", "<i4"), ("levels", "<i4"),
+                     ("offsets", "<u8"), ("neighbors", "<i4")):
+        (n,) = struct.unpack_from("<Q", raw, off)
+        g[name] = np.frombuffer(raw, dtype=dt, count=n, offset=off + 8).copy()
+        off += 8 + n * np.dtype(dt).itemsize
+    (g["entry_point"], g["max_level"], g["efConstruction"], g["efSearch"],
+     g["upper_beam"]) = struct.unpack_from("<5i", raw, off)
+    g["storage_offset"] = off + 20
+    return g
+
+
+def write_hnsw(path: str, graph: dict, d: int, ntotal: int, metric_type: int, write_rows) -> None:
+    """Write an ``IHNf`` file: the HNSW header and graph arrays (faiss ``write_index`` layout) and
+    the flat storage, whose fp32 payload comes from ``write_rows(path, offset)``.  Temporary name +
+    rename, like :func:`write_flat_rows`."""
+    parts = [FOURCC_HNSW_FLAT + struct.pack("<iqqqBi", d, ntotal, _DUMMY, _DUMMY, 1, metric_type)]
+    for name, dt in (("assign_probas", "<f8"), ("cum_nneighbor_per_level", "<i4"), ("levels", "<i4"),
+                     ("offsets", "<u8"), ("neighbors", "<i4")):
+        a = np.ascontiguousarray(graph[name], dtype=dt)
+        parts.append(struct.pack("<Q", a.size) + a.tobytes())
+    parts.append(struct.pack("<5i", graph["entry_point"], graph["max_level"], graph["efConstruction"],
+                             graph["efSearch"], graph["upper_beam"]))
+    parts.append(flat_bytes_header(d, ntotal, metric_type))
+    head = b"".join(parts)
+    tmp = f"{path}.tmp-{os.getpid()}"
+    with open(tmp, "wb") as f:
+        f.write(head)
+    if ntotal:
+        write_rows(tmp, len(head))
+    os.replace(tmp, path)
+
+
+def single_level_graph(knn: np.ndarray, M: int, ef_construction: int, ef_search: int) -> dict:
+    """HNSW graph arrays for a one-level graph: every node on level 0 with the given neighbour
+    lists (n x <=2M ids, -1 padded).  A valid faiss IndexHNSWFlat graph (its search starts at the
+    entry point and walks level 0)."""
+    probas, cum = hnsw_default_probas(M)
+    n = knn.shape[0]
+    nb = np.full((n, 2 * M), -1, dtype="<i4")
+    w = min(knn.shape[1], 2 * M)
+    nb[:, :w] = knn[:, :w]
+    return {"assign_probas": probas, "cum_nneighbor_per_level": cum, "levels": np.ones(n, dtype="<i4"),
+            "offsets": np.arange(n + 1, dtype="<u8") * np.uint64(2 * M), "neighbors": nb.reshape(-1),
+            "entry_point": 0 if n else -1, "max_level": 0 if n else -1, "efConstruction": int(ef_construction),
+            "efSearch": int(ef_search), "upper_beam": 1}
 
 
 def read_index(path: str) -> FaissFile:

@@ -144,18 +144,62 @@ def test_save_rewrites_when_file_changed_or_cleared(VS, tmp_path, monkeypatch):
     assert np.array_equal(ff.vectors, store.index.reconstruct_n(0, 15))
 
 
-def test_hnsw_file_is_rewritten_flat_on_save(VS, tmp_path):
+def test_hnsw_store_saves_ihnf_with_exact_knn_graph(VS, tmp_path):
+    # index_type="hnsw" (the env templates' setting, .env.example:82-83): save() writes an IHNf file
+    # the reference's faiss can read back -- same header/array layout as the reference's own
+    # fixture, storage = the stored rows, graph = exact top-2M neighbours on one level
     import json
     import shutil
+    from oracle import oracle as O
     from photo_search_engine_amd import faiss_format as F
     idx = tmp_path / "photo_search.index"
     shutil.copy(os.path.join(GOLDEN, "ref_photo_search.index"), idx)
     shutil.copy(os.path.join(GOLDEN, "ref_photo_search.index.meta.json"), str(idx) + ".meta.json")
     (tmp_path / "metadata.json").write_text(json.dumps([{"photo_path": f"/p/{i}"} for i in range(77)]))
     store = VS(dimension=4096, index_path=str(idx), metadata_path=str(tmp_path / "metadata.json"),
-               index_type="hnsw", hnsw_m=48, hnsw_ef_construction=320, hnsw_ef_search=192)
+               index_type="hnsw", hnsw_m=8, hnsw_ef_construction=320, hnsw_ef_search=192)
     assert store.load()
     ref = F.read_index(str(idx)).vectors.copy()
     store.save()
     ff = F.read_index(str(idx))
-    assert ff.kind == "flat" and np.array_equal(ff.vectors, ref)
+    assert ff.kind == "hnsw" and np.array_equal(ff.vectors, ref)
+    g = F.read_hnsw_graph(str(idx))
+    probas, cum = F.hnsw_default_probas(8)
+    assert np.array_equal(g["assign_probas"], probas) and np.array_equal(g["cum_nneighbor_per_level"], cum)
+    assert (g["levels"] == 1).all() and (g["efConstruction"], g["efSearch"], g["entry_point"]) == (320, 192, 0)
+    nb = g["neighbors"].reshape(77, 16)
+    _, I = O.knn_exact(ref, ref, 17, "ip")
+    for i in range(77):
+        assert nb[i].tolist() == [int(j) for j in I[i] if j != i][:16]
+    # and it loads back (graph ignored, exact search)
+    s2 = VS(dimension=4096, index_path=str(idx), metadata_path=str(tmp_path / "metadata.json"),
+            index_type="hnsw", hnsw_m=8, hnsw_ef_construction=320, hnsw_ef_search=192)
+    assert s2.load() and s2.get_total_items() == 77
+
+
+def test_reference_hnsw_fixture_rewrites_byte_identical(tmp_path):
+    from photo_search_engine_amd import faiss_format as F
+    src = os.path.join(GOLDEN, "ref_photo_search.index")
+    g = F.read_hnsw_graph(src)
+    ff = F.read_index(src)
+    probas, cum = F.hnsw_default_probas(48)  # faiss set_default_probas, pinned by the fixture
+    assert np.array_equal(g["assign_probas"], probas) and np.array_equal(g["cum_nneighbor_per_level"], cum)
+    out = str(tmp_path / "rt.index")
+
+    def rows(path, off):
+        with open(path, "r+b") as f:
+            f.seek(off)
+            f.write(np.ascontiguousarray(ff.vectors, dtype="<f4").tobytes())
+
+    F.write_hnsw(out, g, ff.d, ff.ntotal, ff.metric_type, rows)
+    assert open(out, "rb").read() == open(src, "rb").read()
+
+
+def test_hnsw_store_above_graph_cap_saves_flat(VS, tmp_path, monkeypatch):
+    from photo_search_engine_amd import faiss_format as F
+    monkeypatch.setenv("VECTOR_HNSW_GRAPH_MAX_ROWS", "10")
+    rng = np.random.default_rng(3)
+    store = VS(dimension=8, index_path=str(tmp_path / "i"), metadata_path=str(tmp_path / "m"), index_type="hnsw")
+    store.add(rng.standard_normal((20, 8)).astype(np.float32), [{} for _ in range(20)])
+    store.save()
+    assert F.read_index(str(tmp_path / "i")).kind == "flat"
