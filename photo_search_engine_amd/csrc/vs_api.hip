@@ -385,7 +385,7 @@ void vs::search_exact_device(vs_index* ix, const float* q_dev, int64_t nq, int k
     if (nq <= 0) return;
     std::shared_lock<std::shared_mutex> lk(ix->rw);
     DeviceGuard dg(ix->device);
-    if (k <= 0 || k > ix->ntotal) throw VsError(VS_ERR_ARG, "k must be in [1, ntotal]");
+    if (k <= 0) throw VsError(VS_ERR_ARG, "k must be > 0");  // k > ntotal: -1 / worst-score padding
     CtxLease L(ix);
     Ctx* c = L.c;
     c->outD.ensure((size_t)nq * k * sizeof(float));

@@ -261,6 +261,23 @@ def test_device_exact_search_re_searches_uncertified_queries(FlatIndex):
     assert ix.uncertified_count() > 0
 
 
+def test_device_exact_search_k_beyond_shard_rows(FlatIndex):
+    # a row shard smaller than k (many GPUs, small corpus): padded like faiss, no error
+    import torch
+    ix = FlatIndex(32, "ip", "bf16")
+    ix.add_synthetic(O.SEED_CORPUS, 0, 5, True)
+    q = O.synth_rows(O.SEED_QUERIES, 0, 12, 32, True, "bf16")
+    qd = torch.from_numpy(q).cuda()
+    S = torch.empty((12, 10), dtype=torch.float64, device="cuda")
+    I = torch.empty((12, 10), dtype=torch.int64, device="cuda")
+    ix.search_device_exact(qd.data_ptr(), 12, 10, None, I.data_ptr(), S.data_ptr(), 7, 0)
+    Se, Ie = O.knn_exact(ix.reconstruct_n(0, 5), q, 10, "ip")
+    Ih = I.cpu().numpy()
+    np.testing.assert_array_equal(Ih[:, :5], Ie[:, :5] + 7)
+    assert (Ih[:, 5:] == -1).all()
+    np.testing.assert_array_equal(S.cpu().numpy()[:, :5], Se[:, :5])
+
+
 def test_device_shard_merge_matches_oracle(FlatIndex):
     # 4 row shards searched separately (one shorter than k -> id -1 padding), merged on the device
     import torch
