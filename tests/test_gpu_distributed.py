@@ -43,9 +43,10 @@ def _worker(rank, world, port, N, d, dtype, nq, k, metric, outdir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("metric,dtype,nq,k", [("ip", "bf16", 40, 25), ("l2", "f32", 3, 10)])
-def test_two_ranks_one_gpu_match_oracle(tmp_path, metric, dtype, nq, k):
-    N, d = 20011, 64
+@pytest.mark.parametrize("metric,dtype,nq,k,N", [("ip", "bf16", 40, 25, 20011), ("l2", "f32", 3, 10, 20011),
+                                                 ("ip", "bf16", 12, 10, 15)])  # last: shards smaller than k
+def test_two_ranks_one_gpu_match_oracle(tmp_path, metric, dtype, nq, k, N):
+    d = 64
     mp.spawn(_worker, args=(2, _free_port(), N, d, dtype, nq, k, metric, str(tmp_path)), nprocs=2, join=True)
     outs = [np.load(tmp_path / f"r{r}.npz") for r in range(2)]
     assert int(outs[0]["row0"]) == 0 and int(outs[1]["row0"]) == int(outs[0]["n"])
@@ -54,5 +55,6 @@ def test_two_ranks_one_gpu_match_oracle(tmp_path, metric, dtype, nq, k):
     Se, Ie = O.knn_exact(x, q, k, metric)
     for o in outs:
         np.testing.assert_array_equal(o["I"], Ie)
-        np.testing.assert_array_equal(o["S"], Se)
-        np.testing.assert_array_equal(o["D"], Se.astype(np.float32))
+        valid = Ie >= 0
+        np.testing.assert_array_equal(o["S"][valid], Se[valid])
+        np.testing.assert_array_equal(o["D"][valid], Se[valid].astype(np.float32))
