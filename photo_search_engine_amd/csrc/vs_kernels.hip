@@ -751,16 +751,17 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
     constexpr bool XP = MODE == 21 || MODE == 22 || MODE == 23;
     constexpr bool LOADS = (MODE != 1 && MODE < 3) || (MODE >= 6 && MODE != 12);  // (incl. seed, stamps)
     constexpr bool MATH = (MODE != 2 && MODE < 6) || MODE == 9 || MODE == 10 || MODE == 13 || MODE == 14 ||
-                          MODE == MF_SEED_MODE || MODE == MF_STAMP_MODE || MODE == 16 || MODE == 17 || MODE == 24 || XP;
+                          MODE == MF_SEED_MODE || MODE == MF_STAMP_MODE || MODE == 16 || MODE == 17 || MODE == 24 ||
+                          MODE == 25 || XP;
     constexpr bool PP = MODE == 11 || MODE == 12;  // ping-pong: waves 4-7 half a K-step behind waves 0-3
     constexpr bool SEED = MODE == MF_SEED_MODE;  // threshold-seed pass: group maxima only
     constexpr bool EPI = MODE < 3 || MODE == 13 || MODE == 14 || SEED || MODE == MF_STAMP_MODE || MODE == 16 ||
-                         MODE == 17 || MODE == 24 || XP;
+                         MODE == 17 || MODE == 24 || MODE == 25 || XP;
     constexpr bool INS = MODE != 13;   // threshold passes insert candidates
     constexpr bool CHECK = MODE != 13 && MODE != 14;  // deferred compaction check + pool flush
     constexpr bool BAR = MODE < 4 || MODE >= 6;  // (incl. seed, stamps)
     constexpr bool READS = MODE < 5 || MODE == 9 || MODE == 10 || MODE == 13 || MODE == 14 || MODE == MF_SEED_MODE ||
-                           MODE == MF_STAMP_MODE || MODE == 16 || MODE == 17 || XP;
+                           MODE == MF_STAMP_MODE || MODE == 16 || MODE == 17 || MODE == 25 || XP;
     constexpr bool QLOAD = MODE != 7;
     constexpr int64_t QSTEP = MODE == 21 ? 0 : 16384;  // 21: every stage re-reads query block 0 (L1-resident)
     constexpr bool NT = MODE == 8 || MODE == 0 || MODE >= 9;
@@ -916,8 +917,10 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
             mf_compute<DT, true>(smem + (s % MF_SLOTS) * MF_SLOT, acc, wm, wn, lane_off);
         } else {
             if (do_issue) {
+                if constexpr (MODE == 25) __builtin_amdgcn_s_setprio(3);  // loader DMA issue ahead of MFMAs
                 if constexpr (BAL) mf_stage_bal<NT>(nA, nB, nslot, tid);
                 else if constexpr (LOADS) mf_stage<QLOAD, NT>(nA, nB, nslot, tid);
+                if constexpr (MODE == 25) __builtin_amdgcn_s_setprio(0);
             }
             if constexpr (STAMP) {
                 __builtin_amdgcn_sched_barrier(0);
@@ -2222,6 +2225,7 @@ static void launch_mfma_mode(const ScreenArgs& a, const uint8_t* qt, int nqb, hi
         case 22: launch_mfma_one<DT, METRIC, 22>(a, qt, nqb, st); break;
         case 23: launch_mfma_one<DT, METRIC, 23>(a, qt, nqb, st); break;
         case 24: launch_mfma_one<DT, METRIC, 24>(a, qt, nqb, st); break;
+        case 25: launch_mfma_one<DT, METRIC, 25>(a, qt, nqb, st); break;
         default: launch_mfma_one<DT, METRIC, 0>(a, qt, nqb, st); break;
     }
 }
