@@ -2204,6 +2204,8 @@ static void launch_mfma_mode(const ScreenArgs& a, const uint8_t* qt, int nqb, hi
         return e ? atoi(e) : 0;
     }();
     switch (mode) {
+        case MF_STAMP_MODE: launch_mfma_one<DT, METRIC, MF_STAMP_MODE>(a, qt, nqb, st); break;
+#ifdef VS_MF_ABLATIONS  // diagnostic builds only (python -m photo_search_engine_amd.build with VS_ABLATIONS=1)
         case 1: launch_mfma_one<DT, METRIC, 1>(a, qt, nqb, st); break;
         case 2: launch_mfma_one<DT, METRIC, 2>(a, qt, nqb, st); break;
         case 3: launch_mfma_one<DT, METRIC, 3>(a, qt, nqb, st); break;
@@ -2218,7 +2220,6 @@ static void launch_mfma_mode(const ScreenArgs& a, const uint8_t* qt, int nqb, hi
         case 12: launch_mfma_one<DT, METRIC, 12>(a, qt, nqb, st); break;
         case 13: launch_mfma_one<DT, METRIC, 13>(a, qt, nqb, st); break;
         case 14: launch_mfma_one<DT, METRIC, 14>(a, qt, nqb, st); break;
-        case MF_STAMP_MODE: launch_mfma_one<DT, METRIC, MF_STAMP_MODE>(a, qt, nqb, st); break;
         case 16: launch_mfma_one<DT, METRIC, 16>(a, qt, nqb, st); break;
         case 17: launch_mfma_one<DT, METRIC, 17>(a, qt, nqb, st); break;
         case 21: launch_mfma_one<DT, METRIC, 21>(a, qt, nqb, st); break;
@@ -2226,6 +2227,7 @@ static void launch_mfma_mode(const ScreenArgs& a, const uint8_t* qt, int nqb, hi
         case 23: launch_mfma_one<DT, METRIC, 23>(a, qt, nqb, st); break;
         case 24: launch_mfma_one<DT, METRIC, 24>(a, qt, nqb, st); break;
         case 25: launch_mfma_one<DT, METRIC, 25>(a, qt, nqb, st); break;
+#endif
         default: launch_mfma_one<DT, METRIC, 0>(a, qt, nqb, st); break;
     }
 }
