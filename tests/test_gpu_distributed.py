@@ -58,3 +58,17 @@ def test_two_ranks_one_gpu_match_oracle(tmp_path, metric, dtype, nq, k, N):
         valid = Ie >= 0
         np.testing.assert_array_equal(o["S"][valid], Se[valid])
         np.testing.assert_array_equal(o["D"][valid], Se[valid].astype(np.float32))
+
+
+def test_four_ranks_one_gpu_match_oracle(tmp_path):
+    # G = 4: the all-gather of packed (score, id) pairs and the 4-way device merge
+    N, d, nq, k = 30001, 48, 20, 15
+    mp.spawn(_worker, args=(4, _free_port(), N, d, "bf16", nq, k, "ip", str(tmp_path)), nprocs=4, join=True)
+    outs = [np.load(tmp_path / f"r{r}.npz") for r in range(4)]
+    assert sum(int(o["n"]) for o in outs) == N
+    x = O.synth_rows(O.SEED_CORPUS, 0, N, d, True, "bf16")
+    q = O.synth_rows(O.SEED_QUERIES, 0, nq, d, True, "bf16")
+    Se, Ie = O.knn_exact(x, q, k, "ip")
+    for o in outs:
+        np.testing.assert_array_equal(o["I"], Ie)
+        np.testing.assert_array_equal(o["S"], Se)
