@@ -60,7 +60,7 @@ struct vs_ivf {
 
 namespace {
 
-constexpr int kPagesPerItem = 16;  // scan work item: up to 16 pages (4096 rows) of one list
+constexpr int kPagesPerItem = 16;  // scan work item: up to 16 pages (4096 rows) of one list (8: +2%, 32: +0.7% scan time)
 
 void check_ivf(const vs_ivf* ix) {
     if (!ix) throw VsError(VS_ERR_ARG, "null IVF index");
