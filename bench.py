@@ -170,7 +170,9 @@ def main():
             "dtype": dtype,
             "data": "synthetic (counter-hash N(0,1) rows, L2-normalised, seeds 20260417/20260418)",
             "config": {"workload": args.workload, "desc": desc, "N": N, "d": d, "batch": nq, "k": k,
-                       "n_local": n_local, "parallelism": f"row-shard x{G}" + (" + RCCL all-gather" if G > 1 else "")},
+                       "n_local": n_local, "parallelism": f"row-shard x{G}" + (
+                           (" + RCCL all-gather" if args.dist_backend == "nccl" else f" + {args.dist_backend} all-gather")
+                           if G > 1 else "")},
             "roofline": {
                 "kernel": f"k_screen_{kind}",
                 "bound": "hbm",
