@@ -63,3 +63,34 @@ def test_corrupt_files_raise(tmp_path):
     p.write_bytes(b"IxFI" + struct.pack("<iqqqBi", 4, 2, 1 << 20, 1 << 20, 1, 0) + struct.pack("<Q", 8) + b"\0" * 16)
     with pytest.raises(F.FaissFormatError):
         F.read_index(str(p))
+
+
+@pytest.mark.parametrize("n", [0, 1, 5])
+def test_single_level_hnsw_roundtrip(tmp_path, n):
+    rng = np.random.default_rng(n)
+    x = rng.standard_normal((n, 6)).astype(np.float32)
+    knn = np.array([[j for j in range(n) if j != i][:4] + [-1] * max(0, 4 - (n - 1)) for i in range(n)],
+                   dtype=np.int32).reshape(n, -1)[:, :4] if n else np.zeros((0, 4), np.int32)
+    g = F.single_level_graph(knn, 2, 40, 16)
+    p = str(tmp_path / "h.index")
+
+    def rows(path, off):
+        with open(path, "r+b") as f:
+            f.seek(off)
+            f.write(x.tobytes())
+
+    F.write_hnsw(p, g, 6, n, 1, rows)
+    ff = F.read_index(p)
+    assert (ff.kind, ff.d, ff.ntotal, ff.metric_type) == ("hnsw", 6, n, 1)
+    assert np.array_equal(ff.vectors, x)
+    h = F.read_hnsw_graph(p)
+    assert h["offsets"].tolist() == [4 * i for i in range(n + 1)]
+    assert (h["entry_point"], h["max_level"]) == ((0, 0) if n else (-1, -1))
+    assert np.array_equal(h["neighbors"].reshape(n, 4), knn)
+
+
+def test_hnsw_default_probas_shape():
+    for M in (4, 16, 32, 48):
+        probas, cum = F.hnsw_default_probas(M)
+        assert cum[0] == 0 and cum[1] == 2 * M and np.all(np.diff(cum[1:]) == M)
+        assert len(probas) == len(cum) - 1 and probas[-1] >= 1e-9 and abs(probas.sum() - 1.0) < 1e-6

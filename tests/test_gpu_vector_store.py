@@ -182,3 +182,19 @@ def test_concurrent_searches_from_many_threads():
             np.testing.assert_array_equal(I, ref[t][1])
             np.testing.assert_array_equal(D, ref[t][0])
     ix.close()
+
+
+def test_write_rows_to_file_errors(tmp_path):
+    from photo_search_engine_amd import _lib
+    from photo_search_engine_amd.index import FlatIndex
+    ix = FlatIndex(8, "ip", "f32")
+    ix.add(np.eye(8, dtype=np.float32))
+    with pytest.raises(_lib.VsError, match="out of bounds"):
+        ix.write_rows(str(tmp_path / "a.bin"), 0, 4, 8)
+    with pytest.raises(_lib.VsError, match="open"):
+        ix.write_rows(str(tmp_path / "no_such_dir" / "a.bin"), 0, 0, 1)
+    ix.write_rows(str(tmp_path / "b.bin"), 16, 2, 3)  # at an offset, file created
+    raw = (tmp_path / "b.bin").read_bytes()
+    assert len(raw) == 16 + 3 * 32
+    np.testing.assert_array_equal(np.frombuffer(raw[16:], dtype="<f4").reshape(3, 8), np.eye(8, dtype=np.float32)[2:5])
+    ix.close()
