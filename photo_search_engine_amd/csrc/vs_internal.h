@@ -27,7 +27,8 @@ constexpr int METRIC_IP = 0, METRIC_L2 = 1;
 
 constexpr int MFMA_QB = 256;   // queries per MFMA screen launch
 constexpr int MFMA_CAP = 768;  // candidate slots per (workgroup, query) in the MFMA screen
-constexpr int MFMA_KP_MAX = 256;
+constexpr int MFMA_KP_MAX = 512;  // = MFMA_CAP - TR: a compacted buffer (Kp keys) plus one tile fits
+static_assert(MFMA_KP_MAX + TR <= MFMA_CAP, "MFMA screen: compaction invariant cnt <= cap - TR");
 constexpr int GEMV_NQ_MAX = 8; // queries per GEMV screen launch
 constexpr int KP_MAX = 2048;   // largest screening depth (merge: >= 2 lists per block)
 constexpr int SELECT_E = 16;   // keys per thread in block selection (256 threads -> 4096 keys)

@@ -67,7 +67,8 @@ def test_gemv_path_exact(FlatIndex, metric, dtype, nq, k):
 
 @pytest.mark.parametrize("metric", ["ip", "l2"])
 @pytest.mark.parametrize("dtype", ["bf16", "f16"])
-@pytest.mark.parametrize("nq,k,N,d", [(40, 10, 9000, 128), (256, 100, 20000, 192), (300, 7, 3001, 72)])
+@pytest.mark.parametrize("nq,k,N,d", [(40, 10, 9000, 128), (256, 100, 20000, 192), (300, 7, 3001, 72),
+                                     (64, 400, 150000, 96)])  # Kp 512: the largest MFMA screening depth
 def test_mfma_path_exact(FlatIndex, metric, dtype, nq, k, N, d):
     ix = FlatIndex(d, metric, dtype)
     ix.add_synthetic(O.SEED_CORPUS, 0, N, True)
