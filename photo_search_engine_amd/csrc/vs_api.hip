@@ -32,11 +32,12 @@ struct Ctx {
     DevBuf qdev, qtile, qinfo, qpad, cand, part, merge_a, merge_b, outD, outI, outS, cert, thr0, seedmax, gcnt;
     DevBuf rows[2];  // read_rows_host: unpacked fp32 chunks
     DevBuf tilectr;  // GEMV screen: tile work-queue counter
+    DevBuf seedacc;  // MFMA seed pass: raw accumulators of each workgroup's seed tile
     PinnedPair pin;  // read_rows_host: pinned landing chunks
     std::vector<int> cert_host;
     ~Ctx() {
         for (DevBuf* b : {&qdev, &qtile, &qinfo, &qpad, &cand, &part, &merge_a, &merge_b, &outD, &outI, &outS, &cert, &thr0,
-                          &seedmax, &gcnt, &rows[0], &rows[1], &tilectr})
+                          &seedmax, &gcnt, &rows[0], &rows[1], &tilectr, &seedacc})
             b->release();
         pin.release();
         if (stream) hipStreamDestroy(stream);
@@ -140,6 +141,11 @@ constexpr int kOptimisticSeedRank = 1;  // seed_rank argument: > 0 selects the o
 constexpr double kOptimisticPassFactor = 8.0;
 constexpr int kOptimisticMinRank = 4;
 
+bool seed_reuse() {
+    static const bool on = !(getenv("VS_SEED_REUSE") && atoi(getenv("VS_SEED_REUSE")) == 0);
+    return on;
+}
+
 bool gemv_dyn() {
     static const bool on = !(getenv("VS_GEMV_DYN") && atoi(getenv("VS_GEMV_DYN")) == 0);
     return on;
@@ -223,6 +229,12 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
         ScreenArgs sa = a;
         sa.G = std::min(sa.G, 512);  // k_seed_select holds up to 8192 maxima per query
         sa.tile_stride = (int)(tiles / sa.G);
+        // seed tile = the first tile of each main-pass workgroup; its raw accumulators are kept so
+        // the main pass starts one tile later (VS_SEED_REUSE=0: sample strided tiles, rescreen all)
+        if (seed_reuse() && sa.G == a.G) {
+            c->seedacc.ensure((size_t)a.G * 128 * MF_WG_THREADS * sizeof(float));
+            sa.seed_acc = c->seedacc.as<float>();
+        }
         const int M = sa.G * 16;
         c->seedmax.ensure(sizeof(float) * MFMA_QB * M);
         sa.seedmax = c->seedmax.as<float>();
@@ -240,6 +252,7 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
         }
         HIP_CHECK(launch_seed_select(sa.seedmax, M, nqb, rank, c->thr0.as<u64>(), st));
         a.thr0 = c->thr0.as<u64>();
+        a.seed_acc = sa.seed_acc;
         optimistic = rank < Kp;
     }
 

@@ -26,6 +26,7 @@ constexpr int DT_F32 = 0, DT_BF16 = 1, DT_F16 = 2;
 constexpr int METRIC_IP = 0, METRIC_L2 = 1;
 
 constexpr int MFMA_QB = 256;   // queries per MFMA screen launch
+constexpr int MF_WG_THREADS = 512;  // MFMA screen workgroup (8 waves)
 constexpr int MFMA_CAP = 768;  // candidate slots per (workgroup, query) in the MFMA screen
 constexpr int MFMA_KP_MAX = 512;  // = MFMA_CAP - TR: a compacted buffer (Kp keys) plus one tile fits
 static_assert(MFMA_KP_MAX + TR <= MFMA_CAP, "MFMA screen: compaction invariant cnt <= cap - TR");
@@ -174,6 +175,8 @@ struct ScreenArgs {
     int lcap;                // = G * Kp
     unsigned long long* stamps;  // diagnostic build only (VS_MF_STAMPS): [G][8 waves][5] phase cycles
     int* next_tile;          // GEMV: tile work-queue counter (zeroed before the launch); null = static ranges
+    float* seed_acc;         // MFMA: [G][512 lanes][128] raw accumulators of each workgroup's seed tile (the
+                             // first tile of its range): written by the seed pass, reused by the main pass
 };
 int gemv_blocks_per_cu(int dt, int nqpad);  // resident k_screen_gemv blocks per CU (occupancy API)
 

@@ -790,9 +790,14 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
     int t0 = (int)((int64_t)a.tiles * blk / a.G);
     int t1 = (int)((int64_t)a.tiles * (blk + 1) / a.G);
     if (a.tile_stride > 0) {
-        t0 = blk * a.tile_stride;
+        // seed pass: one tile per workgroup; with seed_acc, the first tile of the main pass's range
+        // of this workgroup (same G), whose raw accumulators the main pass then reuses
+        t0 = a.seed_acc ? (int)((int64_t)a.tiles * blk / a.G) : blk * a.tile_stride;
         t1 = t0 + 1 <= a.tiles ? t0 + 1 : a.tiles;
     }
+    const bool reuse = !SEED && a.seed_acc != nullptr && t1 > t0;
+    const int tseed = t0;
+    if (reuse) ++t0;
     if (tid < 256) {
         const bool real = tid < nqb;
         const u64 k0 = real ? (a.thr0 ? a.thr0[tid] : 0ull) : ~0ull;
@@ -849,115 +854,21 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
     int ti = t0, ks = 0;
     float sink = 0.0f;
     bool check_pending = false;
-    uint4 pf_a[4], pf_b[8];
-    // stamps: barrier, DMA issue, reads+MFMA, tail of tile-end steps, total, tail of other steps
-    uint64_t ph[6] = {0, 0, 0, 0, 0, 0}, tl = 0;
-    bool tile_end = false;
-    if constexpr (STAMP) tl = __builtin_amdgcn_s_memtime();
-    for (int s = 0; s < S; ++s) {
-        const int left = S - 1 - s;
-        uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
-        if constexpr (STAMP) {
-            __builtin_amdgcn_sched_barrier(0);
-            t0 = __builtin_amdgcn_s_memtime();
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        if constexpr (PAIR) {
-            if ((s & 1) == 0) mf_barrier_drain();  // this pair's two stages landed, previous pair read
-        } else if constexpr (SP) {
-            // stage s+1 landed (its fragments are read during this step); stage s's fragments are in
-            // registers (lgkmcnt(0)), so slot s % 4 is free for stage s+4
-            const int last = S - 1 < s + 3 ? S - 1 : s + 3;  // youngest stage issued so far
-            const int ahead = last - (s + 1);
-            mf_wait_barrier<true>(ahead > 0 ? ahead : 0, wid < 4);
-        } else {
-            mf_wait_barrier<BAR, !QLOAD || BAL>(left < MF_DEPTH - 1 ? left : MF_DEPTH - 1, wid < 4 || BAL);
-        }
-        if constexpr (STAMP) {
-            __builtin_amdgcn_sched_barrier(0);
-            t1 = __builtin_amdgcn_s_memtime();
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        constexpr int AHEAD = SP ? MF_SLOTS : MF_DEPTH;  // stage issued at step s: s + AHEAD
-        const bool do_issue = s + AHEAD < S;
-        const uint8_t* nA = a.corpus + (int64_t)iti * tbytes + (int64_t)iks * 16384;
-        const uint8_t* nB = qt + (int64_t)iks * QSTEP;
-        const uint32_t nslot = ring + (uint32_t)(((s + AHEAD) % MF_SLOTS) * MF_SLOT);
-        if (do_issue) {
-            if (++iks == nks) { iks = 0; ++iti; }
-        }
-        if constexpr (PP) {
-            if (wid < 4) {
-                if constexpr (LOADS) if (do_issue) mf_stage<true, NT>(nA, nB, nslot, tid);
-                mf_read(smem + (s % MF_SLOTS) * MF_SLOT, pf_a, pf_b, wm, wn, lane_off);
-                mf_mfma<DT, 0, 4>(pf_a, pf_b, acc);
-            } else {
-                if (s > 0) mf_mfma<DT, 2, 4>(pf_a, pf_b, acc);
-                __builtin_amdgcn_sched_barrier(0);
-                mf_read(smem + (s % MF_SLOTS) * MF_SLOT, pf_a, pf_b, wm, wn, lane_off);
-                mf_mfma<DT, 0, 2>(pf_a, pf_b, acc);
-            }
-        } else if constexpr (IL) {
-            mf_compute_il<DT, NT>(smem + (s % MF_SLOTS) * MF_SLOT, acc, wm, wn, lane_off, do_issue && wid < 4, nA, nB,
-                                  nslot, wid, lane);
-        } else if constexpr (SP) {
-            if (do_issue && wid < 4) mf_stage<true, NT>(nA, nB, nslot, tid);
-            mf_compute_sp<DT>(smem + ((s + 1) % MF_SLOTS) * MF_SLOT, ca, cb, acc, wm, wn, lane_off);
-        } else if constexpr (PAIR) {
-            if ((s & 1) == 0) {  // the next pair's two stages, into the slots the previous pair used
-#pragma unroll
-                for (int h = 0; h < 2; ++h)
-                    if (s + 2 + h < S) {
-                        mf_stage<true, NT>(a.corpus + (int64_t)pti * tbytes + (int64_t)pks * 16384,
-                                           qt + (int64_t)pks * 16384,
-                                           ring + (uint32_t)(((s + 2 + h) % MF_SLOTS) * MF_SLOT), tid);
-                        if (++pks == nks) { pks = 0; ++pti; }
-                    }
-            }
-            mf_compute<DT, true>(smem + (s % MF_SLOTS) * MF_SLOT, acc, wm, wn, lane_off);
-        } else {
-            if (do_issue) {
-                if constexpr (MODE == 25) __builtin_amdgcn_s_setprio(3);  // loader DMA issue ahead of MFMAs
-                if constexpr (BAL) mf_stage_bal<NT>(nA, nB, nslot, tid);
-                else if constexpr (LOADS) mf_stage<QLOAD, NT>(nA, nB, nslot, tid);
-                if constexpr (MODE == 25) __builtin_amdgcn_s_setprio(0);
-            }
-            if constexpr (STAMP) {
-                __builtin_amdgcn_sched_barrier(0);
-                t2 = __builtin_amdgcn_s_memtime();
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            if constexpr (MODE == 22 || MODE == 23) {
-                const uint8_t* buf = smem + (s % MF_SLOTS) * MF_SLOT;
-                if (MODE == 23 || (s & 1) == 0)
-#pragma unroll
-                    for (int ni = 0; ni < 8; ++ni)
-                        pf_b[ni] = *(const uint4*)(buf + 16384 + wn * 8192 + lane_off + ni * 1024);
-                if (MODE == 22 || (s & 1) == 0)
-#pragma unroll
-                    for (int mi = 0; mi < 4; ++mi) pf_a[mi] = *(const uint4*)(buf + wm * 4096 + lane_off + mi * 1024);
-                mf_mfma<DT, 0, 4>(pf_a, pf_b, acc);
-            } else if constexpr (MATH) mf_compute<DT, READS>(smem + (s % MF_SLOTS) * MF_SLOT, acc, wm, wn, lane_off);
-            if constexpr (STAMP) {
-                __builtin_amdgcn_sched_barrier(0);
-                t3 = __builtin_amdgcn_s_memtime();
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        }
-        if constexpr (STAMP) tile_end = ks == nks - 1;
-        if (ks == nks - 1) {
-            if constexpr (!EPI) {
-#pragma unroll
-                for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-                    for (int ni = 0; ni < 8; ++ni) {
-                        sink += acc[mi][ni][0] + acc[mi][ni][3];
-                        acc[mi][ni] = floatx4{0.f, 0.f, 0.f, 0.f};
-                    }
-            } else {
+    // tile epilogue over the accumulators of tile `ti` (shared by the K loop and the seed tile)
+    auto tile_epilogue = [&](const int ti) {
             // ---- fused top-k epilogue: threshold filter, rare inserts ----
             // Lane-derived indices come from an asm-opaque copy of the lane id, so the compiler
             // cannot hoist them out of the K loop (they would pin VGPRs the MFMA loop needs).
+            if constexpr (SEED) {
+                if (a.seed_acc) {  // raw accumulators of the tile, for the main pass to reuse
+                    // per lane 512 contiguous bytes: one base address, immediate offsets
+                    floatx4* dst = (floatx4*)(a.seed_acc + ((size_t)blk * MF_THREADS + tid) * 128);
+#pragma unroll
+                    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                        for (int ni = 0; ni < 8; ++ni) dst[mi * 8 + ni] = acc[mi][ni];
+                }
+            }
             int olane;
             asm volatile("v_mov_b32 %0, %1" : "=v"(olane) : "v"(lane));
             const int64_t rowbase = (int64_t)ti * TR;
@@ -1064,6 +975,124 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
 #pragma unroll
                 for (int ni = 0; ni < 8; ++ni) acc[mi][ni] = floatx4{0.f, 0.f, 0.f, 0.f};
             check_pending = CHECK && !SEED;
+    };
+    if (reuse) {
+        // the seed pass screened this workgroup's first tile (tseed) and left its raw accumulators:
+        // run its epilogue now, while the DMAs of the next tile are already in flight
+        const floatx4* src = (const floatx4*)(a.seed_acc + ((size_t)blk * MF_THREADS + tid) * 128);
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 8; ++ni) acc[mi][ni] = src[mi * 8 + ni];
+        tile_epilogue(tseed);
+    }
+    uint4 pf_a[4], pf_b[8];
+    // stamps: barrier, DMA issue, reads+MFMA, tail of tile-end steps, total, tail of other steps
+    uint64_t ph[6] = {0, 0, 0, 0, 0, 0}, tl = 0;
+    bool tile_end = false;
+    if constexpr (STAMP) tl = __builtin_amdgcn_s_memtime();
+    for (int s = 0; s < S; ++s) {
+        const int left = S - 1 - s;
+        uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+        if constexpr (STAMP) {
+            __builtin_amdgcn_sched_barrier(0);
+            t0 = __builtin_amdgcn_s_memtime();
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (PAIR) {
+            if ((s & 1) == 0) mf_barrier_drain();  // this pair's two stages landed, previous pair read
+        } else if constexpr (SP) {
+            // stage s+1 landed (its fragments are read during this step); stage s's fragments are in
+            // registers (lgkmcnt(0)), so slot s % 4 is free for stage s+4
+            const int last = S - 1 < s + 3 ? S - 1 : s + 3;  // youngest stage issued so far
+            const int ahead = last - (s + 1);
+            mf_wait_barrier<true>(ahead > 0 ? ahead : 0, wid < 4);
+        } else {
+            mf_wait_barrier<BAR, !QLOAD || BAL>(left < MF_DEPTH - 1 ? left : MF_DEPTH - 1, wid < 4 || BAL);
+        }
+        if constexpr (STAMP) {
+            __builtin_amdgcn_sched_barrier(0);
+            t1 = __builtin_amdgcn_s_memtime();
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        constexpr int AHEAD = SP ? MF_SLOTS : MF_DEPTH;  // stage issued at step s: s + AHEAD
+        const bool do_issue = s + AHEAD < S;
+        const uint8_t* nA = a.corpus + (int64_t)iti * tbytes + (int64_t)iks * 16384;
+        const uint8_t* nB = qt + (int64_t)iks * QSTEP;
+        const uint32_t nslot = ring + (uint32_t)(((s + AHEAD) % MF_SLOTS) * MF_SLOT);
+        if (do_issue) {
+            if (++iks == nks) { iks = 0; ++iti; }
+        }
+        if constexpr (PP) {
+            if (wid < 4) {
+                if constexpr (LOADS) if (do_issue) mf_stage<true, NT>(nA, nB, nslot, tid);
+                mf_read(smem + (s % MF_SLOTS) * MF_SLOT, pf_a, pf_b, wm, wn, lane_off);
+                mf_mfma<DT, 0, 4>(pf_a, pf_b, acc);
+            } else {
+                if (s > 0) mf_mfma<DT, 2, 4>(pf_a, pf_b, acc);
+                __builtin_amdgcn_sched_barrier(0);
+                mf_read(smem + (s % MF_SLOTS) * MF_SLOT, pf_a, pf_b, wm, wn, lane_off);
+                mf_mfma<DT, 0, 2>(pf_a, pf_b, acc);
+            }
+        } else if constexpr (IL) {
+            mf_compute_il<DT, NT>(smem + (s % MF_SLOTS) * MF_SLOT, acc, wm, wn, lane_off, do_issue && wid < 4, nA, nB,
+                                  nslot, wid, lane);
+        } else if constexpr (SP) {
+            if (do_issue && wid < 4) mf_stage<true, NT>(nA, nB, nslot, tid);
+            mf_compute_sp<DT>(smem + ((s + 1) % MF_SLOTS) * MF_SLOT, ca, cb, acc, wm, wn, lane_off);
+        } else if constexpr (PAIR) {
+            if ((s & 1) == 0) {  // the next pair's two stages, into the slots the previous pair used
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                    if (s + 2 + h < S) {
+                        mf_stage<true, NT>(a.corpus + (int64_t)pti * tbytes + (int64_t)pks * 16384,
+                                           qt + (int64_t)pks * 16384,
+                                           ring + (uint32_t)(((s + 2 + h) % MF_SLOTS) * MF_SLOT), tid);
+                        if (++pks == nks) { pks = 0; ++pti; }
+                    }
+            }
+            mf_compute<DT, true>(smem + (s % MF_SLOTS) * MF_SLOT, acc, wm, wn, lane_off);
+        } else {
+            if (do_issue) {
+                if constexpr (MODE == 25) __builtin_amdgcn_s_setprio(3);  // loader DMA issue ahead of MFMAs
+                if constexpr (BAL) mf_stage_bal<NT>(nA, nB, nslot, tid);
+                else if constexpr (LOADS) mf_stage<QLOAD, NT>(nA, nB, nslot, tid);
+                if constexpr (MODE == 25) __builtin_amdgcn_s_setprio(0);
+            }
+            if constexpr (STAMP) {
+                __builtin_amdgcn_sched_barrier(0);
+                t2 = __builtin_amdgcn_s_memtime();
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            if constexpr (MODE == 22 || MODE == 23) {
+                const uint8_t* buf = smem + (s % MF_SLOTS) * MF_SLOT;
+                if (MODE == 23 || (s & 1) == 0)
+#pragma unroll
+                    for (int ni = 0; ni < 8; ++ni)
+                        pf_b[ni] = *(const uint4*)(buf + 16384 + wn * 8192 + lane_off + ni * 1024);
+                if (MODE == 22 || (s & 1) == 0)
+#pragma unroll
+                    for (int mi = 0; mi < 4; ++mi) pf_a[mi] = *(const uint4*)(buf + wm * 4096 + lane_off + mi * 1024);
+                mf_mfma<DT, 0, 4>(pf_a, pf_b, acc);
+            } else if constexpr (MATH) mf_compute<DT, READS>(smem + (s % MF_SLOTS) * MF_SLOT, acc, wm, wn, lane_off);
+            if constexpr (STAMP) {
+                __builtin_amdgcn_sched_barrier(0);
+                t3 = __builtin_amdgcn_s_memtime();
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        if constexpr (STAMP) tile_end = ks == nks - 1;
+        if (ks == nks - 1) {
+            if constexpr (!EPI) {
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                    for (int ni = 0; ni < 8; ++ni) {
+                        sink += acc[mi][ni][0] + acc[mi][ni][3];
+                        acc[mi][ni] = floatx4{0.f, 0.f, 0.f, 0.f};
+                    }
+            } else {
+                tile_epilogue(ti);
             }
         }
         // Deferred compaction check, after the NEXT K-step's barrier: by then every wave's

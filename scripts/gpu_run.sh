@@ -16,6 +16,7 @@ for s in "$@"; do
     gemvab) for v in ${DYN:-0 1 0 1}; do VS_GEMV_DYN=$v timeout -k 10 300 python bench.py --workload cfg2 --steps 50 --warmup 5 --no-cpu-baseline > gpurun_out/gemvab_$v.log 2>&1 || exit 1; grep '^{' gpurun_out/gemvab_$v.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('gemv dyn $v', d['ms_per_step'], d['roofline']['kernel_ms'], d['roofline']['frac'])" >> gpurun_out/gemvab.txt; done ;;
     libab) for v in ${LIBS:-w0 w6 w8 w0 w6 w8}; do VS_LIB_PATH=$GRAFT_REPO_ROOT/abtmp/libvs_$v.so timeout -k 10 300 python bench.py --workload ${WL:-cfg2} --steps 50 --warmup 5 --no-cpu-baseline > gpurun_out/libab_$v.log 2>&1 || exit 1; grep '^{' gpurun_out/libab_$v.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('lib $v', d['ms_per_step'], d['roofline']['kernel_ms'], d['roofline']['frac'])" >> gpurun_out/libab.txt; done ;;
     rfab) for v in ${LIBS:-plain rnt plain rnt}; do VS_LIB_PATH=$GRAFT_REPO_ROOT/abtmp/libvs_$v.so VS_RF_STAMPS=1 timeout -k 10 300 python bench.py --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/rfab_$v.log 2>&1 || exit 1; echo "lib $v $(grep 'rf stamps' gpurun_out/rfab_$v.log | tail -1)" >> gpurun_out/rfab.txt; done ;;
+    seedab) for v in ${SR:-0 1 0 1}; do for rows in 1250000 0; do VS_SEED_REUSE=$v timeout -k 10 300 python bench.py --rows $rows --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/seedab_${v}_$rows.log 2>&1 || exit 1; grep '^{' gpurun_out/seedab_${v}_$rows.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('reuse $v rows $rows', d['ms_per_step'], d['roofline']['kernel_ms'], d['uncertified_first_pass'])" >> gpurun_out/seedab.txt; done; done ;;
     bench_cfg5_g4) VS_IVF_GRID=4 timeout -k 10 900 python bench.py --workload cfg5 --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/bench_cfg5_g4.log 2>&1 ;;
     bench_cfg5_g16) VS_IVF_GRID=16 timeout -k 10 900 python bench.py --workload cfg5 --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/bench_cfg5_g16.log 2>&1 ;;
     bench_cfg2) timeout -k 10 600 python bench.py --workload cfg2 --steps 50 --no-cpu-baseline > gpurun_out/bench_cfg2.log 2>&1 ;;

@@ -212,7 +212,7 @@ def test_seeded_threshold_search_exact(FlatIndex, metric, k):
 
 
 def test_optimistic_seed_failure_falls_back_exactly(FlatIndex):
-    # Adversarial corpus: one near-copy of the query in every SAMPLED tile (tile j * stride) and
+    # Adversarial corpus: one near-copy of the query in every SAMPLED tile (each workgroup's first) and
     # nowhere else, so the optimistic seed threshold (16th best sample maximum) lets fewer than Kp
     # rows through; the certificate must reject it and vs_search must re-search exactly.
     # 32 tiles per CU: the optimistic rank is ceil(8 * Kp / 32) = 8 < the 16 planted rows/query
@@ -222,10 +222,9 @@ def test_optimistic_seed_failure_falls_back_exactly(FlatIndex):
     N = tiles * 256
     x = O.synth_rows(O.SEED_CORPUS, 0, N, d, True, "f32")
     q = O.synth_rows(O.SEED_QUERIES, 0, 16, d, True, "f32")
-    stride = tiles // cu
     rng = np.random.default_rng(11)
-    for j in range(cu):
-        r = j * stride * 256 + 5
+    for j in range(cu):  # the sampled tile of workgroup j: the first of its range
+        r = (tiles * j // cu) * 256 + 5
         x[r] = q[j % 16] + 0.01 * rng.standard_normal(d).astype(np.float32)
     ix = FlatIndex(d, "ip", "bf16")
     ix.add(x)
@@ -243,10 +242,9 @@ def test_device_exact_search_re_searches_uncertified_queries(FlatIndex):
     N = tiles * 256
     x = O.synth_rows(O.SEED_CORPUS, 0, N, d, True, "f32")
     q = O.synth_rows(O.SEED_QUERIES, 0, 16, d, True, "f32")
-    stride = tiles // cu
     rng = np.random.default_rng(11)
-    for j in range(cu):
-        x[j * stride * 256 + 5] = q[j % 16] + 0.01 * rng.standard_normal(d).astype(np.float32)
+    for j in range(cu):  # the sampled tile of workgroup j: the first of its range
+        x[(tiles * j // cu) * 256 + 5] = q[j % 16] + 0.01 * rng.standard_normal(d).astype(np.float32)
     ix = FlatIndex(d, "ip", "bf16")
     ix.add(x)
     qb = O.round_dtype(q, "bf16")
