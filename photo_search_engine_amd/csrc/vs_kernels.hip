@@ -524,11 +524,22 @@ __device__ __forceinline__ void glds16_nt(const void* gptr, uint32_t lds_base) {
                  : "memory", "m0");
 }
 
+// cache-policy variants of the corpus LDS-DMA (ablation modes 26 / 27)
+__device__ __forceinline__ void glds16_sc1nt(const void* gptr, uint32_t lds_base) {
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off sc1 nt" ::"v"(gptr), "s"(lds_base)
+                 : "memory", "m0");
+}
+__device__ __forceinline__ void glds16_sc01nt(const void* gptr, uint32_t lds_base) {
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off sc0 sc1 nt" ::"v"(gptr),
+                 "s"(lds_base)
+                 : "memory", "m0");
+}
+
 // issue one K-step stage: waves 0-3 (the loader waves) issue 8 LDS-DMA instructions per thread
 // (4 corpus + 4 query); waves 4-7 issue none.  Loader waves never store to global memory and the
 // writer waves never load, so each wave's in-order vmcnt holds one kind of traffic: counted waits
 // on the stage ring are never held up behind candidate stores.
-template <bool QLOAD = true, bool NT = false>
+template <bool QLOAD = true, bool NT = false, int POL = 0>
 __device__ __forceinline__ void mf_stage(const uint8_t* __restrict__ gA, const uint8_t* __restrict__ gB,
                                          uint32_t slot_base, int tid) {
     const int w = tid >> 6, lane = tid & 63;
@@ -539,7 +550,9 @@ __device__ __forceinline__ void mf_stage(const uint8_t* __restrict__ gA, const u
         const int g = it * 256 + w * 64 + lane;
         const int row = g >> 2, pos = g & 3;
         const int src = (row << 2) + (pos ^ mf_swz(row));
-        if constexpr (NT) glds16_nt(gA + (size_t)src * 16, base + it * 256 * 16);
+        if constexpr (POL == 2) glds16_sc1nt(gA + (size_t)src * 16, base + it * 256 * 16);
+        else if constexpr (POL == 3) glds16_sc01nt(gA + (size_t)src * 16, base + it * 256 * 16);
+        else if constexpr (NT) glds16_nt(gA + (size_t)src * 16, base + it * 256 * 16);
         else glds16(gA + (size_t)src * 16, base + it * 256 * 16);
     }
     if constexpr (QLOAD) {
@@ -748,20 +761,22 @@ template <int DT, int METRIC, int MODE>
 __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
     // 21 = 0 without the query stream (stale query tile) | 22 = 0 with B fragments re-read every other
     // K-step only | 23 = 0 with A fragments re-read every other K-step only  (energy ablations)
+    // 24 = 0 with software-pipelined fragment reads | 25 = 0 with s_setprio around the DMA issue
+    // 26 / 27 = 0 with the corpus DMA issued "sc1 nt" / "sc0 sc1 nt"  (cache-policy ablations)
     constexpr bool XP = MODE == 21 || MODE == 22 || MODE == 23;
     constexpr bool LOADS = (MODE != 1 && MODE < 3) || (MODE >= 6 && MODE != 12);  // (incl. seed, stamps)
     constexpr bool MATH = (MODE != 2 && MODE < 6) || MODE == 9 || MODE == 10 || MODE == 13 || MODE == 14 ||
                           MODE == MF_SEED_MODE || MODE == MF_STAMP_MODE || MODE == 16 || MODE == 17 || MODE == 24 ||
-                          MODE == 25 || XP;
+                          MODE == 25 || MODE == 26 || MODE == 27 || XP;
     constexpr bool PP = MODE == 11 || MODE == 12;  // ping-pong: waves 4-7 half a K-step behind waves 0-3
     constexpr bool SEED = MODE == MF_SEED_MODE;  // threshold-seed pass: group maxima only
     constexpr bool EPI = MODE < 3 || MODE == 13 || MODE == 14 || SEED || MODE == MF_STAMP_MODE || MODE == 16 ||
-                         MODE == 17 || MODE == 24 || MODE == 25 || XP;
+                         MODE == 17 || MODE == 24 || MODE == 25 || MODE == 26 || MODE == 27 || XP;
     constexpr bool INS = MODE != 13;   // threshold passes insert candidates
     constexpr bool CHECK = MODE != 13 && MODE != 14;  // deferred compaction check + pool flush
     constexpr bool BAR = MODE < 4 || MODE >= 6;  // (incl. seed, stamps)
     constexpr bool READS = MODE < 5 || MODE == 9 || MODE == 10 || MODE == 13 || MODE == 14 || MODE == MF_SEED_MODE ||
-                           MODE == MF_STAMP_MODE || MODE == 16 || MODE == 17 || MODE == 25 || XP;
+                           MODE == MF_STAMP_MODE || MODE == 16 || MODE == 17 || MODE == 25 || MODE == 26 || MODE == 27 || XP;
     constexpr bool QLOAD = MODE != 7;
     constexpr int64_t QSTEP = MODE == 21 ? 0 : 16384;  // 21: every stage re-reads query block 0 (L1-resident)
     constexpr bool NT = MODE == 8 || MODE == 0 || MODE >= 9;
@@ -770,6 +785,7 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
     constexpr bool BAL = MODE == 16;               // balanced DMA issue (4 per wave on all 8 waves)
     constexpr bool PAIR = MODE == 17;              // one barrier per 2 K-steps (needs an even K-step count)
     constexpr bool SP = MODE == 24;                // fragment reads of stage s+1 pipelined under stage s's MFMAs
+    constexpr int POL = MODE == 26 ? 2 : MODE == 27 ? 3 : 0;  // corpus DMA cache policy: sc1 nt / sc0 sc1 nt
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     u64* thr_key = (u64*)(smem + MF_SLOTS * MF_SLOT);
     float* thr_f = (float*)(smem + MF_SLOTS * MF_SLOT + 256 * 8);
@@ -833,7 +849,7 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
             mf_stage_bal<NT>(a.corpus + (int64_t)iti * tbytes + (int64_t)iks * 16384, qt + (int64_t)iks * 16384,
                              ring + (uint32_t)(j * MF_SLOT), tid);
         else if constexpr (LOADS)
-            mf_stage<QLOAD, NT>(a.corpus + (int64_t)iti * tbytes + (int64_t)iks * 16384, qt + (int64_t)iks * QSTEP,
+            mf_stage<QLOAD, NT, POL>(a.corpus + (int64_t)iti * tbytes + (int64_t)iks * 16384, qt + (int64_t)iks * QSTEP,
                                 ring + (uint32_t)(j * MF_SLOT), tid);
         if (++iks == nks) { iks = 0; ++iti; }
     }
@@ -1056,7 +1072,7 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
             if (do_issue) {
                 if constexpr (MODE == 25) __builtin_amdgcn_s_setprio(3);  // loader DMA issue ahead of MFMAs
                 if constexpr (BAL) mf_stage_bal<NT>(nA, nB, nslot, tid);
-                else if constexpr (LOADS) mf_stage<QLOAD, NT>(nA, nB, nslot, tid);
+                else if constexpr (LOADS) mf_stage<QLOAD, NT, POL>(nA, nB, nslot, tid);
                 if constexpr (MODE == 25) __builtin_amdgcn_s_setprio(0);
             }
             if constexpr (STAMP) {
@@ -2257,6 +2273,8 @@ static void launch_mfma_mode(const ScreenArgs& a, const uint8_t* qt, int nqb, hi
         case 23: launch_mfma_one<DT, METRIC, 23>(a, qt, nqb, st); break;
         case 24: launch_mfma_one<DT, METRIC, 24>(a, qt, nqb, st); break;
         case 25: launch_mfma_one<DT, METRIC, 25>(a, qt, nqb, st); break;
+        case 26: launch_mfma_one<DT, METRIC, 26>(a, qt, nqb, st); break;
+        case 27: launch_mfma_one<DT, METRIC, 27>(a, qt, nqb, st); break;
 #endif
         default: launch_mfma_one<DT, METRIC, 0>(a, qt, nqb, st); break;
     }
