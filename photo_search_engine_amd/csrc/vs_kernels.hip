@@ -1787,7 +1787,7 @@ __device__ __forceinline__ void exact_score_q2(const uint8_t* __restrict__ corpu
                 for (int e = 0; e < 8; ++e) {
                     const int i = 8 * g + e;
                     if (i < d) {
-                        const double qq = QLDS ? qs[i] : (double)qg[i];
+                        const double qq = QLDS ? qs[e * ng + g] : (double)qg[i];
                         const double xa = (double)x0[e];
                         if constexpr (METRIC == METRIC_IP) {
                             const double pa = xa * qq;
@@ -1841,7 +1841,10 @@ __global__ void __launch_bounds__(RF_THREADS) k_refine(RefineArgs a, int KP2) {
     const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     constexpr int NW = RF_THREADS / 64;
     // the best Kp keys of the candidate list, compacted into LDS (cq)
-    u64* cq = (u64*)(smem + (((size_t)KP2 * 12 + 7) & ~(size_t)7) + (QLDS ? (size_t)a.d * 8 : 0));
+    // the query sits in LDS transposed, qs[e * ng + g] = q[8 g + e]: lane g of the exact scoring
+    // reads element e of its 8-element group, so a wave's reads are contiguous (conflict-free)
+    const int ng = (a.d + 7) >> 3;
+    u64* cq = (u64*)(smem + (((size_t)KP2 * 12 + 7) & ~(size_t)7) + (QLDS ? (size_t)ng * 64 : 0));
     if (a.stamps && tid == 0) a.stamps[(size_t)q * 6 + 5] = __builtin_amdgcn_s_memtime();
     const u64* src = a.cand + (size_t)q * a.lcap;
     const int n = a.cand_n ? min(a.cand_n[q], a.lcap) : a.Kp;
@@ -1851,7 +1854,7 @@ __global__ void __launch_bounds__(RF_THREADS) k_refine(RefineArgs a, int KP2) {
         minkey_s = ~0ull;
     }
     if constexpr (QLDS)
-        for (int i = tid; i < a.d; i += RF_THREADS) qs[i] = (double)qv[i];
+        for (int i = tid; i < a.d; i += RF_THREADS) qs[(i & 7) * ng + (i >> 3)] = (double)qv[i];
     if (a.stamps && tid == 0) {
         __builtin_amdgcn_sched_barrier(0);
         a.stamps[(size_t)q * 6 + 0] = __builtin_amdgcn_s_memtime();
@@ -1906,7 +1909,7 @@ __global__ void __launch_bounds__(RF_THREADS) k_refine(RefineArgs a, int KP2) {
     if (wid == 1 && METRIC == METRIC_L2) {  // ||q||^2 for the L2 margin (staged query when in LDS)
         double s2 = 0.0;
         for (int i = lane; i < a.d; i += 64) {
-            const double v = QLDS ? qs[i] : (double)qv[i];
+            const double v = QLDS ? qs[(i & 7) * ng + (i >> 3)] : (double)qv[i];
             s2 += v * v;
         }
 #pragma unroll
@@ -2362,8 +2365,9 @@ hipError_t launch_refine(const RefineArgs& a, int nq, hipStream_t st) {
     int KP2 = 1;
     while (KP2 < a.Kp) KP2 <<= 1;
     const size_t base = (size_t)KP2 * 12 + 8 + (size_t)KP2 * 8;  // scores, ids, (query), kept keys
-    const bool qlds = base + (size_t)a.d * 8 <= 148 * 1024;  // query as fp64 in LDS when it fits
-    const size_t lds = qlds ? base + (size_t)a.d * 8 : base;
+    const size_t qbytes = (size_t)((a.d + 7) >> 3) * 64;    // fp64 query, transposed 8-element groups
+    const bool qlds = base + qbytes <= 148 * 1024;  // query as fp64 in LDS when it fits
+    const size_t lds = qlds ? base + qbytes : base;
     if (a.dt == DT_F32) launch_refine_dt<DT_F32>(a, nq, KP2, lds, qlds, st);
     else if (a.dt == DT_BF16) launch_refine_dt<DT_BF16>(a, nq, KP2, lds, qlds, st);
     else launch_refine_dt<DT_F16>(a, nq, KP2, lds, qlds, st);

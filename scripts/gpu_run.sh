@@ -24,7 +24,10 @@ for s in "$@"; do
     ablate) for m in ${MODES:-0 1 2 0}; do VS_MF_ABLATE=$m timeout -k 10 300 python bench.py --no-cpu-baseline --steps 10 > gpurun_out/ablate_$m.log 2>&1 || exit 1; tail -1 gpurun_out/ablate_$m.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('mode $m', d['roofline']['kernel_ms'])" >> gpurun_out/ablate.txt; done ;;
     zero) for m in ${MODES:-9}; do VS_MF_ABLATE=$m timeout -k 10 300 python bench.py --no-cpu-baseline --steps 10 --zero-corpus > gpurun_out/zero_$m.log 2>&1 || exit 1; tail -1 gpurun_out/zero_$m.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('zero mode $m', d['roofline']['kernel_ms'])" >> gpurun_out/ablate.txt; done ;;
     dist2) timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --dist-backend gloo --same-device --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/dist2.log 2>&1 ;;
-    rfstamps) VS_RF_STAMPS=1 timeout -k 10 300 python bench.py --no-cpu-baseline --steps 2 --warmup 1 > gpurun_out/rfstamps.log 2>&1 ;;
+    rfprof) for v in ${LIBS:-plain qt}; do VS_LIB_PATH=$GRAFT_REPO_ROOT/abtmp/libvs_$v.so timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/rfprof_$v -o run --output-format csv -- python3 bench.py --rows ${ROWS:-1250000} --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/rfprof_$v.log 2>&1 || exit 1; echo "lib $v $(grep -h 'k_refine\|k_screen_mfma<1, 0, 0>' gpurun_out/rfprof_$v/*/run_kernel_stats.csv gpurun_out/rfprof_$v/run_kernel_stats.csv 2>/dev/null | cut -d, -f1-4 | tr '\n' ' ')" >> gpurun_out/rfprof.txt; rm -rf gpurun_out/rfprof_$v/*/*trace* gpurun_out/rfprof_$v/*trace*; done ;;
+    rowsweep) for rows in ${ROWSET:-1250000 2500000 5000000 10000000 1250000}; do timeout -k 10 300 python bench.py --rows $rows --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/rowsweep_$rows.log 2>&1 || exit 1; grep '^{' gpurun_out/rowsweep_$rows.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('rows $rows', d['ms_per_step'], d['roofline']['kernel_ms'])" >> gpurun_out/rowsweep.txt; done
+      VS_MF_STAMPS=1 timeout -k 10 300 python bench.py --rows 1250000 --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/stamps_1250k.log 2>&1 ;;
+    rfstamps)VS_RF_STAMPS=1 timeout -k 10 300 python bench.py --no-cpu-baseline --steps 2 --warmup 1 > gpurun_out/rfstamps.log 2>&1 ;;
     stamps) VS_MF_STAMPS=1 timeout -k 10 300 python bench.py --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/stamps.log 2>&1 ;;
     stats) VS_MF_STATS=1 timeout -k 10 300 python bench.py --no-cpu-baseline --steps 2 --warmup 1 > gpurun_out/stats.log 2>&1 ;;
     pmcab) for m in ${MODES:-0 9}; do
