@@ -275,8 +275,8 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
     static const bool stamps_on = getenv("VS_MF_STAMPS") != nullptr;
     unsigned long long* stamps = nullptr;
     if (stamps_on && use_mfma) {
-        HIP_CHECK(hipMalloc(&stamps, sizeof(unsigned long long) * a.G * 8 * 6));
-        HIP_CHECK(hipMemsetAsync(stamps, 0, sizeof(unsigned long long) * a.G * 8 * 6, st));
+        HIP_CHECK(hipMalloc(&stamps, sizeof(unsigned long long) * a.G * 8 * 7));  // + entry/exit per WG
+        HIP_CHECK(hipMemsetAsync(stamps, 0, sizeof(unsigned long long) * a.G * 8 * 7, st));
         a.stamps = stamps;
     }
     if (use_mfma) HIP_CHECK(launch_screen_mfma(ix->dtype, a, c->qtile.as<uint8_t>(), nqb, st));
@@ -291,7 +291,7 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
         a.dbg = nullptr;
     }
     if (stamps) {
-        std::vector<unsigned long long> h((size_t)a.G * 8 * 6);
+        std::vector<unsigned long long> h((size_t)a.G * 8 * 7);
         HIP_CHECK(hipMemcpyAsync(h.data(), stamps, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
         HIP_CHECK(hipStreamSynchronize(st));
         const double steps = (double)((tiles + a.G - 1) / a.G) * (ix->dpad / CH);
@@ -306,6 +306,23 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
                     "| per tile-end step: tail %.0f | total loop per K-step %.0f\n", r ? "writer" : "loader",
                     acc[r][0] / n / steps, acc[r][1] / n / steps, acc[r][2] / n / steps,
                     acc[r][5] / n / (steps - tiles_per_wg), acc[r][3] / n / tiles_per_wg, acc[r][4] / n / steps);
+        }
+        // workgroup entry / exit on the 100 MHz wall clock: launch ramp and straggler tail
+        {
+            const unsigned long long* rt = h.data() + (size_t)a.G * 48;
+            unsigned long long s0 = ~0ull, s1 = 0;
+            std::vector<double> busy, ends;
+            for (int b = 0; b < a.G; ++b) {
+                s0 = std::min(s0, rt[2 * b]);
+                s1 = std::max(s1, rt[2 * b]);
+                busy.push_back((rt[2 * b + 1] - rt[2 * b]) * 0.01);
+            }
+            for (int b = 0; b < a.G; ++b) ends.push_back((rt[2 * b + 1] - s0) * 0.01);
+            std::sort(ends.begin(), ends.end());
+            std::sort(busy.begin(), busy.end());
+            fprintf(stderr, "[vs wg clock] us from first entry: last entry %.1f | exits min %.1f p50 %.1f p90 %.1f max %.1f "
+                    "| busy min %.1f p50 %.1f max %.1f\n", (s1 - s0) * 0.01, ends.front(), ends[ends.size() / 2],
+                    ends[ends.size() * 9 / 10], ends.back(), busy.front(), busy[busy.size() / 2], busy.back());
         }
         hipFree(stamps);
         a.stamps = nullptr;

@@ -173,7 +173,7 @@ struct ScreenArgs {
     u64* glist;              // MFMA path output: per-query compact survivor list [QB][lcap] ...
     int* gcnt;               // ... with its length per query (zeroed by k_pack_qtile)
     int lcap;                // = G * Kp
-    unsigned long long* stamps;  // diagnostic build only (VS_MF_STAMPS): [G][8 waves][5] phase cycles
+    unsigned long long* stamps;  // diagnostic build only (VS_MF_STAMPS): [G][8 waves][6] phase cycles, then [G][2] entry/exit wall clock
     int* next_tile;          // GEMV: tile work-queue counter (zeroed before the launch); null = static ranges
     float* seed_acc;         // MFMA: [G][512 lanes][128] raw accumulators of each workgroup's seed tile (the
                              // first tile of its range): written by the seed pass, reused by the main pass

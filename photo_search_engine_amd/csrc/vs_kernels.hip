@@ -800,6 +800,8 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
     // memory clobber, so the compiler must assume every later memory-clobbering asm (DMA issue,
     // barriers) may write it and can never fold the fragment reads away.
     asm volatile("; lds ring escapes: %0" ::"v"(smem) : "memory");
+    uint64_t rt_entry = 0;  // stamped build: 100 MHz wall clock at workgroup entry / exit
+    if constexpr (MODE == MF_STAMP_MODE) rt_entry = __builtin_amdgcn_s_memrealtime();
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid & 3, wn = wid >> 2;
     const int blk = blockIdx.x;
@@ -1215,6 +1217,13 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
         off = __shfl(off, 0, 64);
         u64* dst = a.glist + (size_t)q * a.lcap + off;
         for (int j = lane; j < n; j += 64) dst[j] = cand[(size_t)q * a.cap + j];
+    }
+    if constexpr (STAMP) {
+        __syncthreads();
+        if (tid == 0 && a.stamps) {
+            a.stamps[(size_t)a.G * 48 + blk * 2] = rt_entry;
+            a.stamps[(size_t)a.G * 48 + blk * 2 + 1] = __builtin_amdgcn_s_memrealtime();
+        }
     }
 }
 

@@ -27,6 +27,7 @@ for s in "$@"; do
     rfprof) for v in ${LIBS:-plain qt}; do VS_LIB_PATH=$GRAFT_REPO_ROOT/abtmp/libvs_$v.so timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/rfprof_$v -o run --output-format csv -- python3 bench.py --rows ${ROWS:-1250000} --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/rfprof_$v.log 2>&1 || exit 1; echo "lib $v $(grep -h 'k_refine\|k_screen_mfma<1, 0, 0>' gpurun_out/rfprof_$v/*/run_kernel_stats.csv gpurun_out/rfprof_$v/run_kernel_stats.csv 2>/dev/null | cut -d, -f1-4 | tr '\n' ' ')" >> gpurun_out/rfprof.txt; rm -rf gpurun_out/rfprof_$v/*/*trace* gpurun_out/rfprof_$v/*trace*; done ;;
     rowsweep) for rows in ${ROWSET:-1250000 2500000 5000000 10000000 1250000}; do timeout -k 10 300 python bench.py --rows $rows --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/rowsweep_$rows.log 2>&1 || exit 1; grep '^{' gpurun_out/rowsweep_$rows.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('rows $rows', d['ms_per_step'], d['roofline']['kernel_ms'])" >> gpurun_out/rowsweep.txt; done
       VS_MF_STAMPS=1 timeout -k 10 300 python bench.py --rows 1250000 --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/stamps_1250k.log 2>&1 ;;
+    k1ab) for rows in ${ROWSET:-1250000 10000000}; do for v in ${PCTS:-100 88 100 88}; do VS_K1_STATIC=$v timeout -k 10 300 python bench.py --rows $rows --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/k1ab_${v}_$rows.log 2>&1 || exit 1; grep '^{' gpurun_out/k1ab_${v}_$rows.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('static% $v rows $rows', d['ms_per_step'], d['roofline']['kernel_ms'], d['uncertified_first_pass'])" >> gpurun_out/k1ab.txt; done; done ;;
     rfstamps)VS_RF_STAMPS=1 timeout -k 10 300 python bench.py --no-cpu-baseline --steps 2 --warmup 1 > gpurun_out/rfstamps.log 2>&1 ;;
     stamps) VS_MF_STAMPS=1 timeout -k 10 300 python bench.py --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/stamps.log 2>&1 ;;
     stats) VS_MF_STATS=1 timeout -k 10 300 python bench.py --no-cpu-baseline --steps 2 --warmup 1 > gpurun_out/stats.log 2>&1 ;;
