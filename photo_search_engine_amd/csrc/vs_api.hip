@@ -200,15 +200,17 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
         a.lcap = a.G * Kp;
     }
 
-    // merge partial lists [nseg][qstride][Kp] down to one list per query; returns it
-    auto merge_all = [&](const u64* src, int nseg, int qstride) -> const u64* {
+    // merge partial lists [nseg][qstride][Kp] down to one list per query (or, with stop_keys, to
+    // the first round whose nseg * Kp <= stop_keys: one query's lists are then contiguous and the
+    // refine selects the best Kp itself); returns it, nseg updated
+    auto merge_all = [&](const u64* src, int& nseg, int qstride, int stop_keys) -> const u64* {
         const int spb = (256 * 16) / Kp;  // k_merge: 4096 keys per block
         const size_t mbytes = (size_t)std::max(1, (nseg + spb - 1) / spb) * nqb * Kp * sizeof(u64);
         c->merge_a.ensure(mbytes);
         c->merge_b.ensure(mbytes);
         u64* bufs[2] = {c->merge_a.as<u64>(), c->merge_b.as<u64>()};
         int which = 0;
-        while (nseg > 1) {
+        while (nseg > 1 && (int64_t)nseg * Kp > stop_keys) {
             int nout = 0;
             HIP_CHECK(launch_merge(src, nseg, qstride, nqb, Kp, bufs[which], &nout, st));
             src = bufs[which];
@@ -339,9 +341,14 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
         r.cand_n = a.gcnt;
         r.lcap = a.lcap;
     } else {  // GEMV: merge the per-block lists down to [q][Kp] (qstride nqb, or part[0] with QB)
-        r.cand = merge_all(a.part, a.G, QB);
+        // one query (the product's call shape): stop the merge tree at <= 2048 keys, which the
+        // refine's one-wave selection takes directly (saves the last k_merge launch).  Needs >= Kp
+        // non-empty keys among them, which every round keeps when the shard has >= Kp rows.
+        int nseg = a.G;
+        const int stop = (nqb == 1 && ix->ntotal >= Kp) ? kRefineOneWaveKeys : 0;
+        r.cand = merge_all(a.part, nseg, QB, stop);
         r.cand_n = nullptr;
-        r.lcap = Kp;
+        r.lcap = nseg * Kp;
     }
     r.Kp = Kp;
     r.q = q;

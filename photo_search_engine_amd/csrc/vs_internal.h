@@ -206,9 +206,10 @@ hipError_t launch_screen_gemv(int dt, const ScreenArgs& a, const float* qp, int 
 hipError_t launch_merge(const u64* in, int nseg, int qstride, int nq, int Kp, u64* out, int* nseg_out,
                         hipStream_t st);
 
+constexpr int kRefineOneWaveKeys = 2048;  // = 64 * RF_WE: lists one wave of k_refine selects from
 struct RefineArgs {
     const u64* cand;       // [nq][lcap] candidate keys: the first cand_n[q] (or, if cand_n is null,
-    const int* cand_n;     //  the first Kp, zero = empty) of each row; the refine keeps the best Kp
+    const int* cand_n;     //  all lcap, zero = empty) of each row; the refine keeps the best Kp
     int lcap;
     int Kp;
     const float* q;        // [nq][d] fp32 (original queries)

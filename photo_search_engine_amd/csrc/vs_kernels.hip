@@ -1836,6 +1836,7 @@ __device__ __forceinline__ void exact_score_q2(const uint8_t* __restrict__ corpu
 constexpr int RF_THREADS = 1024;  // 16 waves per query: Kp / 16 candidates per wave
 constexpr int RF_E = 16;          // candidate keys per thread held in registers for the selection
 constexpr int RF_WE = 32;         // lists up to 64 * RF_WE keys: threshold found by one wave
+static_assert(64 * RF_WE == kRefineOneWaveKeys, "one-wave selection size");
 
 template <int DT, int METRIC, bool QLDS>
 __global__ void __launch_bounds__(RF_THREADS) k_refine(RefineArgs a, int KP2) {
@@ -1856,7 +1857,7 @@ __global__ void __launch_bounds__(RF_THREADS) k_refine(RefineArgs a, int KP2) {
     u64* cq = (u64*)(smem + (((size_t)KP2 * 12 + 7) & ~(size_t)7) + (QLDS ? (size_t)ng * 64 : 0));
     if (a.stamps && tid == 0) a.stamps[(size_t)q * 6 + 5] = __builtin_amdgcn_s_memtime();
     const u64* src = a.cand + (size_t)q * a.lcap;
-    const int n = a.cand_n ? min(a.cand_n[q], a.lcap) : a.Kp;
+    const int n = a.cand_n ? min(a.cand_n[q], a.lcap) : a.lcap;
     const float* qv = a.q + (int64_t)q * a.d;
     if (tid == 0) {
         nv_s = 0;

@@ -326,3 +326,15 @@ def test_sharded_index_single_process_matches_oracle():
     np.testing.assert_array_equal(I.cpu().numpy(), Ie)
     np.testing.assert_array_equal(S.cpu().numpy(), Se)
     sh.close()
+
+
+@pytest.mark.parametrize("metric", ["ip", "l2"])
+@pytest.mark.parametrize("N,k", [(20, 16), (5000, 10), (70_000, 1), (70_000, 100), (300_000, 10), (300_000, 400)])
+def test_single_query_merge_stop_exact(FlatIndex, metric, N, k):
+    # one query: the GEMV path stops its merge tree once <= 2048 keys remain and the refine selects
+    # the best Kp from them (shards of >= Kp rows), else merges to one list; both must be exact
+    ix = FlatIndex(48, metric, "f32")
+    ix.add_synthetic(O.SEED_CORPUS, 0, N, True)
+    for i in range(3):
+        q = O.synth_rows(O.SEED_QUERIES, 100 + i, 1, 48, True, "f32")
+        _check_exact(ix, q, k, metric)
