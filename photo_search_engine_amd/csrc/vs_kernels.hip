@@ -21,6 +21,7 @@ namespace vs {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef int intx4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 // ------------------------------------------------------------------------------------------------
@@ -620,9 +621,14 @@ __device__ __forceinline__ void mf_barrier_drain() {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+constexpr int DT_I8_PROBE = 7;  // ablation mode 28 only: int8 MFMA on the same fragments (results meaningless)
 template <int DT>
 __device__ __forceinline__ floatx4 mfma16(const uint4 a, const uint4 b, floatx4 c) {
-    if constexpr (DT == DT_BF16)
+    if constexpr (DT == DT_I8_PROBE)
+        return __builtin_bit_cast(floatx4, __builtin_amdgcn_mfma_i32_16x16x64_i8(
+                                               __builtin_bit_cast(intx4, a), __builtin_bit_cast(intx4, b),
+                                               __builtin_bit_cast(intx4, c), 0, 0, 0));
+    else if constexpr (DT == DT_BF16)
         return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
                                                        0, 0, 0);
     else
@@ -767,7 +773,7 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
     constexpr bool LOADS = (MODE != 1 && MODE < 3) || (MODE >= 6 && MODE != 12);  // (incl. seed, stamps)
     constexpr bool MATH = (MODE != 2 && MODE < 6) || MODE == 9 || MODE == 10 || MODE == 13 || MODE == 14 ||
                           MODE == MF_SEED_MODE || MODE == MF_STAMP_MODE || MODE == 16 || MODE == 17 || MODE == 24 ||
-                          MODE == 25 || MODE == 26 || MODE == 27 || XP;
+                          MODE == 25 || MODE == 26 || MODE == 27 || MODE == 28 || XP;
     constexpr bool PP = MODE == 11 || MODE == 12;  // ping-pong: waves 4-7 half a K-step behind waves 0-3
     constexpr bool SEED = MODE == MF_SEED_MODE;  // threshold-seed pass: group maxima only
     constexpr bool EPI = MODE < 3 || MODE == 13 || MODE == 14 || SEED || MODE == MF_STAMP_MODE || MODE == 16 ||
@@ -776,7 +782,8 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
     constexpr bool CHECK = MODE != 13 && MODE != 14;  // deferred compaction check + pool flush
     constexpr bool BAR = MODE < 4 || MODE >= 6;  // (incl. seed, stamps)
     constexpr bool READS = MODE < 5 || MODE == 9 || MODE == 10 || MODE == 13 || MODE == 14 || MODE == MF_SEED_MODE ||
-                           MODE == MF_STAMP_MODE || MODE == 16 || MODE == 17 || MODE == 25 || MODE == 26 || MODE == 27 || XP;
+                           MODE == MF_STAMP_MODE || MODE == 16 || MODE == 17 || MODE == 25 || MODE == 26 || MODE == 27 ||
+                           MODE == 28 || XP;
     constexpr bool QLOAD = MODE != 7;
     constexpr int64_t QSTEP = MODE == 21 ? 0 : 16384;  // 21: every stage re-reads query block 0 (L1-resident)
     constexpr bool NT = MODE == 8 || MODE == 0 || MODE >= 9;
@@ -786,6 +793,10 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
     constexpr bool PAIR = MODE == 17;              // one barrier per 2 K-steps (needs an even K-step count)
     constexpr bool SP = MODE == 24;                // fragment reads of stage s+1 pipelined under stage s's MFMAs
     constexpr int POL = MODE == 26 ? 2 : MODE == 27 ? 3 : 0;  // corpus DMA cache policy: sc1 nt / sc0 sc1 nt
+    // 28 = 9 as an int8 screen probe: rows of d int8 (half the bytes, half the K-steps), int8 MFMAs
+    // (16x16x64: twice the K per instruction) on the same LDS stages, no epilogue
+    constexpr bool I8P = MODE == 28;
+    constexpr int MDT = I8P ? DT_I8_PROBE : DT;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     u64* thr_key = (u64*)(smem + MF_SLOTS * MF_SLOT);
     float* thr_f = (float*)(smem + MF_SLOTS * MF_SLOT + 256 * 8);
@@ -829,8 +840,8 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
         flag[2] = 0;
         flag[3] = 0;
     }
-    const int nks = a.dpad / CH;
-    const int64_t tbytes = (int64_t)TR * a.dpad * 2;
+    const int nks = a.dpad / CH / (I8P ? 2 : 1);
+    const int64_t tbytes = (int64_t)TR * a.dpad * (I8P ? 1 : 2);
     const int S = (t1 - t0) * nks;
     u64* cand = a.cand + (size_t)blk * MFMA_QB * a.cap;
     const int trigger = a.cap - TR;
@@ -1092,7 +1103,7 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
 #pragma unroll
                     for (int mi = 0; mi < 4; ++mi) pf_a[mi] = *(const uint4*)(buf + wm * 4096 + lane_off + mi * 1024);
                 mf_mfma<DT, 0, 4>(pf_a, pf_b, acc);
-            } else if constexpr (MATH) mf_compute<DT, READS>(smem + (s % MF_SLOTS) * MF_SLOT, acc, wm, wn, lane_off);
+            } else if constexpr (MATH) mf_compute<MDT, READS>(smem + (s % MF_SLOTS) * MF_SLOT, acc, wm, wn, lane_off);
             if constexpr (STAMP) {
                 __builtin_amdgcn_sched_barrier(0);
                 t3 = __builtin_amdgcn_s_memtime();
@@ -2288,6 +2299,7 @@ static void launch_mfma_mode(const ScreenArgs& a, const uint8_t* qt, int nqb, hi
         case 25: launch_mfma_one<DT, METRIC, 25>(a, qt, nqb, st); break;
         case 26: launch_mfma_one<DT, METRIC, 26>(a, qt, nqb, st); break;
         case 27: launch_mfma_one<DT, METRIC, 27>(a, qt, nqb, st); break;
+        case 28: launch_mfma_one<DT, METRIC, 28>(a, qt, nqb, st); break;
 #endif
         default: launch_mfma_one<DT, METRIC, 0>(a, qt, nqb, st); break;
     }

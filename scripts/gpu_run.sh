@@ -28,6 +28,12 @@ for s in "$@"; do
     rowsweep) for rows in ${ROWSET:-1250000 2500000 5000000 10000000 1250000}; do timeout -k 10 300 python bench.py --rows $rows --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/rowsweep_$rows.log 2>&1 || exit 1; grep '^{' gpurun_out/rowsweep_$rows.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('rows $rows', d['ms_per_step'], d['roofline']['kernel_ms'])" >> gpurun_out/rowsweep.txt; done
       VS_MF_STAMPS=1 timeout -k 10 300 python bench.py --rows 1250000 --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/stamps_1250k.log 2>&1 ;;
     k1ab) for rows in ${ROWSET:-1250000 10000000}; do for v in ${PCTS:-100 88 100 88}; do VS_K1_STATIC=$v timeout -k 10 300 python bench.py --rows $rows --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/k1ab_${v}_$rows.log 2>&1 || exit 1; grep '^{' gpurun_out/k1ab_${v}_$rows.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('static% $v rows $rows', d['ms_per_step'], d['roofline']['kernel_ms'], d['uncertified_first_pass'])" >> gpurun_out/k1ab.txt; done; done ;;
+    i8probe) for m in ${MODES:-0 9 28 9 28}; do VS_LIB_PATH=$GRAFT_REPO_ROOT/abtmp/libvs_abl.so VS_MF_ABLATE=$m timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/i8p_$m -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/i8p_$m.log 2>&1 || exit 1; python3 -c "
+import csv,glob,sys
+for f in glob.glob('gpurun_out/i8p_$m/**/run_kernel_stats.csv', recursive=True) + glob.glob('gpurun_out/i8p_$m/run_kernel_stats.csv'):
+    for r in csv.DictReader(open(f)):
+        if 'k_screen_mfma<1, 0, $m>' in r['Name']: print('mode $m', r['Calls'], r['AverageNs'], r['MinNs'])
+" >> gpurun_out/i8probe.txt; rm -rf gpurun_out/i8p_$m/*/*trace* gpurun_out/i8p_$m/*trace*; done ;;
     rfstamps)VS_RF_STAMPS=1 timeout -k 10 300 python bench.py --no-cpu-baseline --steps 2 --warmup 1 > gpurun_out/rfstamps.log 2>&1 ;;
     stamps) VS_MF_STAMPS=1 timeout -k 10 300 python bench.py --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/stamps.log 2>&1 ;;
     stats) VS_MF_STATS=1 timeout -k 10 300 python bench.py --no-cpu-baseline --steps 2 --warmup 1 > gpurun_out/stats.log 2>&1 ;;
