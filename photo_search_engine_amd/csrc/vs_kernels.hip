@@ -621,10 +621,16 @@ __device__ __forceinline__ void mf_barrier_drain() {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-constexpr int DT_I8_PROBE = 7;  // ablation mode 28 only: int8 MFMA on the same fragments (results meaningless)
+constexpr int DT_I8_PROBE = 7;   // ablation mode 28 only: int8 MFMA on the same fragments (results meaningless)
+constexpr int DT_I8_PROBE2 = 8;  // ablation mode 29 only: two int8 MFMAs per fragment pair (a (hi, lo) query split)
 template <int DT>
 __device__ __forceinline__ floatx4 mfma16(const uint4 a, const uint4 b, floatx4 c) {
-    if constexpr (DT == DT_I8_PROBE)
+    if constexpr (DT == DT_I8_PROBE2) {
+        const intx4 t = __builtin_amdgcn_mfma_i32_16x16x64_i8(__builtin_bit_cast(intx4, a), __builtin_bit_cast(intx4, b),
+                                                              __builtin_bit_cast(intx4, c), 0, 0, 0);
+        return __builtin_bit_cast(floatx4, __builtin_amdgcn_mfma_i32_16x16x64_i8(
+                                               __builtin_bit_cast(intx4, a), __builtin_bit_cast(intx4, b), t, 0, 0, 0));
+    } else if constexpr (DT == DT_I8_PROBE)
         return __builtin_bit_cast(floatx4, __builtin_amdgcn_mfma_i32_16x16x64_i8(
                                                __builtin_bit_cast(intx4, a), __builtin_bit_cast(intx4, b),
                                                __builtin_bit_cast(intx4, c), 0, 0, 0));
@@ -773,7 +779,7 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
     constexpr bool LOADS = (MODE != 1 && MODE < 3) || (MODE >= 6 && MODE != 12);  // (incl. seed, stamps)
     constexpr bool MATH = (MODE != 2 && MODE < 6) || MODE == 9 || MODE == 10 || MODE == 13 || MODE == 14 ||
                           MODE == MF_SEED_MODE || MODE == MF_STAMP_MODE || MODE == 16 || MODE == 17 || MODE == 24 ||
-                          MODE == 25 || MODE == 26 || MODE == 27 || MODE == 28 || XP;
+                          MODE == 25 || MODE == 26 || MODE == 27 || MODE == 28 || MODE == 29 || XP;
     constexpr bool PP = MODE == 11 || MODE == 12;  // ping-pong: waves 4-7 half a K-step behind waves 0-3
     constexpr bool SEED = MODE == MF_SEED_MODE;  // threshold-seed pass: group maxima only
     constexpr bool EPI = MODE < 3 || MODE == 13 || MODE == 14 || SEED || MODE == MF_STAMP_MODE || MODE == 16 ||
@@ -783,7 +789,7 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
     constexpr bool BAR = MODE < 4 || MODE >= 6;  // (incl. seed, stamps)
     constexpr bool READS = MODE < 5 || MODE == 9 || MODE == 10 || MODE == 13 || MODE == 14 || MODE == MF_SEED_MODE ||
                            MODE == MF_STAMP_MODE || MODE == 16 || MODE == 17 || MODE == 25 || MODE == 26 || MODE == 27 ||
-                           MODE == 28 || XP;
+                           MODE == 28 || MODE == 29 || XP;
     constexpr bool QLOAD = MODE != 7;
     constexpr int64_t QSTEP = MODE == 21 ? 0 : 16384;  // 21: every stage re-reads query block 0 (L1-resident)
     constexpr bool NT = MODE == 8 || MODE == 0 || MODE >= 9;
@@ -795,8 +801,9 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
     constexpr int POL = MODE == 26 ? 2 : MODE == 27 ? 3 : 0;  // corpus DMA cache policy: sc1 nt / sc0 sc1 nt
     // 28 = 9 as an int8 screen probe: rows of d int8 (half the bytes, half the K-steps), int8 MFMAs
     // (16x16x64: twice the K per instruction) on the same LDS stages, no epilogue
-    constexpr bool I8P = MODE == 28;
-    constexpr int MDT = I8P ? DT_I8_PROBE : DT;
+    // 29 = 28 with two int8 MFMAs per fragment pair: the MFMA work of a (hi, lo) int8 query split
+    constexpr bool I8P = MODE == 28 || MODE == 29;
+    constexpr int MDT = MODE == 29 ? DT_I8_PROBE2 : I8P ? DT_I8_PROBE : DT;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     u64* thr_key = (u64*)(smem + MF_SLOTS * MF_SLOT);
     float* thr_f = (float*)(smem + MF_SLOTS * MF_SLOT + 256 * 8);
@@ -2300,6 +2307,7 @@ static void launch_mfma_mode(const ScreenArgs& a, const uint8_t* qt, int nqb, hi
         case 26: launch_mfma_one<DT, METRIC, 26>(a, qt, nqb, st); break;
         case 27: launch_mfma_one<DT, METRIC, 27>(a, qt, nqb, st); break;
         case 28: launch_mfma_one<DT, METRIC, 28>(a, qt, nqb, st); break;
+        case 29: launch_mfma_one<DT, METRIC, 29>(a, qt, nqb, st); break;
 #endif
         default: launch_mfma_one<DT, METRIC, 0>(a, qt, nqb, st); break;
     }
