@@ -26,6 +26,23 @@ namespace {
 
 thread_local std::string g_err;
 
+// pinned host staging (grow-only): pageable hipMemcpyAsync is a staged, blocking copy
+struct HostBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    void ensure(size_t want) {
+        if (want <= bytes) return;
+        release();
+        HIP_CHECK(hipHostMalloc(&p, want, hipHostMallocDefault));
+        bytes = want;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+};
+
 // per-call execution context: stream + workspace (pooled; one per concurrent search)
 struct Ctx {
     hipStream_t stream = nullptr;
@@ -34,12 +51,15 @@ struct Ctx {
     DevBuf tilectr;  // GEMV screen: tile work-queue counter
     DevBuf seedacc;  // MFMA seed pass: raw accumulators of each workgroup's seed tile
     PinnedPair pin;  // read_rows_host: pinned landing chunks
-    std::vector<int> cert_host;
+    HostBuf hq;      // vs_search: the query batch, staged for the H2D copy
+    HostBuf hout;    // vs_search: I (int64), D (fp32) and certificates land here; search_exact_device: certificates
     ~Ctx() {
         for (DevBuf* b : {&qdev, &qtile, &qinfo, &qpad, &cand, &part, &merge_a, &merge_b, &outD, &outI, &outS, &cert, &thr0,
                           &seedmax, &gcnt, &rows[0], &rows[1], &tilectr, &seedacc})
             b->release();
         pin.release();
+        hq.release();
+        hout.release();
         if (stream) hipStreamDestroy(stream);
     }
 };
@@ -430,18 +450,19 @@ void vs::search_exact_device(vs_index* ix, const float* q_dev, int64_t nq, int k
     const int Kp = screen_depth(k);
     search_all(ix, c, q_dev, nq, k, Kp, D_dev ? D_dev : c->outD.as<float>(), I_dev, S64_dev, c->cert.as<int>(),
                id_offset, st, kOptimisticSeedRank);
-    c->cert_host.resize((size_t)nq);
-    HIP_CHECK(hipMemcpyAsync(c->cert_host.data(), c->cert.p, (size_t)nq * sizeof(int), hipMemcpyDeviceToHost, st));
+    c->hout.ensure((size_t)nq * sizeof(int));
+    int* cert_h = (int*)c->hout.p;
+    HIP_CHECK(hipMemcpyAsync(cert_h, c->cert.p, (size_t)nq * sizeof(int), hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));
     for (int64_t qi = 0; qi < nq; ++qi) {
         int Kr = Kp;
-        while (!c->cert_host[qi]) {
+        while (!cert_h[qi]) {
             if (Kr >= KP_MAX || Kr >= ix->ntotal)
                 throw VsError(VS_ERR_UNCERTIFIED, "exactness certificate failed at maximum screening depth");
             Kr = (int)std::min<int64_t>(std::min<int64_t>((int64_t)Kr * 4, KP_MAX), round_up(ix->ntotal, 16));
             search_all(ix, c, q_dev + qi * ix->d, 1, k, Kr, D_dev ? D_dev + qi * k : c->outD.as<float>(), I_dev + qi * k,
                        S64_dev ? S64_dev + qi * k : nullptr, c->cert.as<int>(), id_offset, st, /*safe seed*/ 0);
-            HIP_CHECK(hipMemcpyAsync(&c->cert_host[qi], c->cert.p, sizeof(int), hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipMemcpyAsync(&cert_h[qi], c->cert.p, sizeof(int), hipMemcpyDeviceToHost, st));
             HIP_CHECK(hipStreamSynchronize(st));
         }
     }
@@ -728,30 +749,34 @@ int vs_search(vs_index* ix, const float* q, int64_t nq, int32_t k, float* D, int
         c->outD.ensure((size_t)nq * kk * sizeof(float));
         c->outI.ensure((size_t)nq * kk * sizeof(int64_t));
         c->cert.ensure((size_t)nq * sizeof(int));
-        HIP_CHECK(hipMemcpyAsync(c->qdev.p, q, (size_t)nq * ix->d * sizeof(float), hipMemcpyHostToDevice, st));
+        // the caller's buffers are pageable: stage through pinned memory (one memcpy each way)
+        c->hq.ensure((size_t)nq * ix->d * sizeof(float));
+        std::memcpy(c->hq.p, q, (size_t)nq * ix->d * sizeof(float));
+        HIP_CHECK(hipMemcpyAsync(c->qdev.p, c->hq.p, (size_t)nq * ix->d * sizeof(float), hipMemcpyHostToDevice, st));
         int Kp = screen_depth(kk);
-        std::vector<float> Dk((size_t)nq * kk);
-        std::vector<int64_t> Ik((size_t)nq * kk);
-        c->cert_host.resize((size_t)nq);
+        c->hout.ensure((size_t)nq * kk * (sizeof(int64_t) + sizeof(float)) + (size_t)nq * sizeof(int));
+        int64_t* Ik = (int64_t*)c->hout.p;
+        float* Dk = (float*)(Ik + (size_t)nq * kk);
+        int* cert_h = (int*)(Dk + (size_t)nq * kk);
         search_all(ix, c, c->qdev.as<float>(), nq, kk, Kp, c->outD.as<float>(), c->outI.as<int64_t>(), nullptr,
                    c->cert.as<int>(), 0, st, kOptimisticSeedRank);
-        HIP_CHECK(hipMemcpyAsync(Dk.data(), c->outD.p, Dk.size() * sizeof(float), hipMemcpyDeviceToHost, st));
-        HIP_CHECK(hipMemcpyAsync(Ik.data(), c->outI.p, Ik.size() * sizeof(int64_t), hipMemcpyDeviceToHost, st));
-        HIP_CHECK(hipMemcpyAsync(c->cert_host.data(), c->cert.p, (size_t)nq * sizeof(int), hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipMemcpyAsync(Dk, c->outD.p, (size_t)nq * kk * sizeof(float), hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipMemcpyAsync(Ik, c->outI.p, (size_t)nq * kk * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipMemcpyAsync(cert_h, c->cert.p, (size_t)nq * sizeof(int), hipMemcpyDeviceToHost, st));
         HIP_CHECK(hipStreamSynchronize(st));
         // exactness certificate failed for some queries (near-ties deeper than the margin):
         // re-screen those queries one at a time with a 4x deeper candidate set.
         for (int64_t qi = 0; qi < nq; ++qi) {
             int Kr = Kp;
-            while (!c->cert_host[qi]) {
+            while (!cert_h[qi]) {
                 if (Kr >= KP_MAX || Kr >= ix->ntotal)
                     throw VsError(VS_ERR_UNCERTIFIED, "exactness certificate failed at maximum screening depth");
                 Kr = (int)std::min<int64_t>(std::min<int64_t>((int64_t)Kr * 4, KP_MAX), round_up(ix->ntotal, 16));
                 search_all(ix, c, c->qdev.as<float>() + qi * ix->d, 1, kk, Kr, c->outD.as<float>(),
                            c->outI.as<int64_t>(), nullptr, c->cert.as<int>(), 0, st, /*safe seed*/ 0);
-                HIP_CHECK(hipMemcpyAsync(Dk.data() + qi * kk, c->outD.p, kk * sizeof(float), hipMemcpyDeviceToHost, st));
-                HIP_CHECK(hipMemcpyAsync(Ik.data() + qi * kk, c->outI.p, kk * sizeof(int64_t), hipMemcpyDeviceToHost, st));
-                HIP_CHECK(hipMemcpyAsync(&c->cert_host[qi], c->cert.p, sizeof(int), hipMemcpyDeviceToHost, st));
+                HIP_CHECK(hipMemcpyAsync(Dk + qi * kk, c->outD.p, kk * sizeof(float), hipMemcpyDeviceToHost, st));
+                HIP_CHECK(hipMemcpyAsync(Ik + qi * kk, c->outI.p, kk * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+                HIP_CHECK(hipMemcpyAsync(&cert_h[qi], c->cert.p, sizeof(int), hipMemcpyDeviceToHost, st));
                 HIP_CHECK(hipStreamSynchronize(st));
             }
         }
