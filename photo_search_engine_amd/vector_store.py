@@ -120,6 +120,17 @@ class VectorStore:
             return vector
         return (array / norm).astype("float32").tolist()
 
+    def _normalize_query(self, vector) -> np.ndarray:
+        """``np.array([_normalize_vector(vector)], dtype="float32")`` without the Python-list round trip
+        (~0.19 ms of a 0.5 ms call at d=4096): fp32 -> Python float -> fp32 is exact, so the bits
+        are the same."""
+        array = np.array(vector, dtype="float32")
+        if self._normalize:
+            norm = np.linalg.norm(array)
+            if norm != 0:
+                array = (array / norm).astype("float32")
+        return array.reshape(1, -1)
+
     def _normalize_rows(self, rows: np.ndarray) -> np.ndarray:
         """Bulk form of ``_normalize_vector``: each row normalised exactly as the single-row path
         (same numpy calls per row, so the stored bits are identical)."""
@@ -198,9 +209,7 @@ class VectorStore:
             raise ValueError(f"向量维度不匹配: {len(query_embedding)} != {self.dimension}")
 
         k = min(top_k, self.index.ntotal)
-        normalized = self._normalize_vector(query_embedding)
-        vector = np.array([normalized], dtype="float32")
-        distances, indices = self.index.search(vector, k)
+        distances, indices = self.index.search(self._normalize_query(query_embedding), k)
 
         results: List[Dict] = []
         for distance, index in zip(distances[0].tolist(), indices[0].tolist()):

@@ -203,3 +203,18 @@ def test_hnsw_store_above_graph_cap_saves_flat(VS, tmp_path, monkeypatch):
     store.add(rng.standard_normal((20, 8)).astype(np.float32), [{} for _ in range(20)])
     store.save()
     assert F.read_index(str(tmp_path / "i")).kind == "flat"
+
+
+@pytest.mark.parametrize("d", [8, 1536, 4096])
+def test_query_normalisation_skips_list_round_trip_bit_identically(d):
+    # search() normalises its query as an array; the bits must equal the reference's
+    # np.array([_normalize_vector(v)], dtype="float32") (utils/vector_store.py:83-90,189-191)
+    store = vsmod.VectorStore.__new__(vsmod.VectorStore)
+    store._normalize = True
+    rng = np.random.default_rng(d)
+    cases = [(rng.standard_normal(d) * s).astype(np.float32).tolist() for s in (1e-3, 1.0, 7.5, 1e3)]
+    cases.append([0.0] * d)
+    for v in cases:
+        want = np.array([store._normalize_vector(v)], dtype="float32")
+        got = store._normalize_query(v)
+        assert got.shape == want.shape and got.tobytes() == want.tobytes()
