@@ -50,12 +50,13 @@ struct Ctx {
     DevBuf rows[2];  // read_rows_host: unpacked fp32 chunks
     DevBuf tilectr;  // GEMV screen: tile work-queue counter
     DevBuf seedacc;  // MFMA seed pass: raw accumulators of each workgroup's seed tile
+    DevBuf outAll;   // vs_search: I (int64), D (fp32), certificates in one block: ONE D2H copy
     PinnedPair pin;  // read_rows_host: pinned landing chunks
     HostBuf hq;      // vs_search: the query batch, staged for the H2D copy
     HostBuf hout;    // vs_search: I (int64), D (fp32) and certificates land here; search_exact_device: certificates
     ~Ctx() {
         for (DevBuf* b : {&qdev, &qtile, &qinfo, &qpad, &cand, &part, &merge_a, &merge_b, &outD, &outI, &outS, &cert, &thr0,
-                          &seedmax, &gcnt, &rows[0], &rows[1], &tilectr, &seedacc})
+                          &seedmax, &gcnt, &rows[0], &rows[1], &tilectr, &seedacc, &outAll})
             b->release();
         pin.release();
         hq.release();
@@ -202,18 +203,19 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
         // work-queue tiles over exactly the resident blocks (VS_GEMV_DYN=0: static ranges, 8 per CU)
         a.G = (int)std::min<int64_t>(tiles, (int64_t)ix->num_cu * (gemv_dyn() ? gemv_blocks_per_cu(ix->dtype, QB) : 8));
         c->qpad.ensure((size_t)QB * ix->dpad * sizeof(float));
-        HIP_CHECK(launch_pack_qf32(q, nqb, QB, ix->d, ix->dpad, c->qpad.as<float>(), c->qinfo.as<float>(), st));
+        int* ctr = nullptr;
+        if (gemv_dyn()) {  // the work-queue counter is zeroed by the query pack (no separate memset)
+            c->tilectr.ensure(sizeof(int));
+            ctr = c->tilectr.as<int>();
+        }
+        HIP_CHECK(launch_pack_qf32(q, nqb, QB, ix->d, ix->dpad, c->qpad.as<float>(), c->qinfo.as<float>(), st, ctr));
     }
     a.G = std::max(a.G, 1);
     c->cand.ensure((size_t)a.G * QB * a.cap * sizeof(u64));
     c->part.ensure((size_t)a.G * QB * Kp * sizeof(u64));  // GEMV: [G][QB][Kp]; MFMA: [QB][G*Kp] survivor lists
     a.cand = c->cand.as<u64>();
     a.part = c->part.as<u64>();
-    if (!use_mfma && gemv_dyn()) {
-        c->tilectr.ensure(sizeof(int));
-        HIP_CHECK(hipMemsetAsync(c->tilectr.p, 0, sizeof(int), st));
-        a.next_tile = c->tilectr.as<int>();
-    }
+    if (!use_mfma && gemv_dyn()) a.next_tile = c->tilectr.as<int>();
     if (use_mfma) {
         a.glist = c->part.as<u64>();
         a.gcnt = c->gcnt.as<int>();
@@ -754,15 +756,18 @@ int vs_search(vs_index* ix, const float* q, int64_t nq, int32_t k, float* D, int
         std::memcpy(c->hq.p, q, (size_t)nq * ix->d * sizeof(float));
         HIP_CHECK(hipMemcpyAsync(c->qdev.p, c->hq.p, (size_t)nq * ix->d * sizeof(float), hipMemcpyHostToDevice, st));
         int Kp = screen_depth(kk);
-        c->hout.ensure((size_t)nq * kk * (sizeof(int64_t) + sizeof(float)) + (size_t)nq * sizeof(int));
+        // device and pinned host blocks share one layout [I int64 | D fp32 | cert int]
+        const size_t obytes = (size_t)nq * kk * (sizeof(int64_t) + sizeof(float)) + (size_t)nq * sizeof(int);
+        c->hout.ensure(obytes);
+        c->outAll.ensure(obytes);
         int64_t* Ik = (int64_t*)c->hout.p;
         float* Dk = (float*)(Ik + (size_t)nq * kk);
         int* cert_h = (int*)(Dk + (size_t)nq * kk);
-        search_all(ix, c, c->qdev.as<float>(), nq, kk, Kp, c->outD.as<float>(), c->outI.as<int64_t>(), nullptr,
-                   c->cert.as<int>(), 0, st, kOptimisticSeedRank);
-        HIP_CHECK(hipMemcpyAsync(Dk, c->outD.p, (size_t)nq * kk * sizeof(float), hipMemcpyDeviceToHost, st));
-        HIP_CHECK(hipMemcpyAsync(Ik, c->outI.p, (size_t)nq * kk * sizeof(int64_t), hipMemcpyDeviceToHost, st));
-        HIP_CHECK(hipMemcpyAsync(cert_h, c->cert.p, (size_t)nq * sizeof(int), hipMemcpyDeviceToHost, st));
+        int64_t* Id = c->outAll.as<int64_t>();
+        float* Dd = (float*)(Id + (size_t)nq * kk);
+        int* cert_d = (int*)(Dd + (size_t)nq * kk);
+        search_all(ix, c, c->qdev.as<float>(), nq, kk, Kp, Dd, Id, nullptr, cert_d, 0, st, kOptimisticSeedRank);
+        HIP_CHECK(hipMemcpyAsync(c->hout.p, c->outAll.p, obytes, hipMemcpyDeviceToHost, st));
         HIP_CHECK(hipStreamSynchronize(st));
         // exactness certificate failed for some queries (near-ties deeper than the margin):
         // re-screen those queries one at a time with a 4x deeper candidate set.

@@ -197,7 +197,7 @@ hipError_t launch_gather_rows(int dt, const uint8_t* data, const int64_t* ids, i
 hipError_t launch_pack_qtile(int dt, const float* q, int nqb, int d, int dpad, uint8_t* qt, float* qinfo, int* gcnt,
                              hipStream_t st);
 hipError_t launch_pack_qf32(const float* q, int nqb, int nqpad, int d, int dpad, float* qp, float* qinfo,
-                            hipStream_t st);
+                            hipStream_t st, int* ctr = nullptr);  // ctr: zeroed (a screen's tile queue)
 
 hipError_t launch_screen_mfma(int dt, const ScreenArgs& a, const uint8_t* qt, int nqb, hipStream_t st);
 hipError_t launch_screen_gemv(int dt, const ScreenArgs& a, const float* qp, int nqb, int nqpad, hipStream_t st);

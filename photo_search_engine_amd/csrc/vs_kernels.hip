@@ -463,9 +463,11 @@ __global__ void __launch_bounds__(256) k_pack_qtile(const float* __restrict__ q,
 
 // GEMV queries: fp32, [nqpad][dpad] zero padded; q_hat = q
 __global__ void __launch_bounds__(256) k_pack_qf32(const float* __restrict__ q, int nqb, int nqpad, int d, int dpad,
-                                                    float* __restrict__ qp, float* __restrict__ qinfo) {
+                                                    float* __restrict__ qp, float* __restrict__ qinfo,
+                                                    int* __restrict__ ctr) {
     const int lane = threadIdx.x & 63;
     const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (ctr && blockIdx.x == 0 && threadIdx.x == 0) *ctr = 0;  // the GEMV screen's tile queue that follows
     if (r >= nqpad) return;
     double n2 = 0.0;
     for (int i = lane; i < dpad; i += 64) {
@@ -2258,8 +2260,8 @@ hipError_t launch_pack_qtile(int dt, const float* q, int nqb, int d, int dpad, u
 }
 
 hipError_t launch_pack_qf32(const float* q, int nqb, int nqpad, int d, int dpad, float* qp, float* qinfo,
-                            hipStream_t st) {
-    hipLaunchKernelGGL(k_pack_qf32, dim3(blocks4(nqpad)), dim3(256), 0, st, q, nqb, nqpad, d, dpad, qp, qinfo);
+                            hipStream_t st, int* ctr) {
+    hipLaunchKernelGGL(k_pack_qf32, dim3(blocks4(nqpad)), dim3(256), 0, st, q, nqb, nqpad, d, dpad, qp, qinfo, ctr);
     return hipGetLastError();
 }
 
