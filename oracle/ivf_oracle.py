@@ -36,6 +36,47 @@ def assign(x_stored: np.ndarray, c_stored: np.ndarray, metric="ip") -> np.ndarra
     return I[:, 0].copy()
 
 
+def assign_ip_fast(x_stored: np.ndarray, c_stored: np.ndarray, chunk: int = 32768) -> np.ndarray:
+    """``assign`` for the IP metric at sizes where the canonical scan is too slow (BASELINE cfg5:
+    4096 centroids x d=1536): an fp32 GEMM (numpy, any summation order) gives every row's fp32
+    top-2 centroids; where their fp32 gap exceeds twice the fp32 error bound the fp32 winner IS the
+    canonical winner, and every other row is resolved by the canonical fp64 scan (``assign``).
+
+    Bound: any summation order of a d-term fp32 dot product errs by at most
+    gamma_n * sum|x_i c_i| <= gamma_n * ||x|| * ||c||, gamma_n = n u / (1 - n u), n = d + 64
+    (margin for blocked partial sums), u = 2^-24.  If fp32(c1) - fp32(c2) > 2 * bound, every
+    centroid c != c1 has exact(c) <= fp32(c) + bound <= fp32(c2) + bound < fp32(c1) - bound
+    <= exact(c1), so c1 is the unique canonical best.  Same result as ``assign``, by construction.
+    """
+    x_stored = np.ascontiguousarray(x_stored, dtype=np.float32)
+    c_stored = np.ascontiguousarray(c_stored, dtype=np.float32)
+    n, d = x_stored.shape
+    if n == 0:
+        return np.zeros((0,), dtype=np.int64)
+    if c_stored.shape[0] < 2:
+        return np.zeros((n,), dtype=np.int64)
+    u = 2.0 ** -24
+    g = (d + 64) * u / (1.0 - (d + 64) * u)
+    cmax = float(np.max(np.linalg.norm(c_stored.astype(np.float64), axis=1)))
+    out = np.empty((n,), dtype=np.int64)
+    unsure = []
+    ct = np.ascontiguousarray(c_stored.T)
+    for r0 in range(0, n, chunk):
+        xb = x_stored[r0:r0 + chunk]
+        s = xb @ ct  # fp32
+        top2 = np.argpartition(-s, 1, axis=1)[:, :2]
+        s2 = np.take_along_axis(s, top2, axis=1).astype(np.float64)
+        first = np.where(s2[:, 0] >= s2[:, 1], 0, 1)
+        out[r0:r0 + xb.shape[0]] = top2[np.arange(xb.shape[0]), first]
+        gap = np.abs(s2[:, 0] - s2[:, 1])
+        bound = g * np.linalg.norm(xb.astype(np.float64), axis=1) * cmax * 1.01
+        unsure.append(r0 + np.flatnonzero(gap <= 2.0 * bound))
+    unsure = np.concatenate(unsure)
+    if unsure.size:
+        out[unsure] = assign(x_stored[unsure], c_stored, "ip")
+    return out
+
+
 def probe(q: np.ndarray, c_stored: np.ndarray, nprobe: int, metric="ip") -> np.ndarray:
     """Probed lists of every query: exact top-nprobe centroids, best first."""
     nprobe = min(int(nprobe), c_stored.shape[0])
@@ -57,8 +98,11 @@ def search(x_stored: np.ndarray, ids: np.ndarray, lists: np.ndarray, c_stored: n
     S = np.full((nq, k), -np.inf if ip else np.inf, dtype=np.float64)
     I = np.full((nq, k), -1, dtype=np.int64)
     P = probe(q, c_stored, nprobe, metric)
+    # rows of each list, ascending (one sort instead of an isin over all rows per query)
+    by_list = np.argsort(lists, kind="stable")
+    bounds = np.searchsorted(lists[by_list], np.arange(c_stored.shape[0] + 1))
     for a in range(nq):
-        sel = np.flatnonzero(np.isin(lists, P[a]))
+        sel = np.sort(np.concatenate([by_list[bounds[l]:bounds[l + 1]] for l in P[a]]))
         if sel.size == 0:
             continue
         sc = O.canon_scores(x_stored[sel], q[a:a + 1], metric)[0]

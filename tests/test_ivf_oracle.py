@@ -50,3 +50,15 @@ def test_ties_go_to_lower_id():
     lists = IO.assign(x, c, "l2")
     S, I = IO.search(x, np.arange(x.shape[0]), lists, c, base[4:5], 3, 4, "l2")
     assert list(I[0]) == [4, 20, 21]
+
+
+def test_assign_ip_fast_equals_canonical_assign():
+    # the fp32-GEMM shortcut with its rigorous gap test must reproduce the canonical assignment,
+    # including rows exactly or nearly tied between two centroids (resolved canonically)
+    x = O.synth_rows(O.SEED_CORPUS, 0, 4000, 64, True, "f32")
+    c = IO.sample_centroids(x, 40, 6)
+    c[1] = c[0]  # an exact centroid tie: ties -> lower list id
+    c[3] = c[2] + np.float32(1e-7)
+    mid = (c[5] + c[6]) / 2
+    x[:50] = mid / np.linalg.norm(mid)  # rows equidistant from two centroids
+    np.testing.assert_array_equal(IO.assign_ip_fast(x, c, chunk=1000), IO.assign(x, c, "ip"))
