@@ -119,6 +119,9 @@ const char* vs_version(void);
 int vs_set_timing(vs_index* index, int enable);
 int vs_timing_fetch(vs_index* index, float* ms, int cap, int* kernel_kind);
 int64_t vs_uncertified_count(vs_index* index);   /* synchronises the device counter */
+/* pinned host bytes the index holds for vs_search's query / result staging (all contexts); each
+ * context stages at most 8 MiB and loops over query chunks beyond that */
+int64_t vs_host_staging_bytes(vs_index* index);
 
 /* ==== IVF-Flat (BASELINE cfg5) ===========================================
  * Not a reference call site: the reference's VectorStore offers flat and HNSW only

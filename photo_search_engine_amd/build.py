@@ -41,12 +41,10 @@ def _stale(target: str, deps) -> bool:
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
-    """Compile every source for gfx950 and link libvs.so.  VS_ABLATIONS=1 adds the K1 ablation modes
-    (diagnostic builds; use force=True when switching, the library's mtime cannot tell)."""
+    """Compile every source for gfx950 and link libvs.so."""
     if not force and not needs_build():
         return LIB
-    ablate = os.environ.get("VS_ABLATIONS") == "1"
-    obj_dir = OBJ_DIR + ("_ablate" if ablate else "")  # the two builds never share objects
+    obj_dir = OBJ_DIR
     os.makedirs(obj_dir, exist_ok=True)
     headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
     headers.append(os.path.join(HERE, "..", "include", "vs.h"))
@@ -57,8 +55,6 @@ def build(force: bool = False, verbose: bool = False) -> str:
         if force or _stale(obj, [spath] + headers):
             cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-result",
                    "-Wno-unused-value", "-Wno-inline-asm", "-c", spath, "-o", obj + ".tmp.o"]
-            if ablate:  # K1 ablation modes (VS_MF_ABLATE) for profiling
-                cmd.insert(1, "-DVS_MF_ABLATIONS")
             if verbose:
                 print(" ".join(cmd), file=sys.stderr)
             subprocess.run(cmd, check=True)

@@ -26,6 +26,9 @@ namespace {
 
 thread_local std::string g_err;
 
+// pinned staging per context for the host-buffer search (queries in, results out)
+constexpr size_t kPinnedStageCap = 8u << 20;
+
 // pinned host staging (grow-only): pageable hipMemcpyAsync is a staged, blocking copy
 struct HostBuf {
     void* p = nullptr;
@@ -46,6 +49,11 @@ struct HostBuf {
 // per-call execution context: stream + workspace (pooled; one per concurrent search)
 struct Ctx {
     hipStream_t stream = nullptr;
+    // recorded behind the last lease's work on its caller's stream: the next lease (possibly on
+    // another stream) waits on it before touching the workspace, so a device-API search that
+    // returned with kernels still queued is never overwritten by the next caller's pack
+    hipEvent_t idle = nullptr;
+    bool pending = false;
     DevBuf qdev, qtile, qinfo, qpad, cand, part, merge_a, merge_b, outD, outI, outS, cert, thr0, seedmax, gcnt;
     DevBuf rows[2];  // read_rows_host: unpacked fp32 chunks
     DevBuf tilectr;  // GEMV screen: tile work-queue counter
@@ -61,6 +69,7 @@ struct Ctx {
         pin.release();
         hq.release();
         hout.release();
+        if (idle) hipEventDestroy(idle);
         if (stream) hipStreamDestroy(stream);
     }
 };
@@ -102,19 +111,35 @@ Ctx* acquire_ctx(vs_index* ix) {
         return c;
     }
     Ctx* c = new Ctx();
+    ix->pool_all.push_back(c);  // owned by the pool from here on (freed by vs_destroy)
     HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    ix->pool_all.push_back(c);
+    HIP_CHECK(hipEventCreateWithFlags(&c->idle, hipEventDisableTiming));
     return c;
 }
 void release_ctx(vs_index* ix, Ctx* c) {
     std::lock_guard<std::mutex> g(ix->pool_mtx);
     ix->pool_free.push_back(c);
 }
+// A leased context works on `st` (null = the context's own stream): the lease first orders `st`
+// behind the previous lease's work, and on release records the context's idle event on `st`.
 struct CtxLease {
     vs_index* ix;
     Ctx* c;
-    explicit CtxLease(vs_index* i) : ix(i), c(acquire_ctx(i)) {}
-    ~CtxLease() { release_ctx(ix, c); }
+    hipStream_t st;
+    CtxLease(vs_index* i, hipStream_t s, bool own_stream) : ix(i), c(acquire_ctx(i)) {
+        st = own_stream ? c->stream : s;
+        if (c->pending) {
+            hipError_t e = hipStreamWaitEvent(st, c->idle, 0);
+            if (e != hipSuccess) {
+                release_ctx(ix, c);
+                HIP_CHECK(e);
+            }
+        }
+    }
+    ~CtxLease() {
+        c->pending = hipEventRecord(c->idle, st) == hipSuccess;
+        release_ctx(ix, c);
+    }
 };
 
 void ensure_capacity(vs_index* ix, int64_t rows_needed) {
@@ -287,70 +312,8 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
         HIP_CHECK(hipEventCreate(&e1));
         HIP_CHECK(hipEventRecord(e0, st));
     }
-    static const bool dbg_stats = getenv("VS_MF_STATS") != nullptr;
-    unsigned* dbg = nullptr;
-    if (dbg_stats && use_mfma) {
-        HIP_CHECK(hipMalloc(&dbg, 16 * sizeof(unsigned)));
-        HIP_CHECK(hipMemsetAsync(dbg, 0, 16 * sizeof(unsigned), st));
-        a.dbg = dbg;
-    }
-    // diagnostic: VS_MF_STAMPS=1 runs the stamped build of the main screen (VS_MF_ABLATE=15) and
-    // prints per-phase cycles per K-step for loader (0-3) and writer (4-7) waves
-    static const bool stamps_on = getenv("VS_MF_STAMPS") != nullptr;
-    unsigned long long* stamps = nullptr;
-    if (stamps_on && use_mfma) {
-        HIP_CHECK(hipMalloc(&stamps, sizeof(unsigned long long) * a.G * 8 * 7));  // + entry/exit per WG
-        HIP_CHECK(hipMemsetAsync(stamps, 0, sizeof(unsigned long long) * a.G * 8 * 7, st));
-        a.stamps = stamps;
-    }
     if (use_mfma) HIP_CHECK(launch_screen_mfma(ix->dtype, a, c->qtile.as<uint8_t>(), nqb, st));
     else HIP_CHECK(launch_screen_gemv(ix->dtype, a, c->qpad.as<float>(), nqb, QB, st));
-    if (dbg) {
-        unsigned h[16];
-        HIP_CHECK(hipMemcpyAsync(h, dbg, sizeof(h), hipMemcpyDeviceToHost, st));
-        HIP_CHECK(hipStreamSynchronize(st));
-        fprintf(stderr, "[vs stats] inserts=%u slowpath_lanes=%u compactions=%u pool_overflow=%u G=%d seeded=%d\n",
-                h[0], h[1], h[2], h[3], a.G, a.thr0 != nullptr);
-        hipFree(dbg);
-        a.dbg = nullptr;
-    }
-    if (stamps) {
-        std::vector<unsigned long long> h((size_t)a.G * 8 * 7);
-        HIP_CHECK(hipMemcpyAsync(h.data(), stamps, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
-        HIP_CHECK(hipStreamSynchronize(st));
-        const double steps = (double)((tiles + a.G - 1) / a.G) * (ix->dpad / CH);
-        const double tiles_per_wg = (double)((tiles + a.G - 1) / a.G);
-        double acc[2][6] = {};
-        for (int b = 0; b < a.G; ++b)
-            for (int w = 0; w < 8; ++w)
-                for (int i = 0; i < 6; ++i) acc[w >= 4][i] += (double)h[((size_t)b * 8 + w) * 6 + i];
-        for (int r = 0; r < 2; ++r) {
-            const double n = 4.0 * a.G;
-            fprintf(stderr, "[vs stamps] %s waves, cycles per K-step: barrier %.0f dma %.0f reads+mfma %.0f tail %.0f "
-                    "| per tile-end step: tail %.0f | total loop per K-step %.0f\n", r ? "writer" : "loader",
-                    acc[r][0] / n / steps, acc[r][1] / n / steps, acc[r][2] / n / steps,
-                    acc[r][5] / n / (steps - tiles_per_wg), acc[r][3] / n / tiles_per_wg, acc[r][4] / n / steps);
-        }
-        // workgroup entry / exit on the 100 MHz wall clock: launch ramp and straggler tail
-        {
-            const unsigned long long* rt = h.data() + (size_t)a.G * 48;
-            unsigned long long s0 = ~0ull, s1 = 0;
-            std::vector<double> busy, ends;
-            for (int b = 0; b < a.G; ++b) {
-                s0 = std::min(s0, rt[2 * b]);
-                s1 = std::max(s1, rt[2 * b]);
-                busy.push_back((rt[2 * b + 1] - rt[2 * b]) * 0.01);
-            }
-            for (int b = 0; b < a.G; ++b) ends.push_back((rt[2 * b + 1] - s0) * 0.01);
-            std::sort(ends.begin(), ends.end());
-            std::sort(busy.begin(), busy.end());
-            fprintf(stderr, "[vs wg clock] us from first entry: last entry %.1f | exits min %.1f p50 %.1f p90 %.1f max %.1f "
-                    "| busy min %.1f p50 %.1f max %.1f\n", (s1 - s0) * 0.01, ends.front(), ends[ends.size() / 2],
-                    ends[ends.size() * 9 / 10], ends.back(), busy.front(), busy[busy.size() / 2], busy.back());
-        }
-        hipFree(stamps);
-        a.stamps = nullptr;
-    }
     if (timing) {
         HIP_CHECK(hipEventRecord(e1, st));
         std::lock_guard<std::mutex> g(ix->tmtx);
@@ -391,25 +354,7 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
     r.cert = cert;
     r.uncert = ix->d_uncert;
     r.optimistic = optimistic ? 1 : 0;
-    static const bool rf_stamps = getenv("VS_RF_STAMPS") != nullptr;
-    if (rf_stamps) HIP_CHECK(hipMalloc(&r.stamps, sizeof(unsigned long long) * 6 * nqb));
     HIP_CHECK(launch_refine(r, nqb, st));
-    if (rf_stamps) {
-        std::vector<unsigned long long> h((size_t)6 * nqb);
-        HIP_CHECK(hipMemcpyAsync(h.data(), r.stamps, h.size() * 8, hipMemcpyDeviceToHost, st));
-        HIP_CHECK(hipStreamSynchronize(st));
-        double ph[5] = {};
-        for (int qi = 0; qi < nqb; ++qi) {
-            const unsigned long long* t = &h[(size_t)qi * 6];
-            ph[0] += (double)(t[0] - t[5]);  // start -> selection start (query + keys loads, setup)
-            ph[1] += (double)(t[1] - t[0]);  // selection, compaction, count
-            ph[2] += (double)(t[2] - t[1]);  // exact scoring
-            ph[3] += (double)(t[3] - t[2]);  // sort
-        }
-        fprintf(stderr, "[vs rf stamps] cycles per query block: setup %.0f select %.0f score %.0f sort %.0f\n",
-                ph[0] / nqb, ph[1] / nqb, ph[2] / nqb, ph[3] / nqb);
-        hipFree(r.stamps);
-    }
 }
 
 // Full search of nq device queries; outputs device [nq][k].
@@ -445,7 +390,7 @@ void vs::search_exact_device(vs_index* ix, const float* q_dev, int64_t nq, int k
     std::shared_lock<std::shared_mutex> lk(ix->rw);
     DeviceGuard dg(ix->device);
     if (k <= 0) throw VsError(VS_ERR_ARG, "k must be > 0");  // k > ntotal: -1 / worst-score padding
-    CtxLease L(ix);
+    CtxLease L(ix, st, false);
     Ctx* c = L.c;
     c->outD.ensure((size_t)nq * k * sizeof(float));
     c->cert.ensure((size_t)nq * sizeof(int));
@@ -516,7 +461,7 @@ void vs::read_rows_host(vs_index* ix, int64_t i0, int64_t n,
     if (i0 < 0 || n < 0 || i0 + n > ix->ntotal) throw VsError(VS_ERR_ARG, "reconstruct range out of bounds");
     if (n == 0) return;
     DeviceGuard dg(ix->device);
-    CtxLease L(ix);
+    CtxLease L(ix, nullptr, true);
     Ctx* c = L.c;
     const int64_t rpc = stream_chunk_rows(ix->d);
     const size_t cbytes = (size_t)std::min(n, rpc) * ix->d * sizeof(float);
@@ -704,7 +649,7 @@ int vs_search_device(vs_index* ix, const float* q_dev, int64_t nq, int32_t k, fl
         // index's private non-blocking stream: that one is unordered with the caller's producers
         hipStream_t st = (hipStream_t)stream;
         if (ix->ntotal == 0) throw VsError(VS_ERR_ARG, "index is empty");
-        CtxLease L(ix);
+        CtxLease L(ix, st, false);
         search_all(ix, L.c, q_dev, nq, k, screen_depth(k), D_dev, I_dev, S64_dev, nullptr, id_offset, st,
                    kOptimisticSeedRank);
     });
@@ -744,57 +689,68 @@ int vs_search(vs_index* ix, const float* q, int64_t nq, int32_t k, float* D, int
         // k beyond the rows present: search min(k, ntotal), pad the rest (faiss layout)
         const int kk = (int)std::min<int64_t>(k, ix->ntotal);
         if (kk > KP_MAX * 4 / 5) throw VsError(VS_ERR_ARG, "k too large (max " + std::to_string(KP_MAX * 4 / 5) + ")");
-        CtxLease L(ix);
+        CtxLease L(ix, nullptr, true);
         Ctx* c = L.c;
         hipStream_t st = c->stream;
-        c->qdev.ensure((size_t)nq * ix->d * sizeof(float));
-        c->outD.ensure((size_t)nq * kk * sizeof(float));
-        c->outI.ensure((size_t)nq * kk * sizeof(int64_t));
-        c->cert.ensure((size_t)nq * sizeof(int));
-        // the caller's buffers are pageable: stage through pinned memory (one memcpy each way)
-        c->hq.ensure((size_t)nq * ix->d * sizeof(float));
-        std::memcpy(c->hq.p, q, (size_t)nq * ix->d * sizeof(float));
-        HIP_CHECK(hipMemcpyAsync(c->qdev.p, c->hq.p, (size_t)nq * ix->d * sizeof(float), hipMemcpyHostToDevice, st));
-        int Kp = screen_depth(kk);
+        // The caller's buffers are pageable: queries and results go through pinned staging of at
+        // most kPinnedStageCap bytes per context, in chunks of queries (whole MFMA batches when a
+        // chunk holds more than one), so a huge batch never pins its whole size for the index's life.
+        const size_t per_q = std::max((size_t)ix->d * sizeof(float), (size_t)kk * (sizeof(int64_t) + sizeof(float)) + sizeof(int));
+        int64_t chunk = std::max<int64_t>(1, (int64_t)(kPinnedStageCap / per_q));
+        if (chunk >= MFMA_QB) chunk = chunk / MFMA_QB * MFMA_QB;
+        chunk = std::min(chunk, nq);
+        c->qdev.ensure((size_t)chunk * ix->d * sizeof(float));
+        c->outD.ensure((size_t)kk * sizeof(float));
+        c->outI.ensure((size_t)kk * sizeof(int64_t));
+        c->cert.ensure(sizeof(int));
+        c->hq.ensure((size_t)chunk * ix->d * sizeof(float));
         // device and pinned host blocks share one layout [I int64 | D fp32 | cert int]
-        const size_t obytes = (size_t)nq * kk * (sizeof(int64_t) + sizeof(float)) + (size_t)nq * sizeof(int);
-        c->hout.ensure(obytes);
-        c->outAll.ensure(obytes);
-        int64_t* Ik = (int64_t*)c->hout.p;
-        float* Dk = (float*)(Ik + (size_t)nq * kk);
-        int* cert_h = (int*)(Dk + (size_t)nq * kk);
-        int64_t* Id = c->outAll.as<int64_t>();
-        float* Dd = (float*)(Id + (size_t)nq * kk);
-        int* cert_d = (int*)(Dd + (size_t)nq * kk);
-        search_all(ix, c, c->qdev.as<float>(), nq, kk, Kp, Dd, Id, nullptr, cert_d, 0, st, kOptimisticSeedRank);
-        HIP_CHECK(hipMemcpyAsync(c->hout.p, c->outAll.p, obytes, hipMemcpyDeviceToHost, st));
-        HIP_CHECK(hipStreamSynchronize(st));
-        // exactness certificate failed for some queries (near-ties deeper than the margin):
-        // re-screen those queries one at a time with a 4x deeper candidate set.
-        for (int64_t qi = 0; qi < nq; ++qi) {
-            int Kr = Kp;
-            while (!cert_h[qi]) {
-                if (Kr >= KP_MAX || Kr >= ix->ntotal)
-                    throw VsError(VS_ERR_UNCERTIFIED, "exactness certificate failed at maximum screening depth");
-                Kr = (int)std::min<int64_t>(std::min<int64_t>((int64_t)Kr * 4, KP_MAX), round_up(ix->ntotal, 16));
-                search_all(ix, c, c->qdev.as<float>() + qi * ix->d, 1, kk, Kr, c->outD.as<float>(),
-                           c->outI.as<int64_t>(), nullptr, c->cert.as<int>(), 0, st, /*safe seed*/ 0);
-                HIP_CHECK(hipMemcpyAsync(Dk + qi * kk, c->outD.p, kk * sizeof(float), hipMemcpyDeviceToHost, st));
-                HIP_CHECK(hipMemcpyAsync(Ik + qi * kk, c->outI.p, kk * sizeof(int64_t), hipMemcpyDeviceToHost, st));
-                HIP_CHECK(hipMemcpyAsync(&cert_h[qi], c->cert.p, sizeof(int), hipMemcpyDeviceToHost, st));
-                HIP_CHECK(hipStreamSynchronize(st));
-            }
-        }
-        for (int64_t qi = 0; qi < nq; ++qi)
-            for (int j = 0; j < k; ++j) {
-                if (j < kk) {
-                    D[qi * k + j] = Dk[qi * kk + j];
-                    I[qi * k + j] = Ik[qi * kk + j];
-                } else {
-                    D[qi * k + j] = fillD;
-                    I[qi * k + j] = -1;
+        const size_t obytes_max = (size_t)chunk * kk * (sizeof(int64_t) + sizeof(float)) + (size_t)chunk * sizeof(int);
+        c->hout.ensure(obytes_max);
+        c->outAll.ensure(obytes_max);
+        const int Kp = screen_depth(kk);
+        for (int64_t q0 = 0; q0 < nq; q0 += chunk) {
+            const int64_t m = std::min(chunk, nq - q0);
+            std::memcpy(c->hq.p, q + q0 * ix->d, (size_t)m * ix->d * sizeof(float));
+            HIP_CHECK(hipMemcpyAsync(c->qdev.p, c->hq.p, (size_t)m * ix->d * sizeof(float), hipMemcpyHostToDevice, st));
+            const size_t obytes = (size_t)m * kk * (sizeof(int64_t) + sizeof(float)) + (size_t)m * sizeof(int);
+            int64_t* Ik = (int64_t*)c->hout.p;
+            float* Dk = (float*)(Ik + (size_t)m * kk);
+            int* cert_h = (int*)(Dk + (size_t)m * kk);
+            int64_t* Id = c->outAll.as<int64_t>();
+            float* Dd = (float*)(Id + (size_t)m * kk);
+            int* cert_d = (int*)(Dd + (size_t)m * kk);
+            search_all(ix, c, c->qdev.as<float>(), m, kk, Kp, Dd, Id, nullptr, cert_d, 0, st, kOptimisticSeedRank);
+            HIP_CHECK(hipMemcpyAsync(c->hout.p, c->outAll.p, obytes, hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipStreamSynchronize(st));
+            // exactness certificate failed for some queries (near-ties deeper than the margin):
+            // re-screen those queries one at a time with a 4x deeper candidate set.
+            for (int64_t qi = 0; qi < m; ++qi) {
+                int Kr = Kp;
+                while (!cert_h[qi]) {
+                    if (Kr >= KP_MAX || Kr >= ix->ntotal)
+                        throw VsError(VS_ERR_UNCERTIFIED, "exactness certificate failed at maximum screening depth");
+                    Kr = (int)std::min<int64_t>(std::min<int64_t>((int64_t)Kr * 4, KP_MAX), round_up(ix->ntotal, 16));
+                    search_all(ix, c, c->qdev.as<float>() + qi * ix->d, 1, kk, Kr, c->outD.as<float>(),
+                               c->outI.as<int64_t>(), nullptr, c->cert.as<int>(), 0, st, /*safe seed*/ 0);
+                    HIP_CHECK(hipMemcpyAsync(Dk + qi * kk, c->outD.p, kk * sizeof(float), hipMemcpyDeviceToHost, st));
+                    HIP_CHECK(hipMemcpyAsync(Ik + qi * kk, c->outI.p, kk * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+                    HIP_CHECK(hipMemcpyAsync(&cert_h[qi], c->cert.p, sizeof(int), hipMemcpyDeviceToHost, st));
+                    HIP_CHECK(hipStreamSynchronize(st));
                 }
             }
+            for (int64_t qi = 0; qi < m; ++qi)
+                for (int j = 0; j < k; ++j) {
+                    const int64_t o = (q0 + qi) * k + j;
+                    if (j < kk) {
+                        D[o] = Dk[qi * kk + j];
+                        I[o] = Ik[qi * kk + j];
+                    } else {
+                        D[o] = fillD;
+                        I[o] = -1;
+                    }
+                }
+        }
     });
 }
 
@@ -854,6 +810,14 @@ int vs_timing_fetch(vs_index* ix, float* ms, int cap, int* kernel_kind) {
         if (kernel_kind) *kernel_kind = ix->last_kernel_kind;
     });
     return rc == VS_OK ? std::min(count, cap) : rc;
+}
+
+int64_t vs_host_staging_bytes(vs_index* ix) {
+    if (!ix) return -1;
+    std::lock_guard<std::mutex> g(ix->pool_mtx);
+    int64_t b = 0;
+    for (const Ctx* c : ix->pool_all) b += (int64_t)(c->hq.bytes + c->hout.bytes);
+    return b;
 }
 
 int64_t vs_uncertified_count(vs_index* ix) {

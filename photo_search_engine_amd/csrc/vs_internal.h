@@ -23,6 +23,7 @@ namespace vs {
 constexpr int TR = 256;        // rows per tile
 constexpr int CH = 32;         // elements per chunk (= one MFMA K-step)
 constexpr int DT_F32 = 0, DT_BF16 = 1, DT_F16 = 2;
+constexpr int DT_I8 = 3;        // internal: the int8 screen copy (per-row scale, exact int32 MFMA)
 constexpr int METRIC_IP = 0, METRIC_L2 = 1;
 
 constexpr int MFMA_QB = 256;   // queries per MFMA screen launch
@@ -168,15 +169,18 @@ struct ScreenArgs {
     int G;                   // workgroups
     int tile_stride;         // > 0: workgroup b screens only tile b*tile_stride (threshold seeding)
     const u64* thr0;         // [QB] initial per-query key threshold (keys > thr0 kept), or null
-    unsigned* dbg;           // debug counters (VS_MF_STATS): inserts, slow paths, compactions, overflows
     float* seedmax;          // seed pass only: [QB][G*16] maxima of disjoint 16-row groups per query
     u64* glist;              // MFMA path output: per-query compact survivor list [QB][lcap] ...
     int* gcnt;               // ... with its length per query (zeroed by k_pack_qtile)
     int lcap;                // = G * Kp
-    unsigned long long* stamps;  // diagnostic build only (VS_MF_STAMPS): [G][8 waves][6] phase cycles, then [G][2] entry/exit wall clock
     int* next_tile;          // GEMV: tile work-queue counter (zeroed before the launch); null = static ranges
     float* seed_acc;         // MFMA: [G][512 lanes][128] raw accumulators of each workgroup's seed tile (the
                              // first tile of its range): written by the seed pass, reused by the main pass
+    const float* rscale;     // int8 screen: per-row scale s_x (x_hat = s_x * codes)
+    const float* rbeta;      // int8 screen: per-row ||x - x_hat||_2, rounded up
+    const float2* qfac;      // int8 screen: per query (t_q, ||q||), codes q_hat = t_q * int8
+    u64* drop;               // MFMA: per query, max over workgroups of their compaction threshold
+                             // (rows below it were dropped; zeroed by the query pack), or null
 };
 int gemv_blocks_per_cu(int dt, int nqpad);  // resident k_screen_gemv blocks per CU (occupancy API)
 
@@ -227,7 +231,6 @@ struct RefineArgs {
     int* cert;             // [nq] 1 = certified exact (may be null)
     unsigned* uncert;      // device counter (may be null)
     int optimistic;        // screened with an optimistic seed: fewer than Kp candidates = uncertified
-    unsigned long long* stamps;  // diagnostic (VS_RF_STAMPS): [nq][6] phase cycles of block 0's thread 0
     const uint32_t* idmap; // IVF: user id of every storage slot (keys carry slots); null = identity
 };
 hipError_t launch_refine(const RefineArgs& a, int nq, hipStream_t st);

@@ -484,28 +484,30 @@ __global__ void __launch_bounds__(256) k_pack_qf32(const float* __restrict__ q, 
 }
 
 // ------------------------------------------------------------------------------------------------
-// K1: MFMA screen (bf16 / f16 corpus, up to 256 queries per launch)
+// K1: MFMA screen (bf16 / f16 rows, or the int8 screen copy; up to 256 queries per launch)
 // ------------------------------------------------------------------------------------------------
 // Workgroup = 512 threads = 8 waves (2 per SIMD), one per CU, persistent over a contiguous range
 // of row tiles.  Output tile per tile pass: 256 corpus rows (M) x 256 queries (N), K = dpad.
-// Waves 4(M) x 2(N): each wave 64 rows x 128 queries = 4 x 8 MFMA 16x16x32 tiles, 128 acc VGPRs.
+// Waves 4(M) x 2(N): each wave 64 rows x 128 queries = 4 x 8 MFMA 16x16 tiles, 128 acc VGPRs.
 //
-// K-step = 32 elements; its operands are two contiguous 16 KiB blocks (the tile's corpus rows,
-// the query tile) copied by LDS-DMA (global_load_lds_dwordx4, inline asm) into a 4-slot LDS ring
-// MF_DEPTH = 3 K-steps ahead of the MFMAs.  Each K-step waits only for its own stage (counted
-// s_waitcnt vmcnt, raw s_barrier), so three stages (48 KiB of corpus per CU) stay in flight
-// across barriers.  The lane-linear LDS image is XOR-swizzled on the SOURCE address (64 B rows:
-// 16 B piece p of row r holds chunk p ^ perm[(r >> 2) & 3]) so every ds_read_b128 fragment read
-// is bank-conflict free.
+// K-step = one 16 KiB block per operand: 256 rows x 64 B, i.e. 32 bf16/f16 elements
+// (v_mfma_f32_16x16x32_{bf16,f16}) or 64 int8 elements (v_mfma_i32_16x16x64_i8, exact int32
+// accumulation).  Both MFMAs take a lane's 16 B at (row lane & 15, piece lane >> 4) of a 64 B row
+// chunk, so the two element types share the LDS image, the fragment reads and the C layout.  The
+// blocks (the tile's rows, the query tile) are copied by LDS-DMA (global_load_lds_dwordx4, inline
+// asm) into a 4-slot LDS ring MF_DEPTH = 3 K-steps ahead of the MFMAs.  Each K-step waits only for
+// its own stage (counted s_waitcnt vmcnt, raw s_barrier), so three stages (48 KiB of corpus per
+// CU) stay in flight across barriers.  The lane-linear LDS image is XOR-swizzled on the SOURCE
+// address (64 B rows: 16 B piece p of row r holds chunk p ^ perm[(r >> 2) & 3]) so every
+// ds_read_b128 fragment read is bank-conflict free.
 constexpr int MF_SLOT = 32768;  // 16 KiB corpus + 16 KiB queries
 constexpr int MF_SLOTS = 4;
 constexpr int MF_DEPTH = MF_SLOTS - 1;
 constexpr int MF_THREADS = 512;
 constexpr int MF_POOL = 512;  // LDS insert pool of the loader waves (flushed by the writer waves)
-constexpr int MF_SEED_MODE = 20;   // k_screen_mfma MODE of the threshold-seed pass
-constexpr int MF_STAMP_MODE = 15;  // diagnostic: production + per-phase cycle stamps (VS_MF_STAMPS)
 constexpr int MF_SX = 8 * 64 * 8 * 4;  // per-wave insert staging: 64 lanes x 8 fp32 (slow path only)
-constexpr int MF_LDS = MF_SLOTS * MF_SLOT + 256 * 8 + 256 * 4 + 256 * 4 + 16 + MF_POOL * 8 + MF_POOL * 4 + MF_SX;
+constexpr int MF_QFAC = 256 * 8;       // int8 screen: (t_q, ||q||) per query
+constexpr int MF_LDS = MF_SLOTS * MF_SLOT + 256 * 8 + 256 * 4 + 256 * 4 + 16 + MF_POOL * 8 + MF_POOL * 4 + MF_SX + MF_QFAC;
 static_assert(MF_LDS <= 160 * 1024, "LDS budget");
 
 typedef __attribute__((address_space(3))) uint8_t* lds_u8_t;
@@ -517,32 +519,20 @@ __device__ __forceinline__ void glds16(const void* gptr, uint32_t lds_base) {
     asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gptr), "s"(lds_base)
                  : "memory", "m0");
 }
+// the same with the non-temporal hint (corpus blocks are read once per pass)
+__device__ __forceinline__ void glds16_nt(const void* gptr, uint32_t lds_base) {
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off nt" ::"v"(gptr), "s"(lds_base)
+                 : "memory", "m0");
+}
 __device__ __forceinline__ uint32_t lds_addr(const uint8_t* p) { return (uint32_t)(uintptr_t)(lds_u8_t)(p); }
 
 // swizzle: piece position of 16 B chunk c of LDS row r (64 B rows) = c ^ mf_swz(r)
 __device__ __forceinline__ int mf_swz(int r) { return (0x78 >> (2 * ((r >> 2) & 3))) & 3; }
 
-__device__ __forceinline__ void glds16_nt(const void* gptr, uint32_t lds_base) {
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off nt" ::"v"(gptr), "s"(lds_base)
-                 : "memory", "m0");
-}
-
-// cache-policy variants of the corpus LDS-DMA (ablation modes 26 / 27)
-__device__ __forceinline__ void glds16_sc1nt(const void* gptr, uint32_t lds_base) {
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off sc1 nt" ::"v"(gptr), "s"(lds_base)
-                 : "memory", "m0");
-}
-__device__ __forceinline__ void glds16_sc01nt(const void* gptr, uint32_t lds_base) {
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off sc0 sc1 nt" ::"v"(gptr),
-                 "s"(lds_base)
-                 : "memory", "m0");
-}
-
 // issue one K-step stage: waves 0-3 (the loader waves) issue 8 LDS-DMA instructions per thread
 // (4 corpus + 4 query); waves 4-7 issue none.  Loader waves never store to global memory and the
 // writer waves never load, so each wave's in-order vmcnt holds one kind of traffic: counted waits
 // on the stage ring are never held up behind candidate stores.
-template <bool QLOAD = true, bool NT = false, int POL = 0>
 __device__ __forceinline__ void mf_stage(const uint8_t* __restrict__ gA, const uint8_t* __restrict__ gB,
                                          uint32_t slot_base, int tid) {
     const int w = tid >> 6, lane = tid & 63;
@@ -553,86 +543,36 @@ __device__ __forceinline__ void mf_stage(const uint8_t* __restrict__ gA, const u
         const int g = it * 256 + w * 64 + lane;
         const int row = g >> 2, pos = g & 3;
         const int src = (row << 2) + (pos ^ mf_swz(row));
-        if constexpr (POL == 2) glds16_sc1nt(gA + (size_t)src * 16, base + it * 256 * 16);
-        else if constexpr (POL == 3) glds16_sc01nt(gA + (size_t)src * 16, base + it * 256 * 16);
-        else if constexpr (NT) glds16_nt(gA + (size_t)src * 16, base + it * 256 * 16);
-        else glds16(gA + (size_t)src * 16, base + it * 256 * 16);
+        glds16_nt(gA + (size_t)src * 16, base + it * 256 * 16);
     }
-    if constexpr (QLOAD) {
 #pragma unroll
-        for (int it = 0; it < 4; ++it) {
-            const int g = it * 256 + w * 64 + lane;
-            const int row = g >> 2, pos = g & 3;
-            const int src = (row << 2) + (pos ^ mf_swz(row));
-            glds16(gB + (size_t)src * 16, base + it * 256 * 16 + 16384);
-        }
-    }
-}
-
-// balanced stage issue: waves 0-3 the 4 corpus pieces, waves 4-7 the 4 query pieces (4 LDS-DMA
-// instructions per wave per stage; counted waits use 4 per stage on every wave)
-template <bool NT>
-__device__ __forceinline__ void mf_stage_bal(const uint8_t* __restrict__ gA, const uint8_t* __restrict__ gB,
-                                             uint32_t slot_base, int tid) {
-    const int w = tid >> 6, lane = tid & 63;
-    const int wq = w & 3;
-    const uint32_t base = __builtin_amdgcn_readfirstlane(slot_base + (uint32_t)(wq * 64 * 16) + (w >= 4 ? 16384u : 0u));
-    const uint8_t* src0 = w >= 4 ? gB : gA;
-#pragma unroll
-    for (int it = 0; it < 4; ++it) {
-        const int g = it * 256 + wq * 64 + lane;
+    for (int it = 0; it < 4; ++it) {  // the query tile is re-read by every CU: default policy (L2)
+        const int g = it * 256 + w * 64 + lane;
         const int row = g >> 2, pos = g & 3;
         const int src = (row << 2) + (pos ^ mf_swz(row));
-        if (NT && w < 4) glds16_nt(src0 + (size_t)src * 16, base + it * 256 * 16);
-        else glds16(src0 + (size_t)src * 16, base + it * 256 * 16);
+        glds16(gB + (size_t)src * 16, base + it * 256 * 16 + 16384);
     }
 }
 
-// piece g (0..3) of a stage for loader waves: 1 corpus + 1 query LDS-DMA instruction
-template <bool NT = false>
-__device__ __forceinline__ void mf_stage_piece(const uint8_t* __restrict__ gA, const uint8_t* __restrict__ gB,
-                                               uint32_t base, int g4, int w, int lane) {
-    const int g = g4 * 256 + w * 64 + lane;
-    const int row = g >> 2, pos = g & 3;
-    const int src = (row << 2) + (pos ^ mf_swz(row));
-    if constexpr (NT) glds16_nt(gA + (size_t)src * 16, base + g4 * 256 * 16);
-    else glds16(gA + (size_t)src * 16, base + g4 * 256 * 16);
-    glds16(gB + (size_t)src * 16, base + g4 * 256 * 16 + 16384);
-}
-
-// wait until at most `ahead` younger stages (4 LDS-DMA each) are in flight, then barrier
-template <bool BAR, bool HALF = false>
+// wait until at most `ahead` younger stages (8 LDS-DMA each) of a loader wave are in flight, then
+// barrier; writer waves only drain their LDS traffic
 __device__ __forceinline__ void mf_wait_barrier(int ahead, bool loader) {
-    if constexpr (BAR) {
-        if (!loader && !HALF) {
-            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        } else if constexpr (HALF) {
-            if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-            else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        } else {
-            if (ahead >= 3) asm volatile("s_waitcnt vmcnt(24) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-            else if (ahead == 2) asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-            else if (ahead == 1) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        }
-    }
+    if (!loader) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if (ahead >= 3) asm volatile("s_waitcnt vmcnt(24) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if (ahead == 2) asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 __device__ __forceinline__ void mf_barrier_lgkm() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 __device__ __forceinline__ void mf_barrier_drain() {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-constexpr int DT_I8_PROBE = 7;   // ablation mode 28 only: int8 MFMA on the same fragments (results meaningless)
-constexpr int DT_I8_PROBE2 = 8;  // ablation mode 29 only: two int8 MFMAs per fragment pair (a (hi, lo) query split)
+// one 16x16 MFMA tile step; the int8 form accumulates exact int32 (its bits live in the fp32
+// accumulator registers and are converted in the epilogue)
 template <int DT>
 __device__ __forceinline__ floatx4 mfma16(const uint4 a, const uint4 b, floatx4 c) {
-    if constexpr (DT == DT_I8_PROBE2) {
-        const intx4 t = __builtin_amdgcn_mfma_i32_16x16x64_i8(__builtin_bit_cast(intx4, a), __builtin_bit_cast(intx4, b),
-                                                              __builtin_bit_cast(intx4, c), 0, 0, 0);
-        return __builtin_bit_cast(floatx4, __builtin_amdgcn_mfma_i32_16x16x64_i8(
-                                               __builtin_bit_cast(intx4, a), __builtin_bit_cast(intx4, b), t, 0, 0, 0));
-    } else if constexpr (DT == DT_I8_PROBE)
+    if constexpr (DT == DT_I8)
         return __builtin_bit_cast(floatx4, __builtin_amdgcn_mfma_i32_16x16x64_i8(
                                                __builtin_bit_cast(intx4, a), __builtin_bit_cast(intx4, b),
                                                __builtin_bit_cast(intx4, c), 0, 0, 0));
@@ -645,103 +585,27 @@ __device__ __forceinline__ floatx4 mfma16(const uint4 a, const uint4 b, floatx4 
 }
 
 // one K-step: 4 A (corpus) + 8 B (query) fragments by ds_read_b128 at ONE per-lane offset plus
-// immediates ((row >> 2) & 3 of every fragment row equals that of lane & 15), then 32 MFMAs.
-// One K-step with the next stage's LDS-DMA issue interleaved between its MFMA groups: the loader
-// waves' DMA issue then overlaps MFMA execution instead of delaying it.  sched_barrier pins the
-// order (hipcc would otherwise hoist the register-only MFMAs across the asm).
-template <int DT, bool NT>
-__device__ __forceinline__ void mf_compute_il(const uint8_t* buf, floatx4 (&acc)[4][8], int wm, int wn, int lane_off,
-                                              bool issue, const uint8_t* gA, const uint8_t* gB, uint32_t slot_base,
-                                              int w, int lane) {
+// immediates ((row >> 2) & 3 of every fragment row equals that of lane & 15), then 32 MFMAs
+template <int DT>
+__device__ __forceinline__ void mf_compute(const uint8_t* buf, floatx4 (&acc)[4][8], int wm, int wn, int lane_off) {
     uint4 af[4], bfr[8];
     const uint8_t* pa = buf + wm * 4096 + lane_off;
     const uint8_t* pb = buf + 16384 + wn * 8192 + lane_off;
 #pragma unroll
-    for (int ni = 0; ni < 8; ++ni) bfr[ni] = *(const uint4*)(pb + ni * 1024);
-#pragma unroll
     for (int mi = 0; mi < 4; ++mi) af[mi] = *(const uint4*)(pa + mi * 1024);
-    const uint32_t base = __builtin_amdgcn_readfirstlane(slot_base + (uint32_t)(w * 64 * 16));
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi) {
-        __builtin_amdgcn_sched_barrier(0);
-        if (issue) mf_stage_piece<NT>(gA, gB, base, mi, w, lane);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int ni = 0; ni < 8; ++ni) acc[mi][ni] = mfma16<DT>(af[mi], bfr[ni], acc[mi][ni]);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-}
-
-template <int DT, bool READS>
-__device__ __forceinline__ void mf_compute(const uint8_t* buf, floatx4 (&acc)[4][8], int wm, int wn, int lane_off) {
-    uint4 af[4], bfr[8];
-    if constexpr (READS) {
-        const uint8_t* pa = buf + wm * 4096 + lane_off;
-        const uint8_t* pb = buf + 16384 + wn * 8192 + lane_off;
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi) af[mi] = *(const uint4*)(pa + mi * 1024);
-#pragma unroll
-        for (int ni = 0; ni < 8; ++ni) bfr[ni] = *(const uint4*)(pb + ni * 1024);
-    } else {
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi) af[mi] = make_uint4(lane_off + mi, 1u, 2u, 3u);
-#pragma unroll
-        for (int ni = 0; ni < 8; ++ni) bfr[ni] = make_uint4(lane_off + ni, 5u, 6u, 7u);
-    }
+    for (int ni = 0; ni < 8; ++ni) bfr[ni] = *(const uint4*)(pb + ni * 1024);
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
         for (int ni = 0; ni < 8; ++ni) acc[mi][ni] = mfma16<DT>(af[mi], bfr[ni], acc[mi][ni]);
 }
 
-// fragment reads and MFMA groups as separate pieces (for the ping-pong schedule)
-__device__ __forceinline__ void mf_read(const uint8_t* buf, uint4 (&af)[4], uint4 (&bfr)[8], int wm, int wn,
-                                        int lane_off) {
-    const uint8_t* pa = buf + wm * 4096 + lane_off;
-    const uint8_t* pb = buf + 16384 + wn * 8192 + lane_off;
-#pragma unroll
-    for (int ni = 0; ni < 8; ++ni) bfr[ni] = *(const uint4*)(pb + ni * 1024);
-#pragma unroll
-    for (int mi = 0; mi < 4; ++mi) af[mi] = *(const uint4*)(pa + mi * 1024);
-}
-template <int DT, int M0, int M1>
-__device__ __forceinline__ void mf_mfma(const uint4 (&af)[4], const uint4 (&bfr)[8], floatx4 (&acc)[4][8]) {
-#pragma unroll
-    for (int mi = M0; mi < M1; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 8; ++ni) acc[mi][ni] = mfma16<DT>(af[mi], bfr[ni], acc[mi][ni]);
-}
-
-// Software-pipelined K-step (MODE 24): 32 MFMAs on the fragments of stage s already in registers
-// (ca, cb), with the ds_reads of stage s+1 interleaved: next A into na at the start, next B[ni]
-// into cb[ni] right after the MFMA group that last reads cb[ni] (ni-outer order), so only 16
-// extra VGPRs are live and the LDS read latency hides behind the MFMA pipe instead of idling it
-// after every barrier.  sched_barrier pins the order (hipcc would hoist every read to the top).
-template <int DT>
-__device__ __forceinline__ void mf_compute_sp(const uint8_t* nbuf, uint4 (&ca)[4], uint4 (&cb)[8],
-                                              floatx4 (&acc)[4][8], int wm, int wn, int lane_off) {
-    uint4 na[4];
-    const uint8_t* pa = nbuf + wm * 4096 + lane_off;
-    const uint8_t* pb = nbuf + 16384 + wn * 8192 + lane_off;
-#pragma unroll
-    for (int mi = 0; mi < 4; ++mi) na[mi] = *(const uint4*)(pa + mi * 1024);
-#pragma unroll
-    for (int ni = 0; ni < 8; ++ni) {
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi) acc[mi][ni] = mfma16<DT>(ca[mi], cb[ni], acc[mi][ni]);
-        __builtin_amdgcn_sched_barrier(0);
-        cb[ni] = *(const uint4*)(pb + ni * 1024);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int mi = 0; mi < 4; ++mi) ca[mi] = na[mi];
-}
-
-// compact one (workgroup, query) candidate buffer to its best K keys (one wave)
+// compact one (workgroup, query) candidate buffer to its best K keys (one wave); the new threshold
+// is the workgroup's drop bound for the query, published to drop[] (the refine's certificate)
 template <int E>
 __device__ __forceinline__ void mf_wave_compact(u64* __restrict__ buf, int n, int K, u64* thr_key, float* thr_f,
-                                                int lane) {
+                                                u64* drop, int lane) {
     u64 keys[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
@@ -761,51 +625,18 @@ __device__ __forceinline__ void mf_wave_compact(u64* __restrict__ buf, int n, in
     if (lane == 0) {
         *thr_key = t;
         *thr_f = key_score(t);
+        if (drop) atomicMax(drop, t);
     }
 }
 
-// MODE (profiling ablations, VS_MF_ABLATE; results of modes != 0 are meaningless):
-//   0 production | 1 no LDS-DMA stream | 2 no LDS reads + MFMAs | 3 = 1 + no top-k epilogue
-//   4 = 3 + no per-K-step barrier | 5 = 4 + no LDS reads (MFMAs on register operands)
-//   6 loads only (no math, no epilogue) | 7 = 6 without the query stream | 8 = 6 with nt corpus loads
-//   9 loads + math, no epilogue (burst DMA issue) | 10 = 9 with the DMA issue interleaved (as 0)
-//   11 = 9 with the ping-pong schedule (waves 4-7 half a K-step behind) | 12 = 11 without loads
-//   13 = 0 with compare-only epilogue (no inserts, no check) | 14 = 0 without the deferred check/pool flush
-template <int DT, int METRIC, int MODE>
+// SEED: the threshold-seed pass (one tile per workgroup, 16-row-group maxima of the keys only).
+// Keys: bf16/f16 -> the fp32 MFMA score (L2: 2 x.q - ||x||^2); int8 -> the upper bound
+// s_x t_q <c_x, c_q> + ||e_x|| ||q|| of the true inner product (the query-side error term is
+// uniform over rows and sits in the refine's margin).
+template <int DT, int METRIC, bool SEED>
 __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
-    // 21 = 0 without the query stream (stale query tile) | 22 = 0 with B fragments re-read every other
-    // K-step only | 23 = 0 with A fragments re-read every other K-step only  (energy ablations)
-    // 24 = 0 with software-pipelined fragment reads | 25 = 0 with s_setprio around the DMA issue
-    // 26 / 27 = 0 with the corpus DMA issued "sc1 nt" / "sc0 sc1 nt"  (cache-policy ablations)
-    constexpr bool XP = MODE == 21 || MODE == 22 || MODE == 23;
-    constexpr bool LOADS = (MODE != 1 && MODE < 3) || (MODE >= 6 && MODE != 12);  // (incl. seed, stamps)
-    constexpr bool MATH = (MODE != 2 && MODE < 6) || MODE == 9 || MODE == 10 || MODE == 13 || MODE == 14 ||
-                          MODE == MF_SEED_MODE || MODE == MF_STAMP_MODE || MODE == 16 || MODE == 17 || MODE == 24 ||
-                          MODE == 25 || MODE == 26 || MODE == 27 || MODE == 28 || MODE == 29 || XP;
-    constexpr bool PP = MODE == 11 || MODE == 12;  // ping-pong: waves 4-7 half a K-step behind waves 0-3
-    constexpr bool SEED = MODE == MF_SEED_MODE;  // threshold-seed pass: group maxima only
-    constexpr bool EPI = MODE < 3 || MODE == 13 || MODE == 14 || SEED || MODE == MF_STAMP_MODE || MODE == 16 ||
-                         MODE == 17 || MODE == 24 || MODE == 25 || MODE == 26 || MODE == 27 || XP;
-    constexpr bool INS = MODE != 13;   // threshold passes insert candidates
-    constexpr bool CHECK = MODE != 13 && MODE != 14;  // deferred compaction check + pool flush
-    constexpr bool BAR = MODE < 4 || MODE >= 6;  // (incl. seed, stamps)
-    constexpr bool READS = MODE < 5 || MODE == 9 || MODE == 10 || MODE == 13 || MODE == 14 || MODE == MF_SEED_MODE ||
-                           MODE == MF_STAMP_MODE || MODE == 16 || MODE == 17 || MODE == 25 || MODE == 26 || MODE == 27 ||
-                           MODE == 28 || MODE == 29 || XP;
-    constexpr bool QLOAD = MODE != 7;
-    constexpr int64_t QSTEP = MODE == 21 ? 0 : 16384;  // 21: every stage re-reads query block 0 (L1-resident)
-    constexpr bool NT = MODE == 8 || MODE == 0 || MODE >= 9;
-    constexpr bool IL = MODE == 10;  // DMA issue interleaved with the MFMAs (ablation: slower)
-    constexpr bool STAMP = MODE == MF_STAMP_MODE;  // = production + per-phase s_memtime stamps
-    constexpr bool BAL = MODE == 16;               // balanced DMA issue (4 per wave on all 8 waves)
-    constexpr bool PAIR = MODE == 17;              // one barrier per 2 K-steps (needs an even K-step count)
-    constexpr bool SP = MODE == 24;                // fragment reads of stage s+1 pipelined under stage s's MFMAs
-    constexpr int POL = MODE == 26 ? 2 : MODE == 27 ? 3 : 0;  // corpus DMA cache policy: sc1 nt / sc0 sc1 nt
-    // 28 = 9 as an int8 screen probe: rows of d int8 (half the bytes, half the K-steps), int8 MFMAs
-    // (16x16x64: twice the K per instruction) on the same LDS stages, no epilogue
-    // 29 = 28 with two int8 MFMAs per fragment pair: the MFMA work of a (hi, lo) int8 query split
-    constexpr bool I8P = MODE == 28 || MODE == 29;
-    constexpr int MDT = MODE == 29 ? DT_I8_PROBE2 : I8P ? DT_I8_PROBE : DT;
+    constexpr bool I8 = DT == DT_I8;
+    static_assert(!I8 || METRIC == METRIC_IP, "the int8 screen serves inner-product indexes");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     u64* thr_key = (u64*)(smem + MF_SLOTS * MF_SLOT);
     float* thr_f = (float*)(smem + MF_SLOTS * MF_SLOT + 256 * 8);
@@ -815,13 +646,12 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
     int* pool_q = (int*)(smem + MF_SLOTS * MF_SLOT + 256 * 16 + 16 + MF_POOL * 8);
     float* sx = (float*)(smem + MF_SLOTS * MF_SLOT + 256 * 16 + 16 + MF_POOL * 12) + (threadIdx.x >> 6) * 512 +
                 (threadIdx.x & 63) * 8;
+    float2* qfac = (float2*)(smem + MF_SLOTS * MF_SLOT + 256 * 16 + 16 + MF_POOL * 12 + MF_SX);
 
     // The LDS ring is written only by the inline-asm DMA: let the array escape into an asm with a
     // memory clobber, so the compiler must assume every later memory-clobbering asm (DMA issue,
     // barriers) may write it and can never fold the fragment reads away.
     asm volatile("; lds ring escapes: %0" ::"v"(smem) : "memory");
-    uint64_t rt_entry = 0;  // stamped build: 100 MHz wall clock at workgroup entry / exit
-    if constexpr (MODE == MF_STAMP_MODE) rt_entry = __builtin_amdgcn_s_memrealtime();
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid & 3, wn = wid >> 2;
     const int blk = blockIdx.x;
@@ -842,6 +672,7 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
         thr_key[tid] = k0;
         thr_f[tid] = !real ? INFINITY : (k0 == 0ull ? -INFINITY : key_score(k0));
         cnt[tid] = 0;
+        if constexpr (I8) qfac[tid] = real ? a.qfac[tid] : make_float2(0.0f, 0.0f);
     }
     if (tid == 0) {
         flag[0] = 0;
@@ -849,8 +680,8 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
         flag[2] = 0;
         flag[3] = 0;
     }
-    const int nks = a.dpad / CH / (I8P ? 2 : 1);
-    const int64_t tbytes = (int64_t)TR * a.dpad * (I8P ? 1 : 2);
+    const int nks = a.dpad / (I8 ? 64 : CH);  // K-steps per tile (one 16 KiB block each)
+    const int64_t tbytes = (int64_t)TR * a.dpad * (I8 ? 1 : 2);
     const int S = (t1 - t0) * nks;
     u64* cand = a.cand + (size_t)blk * MFMA_QB * a.cap;
     const int trigger = a.cap - TR;
@@ -866,153 +697,139 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
 
     // prologue: stages 0 .. DEPTH-1
     int iti = t0, iks = 0;  // (tile, k-step) of the next stage to issue
-    for (int j = 0; j < (PAIR ? 2 : SP ? MF_SLOTS : MF_DEPTH) && j < S; ++j) {
-        if constexpr (BAL)
-            mf_stage_bal<NT>(a.corpus + (int64_t)iti * tbytes + (int64_t)iks * 16384, qt + (int64_t)iks * 16384,
-                             ring + (uint32_t)(j * MF_SLOT), tid);
-        else if constexpr (LOADS)
-            mf_stage<QLOAD, NT, POL>(a.corpus + (int64_t)iti * tbytes + (int64_t)iks * 16384, qt + (int64_t)iks * QSTEP,
-                                ring + (uint32_t)(j * MF_SLOT), tid);
+    for (int j = 0; j < MF_DEPTH && j < S; ++j) {
+        mf_stage(a.corpus + (int64_t)iti * tbytes + (int64_t)iks * 16384, qt + (int64_t)iks * 16384,
+                 ring + (uint32_t)(j * MF_SLOT), tid);
         if (++iks == nks) { iks = 0; ++iti; }
     }
-    if constexpr (!BAR) mf_barrier_drain();
-    uint4 ca[4], cb[8];  // SP: fragments of the current stage, in registers
-    if constexpr (SP) {
-        if (S > 0) {  // stage 0 landed (stages 1..3 may still fly), then its fragments
-            mf_wait_barrier<true>(S - 1 < 3 ? S - 1 : 3, wid < 4);
-            const uint8_t* pa = smem + wm * 4096 + lane_off;
-            const uint8_t* pb = smem + 16384 + wn * 8192 + lane_off;
-#pragma unroll
-            for (int mi = 0; mi < 4; ++mi) ca[mi] = *(const uint4*)(pa + mi * 1024);
-#pragma unroll
-            for (int ni = 0; ni < 8; ++ni) cb[ni] = *(const uint4*)(pb + ni * 1024);
-        }
-    }
-    int pti = iti, pks = iks;  // PAIR mode: next stage to issue
     int ti = t0, ks = 0;
-    float sink = 0.0f;
     bool check_pending = false;
     // tile epilogue over the accumulators of tile `ti` (shared by the K loop and the seed tile)
     auto tile_epilogue = [&](const int ti) {
-            // ---- fused top-k epilogue: threshold filter, rare inserts ----
-            // Lane-derived indices come from an asm-opaque copy of the lane id, so the compiler
-            // cannot hoist them out of the K loop (they would pin VGPRs the MFMA loop needs).
-            if constexpr (SEED) {
-                if (a.seed_acc) {  // raw accumulators of the tile, for the main pass to reuse
-                    // per lane 512 contiguous bytes: one base address, immediate offsets
-                    floatx4* dst = (floatx4*)(a.seed_acc + ((size_t)blk * MF_THREADS + tid) * 128);
-#pragma unroll
-                    for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-                        for (int ni = 0; ni < 8; ++ni) dst[mi * 8 + ni] = acc[mi][ni];
-                }
-            }
-            int olane;
-            asm volatile("v_mov_b32 %0, %1" : "=v"(olane) : "v"(lane));
-            const int64_t rowbase = (int64_t)ti * TR;
-            const bool full = rowbase + TR <= a.n_valid;
-            const int rid0 = wm * 64 + (olane >> 4) * 4;       // + mi*16 + r
-            const int q0 = wn * 128 + (olane & 15);             // + ni*16
-            float sq[4][4];
-            if constexpr (METRIC == METRIC_L2) {
+        // ---- fused top-k epilogue: threshold filter, rare inserts ----
+        // Lane-derived indices come from an asm-opaque copy of the lane id, so the compiler
+        // cannot hoist them out of the K loop (they would pin VGPRs the MFMA loop needs).
+        if constexpr (SEED) {
+            if (a.seed_acc) {  // raw accumulators of the tile, for the main pass to reuse
+                // per lane 512 contiguous bytes: one base address, immediate offsets
+                floatx4* dst = (floatx4*)(a.seed_acc + ((size_t)blk * MF_THREADS + tid) * 128);
 #pragma unroll
                 for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int64_t gr = rowbase + rid0 + mi * 16 + r;
-                        sq[mi][r] = gr < a.n_valid ? a.sqn[gr] : 0.0f;
-                    }
+                    for (int ni = 0; ni < 8; ++ni) dst[mi * 8 + ni] = acc[mi][ni];
             }
-            if (!full) {  // last tile of the shard: padding rows never qualify
-                // NaN, not -inf: fmaxf skips it and every `>= threshold` test fails, even against
-                // the unseeded threshold -inf (a -inf padding key would enter the candidates and
-                // be rescored exactly as 0, beating a query's all-negative real scores)
-#pragma unroll
-                for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        if (rowbase + rid0 + mi * 16 + r >= a.n_valid)
-#pragma unroll
-                            for (int ni = 0; ni < 8; ++ni) acc[mi][ni][r] = __builtin_nanf("");
-            }
-#pragma unroll
-            for (int ni = 0; ni < 8; ++ni) {
-                const int q = q0 + ni * 16;
-                float v[4][4];
-                float mx = -INFINITY;
-#pragma unroll
-                for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        float sc = acc[mi][ni][r];
-                        if constexpr (METRIC == METRIC_L2) sc = 2.0f * sc - sq[mi][r];
-                        v[mi][r] = sc;
-                        mx = fmaxf(mx, sc);
-                    }
-                // one compare per query column; the insert path runs only where something passes,
-                // and then costs one LDS atomic per lane plus predicated stores
-                if constexpr (SEED) {  // group g = wm*4 + lane/16 of the tile: 16 distinct rows
-                    a.seedmax[(size_t)q * (a.G * 16) + blk * 16 + wm * 4 + (olane >> 4)] = mx;
-                    continue;
-                }
-                const float tf = thr_f[q];
-                if constexpr (!INS) {
-                    sink += mx >= tf ? 1.0f : 0.0f;
-                    continue;
-                }
-                if (mx >= tf) {
-                    const u64 tk = thr_key[q];
-                    uint32_t m = 0;
-#pragma unroll
-                    for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            m |= (v[mi][r] >= tf ? 1u : 0u) << (mi * 4 + r);  // exact ties resolved below
-                        }
-                    if (m) flag[2 + (ti & 1)] = 1;
-                    if (a.dbg) {
-                        atomicAdd(&a.dbg[0], (unsigned)__popc(m));
-                        if (lane == __builtin_amdgcn_readfirstlane(lane)) atomicAdd(&a.dbg[1], 1u);
-                    }
-                    // Compact insert loop (not unrolled: an unrolled insert path for 8 columns x 16
-                    // values costs more in instruction fetch than the rare inserts themselves).  The
-                    // lane's values go through its LDS staging row, 8 at a time, so the loop can
-                    // index them.  Loader waves park keys in the LDS pool; writer waves store them to
-                    // the global candidate buffer.  (A younger VMEM op in a loader wave -- a pool
-                    // overflow store -- only makes its counted ring waits stricter, never looser.)
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        uint32_t mh = (m >> (8 * h)) & 0xFFu;
-                        if (!mh) continue;
-                        *(float4*)(sx) = make_float4(v[2 * h][0], v[2 * h][1], v[2 * h][2], v[2 * h][3]);
-                        *(float4*)(sx + 4) = make_float4(v[2 * h + 1][0], v[2 * h + 1][1], v[2 * h + 1][2],
-                                                         v[2 * h + 1][3]);
-                        while (mh) {
-                            const int j = __builtin_ctz(mh);
-                            mh &= mh - 1u;
-                            const int bit = 8 * h + j;
-                            const u64 key = mk_key(sx[j], (uint32_t)(rowbase + rid0 + (bit >> 2) * 16 + (bit & 3)));
-                            if (key <= tk) continue;  // score == threshold and not ahead of it by id
-                            if (wid < 4) {
-                                const int slot = atomicAdd(&flag[1], 1);
-                                if (slot < MF_POOL) {
-                                    pool_key[slot] = key;
-                                    pool_q[slot] = q;
-                                    continue;
-                                }
-                                if (a.dbg) atomicAdd(&a.dbg[3], 1u);
-                            }
-                            const int slot = atomicAdd(&cnt[q], 1);
-                            if (slot < a.cap) cand[(size_t)q * a.cap + slot] = key;
-                        }
-                    }
-                }
-            }
+        }
+        int olane;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(olane) : "v"(lane));
+        const int64_t rowbase = (int64_t)ti * TR;
+        const int rid0 = wm * 64 + (olane >> 4) * 4;  // + mi*16 + r
+        const int q0 = wn * 128 + (olane & 15);        // + ni*16
+        // padding rows of the shard's last tile never qualify: NaN, not -inf (fmaxf skips it and
+        // every `>= threshold` test fails, even against the unseeded threshold -inf; a -inf key
+        // would enter the candidates and be rescored exactly as 0, beating all-negative scores)
+        uint32_t bad = 0;
+        if (rowbase + TR > a.n_valid) {
 #pragma unroll
             for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-                for (int ni = 0; ni < 8; ++ni) acc[mi][ni] = floatx4{0.f, 0.f, 0.f, 0.f};
-            check_pending = CHECK && !SEED;
+                for (int r = 0; r < 4; ++r)
+                    if (rowbase + rid0 + mi * 16 + r >= a.n_valid) bad |= 1u << (mi * 4 + r);
+        }
+        float sq[4][4], rb[4][4];  // L2: ||x||^2; int8: the row's scale and error norm
+        if constexpr (METRIC == METRIC_L2 || I8) {
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int64_t gr = rowbase + rid0 + mi * 16 + r;
+                    const bool ok = gr < a.n_valid;
+                    if constexpr (I8) {
+                        sq[mi][r] = ok ? a.rscale[gr] : 0.0f;
+                        rb[mi][r] = ok ? a.rbeta[gr] : 0.0f;
+                    } else {
+                        sq[mi][r] = ok ? a.sqn[gr] : 0.0f;
+                    }
+                }
+        }
+#pragma unroll
+        for (int ni = 0; ni < 8; ++ni) {
+            const int q = q0 + ni * 16;
+            float tq = 0.0f, qn = 0.0f;
+            if constexpr (I8) {
+                const float2 f = qfac[q];
+                tq = f.x;
+                qn = f.y;
+            }
+            float v[4][4];
+            float mx = -INFINITY;
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float sc;
+                    if constexpr (I8) {
+                        sc = fmaf(rb[mi][r], qn, (float)__float_as_int(acc[mi][ni][r]) * (sq[mi][r] * tq));
+                    } else {
+                        sc = acc[mi][ni][r];
+                        if constexpr (METRIC == METRIC_L2) sc = 2.0f * sc - sq[mi][r];
+                    }
+                    if (bad & (1u << (mi * 4 + r))) sc = __builtin_nanf("");
+                    v[mi][r] = sc;
+                    mx = fmaxf(mx, sc);
+                }
+            // one compare per query column; the insert path runs only where something passes,
+            // and then costs one LDS atomic per lane plus predicated stores
+            if constexpr (SEED) {  // group g = wm*4 + lane/16 of the tile: 16 distinct rows
+                a.seedmax[(size_t)q * (a.G * 16) + blk * 16 + wm * 4 + (olane >> 4)] = mx;
+                continue;
+            }
+            const float tf = thr_f[q];
+            if (mx >= tf) {
+                const u64 tk = thr_key[q];
+                uint32_t m = 0;
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) m |= (v[mi][r] >= tf ? 1u : 0u) << (mi * 4 + r);  // ties below
+                if (m) flag[2 + (ti & 1)] = 1;
+                // Compact insert loop (not unrolled: an unrolled insert path for 8 columns x 16
+                // values costs more in instruction fetch than the rare inserts themselves).  The
+                // lane's values go through its LDS staging row, 8 at a time, so the loop can
+                // index them.  Loader waves park keys in the LDS pool; writer waves store them to
+                // the global candidate buffer.  (A younger VMEM op in a loader wave -- a pool
+                // overflow store -- only makes its counted ring waits stricter, never looser.)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    uint32_t mh = (m >> (8 * h)) & 0xFFu;
+                    if (!mh) continue;
+                    *(float4*)(sx) = make_float4(v[2 * h][0], v[2 * h][1], v[2 * h][2], v[2 * h][3]);
+                    *(float4*)(sx + 4) = make_float4(v[2 * h + 1][0], v[2 * h + 1][1], v[2 * h + 1][2],
+                                                     v[2 * h + 1][3]);
+                    while (mh) {
+                        const int j = __builtin_ctz(mh);
+                        mh &= mh - 1u;
+                        const int bit = 8 * h + j;
+                        const u64 key = mk_key(sx[j], (uint32_t)(rowbase + rid0 + (bit >> 2) * 16 + (bit & 3)));
+                        if (key <= tk) continue;  // score == threshold and not ahead of it by id
+                        if (wid < 4) {
+                            const int slot = atomicAdd(&flag[1], 1);
+                            if (slot < MF_POOL) {
+                                pool_key[slot] = key;
+                                pool_q[slot] = q;
+                                continue;
+                            }
+                        }
+                        const int slot = atomicAdd(&cnt[q], 1);
+                        if (slot < a.cap) cand[(size_t)q * a.cap + slot] = key;
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 8; ++ni) acc[mi][ni] = floatx4{0.f, 0.f, 0.f, 0.f};
+        check_pending = !SEED;
     };
     if (reuse) {
         // the seed pass screened this workgroup's first tile (tseed) and left its raw accumulators:
@@ -1024,115 +841,17 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
             for (int ni = 0; ni < 8; ++ni) acc[mi][ni] = src[mi * 8 + ni];
         tile_epilogue(tseed);
     }
-    uint4 pf_a[4], pf_b[8];
-    // stamps: barrier, DMA issue, reads+MFMA, tail of tile-end steps, total, tail of other steps
-    uint64_t ph[6] = {0, 0, 0, 0, 0, 0}, tl = 0;
-    bool tile_end = false;
-    if constexpr (STAMP) tl = __builtin_amdgcn_s_memtime();
     for (int s = 0; s < S; ++s) {
         const int left = S - 1 - s;
-        uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
-        if constexpr (STAMP) {
-            __builtin_amdgcn_sched_barrier(0);
-            t0 = __builtin_amdgcn_s_memtime();
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        if constexpr (PAIR) {
-            if ((s & 1) == 0) mf_barrier_drain();  // this pair's two stages landed, previous pair read
-        } else if constexpr (SP) {
-            // stage s+1 landed (its fragments are read during this step); stage s's fragments are in
-            // registers (lgkmcnt(0)), so slot s % 4 is free for stage s+4
-            const int last = S - 1 < s + 3 ? S - 1 : s + 3;  // youngest stage issued so far
-            const int ahead = last - (s + 1);
-            mf_wait_barrier<true>(ahead > 0 ? ahead : 0, wid < 4);
-        } else {
-            mf_wait_barrier<BAR, !QLOAD || BAL>(left < MF_DEPTH - 1 ? left : MF_DEPTH - 1, wid < 4 || BAL);
-        }
-        if constexpr (STAMP) {
-            __builtin_amdgcn_sched_barrier(0);
-            t1 = __builtin_amdgcn_s_memtime();
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        constexpr int AHEAD = SP ? MF_SLOTS : MF_DEPTH;  // stage issued at step s: s + AHEAD
-        const bool do_issue = s + AHEAD < S;
-        const uint8_t* nA = a.corpus + (int64_t)iti * tbytes + (int64_t)iks * 16384;
-        const uint8_t* nB = qt + (int64_t)iks * QSTEP;
-        const uint32_t nslot = ring + (uint32_t)(((s + AHEAD) % MF_SLOTS) * MF_SLOT);
+        mf_wait_barrier(left < MF_DEPTH - 1 ? left : MF_DEPTH - 1, wid < 4);
+        const bool do_issue = s + MF_DEPTH < S;  // stage issued at step s: s + DEPTH
         if (do_issue) {
+            mf_stage(a.corpus + (int64_t)iti * tbytes + (int64_t)iks * 16384, qt + (int64_t)iks * 16384,
+                     ring + (uint32_t)(((s + MF_DEPTH) % MF_SLOTS) * MF_SLOT), tid);
             if (++iks == nks) { iks = 0; ++iti; }
         }
-        if constexpr (PP) {
-            if (wid < 4) {
-                if constexpr (LOADS) if (do_issue) mf_stage<true, NT>(nA, nB, nslot, tid);
-                mf_read(smem + (s % MF_SLOTS) * MF_SLOT, pf_a, pf_b, wm, wn, lane_off);
-                mf_mfma<DT, 0, 4>(pf_a, pf_b, acc);
-            } else {
-                if (s > 0) mf_mfma<DT, 2, 4>(pf_a, pf_b, acc);
-                __builtin_amdgcn_sched_barrier(0);
-                mf_read(smem + (s % MF_SLOTS) * MF_SLOT, pf_a, pf_b, wm, wn, lane_off);
-                mf_mfma<DT, 0, 2>(pf_a, pf_b, acc);
-            }
-        } else if constexpr (IL) {
-            mf_compute_il<DT, NT>(smem + (s % MF_SLOTS) * MF_SLOT, acc, wm, wn, lane_off, do_issue && wid < 4, nA, nB,
-                                  nslot, wid, lane);
-        } else if constexpr (SP) {
-            if (do_issue && wid < 4) mf_stage<true, NT>(nA, nB, nslot, tid);
-            mf_compute_sp<DT>(smem + ((s + 1) % MF_SLOTS) * MF_SLOT, ca, cb, acc, wm, wn, lane_off);
-        } else if constexpr (PAIR) {
-            if ((s & 1) == 0) {  // the next pair's two stages, into the slots the previous pair used
-#pragma unroll
-                for (int h = 0; h < 2; ++h)
-                    if (s + 2 + h < S) {
-                        mf_stage<true, NT>(a.corpus + (int64_t)pti * tbytes + (int64_t)pks * 16384,
-                                           qt + (int64_t)pks * 16384,
-                                           ring + (uint32_t)(((s + 2 + h) % MF_SLOTS) * MF_SLOT), tid);
-                        if (++pks == nks) { pks = 0; ++pti; }
-                    }
-            }
-            mf_compute<DT, true>(smem + (s % MF_SLOTS) * MF_SLOT, acc, wm, wn, lane_off);
-        } else {
-            if (do_issue) {
-                if constexpr (MODE == 25) __builtin_amdgcn_s_setprio(3);  // loader DMA issue ahead of MFMAs
-                if constexpr (BAL) mf_stage_bal<NT>(nA, nB, nslot, tid);
-                else if constexpr (LOADS) mf_stage<QLOAD, NT, POL>(nA, nB, nslot, tid);
-                if constexpr (MODE == 25) __builtin_amdgcn_s_setprio(0);
-            }
-            if constexpr (STAMP) {
-                __builtin_amdgcn_sched_barrier(0);
-                t2 = __builtin_amdgcn_s_memtime();
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            if constexpr (MODE == 22 || MODE == 23) {
-                const uint8_t* buf = smem + (s % MF_SLOTS) * MF_SLOT;
-                if (MODE == 23 || (s & 1) == 0)
-#pragma unroll
-                    for (int ni = 0; ni < 8; ++ni)
-                        pf_b[ni] = *(const uint4*)(buf + 16384 + wn * 8192 + lane_off + ni * 1024);
-                if (MODE == 22 || (s & 1) == 0)
-#pragma unroll
-                    for (int mi = 0; mi < 4; ++mi) pf_a[mi] = *(const uint4*)(buf + wm * 4096 + lane_off + mi * 1024);
-                mf_mfma<DT, 0, 4>(pf_a, pf_b, acc);
-            } else if constexpr (MATH) mf_compute<MDT, READS>(smem + (s % MF_SLOTS) * MF_SLOT, acc, wm, wn, lane_off);
-            if constexpr (STAMP) {
-                __builtin_amdgcn_sched_barrier(0);
-                t3 = __builtin_amdgcn_s_memtime();
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        }
-        if constexpr (STAMP) tile_end = ks == nks - 1;
-        if (ks == nks - 1) {
-            if constexpr (!EPI) {
-#pragma unroll
-                for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-                    for (int ni = 0; ni < 8; ++ni) {
-                        sink += acc[mi][ni][0] + acc[mi][ni][3];
-                        acc[mi][ni] = floatx4{0.f, 0.f, 0.f, 0.f};
-                    }
-            } else {
-                tile_epilogue(ti);
-            }
-        }
+        mf_compute<DT>(smem + (s % MF_SLOTS) * MF_SLOT, acc, wm, wn, lane_off);
+        if (ks == nks - 1) tile_epilogue(ti);
         // Deferred compaction check, after the NEXT K-step's barrier: by then every wave's
         // insert atomics of the finished tile are complete, and every wave reads all 256 LDS
         // counters, so the (rare) decision to compact is uniform without extra barriers.
@@ -1173,42 +892,17 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
                     const int n = cnt[q];
                     if (n > trigger) {
                         mf_wave_compact<MFMA_CAP / 64>(cand + (size_t)q * a.cap, n < a.cap ? n : a.cap, a.Kp,
-                                                       &thr_key[q], &thr_f[q], lane);
+                                                       &thr_key[q], &thr_f[q], a.drop ? a.drop + q : nullptr, lane);
                         if (lane == 0) cnt[q] = a.Kp;
-                        if (a.dbg && lane == 0) atomicAdd(&a.dbg[2], 1u);
                     }
                 }
                 mf_barrier_drain();  // counters / thresholds / compacted buffers published
             }
         }
         if (++ks == nks) { ks = 0; ++ti; }
-        if constexpr (STAMP) {
-            __builtin_amdgcn_sched_barrier(0);
-            const uint64_t t4 = __builtin_amdgcn_s_memtime();
-            __builtin_amdgcn_sched_barrier(0);
-            ph[0] += t1 - t0;
-            ph[1] += t2 - t1;
-            ph[2] += t3 - t2;
-            ph[tile_end ? 3 : 5] += t4 - t3;
-        }
-    }
-    if constexpr (STAMP) {
-        ph[4] = __builtin_amdgcn_s_memtime() - tl;
-        if (lane == 0 && a.stamps)
-            for (int i = 0; i < 6; ++i) a.stamps[((size_t)blk * 8 + wid) * 6 + i] = ph[i];
-    }
-    if constexpr (PP) {
-        if (wid >= 4 && S > 0) mf_mfma<DT, 2, 4>(pf_a, pf_b, acc);
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-            for (int ni = 0; ni < 8; ++ni) sink += acc[mi][ni][0] + acc[mi][ni][3];
-    }
-    if constexpr (!EPI || !INS) {
-        if (sink == 12345.678f) cnt[0] = 1;  // keep the ablated MFMAs alive
     }
     if constexpr (SEED) return;  // no candidates (no DMA is in flight after the last K-step)
-    // ---- flush: pool -> buffers, then best Kp per query -> part[blk][q][Kp] ----
+    // ---- flush: pool -> buffers, then the best <= Kp per query -> the query's survivor list ----
     mf_barrier_drain();
     {
         int np = flag[1];
@@ -1228,7 +922,8 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
         int n = cnt[q];
         if (n > a.cap) n = a.cap;
         if (n > a.Kp) {
-            mf_wave_compact<MFMA_CAP / 64>(cand + (size_t)q * a.cap, n, a.Kp, &thr_key[q], &thr_f[q], lane);
+            mf_wave_compact<MFMA_CAP / 64>(cand + (size_t)q * a.cap, n, a.Kp, &thr_key[q], &thr_f[q],
+                                           a.drop ? a.drop + q : nullptr, lane);
             n = a.Kp;
         }
         if (n == 0) continue;
@@ -1237,13 +932,6 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
         off = __shfl(off, 0, 64);
         u64* dst = a.glist + (size_t)q * a.lcap + off;
         for (int j = lane; j < n; j += 64) dst[j] = cand[(size_t)q * a.cap + j];
-    }
-    if constexpr (STAMP) {
-        __syncthreads();
-        if (tid == 0 && a.stamps) {
-            a.stamps[(size_t)a.G * 48 + blk * 2] = rt_entry;
-            a.stamps[(size_t)a.G * 48 + blk * 2 + 1] = __builtin_amdgcn_s_memrealtime();
-        }
     }
 }
 
@@ -1875,7 +1563,6 @@ __global__ void __launch_bounds__(RF_THREADS) k_refine(RefineArgs a, int KP2) {
     // reads element e of its 8-element group, so a wave's reads are contiguous (conflict-free)
     const int ng = (a.d + 7) >> 3;
     u64* cq = (u64*)(smem + (((size_t)KP2 * 12 + 7) & ~(size_t)7) + (QLDS ? (size_t)ng * 64 : 0));
-    if (a.stamps && tid == 0) a.stamps[(size_t)q * 6 + 5] = __builtin_amdgcn_s_memtime();
     const u64* src = a.cand + (size_t)q * a.lcap;
     const int n = a.cand_n ? min(a.cand_n[q], a.lcap) : a.lcap;
     const float* qv = a.q + (int64_t)q * a.d;
@@ -1885,11 +1572,6 @@ __global__ void __launch_bounds__(RF_THREADS) k_refine(RefineArgs a, int KP2) {
     }
     if constexpr (QLDS)
         for (int i = tid; i < a.d; i += RF_THREADS) qs[(i & 7) * ng + (i >> 3)] = (double)qv[i];
-    if (a.stamps && tid == 0) {
-        __builtin_amdgcn_sched_barrier(0);
-        a.stamps[(size_t)q * 6 + 0] = __builtin_amdgcn_s_memtime();
-        __builtin_amdgcn_sched_barrier(0);
-    }
     int nkept;
     if (n <= RF_THREADS * RF_E) {
         u64 keys[RF_E];
@@ -1947,11 +1629,6 @@ __global__ void __launch_bounds__(RF_THREADS) k_refine(RefineArgs a, int KP2) {
         if (lane == 0) qq_s = s2;
     }
     __syncthreads();
-    if (a.stamps && tid == 0) {
-        __builtin_amdgcn_sched_barrier(0);
-        a.stamps[(size_t)q * 6 + 1] = __builtin_amdgcn_s_memtime();
-        __builtin_amdgcn_sched_barrier(0);
-    }
     const int nv = nv_s;
     for (int j = wid; j < nv; j += 2 * NW) {
         const int j2 = j + NW;
@@ -1974,11 +1651,6 @@ __global__ void __launch_bounds__(RF_THREADS) k_refine(RefineArgs a, int KP2) {
         ids[j] = 0xFFFFFFFFu;
     }
     __syncthreads();
-    if (a.stamps && tid == 0) {
-        __builtin_amdgcn_sched_barrier(0);
-        a.stamps[(size_t)q * 6 + 2] = __builtin_amdgcn_s_memtime();
-        __builtin_amdgcn_sched_barrier(0);
-    }
     // bitonic sort, best first
     for (int size = 2; size <= KP2; size <<= 1) {
         for (int stride = size >> 1; stride > 0; stride >>= 1) {
@@ -1997,11 +1669,6 @@ __global__ void __launch_bounds__(RF_THREADS) k_refine(RefineArgs a, int KP2) {
             }
             __syncthreads();
         }
-    }
-    if (a.stamps && tid == 0) {
-        __builtin_amdgcn_sched_barrier(0);
-        a.stamps[(size_t)q * 6 + 3] = __builtin_amdgcn_s_memtime();
-        __builtin_amdgcn_sched_barrier(0);
     }
     // exactness certificate: every non-candidate row has exact transformed score <= smin + eps
     if (tid == 0) {
@@ -2265,64 +1932,34 @@ hipError_t launch_pack_qf32(const float* q, int nqb, int nqpad, int d, int dpad,
     return hipGetLastError();
 }
 
-template <int DT, int METRIC, int MODE>
+template <int DT, int METRIC, bool SEED>
 static void launch_mfma_one(const ScreenArgs& a, const uint8_t* qt, int nqb, hipStream_t st) {
     static bool attr_set = false;  // benign race: idempotent attribute
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)k_screen_mfma<DT, METRIC, MODE>,
+        (void)hipFuncSetAttribute((const void*)k_screen_mfma<DT, METRIC, SEED>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, MF_LDS);
         attr_set = true;
     }
-    hipLaunchKernelGGL((k_screen_mfma<DT, METRIC, MODE>), dim3(a.G), dim3(MF_THREADS), MF_LDS, st, a, qt, nqb);
+    hipLaunchKernelGGL((k_screen_mfma<DT, METRIC, SEED>), dim3(a.G), dim3(MF_THREADS), MF_LDS, st, a, qt, nqb);
 }
-template <int DT, int METRIC>
-static void launch_mfma_mode(const ScreenArgs& a, const uint8_t* qt, int nqb, hipStream_t st) {
-    static const int mode = [] {
-        if (getenv("VS_MF_STAMPS")) return MF_STAMP_MODE;
-        const char* e = getenv("VS_MF_ABLATE");
-        return e ? atoi(e) : 0;
-    }();
-    switch (mode) {
-        case MF_STAMP_MODE: launch_mfma_one<DT, METRIC, MF_STAMP_MODE>(a, qt, nqb, st); break;
-#ifdef VS_MF_ABLATIONS  // diagnostic builds only (python -m photo_search_engine_amd.build with VS_ABLATIONS=1)
-        case 1: launch_mfma_one<DT, METRIC, 1>(a, qt, nqb, st); break;
-        case 2: launch_mfma_one<DT, METRIC, 2>(a, qt, nqb, st); break;
-        case 3: launch_mfma_one<DT, METRIC, 3>(a, qt, nqb, st); break;
-        case 4: launch_mfma_one<DT, METRIC, 4>(a, qt, nqb, st); break;
-        case 5: launch_mfma_one<DT, METRIC, 5>(a, qt, nqb, st); break;
-        case 6: launch_mfma_one<DT, METRIC, 6>(a, qt, nqb, st); break;
-        case 7: launch_mfma_one<DT, METRIC, 7>(a, qt, nqb, st); break;
-        case 8: launch_mfma_one<DT, METRIC, 8>(a, qt, nqb, st); break;
-        case 9: launch_mfma_one<DT, METRIC, 9>(a, qt, nqb, st); break;
-        case 10: launch_mfma_one<DT, METRIC, 10>(a, qt, nqb, st); break;
-        case 11: launch_mfma_one<DT, METRIC, 11>(a, qt, nqb, st); break;
-        case 12: launch_mfma_one<DT, METRIC, 12>(a, qt, nqb, st); break;
-        case 13: launch_mfma_one<DT, METRIC, 13>(a, qt, nqb, st); break;
-        case 14: launch_mfma_one<DT, METRIC, 14>(a, qt, nqb, st); break;
-        case 16: launch_mfma_one<DT, METRIC, 16>(a, qt, nqb, st); break;
-        case 17: launch_mfma_one<DT, METRIC, 17>(a, qt, nqb, st); break;
-        case 21: launch_mfma_one<DT, METRIC, 21>(a, qt, nqb, st); break;
-        case 22: launch_mfma_one<DT, METRIC, 22>(a, qt, nqb, st); break;
-        case 23: launch_mfma_one<DT, METRIC, 23>(a, qt, nqb, st); break;
-        case 24: launch_mfma_one<DT, METRIC, 24>(a, qt, nqb, st); break;
-        case 25: launch_mfma_one<DT, METRIC, 25>(a, qt, nqb, st); break;
-        case 26: launch_mfma_one<DT, METRIC, 26>(a, qt, nqb, st); break;
-        case 27: launch_mfma_one<DT, METRIC, 27>(a, qt, nqb, st); break;
-        case 28: launch_mfma_one<DT, METRIC, 28>(a, qt, nqb, st); break;
-        case 29: launch_mfma_one<DT, METRIC, 29>(a, qt, nqb, st); break;
-#endif
-        default: launch_mfma_one<DT, METRIC, 0>(a, qt, nqb, st); break;
-    }
-}
-hipError_t launch_screen_mfma(int dt, const ScreenArgs& a, const uint8_t* qt, int nqb, hipStream_t st) {
-    if (dt == DT_BF16) {
-        if (a.metric == METRIC_IP) launch_mfma_mode<DT_BF16, METRIC_IP>(a, qt, nqb, st);
-        else launch_mfma_mode<DT_BF16, METRIC_L2>(a, qt, nqb, st);
+template <bool SEED>
+static hipError_t launch_mfma_dt(int dt, const ScreenArgs& a, const uint8_t* qt, int nqb, hipStream_t st) {
+    if (dt == DT_I8) {
+        if (a.metric != METRIC_IP || !a.rscale || !a.rbeta || !a.qfac) return hipErrorInvalidValue;
+        launch_mfma_one<DT_I8, METRIC_IP, SEED>(a, qt, nqb, st);
+    } else if (dt == DT_BF16) {
+        if (a.metric == METRIC_IP) launch_mfma_one<DT_BF16, METRIC_IP, SEED>(a, qt, nqb, st);
+        else launch_mfma_one<DT_BF16, METRIC_L2, SEED>(a, qt, nqb, st);
+    } else if (dt == DT_F16) {
+        if (a.metric == METRIC_IP) launch_mfma_one<DT_F16, METRIC_IP, SEED>(a, qt, nqb, st);
+        else launch_mfma_one<DT_F16, METRIC_L2, SEED>(a, qt, nqb, st);
     } else {
-        if (a.metric == METRIC_IP) launch_mfma_mode<DT_F16, METRIC_IP>(a, qt, nqb, st);
-        else launch_mfma_mode<DT_F16, METRIC_L2>(a, qt, nqb, st);
+        return hipErrorInvalidValue;
     }
     return hipGetLastError();
+}
+hipError_t launch_screen_mfma(int dt, const ScreenArgs& a, const uint8_t* qt, int nqb, hipStream_t st) {
+    return launch_mfma_dt<false>(dt, a, qt, nqb, st);
 }
 
 template <int DT>
@@ -2408,16 +2045,7 @@ hipError_t launch_refine(const RefineArgs& a, int nq, hipStream_t st) {
 
 hipError_t launch_seed_mfma(int dt, const ScreenArgs& a, const uint8_t* qt, int nqb, hipStream_t st) {
     if (nqb > MFMA_QB || a.tile_stride <= 0 || !a.seedmax) return hipErrorInvalidValue;
-    if (dt == DT_BF16) {
-        if (a.metric == METRIC_IP) launch_mfma_one<DT_BF16, METRIC_IP, MF_SEED_MODE>(a, qt, nqb, st);
-        else launch_mfma_one<DT_BF16, METRIC_L2, MF_SEED_MODE>(a, qt, nqb, st);
-    } else if (dt == DT_F16) {
-        if (a.metric == METRIC_IP) launch_mfma_one<DT_F16, METRIC_IP, MF_SEED_MODE>(a, qt, nqb, st);
-        else launch_mfma_one<DT_F16, METRIC_L2, MF_SEED_MODE>(a, qt, nqb, st);
-    } else {
-        return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
+    return launch_mfma_dt<true>(dt, a, qt, nqb, st);
 }
 
 hipError_t launch_seed_select(const float* seedmax, int M, int nq, int rank, u64* thr0, hipStream_t st) {

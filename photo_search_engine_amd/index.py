@@ -126,6 +126,10 @@ class FlatIndex:
     def uncertified_count(self) -> int:
         return int(check(self._L.vs_uncertified_count(self._h)))
 
+    def host_staging_bytes(self) -> int:
+        """Pinned host bytes held for ``search``'s query / result staging (bounded per context)."""
+        return int(check(self._L.vs_host_staging_bytes(self._h)))
+
     # -- lifecycle ----------------------------------------------------------------------------
     def close(self) -> None:
         if self._h is not None and self._h.value:

@@ -123,8 +123,11 @@ class VectorStore:
     def _normalize_query(self, vector) -> np.ndarray:
         """``np.array([_normalize_vector(vector)], dtype="float32")`` without the Python-list round trip
         (~0.19 ms of a 0.5 ms call at d=4096): fp32 -> Python float -> fp32 is exact, so the bits
-        are the same."""
+        are the same.  Anything but a flat vector takes the reference's own expression (whose
+        extra axes the index then rejects, as faiss does)."""
         array = np.array(vector, dtype="float32")
+        if array.ndim != 1:
+            return np.array([self._normalize_vector(vector)], dtype="float32")
         if self._normalize:
             norm = np.linalg.norm(array)
             if norm != 0:

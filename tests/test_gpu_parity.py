@@ -328,13 +328,35 @@ def test_sharded_index_single_process_matches_oracle():
     sh.close()
 
 
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16"])
 @pytest.mark.parametrize("metric", ["ip", "l2"])
 @pytest.mark.parametrize("N,k", [(20, 16), (5000, 10), (70_000, 1), (70_000, 100), (300_000, 10), (300_000, 400)])
-def test_single_query_merge_stop_exact(FlatIndex, metric, N, k):
+def test_single_query_merge_stop_exact(FlatIndex, metric, N, k, dtype):
     # one query: the GEMV path stops its merge tree once <= 2048 keys remain and the refine selects
-    # the best Kp from them (shards of >= Kp rows), else merges to one list; both must be exact
-    ix = FlatIndex(48, metric, "f32")
+    # the best Kp from them (shards of >= Kp rows), else merges to one list; both must be exact,
+    # for every storage dtype (single queries always take the GEMV path)
+    ix = FlatIndex(48, metric, dtype)
     ix.add_synthetic(O.SEED_CORPUS, 0, N, True)
     for i in range(3):
         q = O.synth_rows(O.SEED_QUERIES, 100 + i, 1, 48, True, "f32")
         _check_exact(ix, q, k, metric)
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_single_query_device_api_s64(FlatIndex, dtype):
+    # the sharded layer's call: one query through vs_search_device with id offset and fp64 outputs
+    import torch
+    N, d, k = 300_000, 48, 37
+    ix = FlatIndex(d, "ip", dtype)
+    ix.add_synthetic(O.SEED_CORPUS, 0, N, True)
+    q = O.synth_rows(O.SEED_QUERIES, 7, 1, d, True, "f32")
+    qd = torch.from_numpy(q).cuda()
+    I = torch.empty((1, k), dtype=torch.int64, device="cuda")
+    S = torch.empty((1, k), dtype=torch.float64, device="cuda")
+    D = torch.empty((1, k), dtype=torch.float32, device="cuda")
+    ix.search_device(qd.data_ptr(), 1, k, D.data_ptr(), I.data_ptr(), S.data_ptr(), 11, 0)
+    torch.cuda.synchronize()
+    Se, Ie = O.knn_exact(ix.reconstruct_n(0, N), q, k, "ip")
+    np.testing.assert_array_equal(I.cpu().numpy(), Ie + 11)
+    np.testing.assert_array_equal(S.cpu().numpy(), Se)
+    np.testing.assert_array_equal(D.cpu().numpy(), Se.astype(np.float32))

@@ -198,3 +198,50 @@ def test_write_rows_to_file_errors(tmp_path):
     assert len(raw) == 16 + 3 * 32
     np.testing.assert_array_equal(np.frombuffer(raw[16:], dtype="<f4").reshape(3, 8), np.eye(8, dtype=np.float32)[2:5])
     ix.close()
+
+
+def test_host_search_stages_large_batches_in_bounded_chunks():
+    # a batch whose queries (16 MiB at d=4096) exceed the 8 MiB pinned staging cap runs in chunks:
+    # exact results, and a later small search leaves the pinned footprint bounded
+    from photo_search_engine_amd.index import FlatIndex
+    d, N = 4096, 3000
+    ix = FlatIndex(d, "ip", "bf16")
+    ix.add_synthetic(O.SEED_CORPUS, 0, N, True)
+    q = O.synth_rows(O.SEED_QUERIES, 0, 1100, d, True, "bf16")
+    D, I = ix.search(q, 12)
+    x = ix.reconstruct_n(0, N)
+    S, Ie = O.knn_exact(x, q, 12, "ip")
+    np.testing.assert_array_equal(I, Ie)
+    np.testing.assert_array_equal(D, S.astype(np.float32))
+    D1, I1 = ix.search(q[:1], 5)
+    np.testing.assert_array_equal(I1, Ie[:1, :5])
+    assert 0 < ix.host_staging_bytes() <= 2 * (8 << 20) + (1 << 20)
+    ix.close()
+
+
+def test_device_search_context_reuse_across_streams_is_ordered():
+    # a device-API search returns with its kernels queued on stream A; the next search on stream B
+    # leases the same pooled context and must not overwrite its workspace before A's kernels ran
+    import torch
+    from photo_search_engine_amd.index import FlatIndex
+    d, N, nq, k = 256, 200_000, 64, 20
+    ix = FlatIndex(d, "ip", "bf16")
+    ix.add_synthetic(O.SEED_CORPUS, 0, N, True)
+    qa = O.synth_rows(O.SEED_QUERIES, 0, nq, d, True, "bf16")
+    qb = O.synth_rows(O.SEED_QUERIES, 500, nq, d, True, "bf16")
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = []
+    for q, s in ((qa, sa), (qb, sb)):
+        with torch.cuda.stream(s):
+            qd = torch.from_numpy(q).cuda()
+            I = torch.empty((nq, k), dtype=torch.int64, device="cuda")
+            S = torch.empty((nq, k), dtype=torch.float64, device="cuda")
+            ix.search_device(qd.data_ptr(), nq, k, None, I.data_ptr(), S.data_ptr(), 0, s.cuda_stream)
+            outs.append((qd, I, S))
+    torch.cuda.synchronize()
+    x = ix.reconstruct_n(0, N)
+    for q, (_, I, S) in zip((qa, qb), outs):
+        Se, Ie = O.knn_exact(x, q, k, "ip")
+        np.testing.assert_array_equal(I.cpu().numpy(), Ie)
+        np.testing.assert_array_equal(S.cpu().numpy(), Se)
+    ix.close()

@@ -218,3 +218,29 @@ def test_query_normalisation_skips_list_round_trip_bit_identically(d):
         want = np.array([store._normalize_vector(v)], dtype="float32")
         got = store._normalize_query(v)
         assert got.shape == want.shape and got.tobytes() == want.tobytes()
+
+
+@pytest.mark.parametrize("normalize", [True, False])
+@pytest.mark.parametrize("d", [8, 1536])
+def test_query_normalisation_float64_and_l2_bit_identical(d, normalize):
+    # float64 lists / arrays and the l2 store (no normalisation) take the same fp32 bits as the
+    # reference's np.array([_normalize_vector(v)], dtype="float32")
+    store = vsmod.VectorStore.__new__(vsmod.VectorStore)
+    store._normalize = normalize
+    rng = np.random.default_rng(d + 1)
+    for s in (1e-3, 1.0, 3e2):
+        v64 = rng.standard_normal(d) * s
+        for v in (v64.tolist(), v64, v64.astype(np.float32)):
+            want = np.array([store._normalize_vector(v)], dtype="float32")
+            got = store._normalize_query(v)
+            assert got.shape == want.shape and got.tobytes() == want.tobytes()
+
+
+def test_query_with_extra_axis_is_rejected_like_the_reference():
+    # a (d, 1) array passes the reference's len() check but its np.array([...]) is 3-D, which the
+    # index rejects; it must not be silently flattened into a valid (1, d) query
+    store = vsmod.VectorStore.__new__(vsmod.VectorStore)
+    for normalize in (True, False):
+        store._normalize = normalize
+        q = store._normalize_query(np.ones((8, 1), dtype=np.float32))
+        assert q.ndim != 2 or q.shape[0] != 1
