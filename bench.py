@@ -26,7 +26,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 WORKLOADS = {
-    # name: (N, d, dtype, nq, k, description)
+    # name: (N, d, dtype, nq, k, description); stored rows are `dtype`
     "cfg3": (10_000_000, 1536, "bf16", 256, 100, "N=10M d=1536 bf16, batch=256, top-100 (MFMA path)"),
     "cfg2": (1_000_000, 1536, "f32", 1, 10, "N=1M d=1536 fp32, batch=1, top-10 (GEMV path)"),
     "cfg4": (100_000_000, 768, "f16", 256, 10, "N=100M d=768 fp16, batch=256, top-10 (row-sharded)"),
@@ -41,6 +41,13 @@ SEED_QUERIES = 20260418
 SEED_CENTROIDS = 20260419
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 MFMA_BF16_PEAK_TF = 2500.0
+MFMA_I8_PEAK_TOPS = 5000.0  # MI355X_MICROARCH.md: I8 16x16x64 runs at 2x the BF16 rate per clock
+DEFAULT_SCREEN = {"cfg3": "int8"}  # flat workloads not listed: the native screen
+METRICS = {
+    "cfg3": "kNN queries/sec + recall@10 vs FAISS, N=10M d=1536 batch=256",
+    "cfg2": "kNN queries/sec vs FAISS, N=1M d=1536 fp32 batch=1 top-10",
+    "cfg4": "kNN queries/sec vs FAISS, N=100M d=768 fp16 batch=256 top-10",
+}
 
 
 def parse():
@@ -50,6 +57,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="cfg3", choices=sorted(WORKLOADS) + sorted(IVF_WORKLOADS))
     ap.add_argument("--rows", type=int, default=0, help="override corpus rows (testing)")
+    ap.add_argument("--screen", default=None, choices=["native", "int8"],
+                    help="flat workloads: the screen of the timed steps (default: int8 for cfg3, else native); "
+                         "with int8 the native screen is timed too and reported beside it")
     ap.add_argument("--cpu-sample-rows", type=int, default=0,
                     help="rows of the corpus the CPU baseline scans (default: the whole corpus if host memory allows)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -115,49 +125,77 @@ def main():
     stream = torch.cuda.current_stream(dev)
     synthesize_device(local, SEED_QUERIES, 0, nq, d, q.data_ptr(), True, dtype, stream.cuda_stream)
     torch.cuda.synchronize()
+    screen = args.screen or DEFAULT_SCREEN.get(args.workload, "native")
     t_build = time.time() - t_build
     result = {}
 
     def step():
         result["D"], result["I"], result["S"] = sh.search(q, k)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    ix.timing_fetch()  # drop warmup events
-    ix.set_timing(True)
-    if G > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if G > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    ix.set_timing(False)
-    kms, kind = ix.timing_fetch()
-    if G > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    uncert = ix.uncertified_count()
+    def timed(scr):
+        """warmup + exactly `steps` timed steps on screen `scr`: (elapsed s over ranks, kernel ms, kind, uncert)"""
+        t_sw = time.time()
+        ix.set_screen(scr)  # int8: builds the int8 copy of the shard's rows (untimed)
+        t_sw = time.time() - t_sw
+        u0 = ix.uncertified_count()
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        ix.timing_fetch()  # drop warmup events
+        ix.set_timing(True)
+        if G > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        if G > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        ix.set_timing(False)
+        km, kd = ix.timing_fetch()
+        if G > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el, km, kd, ix.uncertified_count() - u0, t_sw
+
+    es = 2 if dtype in ("bf16", "f16") else 4
+    alt = None
+    if screen == "int8":  # the native (bf16 MFMA) screen of the same corpus, reported beside it
+        el_n, km_n, kind_n, unc_n, _ = timed("native")
+        res_native = {k_: v.clone() for k_, v in result.items()}
+        kn = float(np.mean(km_n)) if km_n else float("nan")
+        bytes_n = n_local * d * es + nq * d * es + nq * k * 12
+        alt = {"screen": "native", "kernel": f"k_screen_{kind_n}", "value": round(nq * args.steps / el_n, 2),
+               "ms_per_step": round(el_n * 1e3 / args.steps, 4), "kernel_ms": round(kn, 4),
+               "hbm_frac": round(bytes_n / (kn * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+               "uncertified_first_pass": unc_n}
+    elapsed, kms, kind, uncert, t_switch = timed(screen)
+    if alt is not None:  # both screens return the same exact answer
+        alt["identical_results"] = bool(torch.equal(result["I"], res_native["I"]) and
+                                        torch.equal(result["S"], res_native["S"]))
+        del res_native
 
     ms_per_step = elapsed * 1e3 / args.steps
     qps = nq * args.steps / elapsed
     kavg = float(np.mean(kms)) if kms else float("nan")
-    es = 2 if dtype in ("bf16", "f16") else 4
-    alg_bytes = n_local * d * es + nq * d * es + nq * k * 12
+    if kind == "mfma_i8":
+        # streamed per launch: the int8 codes + per-row (scale, error norm) + int8 queries + lists
+        alg_bytes = n_local * d + n_local * 4 + nq * d + nq * k * 12
+        peak_flops = MFMA_I8_PEAK_TOPS
+    else:
+        alg_bytes = n_local * d * es + nq * d * es + nq * k * 12
+        peak_flops = MFMA_BF16_PEAK_TF
     alg_flops = 2.0 * n_local * d * nq
     achieved_gbs = alg_bytes / (kavg * 1e-3) / 1e9
-    traffic = _traffic(args.traffic_file or os.path.join(REPO, "profiles", f"traffic_{args.workload}.json"),
-                       args.workload, n_local)
+    traffic = _traffic(args.traffic_file, args.workload, n_local, kind)
 
     out = None
     if rank == 0:
         out = {
-            "metric": "kNN queries/sec + recall@10 vs FAISS, N=10M d=1536 batch=256",
+            "metric": METRICS[args.workload],
             "value": round(qps, 2),
             "unit": "queries/s",
             "n_gpus": G,
@@ -167,10 +205,11 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": dtype,
+            "dtype": "int8" if kind == "mfma_i8" else dtype,
             "data": "synthetic (counter-hash N(0,1) rows, L2-normalised, seeds 20260417/20260418)",
             "config": {"workload": args.workload, "desc": desc, "N": N, "d": d, "batch": nq, "k": k,
-                       "n_local": n_local, "parallelism": f"row-shard x{G}" + (
+                       "n_local": n_local, "stored_rows": dtype, "screen": screen,
+                       "parallelism": f"row-shard x{G}" + (
                            (" + RCCL all-gather" if args.dist_backend == "nccl" else f" + {args.dist_backend} all-gather")
                            if G > 1 else "")},
             "roofline": {
@@ -184,12 +223,18 @@ def main():
                 "kernel_ms": round(kavg, 4),
                 "alg_bytes_per_launch": alg_bytes,
                 "mfma_tflops": round(alg_flops / (kavg * 1e-3) / 1e12, 1),
-                "mfma_frac": round(alg_flops / (kavg * 1e-3) / 1e12 / MFMA_BF16_PEAK_TF, 4),
+                "mfma_frac": round(alg_flops / (kavg * 1e-3) / 1e12 / peak_flops, 4),
+                "mfma_peak_tflops": peak_flops,
             },
             # first-pass certificate failures; every one was re-searched exactly (search_device_exact)
             "uncertified_first_pass": uncert,
             "build_s": round(t_build, 2),
         }
+        if kind == "mfma_i8":
+            out["int8_copy"] = {"hbm_bytes": n_local * (d + 4), "build_s": round(t_switch, 2),
+                                "note": "int8 codes + bf16 (scale, error norm) per row, on top of the stored rows"}
+        if alt is not None:
+            out["native_screen"] = alt
     if rank == 0 and G == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"], out["recall@10"], out["parity"] = cpu_baseline_and_recall(
             args, N, d, dtype, nq, k, local, torch, (result["D"].cpu().numpy(), result["I"].cpu().numpy()))
@@ -253,15 +298,19 @@ def cpu_baseline_and_recall(args, N, d, dtype, nq, k, local, torch, gpu_full):
     return cpu, round(rec10, 6), parity
 
 
-def _traffic(path: str, workload: str, n_local: int):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary of this configuration."""
-    try:
-        with open(path) as f:
-            tr = json.load(f)
-    except (OSError, ValueError):
-        return None
-    if tr.get("workload") == workload and tr.get("n_local") == n_local:
-        return tr.get("hbm_bytes_per_launch")
+def _traffic(path, workload: str, n_local: int, kind: str = ""):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary of this
+    configuration (profiles/traffic_<workload>_<kind>[_n<rows>].json, scripts/prof_summary.py)."""
+    import glob
+    paths = [path] if path else sorted(glob.glob(os.path.join(REPO, "profiles", f"traffic_{workload}_{kind}*.json")))
+    for p in paths:
+        try:
+            with open(p) as f:
+                tr = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if tr.get("workload") == workload and tr.get("n_local") == n_local:
+            return tr.get("hbm_bytes_per_launch")
     return None
 
 
@@ -475,7 +524,7 @@ def run_ivf(args):
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": _traffic(os.path.join(REPO, "profiles", "traffic_cfg5.json"), "cfg5", N),
+            "traffic": _traffic(None, "cfg5", N, "ivf_scan"),
             "kernel_ms": round(kavg, 4),
             "alg_bytes_per_launch": alg_bytes,
         },

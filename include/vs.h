@@ -41,6 +41,7 @@ typedef struct vs_index vs_index;
 
 enum { VS_METRIC_IP = 0, VS_METRIC_L2 = 1 };
 enum { VS_DTYPE_F32 = 0, VS_DTYPE_BF16 = 1, VS_DTYPE_F16 = 2 };
+enum { VS_SCREEN_NATIVE = 0, VS_SCREEN_I8 = 1 };
 
 enum {
     VS_OK = 0,
@@ -103,6 +104,17 @@ int vs_reconstruct_n(vs_index* index, int64_t i0, int64_t n, float* out); /* hos
  * never truncated): a full rewrite, or an append of the rows added since the last save. */
 int vs_add_from_file(vs_index* index, const char* path, int64_t byte_offset, int64_t n);
 int vs_write_rows_to_file(vs_index* index, const char* path, int64_t byte_offset, int64_t i0, int64_t n);
+
+/* ---- screen selection (no reference counterpart: faiss IndexFlat has one exact scan).
+ * VS_SCREEN_NATIVE (default): batches screen the stored rows (bf16/f16 MFMA, or the fp32 GEMV).
+ * VS_SCREEN_I8: the index keeps an int8 copy of its rows (per-row scale, +1 byte per element,
+ * built from the stored values now and on every add) and batches of > 8 queries with k <= 1024
+ * screen it with int8 MFMAs under a proven per-row error bound; an adaptive exact refine then
+ * scores every candidate the bound cannot exclude.  Results are identical to the native path
+ * (same exact ids and scores); queries the certificate rejects are re-searched natively.
+ * Inner-product indexes only. */
+int vs_set_screen(vs_index* index, int screen);
+int vs_screen(const vs_index* index);
 
 /* ---- introspection */
 int64_t vs_ntotal(const vs_index* index);

@@ -71,6 +71,8 @@ _SIGS = {
     "vs_device": (ctypes.c_int, [_vp]),
     "vs_last_error": (ctypes.c_char_p, []),
     "vs_version": (ctypes.c_char_p, []),
+    "vs_set_screen": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "vs_screen": (ctypes.c_int, [_vp]),
     "vs_set_timing": (ctypes.c_int, [_vp, ctypes.c_int]),
     "vs_timing_fetch": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
     "vs_uncertified_count": (_c_i64, [_vp]),

@@ -55,6 +55,7 @@ struct Ctx {
     hipEvent_t idle = nullptr;
     bool pending = false;
     DevBuf qdev, qtile, qinfo, qpad, cand, part, merge_a, merge_b, outD, outI, outS, cert, thr0, seedmax, gcnt;
+    DevBuf qfac, qeps, drop;  // int8 screen: per-query code scale and norm, refine margin, drop bounds
     DevBuf rows[2];  // read_rows_host: unpacked fp32 chunks
     DevBuf tilectr;  // GEMV screen: tile work-queue counter
     DevBuf seedacc;  // MFMA seed pass: raw accumulators of each workgroup's seed tile
@@ -64,7 +65,7 @@ struct Ctx {
     HostBuf hout;    // vs_search: I (int64), D (fp32) and certificates land here; search_exact_device: certificates
     ~Ctx() {
         for (DevBuf* b : {&qdev, &qtile, &qinfo, &qpad, &cand, &part, &merge_a, &merge_b, &outD, &outI, &outS, &cert, &thr0,
-                          &seedmax, &gcnt, &rows[0], &rows[1], &tilectr, &seedacc, &outAll})
+                          &seedmax, &gcnt, &rows[0], &rows[1], &tilectr, &seedacc, &outAll, &qfac, &qeps, &drop})
             b->release();
         pin.release();
         hq.release();
@@ -87,6 +88,13 @@ struct vs_index {
     unsigned* d_maxsq = nullptr;
     unsigned* d_uncert = nullptr;
     float maxsq = 0.0f;
+    // int8 screen copy (VS_SCREEN_I8): codes in row tiles of 64-element chunks + per-row scale and
+    // error norm; d_maxsq[2..3] = max ||x_hat||, max error norm (fp32 bits, certificate margins)
+    int screen = VS_SCREEN_NATIVE;
+    int dpad8 = 0;
+    int64_t cap8 = 0;
+    uint8_t* data8 = nullptr;
+    uint32_t* rsb = nullptr;  // per row: bf16 scale | bf16 error norm (rounded up) << 16
     hipStream_t own = nullptr;  // ingest stream
     DevBuf stage[2];            // add_rows_host: fp32 chunks on the device ...
     PinnedPair pin;             // ... and their pinned host sources
@@ -98,7 +106,7 @@ struct vs_index {
     std::atomic<bool> timing{false};
     std::mutex tmtx;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> tev;
-    int last_kernel_kind = 0;  // 1 = mfma, 2 = gemv
+    int last_kernel_kind = 0;  // 1 = mfma, 2 = gemv, 3 = int8 mfma
 };
 
 namespace {
@@ -142,6 +150,8 @@ struct CtxLease {
     }
 };
 
+void ensure_capacity_i8(vs_index* ix);
+
 void ensure_capacity(vs_index* ix, int64_t rows_needed) {
     const int64_t want = round_up(rows_needed, TR);
     if (want <= ix->cap_rows) return;
@@ -169,6 +179,48 @@ void ensure_capacity(vs_index* ix, int64_t rows_needed) {
     ix->data = nd;
     ix->sqn = ns;
     ix->cap_rows = ncap;
+    ensure_capacity_i8(ix);
+}
+
+void free_i8(vs_index* ix) {
+    if (ix->data8) (void)hipFree(ix->data8);
+    if (ix->rsb) (void)hipFree(ix->rsb);
+    ix->data8 = nullptr;
+    ix->rsb = nullptr;
+    ix->cap8 = 0;
+}
+
+// grow the int8 screen copy to ix->cap_rows rows (device copy of the rows present; the old and new
+// arrays coexist only for the copy, as for the primary rows)
+void ensure_capacity_i8(vs_index* ix) {
+    if (ix->screen != VS_SCREEN_I8 || ix->cap8 >= ix->cap_rows) return;
+    const int64_t ncap = ix->cap_rows;
+    const size_t tb8 = (size_t)TR * ix->dpad8;
+    uint8_t* nd = nullptr;
+    uint32_t* nr = nullptr;
+    hipError_t e = hipMalloc(&nd, (size_t)(ncap / TR) * tb8);
+    if (e == hipSuccess) e = hipMalloc(&nr, (size_t)ncap * sizeof(uint32_t));
+    if (e != hipSuccess) {
+        if (nd) hipFree(nd);
+        HIP_CHECK(e);
+    }
+    if (ix->data8 && ix->ntotal > 0) {
+        const int64_t used_tiles = (ix->ntotal + TR - 1) / TR;
+        HIP_CHECK(hipMemcpyAsync(nd, ix->data8, (size_t)used_tiles * tb8, hipMemcpyDeviceToDevice, ix->own));
+        HIP_CHECK(hipMemcpyAsync(nr, ix->rsb, (size_t)ix->ntotal * sizeof(uint32_t), hipMemcpyDeviceToDevice, ix->own));
+    }
+    HIP_CHECK(hipStreamSynchronize(ix->own));
+    free_i8(ix);
+    ix->data8 = nd;
+    ix->rsb = nr;
+    ix->cap8 = ncap;
+}
+
+// int8 screen copy of rows [r0, r0 + n) once they are packed (stream-ordered after the pack)
+void quantize_rows(vs_index* ix, int64_t r0, int64_t n, hipStream_t st) {
+    if (ix->screen != VS_SCREEN_I8 || n <= 0) return;
+    HIP_CHECK(launch_quant_rows(ix->dtype, ix->data, ix->dpad, r0, n, ix->d, ix->data8, ix->dpad8, ix->rsb,
+                                ix->d_maxsq + 2, st));
 }
 
 void refresh_maxsq(vs_index* ix) {
@@ -197,10 +249,116 @@ bool gemv_dyn() {
     return on;
 }
 
+// The int8 pre-screen serves first passes of MFMA-sized batches (k <= I8_MAX_K) of an index with
+// VS_SCREEN_I8; a query its certificate rejects is re-searched by the caller on the native path.
+bool use_i8(const vs_index* ix, int nqb, int k) {
+    return ix->screen == VS_SCREEN_I8 && nqb > GEMV_NQ_MAX && k <= I8_MAX_K;
+}
+// union of survivors the int8 seed aims at: ~kI8UnionPerK * k rows above the seeded threshold
+// (cfg3: k = 100 -> 6,400; the refine scores ~1.3k of them)
+constexpr double kI8UnionPerK = 64.0;
+constexpr double kI8UnionMin = 1024.0;
+
+// int8 pre-screen of one query block: pack int8 query codes -> seed pass -> int8 MFMA screen with
+// upper-bound keys -> adaptive exact refine (k_refine_wide).  q: device fp32 [nqb][d].
+void search_block_i8(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float* D, int64_t* I, double* S64,
+                     int* cert, int64_t id_offset, hipStream_t st) {
+    const int64_t tiles = (ix->ntotal + TR - 1) / TR;
+    ScreenArgs a{};
+    a.corpus = ix->data8;
+    a.n_valid = ix->ntotal;
+    a.tiles = (int)tiles;
+    a.dpad = ix->dpad8;
+    a.d = ix->d;
+    a.metric = METRIC_IP;
+    a.Kp = MFMA_KP_MAX;  // per workgroup and query; the refine's depth is adaptive
+    a.cap = MFMA_CAP;
+    a.G = (int)std::max<int64_t>(1, std::min<int64_t>(tiles, ix->num_cu));
+    a.rsb = ix->rsb;
+    c->qtile.ensure((size_t)MFMA_QB * ix->dpad8);
+    c->qfac.ensure(sizeof(float2) * MFMA_QB);
+    c->qeps.ensure(sizeof(float) * MFMA_QB);
+    c->drop.ensure(sizeof(u64) * MFMA_QB);
+    c->gcnt.ensure(sizeof(int) * MFMA_QB);
+    HIP_CHECK(launch_pack_qtile_i8(q, nqb, ix->d, ix->dpad8, c->qtile.as<uint8_t>(), c->qfac.as<float2>(),
+                                   c->qeps.as<float>(), ix->d_maxsq + 2, c->gcnt.as<int>(), c->drop.as<u64>(), st));
+    a.qfac = c->qfac.as<float2>();
+    a.drop = c->drop.as<u64>();
+    a.lcap = a.G * a.Kp;
+    c->cand.ensure((size_t)a.G * MFMA_QB * a.cap * sizeof(u64));
+    c->part.ensure((size_t)MFMA_QB * a.lcap * sizeof(u64));
+    a.cand = c->cand.as<u64>();
+    a.glist = c->part.as<u64>();
+    a.gcnt = c->gcnt.as<int>();
+    a.thr0 = nullptr;
+    if (tiles >= 4 * (int64_t)a.G) {  // optimistic threshold seed from one tile per workgroup
+        ScreenArgs sa = a;
+        sa.G = std::min(sa.G, 512);
+        sa.tile_stride = (int)(tiles / sa.G);
+        if (seed_reuse() && sa.G == a.G) {
+            c->seedacc.ensure((size_t)a.G * 128 * MF_WG_THREADS * sizeof(float));
+            sa.seed_acc = c->seedacc.as<float>();
+        }
+        const int M = sa.G * 16;
+        c->seedmax.ensure(sizeof(float) * MFMA_QB * M);
+        sa.seedmax = c->seedmax.as<float>();
+        HIP_CHECK(launch_seed_mfma(DT_I8, sa, c->qtile.as<uint8_t>(), nqb, st));
+        c->thr0.ensure(sizeof(u64) * MFMA_QB);
+        static const double per_k = getenv("VS_I8_UNION") ? atof(getenv("VS_I8_UNION")) : kI8UnionPerK;  // A/B knob
+        const double target = std::max(per_k * k, kI8UnionMin);
+        const double r = std::ceil(target * (double)sa.G * TR / (double)ix->ntotal);
+        const int rank = (int)std::min<double>(std::max<double>(r, (double)kOptimisticMinRank), (double)M);
+        HIP_CHECK(launch_seed_select(sa.seedmax, M, nqb, rank, c->thr0.as<u64>(), st));
+        a.thr0 = c->thr0.as<u64>();
+        a.seed_acc = sa.seed_acc;
+    }
+    const bool timing = ix->timing.load();
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (timing) {
+        HIP_CHECK(hipEventCreate(&e0));
+        HIP_CHECK(hipEventCreate(&e1));
+        HIP_CHECK(hipEventRecord(e0, st));
+    }
+    HIP_CHECK(launch_screen_mfma(DT_I8, a, c->qtile.as<uint8_t>(), nqb, st));
+    if (timing) {
+        HIP_CHECK(hipEventRecord(e1, st));
+        std::lock_guard<std::mutex> g(ix->tmtx);
+        ix->tev.emplace_back(e0, e1);
+        ix->last_kernel_kind = 3;
+    }
+    RefineArgs r{};
+    r.cand = a.glist;
+    r.cand_n = a.gcnt;
+    r.lcap = a.lcap;
+    r.Kp = a.Kp;
+    r.q = q;
+    r.d = ix->d;
+    r.dpad = ix->dpad;
+    r.dt = ix->dtype;
+    r.metric = METRIC_IP;
+    r.corpus = ix->data;
+    r.k = k;
+    r.n_valid = ix->ntotal;
+    r.id_offset = id_offset;
+    r.D = D;
+    r.I = I;
+    r.S64 = S64;
+    r.cert = cert;
+    r.uncert = ix->d_uncert;
+    r.qeps = c->qeps.as<float>();
+    r.drop = a.drop;
+    r.thr0 = a.thr0;
+    HIP_CHECK(launch_refine_wide(r, nqb, (int)round_up(2 * k + 32, 32), st));
+}
+
 // Enqueue one query block through screen -> merge -> refine.  q: device fp32 [nqb][d].
 // seed_rank: 0 = proven (safe) seed, > 0 = optimistic seed at that sample rank (see k_seed_select)
 void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, float* D, int64_t* I, double* S64,
                   int* cert, int64_t id_offset, hipStream_t st, int seed_rank) {
+    if (seed_rank > 0 && use_i8(ix, nqb, k)) {
+        search_block_i8(ix, c, q, nqb, k, D, I, S64, cert, id_offset, st);
+        return;
+    }
     const int64_t tiles = (ix->ntotal + TR - 1) / TR;
     const bool use_mfma = ix->dtype != DT_F32 && nqb > GEMV_NQ_MAX && Kp <= MFMA_KP_MAX;
     ScreenArgs a{};
@@ -362,7 +520,8 @@ void search_all(vs_index* ix, Ctx* c, const float* q, int64_t nq, int k, int Kp,
                 int* cert, int64_t id_offset, hipStream_t st, int seed_rank) {
     const int64_t tiles = (ix->ntotal + TR - 1) / TR;
     (void)tiles;
-    const bool mfma_ok = ix->dtype != DT_F32 && Kp <= MFMA_KP_MAX;
+    const bool mfma_ok = (seed_rank > 0 && ix->screen == VS_SCREEN_I8 && k <= I8_MAX_K) ||
+                         (ix->dtype != DT_F32 && Kp <= MFMA_KP_MAX);
     int64_t done = 0;
     while (done < nq) {
         const int64_t rem = nq - done;
@@ -443,6 +602,7 @@ void vs::add_rows_host(vs_index* ix, int64_t n, const std::function<void(int64_t
                                        ix->ntotal + r0, ix->sqn, ix->d_maxsq, ix->own));
             HIP_CHECK(hipEventRecord(ix->pin.done[b], ix->own));
         }
+        quantize_rows(ix, ix->ntotal, n, ix->own);
         HIP_CHECK(hipStreamSynchronize(ix->own));
     } catch (...) {
         (void)hipStreamSynchronize(ix->own);  // the pinned chunks may still be in flight
@@ -526,8 +686,9 @@ int vs_create(int d, int metric, int dtype, int device, vs_index** out) {
         ix->num_cu = prop.multiProcessorCount;
         try {
             HIP_CHECK(hipStreamCreateWithFlags(&ix->own, hipStreamNonBlocking));
-            HIP_CHECK(hipMalloc(&ix->d_maxsq, sizeof(unsigned) * 2));
-            HIP_CHECK(hipMemset(ix->d_maxsq, 0, sizeof(unsigned) * 2));
+            // [0] max ||x||^2, [1] uncertified counter, [2..3] int8 screen maxima (fp32 bits)
+            HIP_CHECK(hipMalloc(&ix->d_maxsq, sizeof(unsigned) * 4));
+            HIP_CHECK(hipMemset(ix->d_maxsq, 0, sizeof(unsigned) * 4));
             ix->d_uncert = ix->d_maxsq + 1;
         } catch (...) {
             delete ix;
@@ -553,6 +714,7 @@ void vs_destroy(vs_index* ix) {
         if (ix->data) hipFree(ix->data);
         if (ix->sqn) hipFree(ix->sqn);
         if (ix->d_maxsq) hipFree(ix->d_maxsq);
+        free_i8(ix);
         if (ix->own) hipStreamDestroy(ix->own);
     }
     delete ix;
@@ -566,6 +728,7 @@ int vs_reset(vs_index* ix) {
         ix->ntotal = 0;
         ix->maxsq = 0.0f;
         HIP_CHECK(hipMemsetAsync(ix->d_maxsq, 0, sizeof(unsigned), ix->own));
+        HIP_CHECK(hipMemsetAsync(ix->d_maxsq + 2, 0, 2 * sizeof(unsigned), ix->own));
         HIP_CHECK(hipStreamSynchronize(ix->own));
     });
 }
@@ -597,6 +760,7 @@ int vs_add_device(vs_index* ix, const float* x_dev, int64_t n, void* stream) {
         // index's private non-blocking stream: that one is unordered with the caller's producers
         hipStream_t st = (hipStream_t)stream;
         HIP_CHECK(launch_pack_rows(ix->dtype, x_dev, n, ix->d, ix->dpad, ix->data, ix->ntotal, ix->sqn, ix->d_maxsq, st));
+        quantize_rows(ix, ix->ntotal, n, st);
         HIP_CHECK(hipStreamSynchronize(st));
         ix->ntotal += n;
         refresh_maxsq(ix);
@@ -614,6 +778,7 @@ int vs_add_synthetic(vs_index* ix, uint64_t seed, int64_t global_row0, int64_t n
         ensure_capacity(ix, ix->ntotal + n);
         HIP_CHECK(launch_synth_rows(ix->dtype, seed, global_row0, n, ix->d, ix->dpad, ix->data, ix->ntotal, normalize,
                                     ix->sqn, ix->d_maxsq, ix->own));
+        quantize_rows(ix, ix->ntotal, n, ix->own);
         HIP_CHECK(hipStreamSynchronize(ix->own));
         ix->ntotal += n;
         refresh_maxsq(ix);
@@ -783,6 +948,38 @@ int vs_dim(const vs_index* ix) { return ix ? ix->d : -1; }
 int vs_metric(const vs_index* ix) { return ix ? ix->metric : -1; }
 int vs_dtype(const vs_index* ix) { return ix ? ix->dtype : -1; }
 int vs_device(const vs_index* ix) { return ix ? ix->device : -1; }
+
+int vs_set_screen(vs_index* ix, int screen) {
+    return guarded([&] {
+        check_index(ix);
+        if (screen != VS_SCREEN_NATIVE && screen != VS_SCREEN_I8) throw VsError(VS_ERR_ARG, "screen must be 0 (native) or 1 (int8)");
+        if (screen == VS_SCREEN_I8 && ix->metric != VS_METRIC_IP)
+            throw VsError(VS_ERR_ARG, "the int8 screen serves inner-product indexes");
+        std::unique_lock<std::shared_mutex> lk(ix->rw);
+        DeviceGuard dg(ix->device);
+        if (screen == ix->screen) return;
+        if (screen == VS_SCREEN_NATIVE) {
+            HIP_CHECK(hipDeviceSynchronize());  // searches in flight may still read the int8 copy
+            free_i8(ix);
+            ix->screen = VS_SCREEN_NATIVE;
+            return;
+        }
+        ix->screen = VS_SCREEN_I8;
+        ix->dpad8 = (int)std::max<int64_t>(round_up(ix->d, 64), 128);  // >= 2 K-steps per tile (see dpad)
+        try {
+            HIP_CHECK(hipMemsetAsync(ix->d_maxsq + 2, 0, 2 * sizeof(unsigned), ix->own));
+            ensure_capacity_i8(ix);
+            quantize_rows(ix, 0, ix->ntotal, ix->own);
+            HIP_CHECK(hipStreamSynchronize(ix->own));
+        } catch (...) {
+            free_i8(ix);
+            ix->screen = VS_SCREEN_NATIVE;
+            throw;
+        }
+    });
+}
+
+int vs_screen(const vs_index* ix) { return ix ? ix->screen : -1; }
 
 int vs_set_timing(vs_index* ix, int enable) {
     return guarded([&] {

@@ -176,8 +176,8 @@ struct ScreenArgs {
     int* next_tile;          // GEMV: tile work-queue counter (zeroed before the launch); null = static ranges
     float* seed_acc;         // MFMA: [G][512 lanes][128] raw accumulators of each workgroup's seed tile (the
                              // first tile of its range): written by the seed pass, reused by the main pass
-    const float* rscale;     // int8 screen: per-row scale s_x (x_hat = s_x * codes)
-    const float* rbeta;      // int8 screen: per-row ||x - x_hat||_2, rounded up
+    const uint32_t* rsb;     // int8 screen, per row: bf16 scale s_x (x_hat = s_x * codes) in the low half,
+                             // bf16 ||x - x_hat||_2 rounded up in the high half
     const float2* qfac;      // int8 screen: per query (t_q, ||q||), codes q_hat = t_q * int8
     u64* drop;               // MFMA: per query, max over workgroups of their compaction threshold
                              // (rows below it were dropped; zeroed by the query pack), or null
@@ -231,9 +231,20 @@ struct RefineArgs {
     int* cert;             // [nq] 1 = certified exact (may be null)
     unsigned* uncert;      // device counter (may be null)
     int optimistic;        // screened with an optimistic seed: fewer than Kp candidates = uncertified
+    const float* qeps;     // int8 screen (k_refine_wide): per query, true score <= key_score + qeps
+    const u64* drop;       // MFMA: per query, the workgroups' largest compaction threshold (or null)
+    const u64* thr0;       // the screen's starting threshold per query (or null = none)
     const uint32_t* idmap; // IVF: user id of every storage slot (keys carry slots); null = identity
 };
 hipError_t launch_refine(const RefineArgs& a, int nq, hipStream_t st);
+// exact refine behind the int8 screen: adaptive two-phase depth (KA keys first), IP only
+hipError_t launch_refine_wide(const RefineArgs& a, int nq, int KA, hipStream_t st);
+constexpr int I8_MAX_K = 1024;  // largest k the int8 screen serves (k_refine_wide: 2 * KA <= RFW_CAP)
+// int8 screen copy of stored rows [r0, r0 + n) (maxes[0..1]: running max ||x_hat||, max beta)
+hipError_t launch_quant_rows(int dt, const uint8_t* data, int dpad, int64_t r0, int64_t n, int d, uint8_t* data8,
+                             int dpad8, uint32_t* rsb, unsigned* maxes, hipStream_t st);
+hipError_t launch_pack_qtile_i8(const float* q, int nqb, int d, int dpad8, uint8_t* qt, float2* qfac, float* qeps,
+                                const unsigned* maxes, int* gcnt, u64* drop, hipStream_t st);
 
 // ---- IVF-Flat (vs_ivf.hip) ---------------------------------------------------------------------
 // Inverted lists are chains of pages: a page is one row tile (TR rows, the flat layout above) of

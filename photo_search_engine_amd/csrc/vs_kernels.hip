@@ -461,6 +461,121 @@ __global__ void __launch_bounds__(256) k_pack_qtile(const float* __restrict__ q,
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// int8 screen copy (DESIGN §5 "int8 screen").  Per row, over its STORED values x: scale
+// s = bf16(max|x| / 127), codes c = rint(x / s) in [-127, 127], and the exact error norm
+// beta = ||x - s c||_2 (fp64, rounded up to bf16); (s, beta) packed in one u32 per row (the screen
+// epilogue reads 4 B per row).  Also the running maxima of ||s c|| and beta
+// (maxes[0], maxes[1], fp32 bits) that bound the query-side and rounding terms of the refine's
+// certificate.  The codes need not be the nearest: whatever rint gives, beta is measured.
+// Layout: row tiles of TR rows, 64-element chunks, [chunk][row][64 B] -- one 16 KiB block per
+// MFMA K-step, the same block geometry as the bf16 layout.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ float f32_up(double v) {  // smallest fp32 >= v (v >= 0, finite)
+    float f = (float)v;
+    if ((double)f < v) f = __uint_as_float(__float_as_uint(f) + 1u);
+    return f;
+}
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#pragma unroll
+    for (int s = 32; s > 0; s >>= 1) v += __shfl_xor(v, s, 64);
+    return v;
+}
+
+// one wave per row
+__device__ __forceinline__ uint32_t bf16_bits_up(float f) {  // smallest bf16 >= f (f >= 0, finite)
+    const uint32_t u = __float_as_uint(f);
+    return (u >> 16) + ((u & 0xFFFFu) ? 1u : 0u);
+}
+
+template <int DT>
+__global__ void __launch_bounds__(256) k_quant_rows(const uint8_t* __restrict__ data, int dpad, int64_t r0, int64_t n,
+                                                     int d, uint8_t* __restrict__ data8, int dpad8,
+                                                     uint32_t* __restrict__ rsb, unsigned* __restrict__ maxes) {
+    constexpr int ES = DT == DT_F32 ? 4 : 2;
+    const int lane = threadIdx.x & 63;
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= n) return;
+    const int64_t row = r0 + r;
+    float mx = 0.0f;
+    for (int i = lane; i < d; i += 64) mx = fmaxf(mx, fabsf(load_elem<DT>(data + tiled_off(row, i, dpad, ES))));
+#pragma unroll
+    for (int s = 32; s > 0; s >>= 1) mx = fmaxf(mx, __shfl_xor(mx, s, 64));
+    const uint32_t sbits = f32_to_bf16_rne(mx / 127.0f);
+    const float sc = bf16_bits_to_f32(sbits);  // the scale as stored: codes and error use exactly it
+    uint8_t* dst = data8 + (row / TR) * (int64_t)TR * dpad8 + (row % TR) * 64;
+    double e2 = 0.0, c2 = 0.0;
+    for (int i = lane; i < dpad8; i += 64) {
+        int c = 0;
+        float x = 0.0f;
+        if (i < d) {
+            x = load_elem<DT>(data + tiled_off(row, i, dpad, ES));
+            if (sc > 0.0f) c = max(-127, min(127, (int)rintf(x / sc)));
+        }
+        dst[(int64_t)(i >> 6) * TR * 64 + (i & 63)] = (uint8_t)(int8_t)c;
+        // exact in fp64: c != 0 needs |x| >= s / 2, so x and s c span < 53 bits; c == 0 gives e = x
+        const double e = (double)x - (double)sc * (double)c;
+        e2 += e * e;
+        c2 += (double)(c * c);
+    }
+    e2 = wave_sum_f64(e2);
+    c2 = wave_sum_f64(c2);
+    if (lane == 0) {
+        const uint32_t bbits = bf16_bits_up(f32_up(sqrt(e2) * (1.0 + 1e-9)));
+        rsb[row] = sbits | (bbits << 16);
+        atomicMax(&maxes[0], __float_as_uint(f32_up(sqrt(c2) * (double)sc * (1.0 + 1e-9))));
+        atomicMax(&maxes[1], bbits << 16);  // the fp32 bits of the bf16 bound
+    }
+}
+
+// int8 query tile [nks8][256][64] (codes of q / t_q, t_q = max|q| / 127) for the int8 MFMA screen,
+// one wave per query.  qfac = (t_q, ||q|| rounded up); qeps = the query-side margin of the
+// screen key (key = s_x t_q <c_x, c_q> + beta_x ||q||, see k_screen_mfma):
+//   true <x, q> <= key + ||s_x c_x|| ||q - t_q c_q|| + rounding <= key_score + qeps.
+// Also zeroes the survivor-list lengths and the workgroup drop bounds of the screen that follows.
+__global__ void __launch_bounds__(256) k_pack_qtile_i8(const float* __restrict__ q, int nqb, int d, int dpad8,
+                                                        uint8_t* __restrict__ qt, float2* __restrict__ qfac,
+                                                        float* __restrict__ qeps, const unsigned* __restrict__ maxes,
+                                                        int* __restrict__ gcnt, u64* __restrict__ drop) {
+    const int lane = threadIdx.x & 63;
+    const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= MFMA_QB) return;
+    if (lane == 0) {
+        gcnt[r] = 0;
+        drop[r] = 0ull;
+    }
+    float mx = 0.0f;
+    if (r < nqb)
+        for (int i = lane; i < d; i += 64) mx = fmaxf(mx, fabsf(q[(int64_t)r * d + i]));
+#pragma unroll
+    for (int s = 32; s > 0; s >>= 1) mx = fmaxf(mx, __shfl_xor(mx, s, 64));
+    const float t = mx / 127.0f;
+    double e2 = 0.0, n2 = 0.0, c2 = 0.0;
+    for (int i = lane; i < dpad8; i += 64) {
+        const float v = (r < nqb && i < d) ? q[(int64_t)r * d + i] : 0.0f;
+        const int c = t > 0.0f ? max(-127, min(127, (int)rintf(v / t))) : 0;
+        qt[(int64_t)(i >> 6) * MFMA_QB * 64 + (int64_t)r * 64 + (i & 63)] = (uint8_t)(int8_t)c;
+        const double e = (double)v - (double)t * (double)c;
+        e2 += e * e;
+        n2 += (double)v * v;
+        c2 += (double)(c * c);
+    }
+    e2 = wave_sum_f64(e2);
+    n2 = wave_sum_f64(n2);
+    c2 = wave_sum_f64(c2);
+    if (lane == 0 && r < nqb) {
+        const float qn = f32_up(sqrt(n2) * (1.0 + 1e-9));
+        const double eq = sqrt(e2) * (1.0 + 1e-9);
+        const double qh = sqrt(c2) * (double)t * (1.0 + 1e-9);  // ||t_q c_q||
+        const double X = (double)__uint_as_float(maxes[0]), B = (double)__uint_as_float(maxes[1]);
+        // the key's fp32 evaluation fl(fl(fl(acc) * fl(s t)) + beta qn): <= 5 roundings relative
+        // 2^-24 of |sigma| + beta qn, |sigma| <= X ||t_q c_q||
+        const double slop = 5.0 * 5.9604644775390625e-08 * (X * qh + B * (double)qn) + 1e-30;
+        qfac[r] = make_float2(t, qn);
+        qeps[r] = f32_up((X * eq + slop) * (1.0 + 1e-9));
+    }
+}
+
 // GEMV queries: fp32, [nqpad][dpad] zero padded; q_hat = q
 __global__ void __launch_bounds__(256) k_pack_qf32(const float* __restrict__ q, int nqb, int nqpad, int d, int dpad,
                                                     float* __restrict__ qp, float* __restrict__ qinfo,
@@ -704,6 +819,16 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
     }
     int ti = t0, ks = 0;
     bool check_pending = false;
+    // int8: the tile's packed per-row (scale, error norm), 16 rows per lane, loaded PF_LEAD K-steps
+    // before its epilogue so the HBM latency hides behind the MFMAs (rows past the shard read the
+    // allocation's padding; the epilogue masks them)
+    uint4 pf_rsb[4] = {};
+    const int pf_ks = nks > 8 ? nks - 8 : 0;
+    auto prefetch_rsb = [&](int tile) {
+        const uint32_t* p = a.rsb + (int64_t)tile * TR + wm * 64 + (lane >> 4) * 4;
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) pf_rsb[mi] = *(const uint4*)(p + mi * 16);
+    };
     // tile epilogue over the accumulators of tile `ti` (shared by the K loop and the seed tile)
     auto tile_epilogue = [&](const int ti) {
         // ---- fused top-k epilogue: threshold filter, rare inserts ----
@@ -735,20 +860,24 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
                 for (int r = 0; r < 4; ++r)
                     if (rowbase + rid0 + mi * 16 + r >= a.n_valid) bad |= 1u << (mi * 4 + r);
         }
-        float sq[4][4], rb[4][4];  // L2: ||x||^2; int8: the row's scale and error norm
-        if constexpr (METRIC == METRIC_L2 || I8) {
+        float sq[4][4], rb[4][4];  // L2: ||x||^2; int8: the row's scale and error norm (prefetched)
+        if constexpr (I8) {
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi) {
+                const uint32_t w4[4] = {pf_rsb[mi].x, pf_rsb[mi].y, pf_rsb[mi].z, pf_rsb[mi].w};
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    sq[mi][r] = __uint_as_float(w4[r] << 16);
+                    rb[mi][r] = __uint_as_float(w4[r] & 0xFFFF0000u);
+                }
+            }
+        } else if constexpr (METRIC == METRIC_L2) {
 #pragma unroll
             for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int64_t gr = rowbase + rid0 + mi * 16 + r;
-                    const bool ok = gr < a.n_valid;
-                    if constexpr (I8) {
-                        sq[mi][r] = ok ? a.rscale[gr] : 0.0f;
-                        rb[mi][r] = ok ? a.rbeta[gr] : 0.0f;
-                    } else {
-                        sq[mi][r] = ok ? a.sqn[gr] : 0.0f;
-                    }
+                    sq[mi][r] = gr < a.n_valid ? a.sqn[gr] : 0.0f;
                 }
         }
 #pragma unroll
@@ -839,6 +968,7 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
         for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
             for (int ni = 0; ni < 8; ++ni) acc[mi][ni] = src[mi * 8 + ni];
+        if constexpr (I8) prefetch_rsb(tseed);
         tile_epilogue(tseed);
     }
     for (int s = 0; s < S; ++s) {
@@ -850,6 +980,8 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
                      ring + (uint32_t)(((s + MF_DEPTH) % MF_SLOTS) * MF_SLOT), tid);
             if (++iks == nks) { iks = 0; ++iti; }
         }
+        if constexpr (I8)
+            if (ks == pf_ks) prefetch_rsb(ti);
         mf_compute<DT>(smem + (s % MF_SLOTS) * MF_SLOT, acc, wm, wn, lane_off);
         if (ks == nks - 1) tile_epilogue(ti);
         // Deferred compaction check, after the NEXT K-step's barrier: by then every wave's
@@ -1704,6 +1836,252 @@ __global__ void __launch_bounds__(RF_THREADS) k_refine(RefineArgs a, int KP2) {
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// K5w: exact refine behind the int8 screen -- adaptive depth, two phases, one block per query.
+// The screen keys are upper bounds: true <x, q> <= key_score + qeps[q] (k_pack_qtile_i8).
+//  A: the best KA keys of the query's survivor list are scored exactly (canonical fp64); T' = the
+//     k-th best of them is a lower bound of the final k-th best exact score T.
+//  B: every other key with key_score >= T' - qeps could still reach T': those rows are scored too.
+//     Every survivor left unscored has true < T' <= T.
+//  Certificate: rows never listed (below the seed threshold thr0 or a workgroup's compaction bound
+//  drop) have true <= key_score(max(thr0, drop)) + qeps, which must be < T; and the rows scored
+//  must fit the block's RFW_CAP slots.
+// ------------------------------------------------------------------------------------------------
+constexpr int RFW_CAP = 8192;  // rows scored per query (fp64 score + id in LDS)
+
+// order-preserving block compaction of this thread's keys in [lo, hi) to ids[base + ...]; returns
+// the block total
+template <int E>
+__device__ __forceinline__ int block_write_ids(const u64 (&keys)[E], u64 lo, u64 hi, uint32_t* out, int cap, int* red) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    int c = 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) c += (keys[e] >= lo && keys[e] < hi) ? 1 : 0;
+    int incl = c;
+#pragma unroll
+    for (int s = 1; s < 64; s <<= 1) {
+        const int v = __shfl_up(incl, s, 64);
+        if (lane >= s) incl += v;
+    }
+    if (lane == 63) red[w] = incl;
+    __syncthreads();
+    int base = 0, total = 0;
+    for (int i = 0; i < nw; ++i) {
+        if (i < w) base += red[i];
+        total += red[i];
+    }
+    __syncthreads();
+    int pos = base + incl - c;
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+        if (keys[e] >= lo && keys[e] < hi) {
+            if (pos < cap) out[pos] = key_id(keys[e]);
+            ++pos;
+        }
+    return total;
+}
+
+// scores of ids[lo, hi) into sc[lo, hi): 16 waves, two rows in flight per wave
+template <int DT, bool QLDS>
+__device__ __forceinline__ void rfw_score(const RefineArgs& a, const uint32_t* ids, double* sc, int lo, int hi,
+                                          const double* qs, const float* qv) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    constexpr int NW = RF_THREADS / 64;
+    for (int j = lo + wid; j < hi; j += 2 * NW) {
+        const int j2 = j + NW;
+        double s0, s1;
+        exact_score_q2<DT, METRIC_IP, QLDS>(a.corpus, ids[j], j2 < hi ? (int64_t)ids[j2] : -1, qs, qv, a.d, a.dpad,
+                                            lane, s0, s1);
+        if (lane == 0) {
+            sc[j] = s0;
+            if (j2 < hi) sc[j2] = s1;
+        }
+    }
+}
+
+// bitonic sort of (sc, ids)[0, n2) best first (n2 a power of two, padding = worst)
+__device__ __forceinline__ void rfw_sort(double* sc, uint32_t* ids, int n2) {
+    for (int size = 2; size <= n2; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int i = threadIdx.x; i < n2; i += blockDim.x) {
+                const int j = i ^ stride;
+                if (j > i) {
+                    const bool up = (i & size) == 0;
+                    const double si = sc[i], sj = sc[j];
+                    const uint32_t ii = ids[i], ij = ids[j];
+                    const bool jb = better_exact(sj, ij, si, ii, METRIC_IP);
+                    if (up ? jb : !jb) {
+                        sc[i] = sj; sc[j] = si;
+                        ids[i] = ij; ids[j] = ii;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+template <int DT, bool QLDS>
+__global__ void __launch_bounds__(RF_THREADS) k_refine_wide(RefineArgs a, int KA) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    double* sc = (double*)smem;                                  // [RFW_CAP]
+    uint32_t* ids = (uint32_t*)(smem + (size_t)RFW_CAP * 8);     // [RFW_CAP]
+    double* qs = (double*)(smem + (size_t)RFW_CAP * 12);         // fp64 query, transposed groups
+    __shared__ int red[RF_THREADS / 64];
+    __shared__ int nb_s;
+    const int q = blockIdx.x, tid = threadIdx.x;
+    const int ng = (a.d + 7) >> 3;
+    const u64* src = a.cand + (size_t)q * a.lcap;
+    const int n = min(a.cand_n[q], a.lcap);
+    const float* qv = a.q + (int64_t)q * a.d;
+    if constexpr (QLDS)
+        for (int i = tid; i < a.d; i += RF_THREADS) qs[(i & 7) * ng + (i >> 3)] = (double)qv[i];
+    const double eps = (double)a.qeps[q];
+    const double worst = -INFINITY;
+    // ---- phase A: the best KA keys ----
+    u64 keys[RF_E];
+    const bool inreg = n <= RF_THREADS * RF_E;
+#pragma unroll
+    for (int e = 0; e < RF_E; ++e) {
+        const int j = tid + RF_THREADS * e;
+        keys[e] = (inreg && j < n) ? src[j] : 0ull;
+    }
+    u64 tA = 1ull;  // keys >= tA form phase A
+    if (n > KA) tA = inreg ? block_kth<RF_E>(keys, KA, red) : block_kth_mem(src, n, KA, red);
+    int nA;
+    if (inreg) {
+        nA = block_write_ids<RF_E>(keys, tA, ~0ull, ids, RFW_CAP, red);
+    } else {  // very long lists: the phase-A set from memory (block_compact_mem writes keys)
+        nA = 0;
+        for (int r0 = 0; r0 < n; r0 += RF_THREADS) {
+            const int j = r0 + tid;
+            const u64 k = j < n ? src[j] : 0ull;
+            const bool keep = k >= tA;
+            const u64 m = __ballot(keep);
+            if ((tid & 63) == 0) red[tid >> 6] = __popcll(m);
+            __syncthreads();
+            int wb = 0, tot = 0;
+            for (int i = 0; i < RF_THREADS / 64; ++i) {
+                if (i < (tid >> 6)) wb += red[i];
+                tot += red[i];
+            }
+            __syncthreads();
+            const int pos = nA + wb + lane_prefix(m);
+            if (keep && pos < RFW_CAP) ids[pos] = key_id(k);
+            nA += tot;
+        }
+    }
+    nA = min(nA, RFW_CAP);
+    __syncthreads();
+    rfw_score<DT, QLDS>(a, ids, sc, 0, nA, qs, qv);
+    __syncthreads();
+    int nA2 = 1;
+    while (nA2 < nA) nA2 <<= 1;
+    for (int j = nA + tid; j < nA2; j += RF_THREADS) {
+        sc[j] = worst;
+        ids[j] = 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    rfw_sort(sc, ids, nA2);  // phase A best first (nA2 <= RFW_CAP: KA <= RFW_CAP / 2)
+    const double Tp = nA >= a.k ? sc[a.k - 1] : -INFINITY;
+    // ---- phase B: keys in [tB, tA) whose bound reaches T' ----
+    u64 tB = 1ull;
+    if (Tp > -INFINITY) {
+        float f = (float)(Tp - eps);
+        if ((double)f > Tp - eps) f = nextafterf(f, -INFINITY);  // round down: keys below tB score < T' - eps
+        tB = (u64)ord_f32(f) << 32;
+        if (tB == 0ull) tB = 1ull;
+    }
+    int nB = 0;
+    if (tB < tA) {
+        if (inreg) {
+            nB = block_write_ids<RF_E>(keys, tB, tA, ids + nA2, RFW_CAP - nA2, red);
+        } else {
+            for (int r0 = 0; r0 < n; r0 += RF_THREADS) {
+                const int j = r0 + tid;
+                const u64 k = j < n ? src[j] : 0ull;
+                const bool keep = k >= tB && k < tA;
+                const u64 m = __ballot(keep);
+                if ((tid & 63) == 0) red[tid >> 6] = __popcll(m);
+                __syncthreads();
+                int wb = 0, tot = 0;
+                for (int i = 0; i < RF_THREADS / 64; ++i) {
+                    if (i < (tid >> 6)) wb += red[i];
+                    tot += red[i];
+                }
+                __syncthreads();
+                const int pos = nB + wb + lane_prefix(m);
+                if (keep && pos < RFW_CAP - nA2) ids[nA2 + pos] = key_id(k);
+                nB += tot;
+            }
+        }
+    }
+    const bool overflow = nA2 + nB > RFW_CAP;
+    nB = min(nB, RFW_CAP - nA2);
+    __syncthreads();
+    rfw_score<DT, QLDS>(a, ids, sc, nA2, nA2 + nB, qs, qv);
+    __syncthreads();
+    // phase-B rows that beat T' join the phase-A list (order-preserving compaction in place)
+    if (tid == 0) nb_s = 0;
+    __syncthreads();
+    for (int r0 = 0; r0 < nB; r0 += RF_THREADS) {
+        const int j = r0 + tid;
+        const bool keep = j < nB && !(sc[nA2 + j] < Tp);  // >= T' (T' = -inf: every row)
+        const double s = keep ? sc[nA2 + j] : 0.0;
+        const uint32_t id = keep ? ids[nA2 + j] : 0u;
+        const u64 m = __ballot(keep);
+        if ((tid & 63) == 0) red[tid >> 6] = __popcll(m);
+        __syncthreads();
+        int wb = 0, tot = 0;
+        for (int i = 0; i < RF_THREADS / 64; ++i) {
+            if (i < (tid >> 6)) wb += red[i];
+            tot += red[i];
+        }
+        const int base = nb_s;
+        __syncthreads();
+        if (keep) {
+            const int pos = nA + base + wb + lane_prefix(m);
+            sc[pos] = s;
+            ids[pos] = id;
+        }
+        if (tid == 0) nb_s = base + tot;
+        __syncthreads();
+    }
+    const int nF = nA + nb_s;
+    int nF2 = 1;
+    while (nF2 < nF) nF2 <<= 1;
+    for (int j = nF + tid; j < nF2; j += RF_THREADS) {
+        sc[j] = worst;
+        ids[j] = 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    if (nb_s > 0) rfw_sort(sc, ids, nF2);
+    // ---- certificate ----
+    if (tid == 0) {
+        u64 th = a.drop ? a.drop[q] : 0ull;
+        if (a.thr0 && a.thr0[q] > th) th = a.thr0[q];
+        int cert = overflow ? 0 : 1;
+        if (cert && th != 0ull) {  // some rows were never listed
+            const double T = nF >= a.k ? sc[a.k - 1] : -INFINITY;
+            cert = ((double)key_score(th) + eps < T) ? 1 : 0;
+        }
+        if (a.cert) a.cert[q] = cert;
+        if (!cert && a.uncert) atomicAdd(a.uncert, 1u);
+    }
+    for (int j = tid; j < a.k; j += RF_THREADS) {
+        const size_t o = (size_t)q * a.k + j;
+        if (j < nF) {
+            if (a.D) a.D[o] = (float)sc[j];
+            a.I[o] = (int64_t)ids[j] + a.id_offset;
+            if (a.S64) a.S64[o] = sc[j];
+        } else {
+            if (a.D) a.D[o] = -3.402823466e+38f;
+            a.I[o] = -1;
+            if (a.S64) a.S64[o] = -1.7976931348623157e308;
+        }
+    }
+}
+
 // seed threshold from 16-row group maxima (one block per query): the rank-th largest maximum T
 // has `rank` DISTINCT rows scoring >= T, so T never exceeds the true rank-th best screen score and
 // the key just below every score >= T, (ord(T) << 32) | 0, is a valid starting threshold
@@ -1926,6 +2304,27 @@ hipError_t launch_pack_qtile(int dt, const float* q, int nqb, int d, int dpad, u
     return hipGetLastError();
 }
 
+hipError_t launch_quant_rows(int dt, const uint8_t* data, int dpad, int64_t r0, int64_t n, int d, uint8_t* data8,
+                             int dpad8, uint32_t* rsb, unsigned* maxes, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    const int64_t CHUNK = 1 << 22;  // rows per launch (grid-size bound)
+    for (int64_t c0 = 0; c0 < n; c0 += CHUNK) {
+        const int64_t m = n - c0 < CHUNK ? n - c0 : CHUNK;
+        VS_DISPATCH_DT(dt, k_quant_rows, dim3(blocks4(m)), dim3(256), 0, st, data, dpad, r0 + c0, m, d, data8, dpad8,
+                       rsb, maxes);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+hipError_t launch_pack_qtile_i8(const float* q, int nqb, int d, int dpad8, uint8_t* qt, float2* qfac, float* qeps,
+                                const unsigned* maxes, int* gcnt, u64* drop, hipStream_t st) {
+    hipLaunchKernelGGL(k_pack_qtile_i8, dim3(MFMA_QB / 4), dim3(256), 0, st, q, nqb, d, dpad8, qt, qfac, qeps, maxes,
+                       gcnt, drop);
+    return hipGetLastError();
+}
+
 hipError_t launch_pack_qf32(const float* q, int nqb, int nqpad, int d, int dpad, float* qp, float* qinfo,
                             hipStream_t st, int* ctr) {
     hipLaunchKernelGGL(k_pack_qf32, dim3(blocks4(nqpad)), dim3(256), 0, st, q, nqb, nqpad, d, dpad, qp, qinfo, ctr);
@@ -1945,7 +2344,7 @@ static void launch_mfma_one(const ScreenArgs& a, const uint8_t* qt, int nqb, hip
 template <bool SEED>
 static hipError_t launch_mfma_dt(int dt, const ScreenArgs& a, const uint8_t* qt, int nqb, hipStream_t st) {
     if (dt == DT_I8) {
-        if (a.metric != METRIC_IP || !a.rscale || !a.rbeta || !a.qfac) return hipErrorInvalidValue;
+        if (a.metric != METRIC_IP || !a.rsb || !a.qfac) return hipErrorInvalidValue;
         launch_mfma_one<DT_I8, METRIC_IP, SEED>(a, qt, nqb, st);
     } else if (dt == DT_BF16) {
         if (a.metric == METRIC_IP) launch_mfma_one<DT_BF16, METRIC_IP, SEED>(a, qt, nqb, st);
@@ -2040,6 +2439,37 @@ hipError_t launch_refine(const RefineArgs& a, int nq, hipStream_t st) {
     if (a.dt == DT_F32) launch_refine_dt<DT_F32>(a, nq, KP2, lds, qlds, st);
     else if (a.dt == DT_BF16) launch_refine_dt<DT_BF16>(a, nq, KP2, lds, qlds, st);
     else launch_refine_dt<DT_F16>(a, nq, KP2, lds, qlds, st);
+    return hipGetLastError();
+}
+
+template <int DT, bool QLDS>
+static void launch_refine_wide_one(const RefineArgs& a, int nq, int KA, size_t lds, hipStream_t st) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_refine_wide<DT, QLDS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  152 * 1024);
+        (void)hipGetLastError();
+        attr = true;
+    }
+    hipLaunchKernelGGL((k_refine_wide<DT, QLDS>), dim3(nq), dim3(RF_THREADS), lds, st, a, KA);
+}
+
+hipError_t launch_refine_wide(const RefineArgs& a, int nq, int KA, hipStream_t st) {
+    if (a.metric != METRIC_IP || !a.qeps || !a.cand_n || KA <= 0 || 2 * KA > RFW_CAP) return hipErrorInvalidValue;
+    const size_t base = (size_t)RFW_CAP * 12;
+    const size_t qbytes = (size_t)((a.d + 7) >> 3) * 64;
+    const bool qlds = base + qbytes <= 148 * 1024;
+    const size_t lds = qlds ? base + qbytes : base;
+    if (a.dt == DT_F32) {
+        if (qlds) launch_refine_wide_one<DT_F32, true>(a, nq, KA, lds, st);
+        else launch_refine_wide_one<DT_F32, false>(a, nq, KA, lds, st);
+    } else if (a.dt == DT_BF16) {
+        if (qlds) launch_refine_wide_one<DT_BF16, true>(a, nq, KA, lds, st);
+        else launch_refine_wide_one<DT_BF16, false>(a, nq, KA, lds, st);
+    } else {
+        if (qlds) launch_refine_wide_one<DT_F16, true>(a, nq, KA, lds, st);
+        else launch_refine_wide_one<DT_F16, false>(a, nq, KA, lds, st);
+    }
     return hipGetLastError();
 }
 

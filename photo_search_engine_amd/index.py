@@ -87,6 +87,21 @@ class FlatIndex:
     def reset(self) -> None:
         check(self._L.vs_reset(self._h))
 
+    # -- screen selection ----------------------------------------------------------------------
+    SCREENS = {"native": 0, "int8": 1}
+
+    def set_screen(self, screen: str) -> None:
+        """``"int8"``: keep an int8 copy of the rows and screen query batches with int8 MFMAs under
+        a proven error bound (exact results, include/vs.h); ``"native"``: screen the stored rows."""
+        if screen not in self.SCREENS:
+            raise ValueError(f"unknown screen {screen!r}")
+        check(self._L.vs_set_screen(self._h, self.SCREENS[screen]))
+
+    @property
+    def screen(self) -> str:
+        v = int(self._L.vs_screen(self._h))
+        return {0: "native", 1: "int8"}.get(v, "unknown")
+
     # -- persistence (faiss read_index / write_index payloads, streamed file <-> HBM) ---------------
     def add_from_file(self, path: str, byte_offset: int, n: int) -> None:
         """Append rows [0, n) of the row-major fp32 payload at ``byte_offset`` of ``path``."""
@@ -121,7 +136,7 @@ class FlatIndex:
         buf = (ctypes.c_float * cap)()
         kind = ctypes.c_int(0)
         n = check(self._L.vs_timing_fetch(self._h, buf, cap, ctypes.byref(kind)))
-        return [float(buf[i]) for i in range(n)], {1: "mfma", 2: "gemv"}.get(kind.value, "none")
+        return [float(buf[i]) for i in range(n)], {1: "mfma", 2: "gemv", 3: "mfma_i8"}.get(kind.value, "none")
 
     def uncertified_count(self) -> int:
         return int(check(self._L.vs_uncertified_count(self._h)))

@@ -81,8 +81,12 @@ def main():
         if "GRBM_GUI_ACTIVE" in flat and flat.get("dur_s"):
             flat["clock_ghz"] = flat["GRBM_GUI_ACTIVE"] / 8 / flat["dur_s"] / 1e9
         summary["kernels"][f"{name} grid={grid}"] = flat
-    # the dominant screen launch (largest mean duration among k_screen_*)
-    screens = {k: v for k, v in summary["kernels"].items() if "k_screen" in k and v.get("dur_s")}
+    # the bench's dominant screen (its roofline kernel; the seed pass's <.., true> variant excluded)
+    kind = (bench_line or {}).get("roofline", {}).get("kernel", "")
+    pat = {"k_screen_mfma_i8": "k_screen_mfma<3,", "k_screen_mfma": "k_screen_mfma<", "k_screen_gemv": "k_screen_gemv"}
+    screens = {k: v for k, v in summary["kernels"].items()
+               if pat.get(kind, "k_screen") in k and "true>" not in k and v.get("dur_s")
+               and not (kind == "k_screen_mfma" and "k_screen_mfma<3," in k)}
     if screens and bench_line and bench_line["config"]["workload"] != "cfg5":
         top = max(screens, key=lambda k: screens[k]["dur_s"])
         t = screens[top]
@@ -94,7 +98,8 @@ def main():
                    "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
                    "profiled_kernel_ms": t["dur_s"] * 1e3, "clock_ghz": t.get("clock_ghz"),
                    "source": f"profiles/{tag}_pmc.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes)"}
-        with open(os.path.join(prof, f"traffic_{cfg['workload']}.json"), "w") as f:
+        suffix = "" if cfg["n_local"] == cfg.get("N") else f"_n{cfg['n_local']}"
+        with open(os.path.join(prof, f"traffic_{cfg['workload']}_{kind.replace('k_screen_', '')}{suffix}.json"), "w") as f:
             json.dump(traffic, f, indent=1)
         summary["dominant"] = traffic
     # IVF (cfg5): one search launches k_ivf_scan once per query-count class; traffic per search =
@@ -114,7 +119,7 @@ def main():
                    "hbm_bytes_per_launch": rd + wr, "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
                    "profiled_kernel_ms": scan_ns * 1e-6 / searches,
                    "source": f"profiles/{tag}_pmc.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes)"}
-        with open(os.path.join(prof, "traffic_cfg5.json"), "w") as f:
+        with open(os.path.join(prof, "traffic_cfg5_ivf_scan.json"), "w") as f:
             json.dump(traffic, f, indent=1)
         summary["dominant"] = traffic
     with open(os.path.join(prof, f"{tag}_pmc.json"), "w") as f:
