@@ -20,6 +20,7 @@
 namespace vs {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef int intx4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
@@ -529,7 +530,7 @@ __global__ void __launch_bounds__(256) k_quant_rows(const uint8_t* __restrict__ 
 }
 
 // int8 query tile [nks8][256][64] (codes of q / t_q, t_q = max|q| / 127) for the int8 MFMA screen,
-// one wave per query.  qfac = (t_q, ||q|| rounded up); qeps = the query-side margin of the
+// one wave per query.  qfac = (t_q, ||q|| rounded up / t_q); qeps = the query-side margin of the
 // screen key (key = s_x t_q <c_x, c_q> + beta_x ||q||, see k_screen_mfma):
 //   true <x, q> <= key + ||s_x c_x|| ||q - t_q c_q|| + rounding <= key_score + qeps.
 // Also zeroes the survivor-list lengths and the workgroup drop bounds of the screen that follows.
@@ -568,10 +569,12 @@ __global__ void __launch_bounds__(256) k_pack_qtile_i8(const float* __restrict__
         const double eq = sqrt(e2) * (1.0 + 1e-9);
         const double qh = sqrt(c2) * (double)t * (1.0 + 1e-9);  // ||t_q c_q||
         const double X = (double)__uint_as_float(maxes[0]), B = (double)__uint_as_float(maxes[1]);
-        // the key's fp32 evaluation fl(fl(fl(acc) * fl(s t)) + beta qn): <= 5 roundings relative
-        // 2^-24 of |sigma| + beta qn, |sigma| <= X ||t_q c_q||
-        const double slop = 5.0 * 5.9604644775390625e-08 * (X * qh + B * (double)qn) + 1e-30;
-        qfac[r] = make_float2(t, qn);
+        // the key's fp32 evaluation t * fma(beta, fl(qn / t), fl(s * fl(acc))): <= 6 roundings
+        // relative 2^-24 of |sigma| + beta qn (|sigma| <= X ||t_q c_q||); 8 of them budgeted
+        const double slop = 8.0 * 5.9604644775390625e-08 * (X * qh + B * (double)qn) + 1e-30;
+        // the screen computes key = t_q * (s_x acc + beta_x * (||q|| / t_q)); a zero query has t_q = 0
+        // and every key 0
+        qfac[r] = make_float2(t, t > 0.0f ? qn / t : 0.0f);
         qeps[r] = f32_up((X * eq + slop) * (1.0 + 1e-9));
     }
 }
@@ -883,29 +886,49 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
 #pragma unroll
         for (int ni = 0; ni < 8; ++ni) {
             const int q = q0 + ni * 16;
-            float tq = 0.0f, qn = 0.0f;
+            // int8: values in the query's scaled domain v = s_x <c_x, c_q> + beta_x ||q|| / t_q (one
+            // convert, one multiply, one fma per value, in packed pairs); the key is t_q * v
+            float tq = 1.0f;
+            float v[4][4];
             if constexpr (I8) {
                 const float2 f = qfac[q];
                 tq = f.x;
-                qn = f.y;
+                const floatx2 u2 = {f.y, f.y};
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const floatx2 av = {(float)__float_as_int(acc[mi][ni][2 * h]),
+                                            (float)__float_as_int(acc[mi][ni][2 * h + 1])};
+                        const floatx2 s2 = {sq[mi][2 * h], sq[mi][2 * h + 1]};
+                        const floatx2 b2 = {rb[mi][2 * h], rb[mi][2 * h + 1]};
+                        const floatx2 vv = __builtin_elementwise_fma(b2, u2, av * s2);
+                        v[mi][2 * h] = vv.x;
+                        v[mi][2 * h + 1] = vv.y;
+                    }
+            } else {
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        float sc = acc[mi][ni][r];
+                        if constexpr (METRIC == METRIC_L2) sc = 2.0f * sc - sq[mi][r];
+                        v[mi][r] = sc;
+                    }
             }
-            float v[4][4];
+            if (bad) {  // the shard's last tile only
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (bad & (1u << (mi * 4 + r))) v[mi][r] = __builtin_nanf("");
+            }
             float mx = -INFINITY;
 #pragma unroll
             for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    float sc;
-                    if constexpr (I8) {
-                        sc = fmaf(rb[mi][r], qn, (float)__float_as_int(acc[mi][ni][r]) * (sq[mi][r] * tq));
-                    } else {
-                        sc = acc[mi][ni][r];
-                        if constexpr (METRIC == METRIC_L2) sc = 2.0f * sc - sq[mi][r];
-                    }
-                    if (bad & (1u << (mi * 4 + r))) sc = __builtin_nanf("");
-                    v[mi][r] = sc;
-                    mx = fmaxf(mx, sc);
-                }
+                for (int r = 0; r < 4; ++r) mx = fmaxf(mx, v[mi][r]);
+            if constexpr (I8) mx *= tq;  // monotone: fl(t * max v) = max fl(t * v)
             // one compare per query column; the insert path runs only where something passes,
             // and then costs one LDS atomic per lane plus predicated stores
             if constexpr (SEED) {  // group g = wm*4 + lane/16 of the tile: 16 distinct rows
@@ -919,7 +942,10 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
 #pragma unroll
                 for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) m |= (v[mi][r] >= tf ? 1u : 0u) << (mi * 4 + r);  // ties below
+                    for (int r = 0; r < 4; ++r) {
+                        if constexpr (I8) v[mi][r] *= tq;  // the keys' scores
+                        m |= (v[mi][r] >= tf ? 1u : 0u) << (mi * 4 + r);  // ties below
+                    }
                 if (m) flag[2 + (ti & 1)] = 1;
                 // Compact insert loop (not unrolled: an unrolled insert path for 8 columns x 16
                 // values costs more in instruction fetch than the rare inserts themselves).  The

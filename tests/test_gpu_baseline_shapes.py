@@ -115,6 +115,10 @@ def test_cfg3_full_shape_vs_faiss32(FlatIndex):
     ix.add_synthetic(O.SEED_CORPUS, 0, N, True)
     q = O.synth_rows(O.SEED_QUERIES, 0, nq, d, True, "bf16")
     D, I = ix.search(q, k)
+    ix.set_screen("int8")  # the bench's default screen at this shape: the same exact answer
+    D8, I8 = ix.search(q, k)
+    np.testing.assert_array_equal(I8, I)
+    np.testing.assert_array_equal(D8, D)
     assert ix.uncertified_count() == 0
     ix.close()
     x = O.synth_rows(O.SEED_CORPUS, 0, N, d, True, "bf16")  # the stored values, upcast (61 GB)
