@@ -69,6 +69,8 @@ def parse():
     ap.add_argument("--zero-corpus", action="store_true",
                     help="diagnostic only: all-zero corpus rows (DVFS/power test with VS_MF_ABLATE=9; results meaningless)")
     ap.add_argument("--no-recall", action="store_true", help="cfg5: skip the exact ground truth (profiling runs)")
+    ap.add_argument("--skew", type=float, default=0.0,
+                    help="cfg5: Zipf exponent of the cluster sizes (0 = equal-sized clusters; 1.1 = a heavy head)")
     ap.add_argument("--iso-data", action="store_true",
                     help="cfg5: isotropic rows (the flat bench's data) instead of the Gaussian mixture")
     ap.add_argument("--traffic-file", default=None,
@@ -252,10 +254,26 @@ def _host_mem_bytes() -> int:
         return 0
 
 
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline_and_recall(args, N, d, dtype, nq, k, local, torch, gpu_full):
     """CPU baseline: the faiss IndexFlatIP fp32 restatement (oracle/vs_oracle.c, OpenMP) on this
-    host's cores over the corpus (whole corpus by default: ~5 s of 16-thread work at cfg3, so no
-    extrapolation), plus recall@10 / exact-match of the GPU path against it on the same rows."""
+    host's cores, over the whole corpus when it fits the host-memory budget (cfg3: ~7 s of 16-thread
+    work, so no extrapolation), else a leading row sample scaled by N / rows; plus recall@10 and the
+    exact-id match of the GPU path against it on the same rows (the GPU re-searches the sample when
+    it is not the whole corpus).  Batches of >= 20 queries take faiss' BLAS path on all threads;
+    single queries take faiss' sequential scan, which runs on ONE thread (faiss parallelises that path
+    over queries only), so batch=1 workloads report the one-thread rate and, beside it, the rate of
+    `threads` concurrent single-query calls.  Every line also carries one single query's latency."""
     from oracle import oracle as O
     from photo_search_engine_amd.index import FlatIndex
 
@@ -272,12 +290,30 @@ def cpu_baseline_and_recall(args, N, d, dtype, nq, k, local, torch, gpu_full):
     x = O.synth_rows(SEED_CORPUS, 0, ns, d, True, dtype)  # the GPU's stored values, upcast to fp32
     t_gen = time.perf_counter() - t0
     q = O.synth_rows(SEED_QUERIES, 0, nq, d, True, dtype)
-    O.knn_faiss_fp32(x[:1000], q[:2], 5, "ip", threads)  # warm
+    O.knn_faiss_fp32(x[:1000], q[:1], 5, "ip", 1)  # warm
+    scale = N / ns
+    # one query through faiss' sequential scan (one thread), scaled to the whole corpus
     t0 = time.perf_counter()
-    Dc, Ic = O.knn_faiss_fp32(x, q, k, "ip", threads)
-    tc = time.perf_counter() - t0
+    D1, I1 = O.knn_faiss_fp32(x, q[:1], k, "ip", 1)
+    t1 = (time.perf_counter() - t0) * scale
+    if nq == 1:
+        qm = O.synth_rows(SEED_QUERIES, 0, threads, d, True, dtype)
+        t0 = time.perf_counter()
+        O.knn_faiss_fp32(x, qm, k, "ip", threads)  # `threads` single queries at once (< 20: sequential path)
+        tm = (time.perf_counter() - t0) * scale
+        Dc, Ic = D1, I1
+        cpu_qps, used = 1.0 / t1, 1
+        how = (f"faiss IndexFlatIP fp32 restatement (oracle/vs_oracle.c), single query: faiss' sequential scan on one "
+               f"thread, {t1 * 1e3:.1f} ms per query; {threads} concurrent single-query scans on {threads} threads: "
+               f"{threads / tm:.2f} queries/s")
+    else:
+        t0 = time.perf_counter()
+        Dc, Ic = O.knn_faiss_fp32(x, q, k, "ip", threads)
+        tc = (time.perf_counter() - t0) * scale
+        cpu_qps, used = nq / tc, threads
+        how = (f"faiss IndexFlatIP fp32 restatement (oracle/vs_oracle.c: blocked fp32 GEMM + per-thread heaps, "
+               f"{threads} OpenMP threads) for the same {nq} queries (k={k}): {tc:.2f} s of search")
     del x
-    cpu_qps_full = nq / (tc * (N / ns))
     if ns == N:
         Dg, Ig = gpu_full
     else:  # GPU on the same sample
@@ -285,20 +321,20 @@ def cpu_baseline_and_recall(args, N, d, dtype, nq, k, local, torch, gpu_full):
         ix.add_synthetic(SEED_CORPUS, 0, ns, True)
         Dg, Ig = ix.search(q, k)
         ix.close()
-    rec10 = O.recall_at(Ig, Ic, 10)
+    rec10 = O.recall_at(Ig, Ic, min(10, k))
     exact_match = float(np.mean(Ig == Ic))
     max_err = float(np.max(np.abs(Dg.astype(np.float64) - Dc)))
-    scope = "the whole corpus" if ns == N else f"the first {ns} rows, scaled by N/{ns}"
-    cpu = {"value": round(cpu_qps_full, 3), "unit": "queries/s", "cores": threads, "kind": "port",
-           "sample": f"faiss IndexFlatIP fp32 restatement (oracle/vs_oracle.c: blocked fp32 GEMM + per-thread heaps, "
-                     f"{threads} OpenMP threads) over {scope} ({ns} x {d}) for the same {nq} queries (k={k}): "
-                     f"{tc:.2f} s of search (+{t_gen:.1f} s to generate the rows, untimed)"}
+    scope = "the whole corpus" if ns == N else f"the first {ns} rows, timings scaled by N/{ns}"
+    cpu = {"value": round(cpu_qps, 3), "unit": "queries/s", "cores": used, "kind": "port",
+           "cpu_model": _cpu_model(), "host_threads": threads,
+           "latency_nq1_ms": round(t1 * 1e3, 2),
+           "sample": f"{how}; over {scope} ({ns} x {d}); +{t_gen:.1f} s to generate the rows, untimed"}
     parity = {"rows": ns, "exact_id_match_vs_faiss32": round(exact_match, 6),
               "max_abs_score_err_vs_faiss32": max_err}
     return cpu, round(rec10, 6), parity
 
 
-def _traffic(path, workload: str, n_local: int, kind: str = ""):
+def _traffic(path, workload: str, n_local: int, kind: str = "", skew: float = 0.0):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary of this
     configuration (profiles/traffic_<workload>_<kind>[_n<rows>].json, scripts/prof_summary.py)."""
     import glob
@@ -309,7 +345,7 @@ def _traffic(path, workload: str, n_local: int, kind: str = ""):
                 tr = json.load(f)
         except (OSError, ValueError):
             continue
-        if tr.get("workload") == workload and tr.get("n_local") == n_local:
+        if tr.get("workload") == workload and tr.get("n_local") == n_local and float(tr.get("skew", 0.0)) == skew:
             return tr.get("hbm_bytes_per_launch")
     return None
 
@@ -342,18 +378,25 @@ class _heartbeat:
         _progress(f"{self.msg}: done")
 
 
-def _mixture_rows(seed, r0, m, d, centroids, sigma, dev, stream):
+def _mixture_rows(seed, r0, m, d, centroids, sigma, dev, stream, cdf=None):
     """Synthetic IVF corpus / query rows: a Gaussian mixture over the coarse centroids (the data
-    model IVF exists for).  Row i = normalise(c[h(i) mod nlist] + sigma * g_i), g_i the unit
-    counter-hash Gaussian row i of `seed` (bit-identical generator of oracle/vs_oracle.c), h a
-    multiplicative hash.  Deterministic: elementwise torch ops + the row norm on the same device."""
+    model IVF exists for).  Row i = normalise(c[cid(i)] + sigma * g_i), g_i the unit counter-hash
+    Gaussian row i of `seed` (bit-identical generator of oracle/vs_oracle.c).  cid(i) = h(i) mod
+    nlist for equal-sized clusters (h a multiplicative hash), or, with `cdf` (the cumulative cluster
+    weights), the inverse CDF of the hashed uniform h(i) / 2^31: Zipf-sized clusters.
+    Deterministic: elementwise torch ops + the row norm on the same device."""
     import torch
 
     from photo_search_engine_amd.index import synthesize_device
     g = torch.empty((m, d), dtype=torch.float32, device=dev)
     synthesize_device(dev.index, seed, r0, m, d, g.data_ptr(), True, "f32", stream)
     rows = torch.arange(r0, r0 + m, dtype=torch.int64, device=dev)
-    cid = ((rows * 2654435761) >> 7) % centroids.shape[0]
+    h = ((rows * 2654435761) >> 7)
+    if cdf is None:
+        cid = h % centroids.shape[0]
+    else:
+        u = ((h * 0x9E3779B1) & 0x7FFFFFFF).to(torch.float64) / 2147483648.0
+        cid = torch.clamp(torch.searchsorted(cdf, u), max=centroids.shape[0] - 1)
     x = centroids[cid] + sigma * g
     return x / torch.linalg.vector_norm(x, dim=1, keepdim=True)
 
@@ -389,8 +432,15 @@ def run_ivf(args):
     torch.cuda.synchronize()
     ix.set_centroids(c.cpu().numpy())
 
+    cdf = None
+    if args.skew > 0:  # Zipf(skew) cluster weights over a seeded permutation of the centroids
+        rng = np.random.default_rng(SEED_CENTROIDS)
+        w = 1.0 / np.arange(1, nlist + 1, dtype=np.float64) ** args.skew
+        w = w[rng.permutation(nlist)]
+        cdf = torch.from_numpy(np.cumsum(w) / w.sum()).to(dev)
+
     def corpus_chunk(r0, m):
-        return _mixture_rows(SEED_CORPUS, r0, m, d, c, sigma, dev, stream)
+        return _mixture_rows(SEED_CORPUS, r0, m, d, c, sigma, dev, stream, cdf)
 
     if args.iso_data:
         with _heartbeat(f"cfg5 build (isotropic rows): assigning and packing {N} rows"):
@@ -404,7 +454,7 @@ def run_ivf(args):
                 x = corpus_chunk(r0, min(chunk, N - r0))
                 ix.add_device(x.data_ptr(), x.shape[0], stream)
                 del x
-        q = _mixture_rows(SEED_QUERIES, 0, nq, d, c, sigma, dev, stream).contiguous()
+        q = _mixture_rows(SEED_QUERIES, 0, nq, d, c, sigma, dev, stream, cdf).contiguous()
     D = torch.empty((nq, k), dtype=torch.float32, device=dev)
     I = torch.empty((nq, k), dtype=torch.int64, device=dev)
     S = torch.empty((nq, k), dtype=torch.float64, device=dev)
@@ -499,8 +549,9 @@ def run_ivf(args):
                           f"flat-row score {float(xi.astype(np.float64) @ qh[a].astype(np.float64)):.9f}  "
                           f"gen row[:3] {corpus_chunk(i, 1).cpu().numpy()[0, :3].tolist()} flat row[:3] {xi[:3].tolist()}")
     data = ("synthetic isotropic (counter-hash N(0,1) rows, L2-normalised, seeds 20260417/20260418)" if args.iso_data
-            else f"synthetic Gaussian mixture: normalise(centroid[hash(i) % {nlist}] + {sigma} * unit counter-hash "
-                 "Gaussian row i), seeds 20260417 (rows) / 20260418 (queries) / 20260419 (centroids)")
+            else f"synthetic Gaussian mixture: normalise(centroid[cid(i)] + {sigma} * unit counter-hash Gaussian row i), "
+                 + (f"Zipf({args.skew}) cluster sizes" if args.skew > 0 else f"cid = hash(i) % {nlist}")
+                 + ", seeds 20260417 (rows) / 20260418 (queries) / 20260419 (centroids)")
     out = {
         "metric": f"kNN queries/sec + recall@10 vs exact flat, IVF-Flat nlist={nlist} nprobe={nprobe} N=50M d=1536 batch=256",
         "value": round(nq * args.steps / elapsed, 2),
@@ -516,6 +567,7 @@ def run_ivf(args):
         "data": data,
         "config": {"workload": args.workload, "desc": desc, "N": N, "d": d, "batch": nq, "k": k, "nlist": nlist,
                    "nprobe": nprobe, "list_rows_min_max": [int(sizes.min()), int(sizes.max())],
+                   "list_rows_median": int(np.median(sizes)), "skew": args.skew,
                    "parallelism": "1 GPU"},
         "roofline": {
             "kernel": "k_ivf_scan",
@@ -524,7 +576,7 @@ def run_ivf(args):
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": _traffic(None, "cfg5", N, "ivf_scan"),
+            "traffic": _traffic(None, "cfg5", N, "ivf_scan", args.skew),
             "kernel_ms": round(kavg, 4),
             "alg_bytes_per_launch": alg_bytes,
         },
@@ -534,18 +586,25 @@ def run_ivf(args):
         "probed_recall@10": round(got / max(need, 1), 6) if parts_S else None,
     }
     if not args.no_cpu_baseline:
-        out["cpu_baseline"] = ivf_cpu_baseline(d, dtype, qh, k, pairs)
+        out["cpu_baseline"] = ivf_cpu_baseline(d, dtype, qh, k, pairs, ix.centroids(), nprobe)
     print(json.dumps(out), flush=True)
     ix.close()
 
 
-def ivf_cpu_baseline(d, dtype, qh, k, pairs):
-    """faiss IndexIVFFlat's scan restated on the host (oracle/vs_oracle.c fp32 sequential scan, one
-    query per OpenMP thread as faiss parallelises IVF search over queries), timed on a contiguous
-    row sample and scaled to the batch's (row, query) pair count."""
+def ivf_cpu_baseline(d, dtype, qh, k, pairs, centroids, nprobe):
+    """faiss IndexIVFFlat search restated on the host: the coarse probe (the faiss fp32 flat
+    restatement over the centroids, BLAS path, all threads) timed in full, plus the list scans
+    (oracle/vs_oracle.c fp32 sequential scan, one query per OpenMP thread as faiss parallelises IVF
+    search over queries) timed on a contiguous row sample and scaled to the batch's (row, query)
+    pair count."""
     from oracle import oracle as O
     cores = len(os.sched_getaffinity(0))
     threads = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores) or cores), 16)
+    qa = np.ascontiguousarray(qh, dtype=np.float32)
+    O.knn_faiss_fp32(centroids[:256], qa[:32], 4, "ip", threads)  # warm
+    t0 = time.perf_counter()
+    O.knn_faiss_fp32(np.ascontiguousarray(centroids), qa, nprobe, "ip", threads)
+    t_probe = time.perf_counter() - t0
     R = 400_000
     x = O.synth_rows(SEED_CORPUS, 0, R, d, True, dtype)
     qs = np.ascontiguousarray(qh[:threads])
@@ -555,10 +614,14 @@ def ivf_cpu_baseline(d, dtype, qh, k, pairs):
     t = time.perf_counter() - t0
     rate = R * qs.shape[0] / t  # (row, query) pairs per second
     nq = qh.shape[0]
-    return {"value": round(nq / (pairs / rate), 3), "unit": "queries/s", "cores": threads, "kind": "port",
-            "sample": f"IVF list scan restated (oracle/vs_oracle.c fp32 sequential scan, {threads} queries on "
-                      f"{threads} OpenMP threads) over {R} rows in {t:.2f} s = {rate / 1e6:.1f} M row-query pairs/s, "
-                      f"scaled to this batch's {pairs / 1e6:.1f} M pairs (probe cost not included)"}
+    t_scan = pairs / rate
+    return {"value": round(nq / (t_probe + t_scan), 3), "unit": "queries/s", "cores": threads, "kind": "port",
+            "cpu_model": _cpu_model(),
+            "sample": f"coarse probe (faiss flat fp32 restatement, {nq} queries x {centroids.shape[0]} centroids, top-"
+                      f"{nprobe}) {t_probe * 1e3:.1f} ms, timed in full; list scans restated (oracle/vs_oracle.c fp32 "
+                      f"sequential scan, {threads} queries on {threads} OpenMP threads) over {R} rows in {t:.2f} s = "
+                      f"{rate / 1e6:.1f} M row-query pairs/s, scaled to this batch's {pairs / 1e6:.1f} M pairs "
+                      f"({t_scan:.2f} s)"}
 
 
 if __name__ == "__main__":

@@ -115,11 +115,13 @@ def main():
         kt = list(csv.DictReader(open(os.path.join(src, "kt", "kt_kernel_trace.csv"))))
         scan_ns = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in kt if "k_ivf_scan" in r["Kernel_Name"])
         rd, wr = tot["pmc_fetch"] * 1024 * 2 / searches, tot["pmc_write"] * 1024 / searches
-        traffic = {"workload": "cfg5", "n_local": bench_line["config"]["N"], "kernel": "k_ivf_scan (all class launches of one search)",
+        skew = float(bench_line["config"].get("skew", 0.0) or 0.0)
+        traffic = {"workload": "cfg5", "n_local": bench_line["config"]["N"], "skew": skew,
+                   "kernel": "k_ivf_scan (all scan launches of one search)",
                    "hbm_bytes_per_launch": rd + wr, "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
                    "profiled_kernel_ms": scan_ns * 1e-6 / searches,
                    "source": f"profiles/{tag}_pmc.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes)"}
-        with open(os.path.join(prof, "traffic_cfg5_ivf_scan.json"), "w") as f:
+        with open(os.path.join(prof, "traffic_cfg5_ivf_scan" + (f"_skew{skew:g}" if skew else "") + ".json"), "w") as f:
             json.dump(traffic, f, indent=1)
         summary["dominant"] = traffic
     with open(os.path.join(prof, f"{tag}_pmc.json"), "w") as f:
