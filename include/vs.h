@@ -135,6 +135,30 @@ int64_t vs_uncertified_count(vs_index* index);   /* synchronises the device coun
  * context stages at most 8 MiB and loops over query chunks beyond that */
 int64_t vs_host_staging_bytes(vs_index* index);
 
+/* ==== multi-device flat index (one process, several GPUs; SURVEY.md §8 b/e) =================
+ * The reference holds ONE index in ONE process (main.py:59-68 -> utils/vector_store.py:72-81); this
+ * handle keeps that contract over G devices.  Rows are dealt in chunks of 2^16 consecutive ids
+ * (chunk j on dev_ids[j mod G]), so ids stay insertion order 0..ntotal-1 under incremental and bulk
+ * adds.  vs_multi_search runs every shard's exact search concurrently (one host worker + stream per
+ * device), maps local ids to global ids on each device, copies the per-shard (fp64 score, id) lists
+ * to dev_ids[0] over xGMI peer copies and merges them there (vs_merge_shards_device's kernel):
+ * results equal a single index over all rows.  Devices may repeat (several shards on one GPU).
+ * Calls on one handle are serialised. */
+typedef struct vs_multi vs_multi;
+
+int vs_multi_create(int d, int metric, int dtype, int n_dev, const int* dev_ids, vs_multi** out);
+void vs_multi_destroy(vs_multi* m);
+int vs_multi_add(vs_multi* m, const float* x, int64_t n);                           /* host rows */
+int vs_multi_add_from_file(vs_multi* m, const char* path, int64_t byte_offset, int64_t n);
+int vs_multi_write_rows_to_file(vs_multi* m, const char* path, int64_t byte_offset, int64_t i0, int64_t n);
+int vs_multi_search(vs_multi* m, const float* q, int64_t nq, int32_t k, float* D, int64_t* I);
+int vs_multi_reconstruct_n(vs_multi* m, int64_t i0, int64_t n, float* out);
+int vs_multi_reset(vs_multi* m);
+int vs_multi_set_screen(vs_multi* m, int screen);
+int64_t vs_multi_ntotal(const vs_multi* m);
+int vs_multi_ndev(const vs_multi* m);
+int64_t vs_multi_shard_rows(const vs_multi* m, int shard);
+
 /* ==== IVF-Flat (BASELINE cfg5) ===========================================
  * Not a reference call site: the reference's VectorStore offers flat and HNSW only
  * (utils/vector_store.py:51-53, 72-81).  This is the faiss IndexIVFFlat surface (faiss-cpu,

@@ -77,6 +77,20 @@ _SIGS = {
     "vs_timing_fetch": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
     "vs_uncertified_count": (_c_i64, [_vp]),
     "vs_host_staging_bytes": (_c_i64, [_vp]),
+    # multi-device flat index
+    "vs_multi_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp,
+                                       ctypes.POINTER(_vp)]),
+    "vs_multi_destroy": (None, [_vp]),
+    "vs_multi_add": (ctypes.c_int, [_vp, _vp, _c_i64]),
+    "vs_multi_add_from_file": (ctypes.c_int, [_vp, ctypes.c_char_p, _c_i64, _c_i64]),
+    "vs_multi_write_rows_to_file": (ctypes.c_int, [_vp, ctypes.c_char_p, _c_i64, _c_i64, _c_i64]),
+    "vs_multi_search": (ctypes.c_int, [_vp, _vp, _c_i64, ctypes.c_int32, _vp, _vp]),
+    "vs_multi_reconstruct_n": (ctypes.c_int, [_vp, _c_i64, _c_i64, _vp]),
+    "vs_multi_reset": (ctypes.c_int, [_vp]),
+    "vs_multi_set_screen": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "vs_multi_ntotal": (_c_i64, [_vp]),
+    "vs_multi_ndev": (ctypes.c_int, [_vp]),
+    "vs_multi_shard_rows": (_c_i64, [_vp, ctypes.c_int]),
     # IVF-Flat
     "vs_ivf_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      ctypes.POINTER(_vp)]),

@@ -1,0 +1,384 @@
+// vs_multi.hip -- one exact flat index over several GPUs of ONE process (include/vs.h "multi-device").
+//
+// The reference builds one VectorStore in one process (/root/reference/main.py:59-68) over one
+// faiss index (utils/vector_store.py:72-81).  This handle keeps that shape -- one object, host
+// buffers in and out -- while the rows live on G devices:
+//   * rows are dealt in chunks of C = 2^16 consecutive ids: chunk j lives on device j mod G, so
+//     incremental adds (add_item, one row at a time) and bulk loads stay balanced, and the global
+//     id of local row l of device g is ((l >> 16) * G + g) << 16 | (l & 0xFFFF) -- no id tables;
+//   * a search runs every shard's exact search (vs_search_device_exact) concurrently, one host
+//     worker and one stream per device; each shard maps its local ids to global ids on its device
+//     and copies its (fp64 score, id) lists to device 0 over xGMI (peer copies); device 0 merges
+//     the G sorted lists (k_merge_shards: score, then lower global id) and returns D / I.
+// The merged order is total, so the result equals one index over all rows, bit for bit.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <condition_variable>
+#include <cstring>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "../../include/vs.h"
+#include "vs_internal.h"
+
+using namespace vs;
+
+namespace {
+
+constexpr int kChunkBits = 16;
+constexpr int64_t kChunk = int64_t(1) << kChunkBits;
+
+__global__ void __launch_bounds__(256) k_local_to_global(int64_t* __restrict__ I, int64_t n, int G, int g) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const int64_t l = I[i];
+    if (l < 0) return;
+    I[i] = ((((l >> kChunkBits) * G) + g) << kChunkBits) | (l & (kChunk - 1));
+}
+
+// persistent worker per device: run(job) hands a job to every worker and waits for all
+struct Pool {
+    std::vector<std::thread> th;
+    std::mutex mu;
+    std::condition_variable cv, done_cv;
+    std::function<void(int)> job;
+    uint64_t gen = 0;
+    int pending = 0;
+    bool stop = false;
+    std::vector<std::string> errs;
+    std::vector<int> codes;
+
+    explicit Pool(int n) : errs(n), codes(n, VS_OK) {
+        for (int w = 0; w < n; ++w)
+            th.emplace_back([this, w] {
+                uint64_t seen = 0;
+                for (;;) {
+                    std::function<void(int)> j;
+                    {
+                        std::unique_lock<std::mutex> lk(mu);
+                        cv.wait(lk, [&] { return stop || gen != seen; });
+                        if (stop) return;
+                        seen = gen;
+                        j = job;
+                    }
+                    int code = VS_OK;
+                    std::string msg;
+                    try {
+                        j(w);
+                    } catch (const VsError& e) {
+                        code = e.code;
+                        msg = e.what();
+                    } catch (const std::exception& e) {
+                        code = VS_ERR_INTERNAL;
+                        msg = e.what();
+                    }
+                    std::lock_guard<std::mutex> lk(mu);
+                    codes[w] = code;
+                    errs[w] = msg;
+                    if (--pending == 0) done_cv.notify_all();
+                }
+            });
+    }
+    ~Pool() {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            stop = true;
+        }
+        cv.notify_all();
+        for (auto& t : th) t.join();
+    }
+    // runs f(w) on every worker w; rethrows the first worker failure
+    void run(const std::function<void(int)>& f) {
+        std::unique_lock<std::mutex> lk(mu);
+        job = f;
+        pending = (int)th.size();
+        ++gen;
+        cv.notify_all();
+        done_cv.wait(lk, [&] { return pending == 0; });
+        for (size_t w = 0; w < th.size(); ++w)
+            if (codes[w] != VS_OK) throw VsError(codes[w], "device shard " + std::to_string(w) + ": " + errs[w]);
+    }
+};
+
+void throw_rc(int rc) {
+    if (rc != VS_OK) throw VsError(rc, vs_last_error());
+}
+
+}  // namespace
+
+struct vs_multi {
+    int d = 0, metric = 0, dtype = 0, G = 0;
+    std::vector<int> dev;
+    std::vector<vs_index*> ix;
+    std::vector<hipStream_t> st;
+    std::vector<DevBuf> qdev, S, I;  // per device: queries, per-shard fp64 scores / global ids
+    DevBuf gS, gI, oS, oI, oD;       // device 0: gathered [G][nq][k] lists, merged outputs
+    hipEvent_t* ready = nullptr;     // per device: its lists landed on device 0
+    int64_t ntotal = 0;
+    std::mutex mu;                   // searches and adds are serialised on a multi-device handle
+    Pool* pool = nullptr;
+};
+
+namespace {
+
+// rows [r0, r0 + n) of the global id space split into per-device contiguous pieces, in order
+struct Piece {
+    int g;
+    int64_t src;  // offset (rows) into the caller's batch
+    int64_t n;
+};
+std::vector<std::vector<Piece>> split_rows(int G, int64_t r0, int64_t n) {
+    std::vector<std::vector<Piece>> out(G);
+    int64_t i = 0;
+    while (i < n) {
+        const int64_t gid = r0 + i;
+        const int64_t chunk = gid >> kChunkBits;
+        const int64_t m = std::min(n - i, ((chunk + 1) << kChunkBits) - gid);
+        out[(int)(chunk % G)].push_back({(int)(chunk % G), i, m});
+        i += m;
+    }
+    return out;
+}
+
+void locate(const vs_multi* m, int64_t id, int* g, int64_t* local) {
+    const int64_t chunk = id >> kChunkBits;
+    *g = (int)(chunk % m->G);
+    *local = ((chunk / m->G) << kChunkBits) | (id & (kChunk - 1));
+}
+
+}  // namespace
+
+extern "C" {
+
+int vs_multi_create(int d, int metric, int dtype, int n_dev, const int* dev_ids, vs_multi** out) {
+    return guarded([&] {
+        if (!out) throw VsError(VS_ERR_ARG, "out is null");
+        *out = nullptr;
+        if (n_dev <= 0 || n_dev > 64 || !dev_ids) throw VsError(VS_ERR_ARG, "n_dev must be in [1, 64] with a device list");
+        vs_multi* m = new vs_multi();
+        m->d = d;
+        m->metric = metric;
+        m->dtype = dtype;
+        m->G = n_dev;
+        try {
+            for (int g = 0; g < n_dev; ++g) {
+                m->dev.push_back(dev_ids[g]);
+                vs_index* x = nullptr;
+                throw_rc(vs_create(d, metric, dtype, dev_ids[g], &x));
+                m->ix.push_back(x);
+                DeviceGuard dg(dev_ids[g]);
+                hipStream_t s = nullptr;
+                HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+                m->st.push_back(s);
+                if (dev_ids[g] != dev_ids[0]) {  // xGMI peer path to device 0 (best effort: copies work either way)
+                    int can = 0;
+                    if (hipDeviceCanAccessPeer(&can, dev_ids[g], dev_ids[0]) == hipSuccess && can)
+                        (void)hipDeviceEnablePeerAccess(dev_ids[0], 0);
+                    (void)hipGetLastError();
+                }
+            }
+            m->qdev.resize(n_dev);
+            m->S.resize(n_dev);
+            m->I.resize(n_dev);
+            m->ready = new hipEvent_t[n_dev]();
+            for (int g = 0; g < n_dev; ++g) {
+                DeviceGuard dg(dev_ids[g]);
+                HIP_CHECK(hipEventCreateWithFlags(&m->ready[g], hipEventDisableTiming));
+            }
+            m->pool = new Pool(n_dev);
+        } catch (...) {
+            vs_multi_destroy(m);
+            throw;
+        }
+        *out = m;
+    });
+}
+
+void vs_multi_destroy(vs_multi* m) {
+    if (!m) return;
+    delete m->pool;
+    for (int g = 0; g < (int)m->ix.size(); ++g) {
+        DeviceGuard dg(m->dev[g]);
+        (void)hipDeviceSynchronize();
+        m->qdev[g].release();
+        m->S[g].release();
+        m->I[g].release();
+        if (m->ready && m->ready[g]) hipEventDestroy(m->ready[g]);
+        if (g < (int)m->st.size() && m->st[g]) hipStreamDestroy(m->st[g]);
+        vs_destroy(m->ix[g]);
+    }
+    if (!m->dev.empty()) {
+        DeviceGuard dg(m->dev[0]);
+        for (DevBuf* b : {&m->gS, &m->gI, &m->oS, &m->oI, &m->oD}) b->release();
+    }
+    delete[] m->ready;
+    delete m;
+}
+
+int vs_multi_add(vs_multi* m, const float* x, int64_t n) {
+    return guarded([&] {
+        if (!m) throw VsError(VS_ERR_ARG, "null handle");
+        if (n < 0) throw VsError(VS_ERR_ARG, "n must be >= 0");
+        if (n == 0) return;
+        if (!x) throw VsError(VS_ERR_ARG, "x is null");
+        std::lock_guard<std::mutex> lk(m->mu);
+        const auto pieces = split_rows(m->G, m->ntotal, n);
+        m->pool->run([&](int g) {
+            for (const Piece& p : pieces[g]) throw_rc(vs_add(m->ix[g], x + p.src * m->d, p.n));
+        });
+        m->ntotal += n;
+    });
+}
+
+int vs_multi_add_from_file(vs_multi* m, const char* path, int64_t byte_offset, int64_t n) {
+    return guarded([&] {
+        if (!m || !path) throw VsError(VS_ERR_ARG, "null argument");
+        if (n < 0 || byte_offset < 0) throw VsError(VS_ERR_ARG, "bad range");
+        if (n == 0) return;
+        std::lock_guard<std::mutex> lk(m->mu);
+        const auto pieces = split_rows(m->G, m->ntotal, n);
+        m->pool->run([&](int g) {
+            for (const Piece& p : pieces[g])
+                throw_rc(vs_add_from_file(m->ix[g], path, byte_offset + p.src * m->d * (int64_t)sizeof(float), p.n));
+        });
+        m->ntotal += n;
+    });
+}
+
+int vs_multi_write_rows_to_file(vs_multi* m, const char* path, int64_t byte_offset, int64_t i0, int64_t n) {
+    return guarded([&] {
+        if (!m || !path) throw VsError(VS_ERR_ARG, "null argument");
+        if (i0 < 0 || n < 0 || i0 + n > m->ntotal) throw VsError(VS_ERR_ARG, "row range out of bounds");
+        if (n == 0) return;
+        std::lock_guard<std::mutex> lk(m->mu);
+        const auto pieces = split_rows(m->G, i0, n);
+        m->pool->run([&](int g) {  // disjoint file ranges: the devices write concurrently
+            for (const Piece& p : pieces[g]) {
+                int gg;
+                int64_t local;
+                locate(m, i0 + p.src, &gg, &local);
+                throw_rc(vs_write_rows_to_file(m->ix[g], path, byte_offset + p.src * m->d * (int64_t)sizeof(float), local,
+                                               p.n));
+            }
+        });
+    });
+}
+
+int vs_multi_search(vs_multi* m, const float* q, int64_t nq, int32_t k, float* D, int64_t* I) {
+    return guarded([&] {
+        if (!m) throw VsError(VS_ERR_ARG, "null handle");
+        if (nq < 0) throw VsError(VS_ERR_ARG, "nq must be >= 0");
+        if (k <= 0) throw VsError(VS_ERR_ARG, "k must be > 0");
+        if (nq == 0) return;
+        if (!q || !D || !I) throw VsError(VS_ERR_ARG, "null host buffer");
+        std::lock_guard<std::mutex> lk(m->mu);
+        const float fillD = m->metric == VS_METRIC_IP ? -3.402823466e+38f : 3.402823466e+38f;
+        const int kk = (int)std::min<int64_t>(k, m->ntotal);
+        if (kk == 0) {
+            for (int64_t i = 0; i < nq * k; ++i) {
+                D[i] = fillD;
+                I[i] = -1;
+            }
+            return;
+        }
+        if (kk > KP_MAX * 4 / 5) throw VsError(VS_ERR_ARG, "k too large (max " + std::to_string(KP_MAX * 4 / 5) + ")");
+        const int G = m->G;
+        const size_t lb = (size_t)nq * kk;
+        {
+            DeviceGuard dg(m->dev[0]);
+            m->gS.ensure(lb * G * sizeof(double));
+            m->gI.ensure(lb * G * sizeof(int64_t));
+            m->oS.ensure(lb * sizeof(double));
+            m->oI.ensure(lb * sizeof(int64_t));
+            m->oD.ensure(lb * sizeof(float));
+        }
+        m->pool->run([&](int g) {
+            DeviceGuard dg(m->dev[g]);
+            hipStream_t s = m->st[g];
+            m->qdev[g].ensure((size_t)nq * m->d * sizeof(float));
+            m->S[g].ensure(lb * sizeof(double));
+            m->I[g].ensure(lb * sizeof(int64_t));
+            double* Sg = m->S[g].as<double>();
+            int64_t* Ig = m->I[g].as<int64_t>();
+            HIP_CHECK(hipMemcpyAsync(m->qdev[g].p, q, (size_t)nq * m->d * sizeof(float), hipMemcpyHostToDevice, s));
+            if (vs_ntotal(m->ix[g]) > 0) {
+                // exact per shard (uncertified screens re-searched on this device before it returns)
+                throw_rc(vs_search_device_exact(m->ix[g], m->qdev[g].as<float>(), nq, kk, nullptr, Ig, Sg, 0, s));
+                hipLaunchKernelGGL(k_local_to_global, dim3((unsigned)((lb + 255) / 256)), dim3(256), 0, s, Ig,
+                                   (int64_t)lb, G, g);
+                HIP_CHECK(hipGetLastError());
+            } else {  // an empty shard contributes only padding
+                std::vector<double> ws(lb, m->metric == VS_METRIC_IP ? -1.7976931348623157e308 : 1.7976931348623157e308);
+                std::vector<int64_t> wi(lb, -1);
+                HIP_CHECK(hipMemcpyAsync(Sg, ws.data(), lb * sizeof(double), hipMemcpyHostToDevice, s));
+                HIP_CHECK(hipMemcpyAsync(Ig, wi.data(), lb * sizeof(int64_t), hipMemcpyHostToDevice, s));
+                HIP_CHECK(hipStreamSynchronize(s));
+            }
+            // this shard's lists into slot g of device 0's gather buffers (xGMI peer copy)
+            HIP_CHECK(hipMemcpyPeerAsync(m->gS.as<double>() + lb * g, m->dev[0], Sg, m->dev[g], lb * sizeof(double), s));
+            HIP_CHECK(hipMemcpyPeerAsync(m->gI.as<int64_t>() + lb * g, m->dev[0], Ig, m->dev[g], lb * sizeof(int64_t), s));
+            HIP_CHECK(hipEventRecord(m->ready[g], s));
+        });
+        DeviceGuard dg(m->dev[0]);
+        hipStream_t s0 = m->st[0];
+        for (int g = 1; g < G; ++g) HIP_CHECK(hipStreamWaitEvent(s0, m->ready[g], 0));
+        HIP_CHECK(launch_merge_shards(m->metric, m->gS.as<double>(), m->gI.as<int64_t>(), G, nq, kk, m->oS.as<double>(),
+                                      m->oI.as<int64_t>(), m->oD.as<float>(), s0));
+        std::vector<float> Dk(lb);
+        std::vector<int64_t> Ik(lb);
+        HIP_CHECK(hipMemcpyAsync(Dk.data(), m->oD.p, lb * sizeof(float), hipMemcpyDeviceToHost, s0));
+        HIP_CHECK(hipMemcpyAsync(Ik.data(), m->oI.p, lb * sizeof(int64_t), hipMemcpyDeviceToHost, s0));
+        HIP_CHECK(hipStreamSynchronize(s0));
+        for (int64_t a = 0; a < nq; ++a)
+            for (int j = 0; j < k; ++j) {
+                D[a * k + j] = j < kk ? Dk[a * kk + j] : fillD;
+                I[a * k + j] = j < kk ? Ik[a * kk + j] : -1;
+            }
+    });
+}
+
+int vs_multi_reconstruct_n(vs_multi* m, int64_t i0, int64_t n, float* out) {
+    return guarded([&] {
+        if (!m || !out) throw VsError(VS_ERR_ARG, "null argument");
+        if (i0 < 0 || n < 0 || i0 + n > m->ntotal) throw VsError(VS_ERR_ARG, "reconstruct range out of bounds");
+        if (n == 0) return;
+        std::lock_guard<std::mutex> lk(m->mu);
+        const auto pieces = split_rows(m->G, i0, n);
+        m->pool->run([&](int g) {
+            for (const Piece& p : pieces[g]) {
+                int gg;
+                int64_t local;
+                locate(m, i0 + p.src, &gg, &local);
+                throw_rc(vs_reconstruct_n(m->ix[g], local, p.n, out + p.src * m->d));
+            }
+        });
+    });
+}
+
+int vs_multi_reset(vs_multi* m) {
+    return guarded([&] {
+        if (!m) throw VsError(VS_ERR_ARG, "null handle");
+        std::lock_guard<std::mutex> lk(m->mu);
+        for (vs_index* x : m->ix) throw_rc(vs_reset(x));
+        m->ntotal = 0;
+    });
+}
+
+int vs_multi_set_screen(vs_multi* m, int screen) {
+    return guarded([&] {
+        if (!m) throw VsError(VS_ERR_ARG, "null handle");
+        std::lock_guard<std::mutex> lk(m->mu);
+        m->pool->run([&](int g) { throw_rc(vs_set_screen(m->ix[g], screen)); });
+    });
+}
+
+int64_t vs_multi_ntotal(const vs_multi* m) { return m ? m->ntotal : -1; }
+int vs_multi_ndev(const vs_multi* m) { return m ? m->G : -1; }
+int64_t vs_multi_shard_rows(const vs_multi* m, int g) {
+    return (m && g >= 0 && g < m->G) ? vs_ntotal(m->ix[g]) : -1;
+}
+
+}  // extern "C"

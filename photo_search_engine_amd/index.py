@@ -173,3 +173,99 @@ def synthesize_device(device: int, seed: int, global_row0: int, n: int, d: int, 
     L = _lib.load()
     check(L.vs_synthesize(int(device), int(seed), int(global_row0), int(n), int(d), int(bool(normalize)),
                           DTYPE_CODES[dtype], out_ptr, stream or None))
+
+
+class MultiDeviceFlatIndex:
+    """One exact flat index over several GPUs of this process (``vs_multi_*``, include/vs.h).
+
+    The same faiss-IndexFlat-shaped surface as :class:`FlatIndex` (``ntotal``, ``d``,
+    ``metric_type``, ``add``, ``search``, ``reconstruct``, ``reconstruct_n``, ``reset`` and the
+    persistence hooks), so ``VectorStore`` holds it in ``.index`` unchanged; rows are dealt over the
+    devices in chunks of 65,536 ids and every search merges the per-device exact top-k on
+    ``devices[0]`` (the result equals one index over all rows).  A device may be listed more than
+    once (several shards on one GPU).
+    """
+
+    def __init__(self, d: int, metric: str = "ip", dtype: str = "f32", devices=(0,)) -> None:
+        self._h = None
+        L = _lib.load()
+        m = metric.lower()
+        if m in ("ip", "cosine", "inner_product"):
+            code = METRIC_IP
+        elif m in ("l2", "euclidean"):
+            code = METRIC_L2
+        else:
+            raise ValueError(f"unknown metric {metric!r}")
+        if dtype not in DTYPE_CODES:
+            raise ValueError(f"unknown dtype {dtype!r}")
+        devs = [int(x) for x in devices]
+        if not devs:
+            raise ValueError("devices must name at least one GPU")
+        arr = (ctypes.c_int * len(devs))(*devs)
+        h = ctypes.c_void_p()
+        check(L.vs_multi_create(int(d), code, DTYPE_CODES[dtype], len(devs), arr, ctypes.byref(h)))
+        self._h = h
+        self._L = L
+        self.d = int(d)
+        self.metric_type = code
+        self.dtype = dtype
+        self.devices = devs
+
+    @property
+    def ntotal(self) -> int:
+        return int(self._L.vs_multi_ntotal(self._h))
+
+    def shard_rows(self):
+        return [int(self._L.vs_multi_shard_rows(self._h, g)) for g in range(len(self.devices))]
+
+    def add(self, x) -> None:
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        if x.ndim != 2 or x.shape[1] != self.d:
+            raise ValueError(f"add expects an (n, {self.d}) array, got {x.shape}")
+        check(self._L.vs_multi_add(self._h, _ptr(x), x.shape[0]))
+
+    def search(self, q, k: int) -> Tuple[np.ndarray, np.ndarray]:
+        q = np.ascontiguousarray(q, dtype=np.float32)
+        if q.ndim != 2 or q.shape[1] != self.d:
+            raise ValueError(f"search expects an (nq, {self.d}) array, got {q.shape}")
+        k = int(k)
+        if k <= 0:
+            raise _lib.VsError(_lib.VS_ERR_ARG, "k must be > 0")
+        D = np.empty((q.shape[0], k), dtype=np.float32)
+        I = np.empty((q.shape[0], k), dtype=np.int64)
+        check(self._L.vs_multi_search(self._h, _ptr(q), q.shape[0], k, _ptr(D), _ptr(I)))
+        return D, I
+
+    def reconstruct_n(self, i0: int, n: int) -> np.ndarray:
+        out = np.empty((int(n), self.d), dtype=np.float32)
+        if n:
+            check(self._L.vs_multi_reconstruct_n(self._h, int(i0), int(n), _ptr(out)))
+        return out
+
+    def reconstruct(self, i: int) -> np.ndarray:
+        return self.reconstruct_n(int(i), 1)[0]
+
+    def reset(self) -> None:
+        check(self._L.vs_multi_reset(self._h))
+
+    def set_screen(self, screen: str) -> None:
+        if screen not in FlatIndex.SCREENS:
+            raise ValueError(f"unknown screen {screen!r}")
+        check(self._L.vs_multi_set_screen(self._h, FlatIndex.SCREENS[screen]))
+
+    def add_from_file(self, path: str, byte_offset: int, n: int) -> None:
+        check(self._L.vs_multi_add_from_file(self._h, os.fsencode(path), int(byte_offset), int(n)))
+
+    def write_rows(self, path: str, byte_offset: int, i0: int, n: int) -> None:
+        check(self._L.vs_multi_write_rows_to_file(self._h, os.fsencode(path), int(byte_offset), int(i0), int(n)))
+
+    def close(self) -> None:
+        if self._h is not None and self._h.value:
+            self._L.vs_multi_destroy(self._h)
+        self._h = None
+
+    def __del__(self) -> None:  # pragma: no cover - interpreter shutdown ordering
+        try:
+            self.close()
+        except Exception:
+            pass

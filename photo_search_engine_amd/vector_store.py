@@ -19,8 +19,10 @@ What changes underneath:
 Normalisation stays on the host in numpy, bit-identical to the reference
 (utils/vector_store.py:83-90), so stored vectors and query vectors are the same fp32 values.
 
-Environment knobs (new, optional): ``VECTOR_DEVICE`` (GPU ordinal, default 0) and
-``VECTOR_DTYPE`` (f32 | bf16 | f16 storage, default f32 = the reference's storage precision).
+Environment knobs (new, optional): ``VECTOR_DEVICE`` (GPU ordinal, default 0), ``VECTOR_DEVICES``
+(e.g. ``0,1,2,3,4,5,6,7``: one index over those GPUs of this process, include/vs.h vs_multi_*),
+``VECTOR_DTYPE`` (f32 | bf16 | f16 storage, default f32 = the reference's storage precision) and
+``VECTOR_SCREEN`` (native | int8: the batched-search screen of an inner-product index).
 """
 from __future__ import annotations
 
@@ -31,16 +33,25 @@ from typing import Any, Dict, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import faiss_format
-from .index import FlatIndex
+from .index import FlatIndex, MultiDeviceFlatIndex
 
 METRIC_INNER_PRODUCT = 0
 METRIC_L2 = 1
 
 
-def _default_index_factory(dimension: int, metric: str) -> FlatIndex:
-    device = int(os.environ.get("VECTOR_DEVICE", "0") or 0)
+def _default_index_factory(dimension: int, metric: str):
     dtype = (os.environ.get("VECTOR_DTYPE", "f32") or "f32").strip().lower()
-    return FlatIndex(dimension, metric="ip" if metric == "cosine" else "l2", dtype=dtype, device=device)
+    kind = "ip" if metric == "cosine" else "l2"
+    devices = [d.strip() for d in (os.environ.get("VECTOR_DEVICES", "") or "").split(",") if d.strip()]
+    if len(devices) > 1:  # one index over several GPUs of this process (rows dealt in 64k-id chunks)
+        index = MultiDeviceFlatIndex(dimension, metric=kind, dtype=dtype, devices=[int(d) for d in devices])
+    else:
+        device = int(devices[0]) if devices else int(os.environ.get("VECTOR_DEVICE", "0") or 0)
+        index = FlatIndex(dimension, metric=kind, dtype=dtype, device=device)
+    screen = (os.environ.get("VECTOR_SCREEN", "") or "").strip().lower()
+    if screen and kind == "ip":
+        index.set_screen(screen)
+    return index
 
 
 # Module-level hook: tests may substitute a checker-backed index with the same surface.
