@@ -360,7 +360,7 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
         return;
     }
     const int64_t tiles = (ix->ntotal + TR - 1) / TR;
-    const bool use_mfma = ix->dtype != DT_F32 && nqb > GEMV_NQ_MAX && Kp <= MFMA_KP_MAX;
+    const bool use_mfma = ix->dtype != DT_F32 && nqb > GEMV_NQ_MAX;
     ScreenArgs a{};
     a.corpus = ix->data;
     a.n_valid = ix->ntotal;
@@ -369,7 +369,9 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
     a.d = ix->d;
     a.metric = ix->metric;
     a.sqn = ix->sqn;
-    a.Kp = Kp;
+    // MFMA: each workgroup keeps its best min(Kp, MFMA_KP_MAX) per query; deeper screens certify
+    // against the workgroups' compaction bounds (drop) in the refine
+    a.Kp = use_mfma ? std::min(Kp, MFMA_KP_MAX) : Kp;
     int QB;
     c->qinfo.ensure(sizeof(float) * 2 * MFMA_QB);
     if (use_mfma) {
@@ -378,8 +380,9 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
         a.G = (int)std::min<int64_t>(tiles, ix->num_cu);
         c->qtile.ensure((size_t)MFMA_QB * ix->dpad * 2);
         c->gcnt.ensure(sizeof(int) * MFMA_QB);
+        c->drop.ensure(sizeof(u64) * MFMA_QB);
         HIP_CHECK(launch_pack_qtile(ix->dtype, q, nqb, ix->d, ix->dpad, c->qtile.as<uint8_t>(), c->qinfo.as<float>(),
-                                    c->gcnt.as<int>(), st));
+                                    c->gcnt.as<int>(), c->drop.as<u64>(), st));
     } else {
         QB = nqb <= 1 ? 1 : nqb <= 2 ? 2 : nqb <= 4 ? 4 : 8;
         a.cap = (int)round_up(Kp + 2 * TR, 256);
@@ -395,21 +398,22 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
     }
     a.G = std::max(a.G, 1);
     c->cand.ensure((size_t)a.G * QB * a.cap * sizeof(u64));
-    c->part.ensure((size_t)a.G * QB * Kp * sizeof(u64));  // GEMV: [G][QB][Kp]; MFMA: [QB][G*Kp] survivor lists
+    c->part.ensure((size_t)a.G * QB * a.Kp * sizeof(u64));  // GEMV: [G][QB][Kp]; MFMA: [QB][G*Kp] survivor lists
     a.cand = c->cand.as<u64>();
     a.part = c->part.as<u64>();
     if (!use_mfma && gemv_dyn()) a.next_tile = c->tilectr.as<int>();
     if (use_mfma) {
         a.glist = c->part.as<u64>();
         a.gcnt = c->gcnt.as<int>();
-        a.lcap = a.G * Kp;
+        a.lcap = a.G * a.Kp;
+        a.drop = c->drop.as<u64>();
     }
 
     // merge partial lists [nseg][qstride][Kp] down to one list per query (or, with stop_keys, to
     // the first round whose nseg * Kp <= stop_keys: one query's lists are then contiguous and the
     // refine selects the best Kp itself); returns it, nseg updated
     auto merge_all = [&](const u64* src, int& nseg, int qstride, int stop_keys) -> const u64* {
-        const int spb = (256 * 16) / Kp;  // k_merge: 4096 keys per block
+        const int spb = (256 * (Kp > 2048 ? 32 : 16)) / Kp;  // k_merge: 4096 / 8192 keys per block
         const size_t mbytes = (size_t)std::max(1, (nseg + spb - 1) / spb) * nqb * Kp * sizeof(u64);
         c->merge_a.ensure(mbytes);
         c->merge_b.ensure(mbytes);
@@ -451,7 +455,9 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
         int rank = Kp;
         if (seed_rank > 0) {
             const double sampled = (double)sa.G * TR;
-            const double r = std::ceil(kOptimisticPassFactor * Kp * sampled / (double)ix->ntotal);
+            // deep screens aim lower (~12k listed rows per query), so the refine selects in registers
+            const double factor = std::min(kOptimisticPassFactor, 12288.0 / Kp);
+            const double r = std::ceil(factor * Kp * sampled / (double)ix->ntotal);
             // floor: at rank 1 a sample maximum that falls inside the true top-Kp leaves fewer than
             // Kp survivors (probability ~Kp * sampled / N per query, ~2% at 100M rows); with >= 4
             // sampled rows required in the top-Kp the failure odds drop to ~(that)^4 / 24
@@ -494,6 +500,7 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
         r.lcap = nseg * Kp;
     }
     r.Kp = Kp;
+    r.drop = a.drop;
     r.q = q;
     r.d = ix->d;
     r.dpad = ix->dpad;
@@ -520,8 +527,7 @@ void search_all(vs_index* ix, Ctx* c, const float* q, int64_t nq, int k, int Kp,
                 int* cert, int64_t id_offset, hipStream_t st, int seed_rank) {
     const int64_t tiles = (ix->ntotal + TR - 1) / TR;
     (void)tiles;
-    const bool mfma_ok = (seed_rank > 0 && ix->screen == VS_SCREEN_I8 && k <= I8_MAX_K) ||
-                         (ix->dtype != DT_F32 && Kp <= MFMA_KP_MAX);
+    const bool mfma_ok = (seed_rank > 0 && ix->screen == VS_SCREEN_I8 && k <= I8_MAX_K) || ix->dtype != DT_F32;
     int64_t done = 0;
     while (done < nq) {
         const int64_t rem = nq - done;

@@ -29,10 +29,12 @@ constexpr int METRIC_IP = 0, METRIC_L2 = 1;
 constexpr int MFMA_QB = 256;   // queries per MFMA screen launch
 constexpr int MF_WG_THREADS = 512;  // MFMA screen workgroup (8 waves)
 constexpr int MFMA_CAP = 768;  // candidate slots per (workgroup, query) in the MFMA screen
-constexpr int MFMA_KP_MAX = 512;  // = MFMA_CAP - TR: a compacted buffer (Kp keys) plus one tile fits
+constexpr int MFMA_KP_MAX = 512;  // per-(workgroup, query) screening depth of the MFMA screen (= MFMA_CAP - TR:
+                                  // a compacted buffer plus one tile fits); deeper searches keep 512 per
+                                  // workgroup and certify against the workgroups' drop bounds
 static_assert(MFMA_KP_MAX + TR <= MFMA_CAP, "MFMA screen: compaction invariant cnt <= cap - TR");
 constexpr int GEMV_NQ_MAX = 8; // queries per GEMV screen launch
-constexpr int KP_MAX = 2048;   // largest screening depth (merge: >= 2 lists per block)
+constexpr int KP_MAX = 4096;   // largest screening depth (k <= 3276; k_refine sorts 4096 keys in LDS)
 constexpr int SELECT_E = 16;   // keys per thread in block selection (256 threads -> 4096 keys)
 
 inline int es_of(int dt) { return dt == DT_F32 ? 4 : 2; }
@@ -199,7 +201,7 @@ hipError_t launch_gather_rows(int dt, const uint8_t* data, const int64_t* ids, i
 // queries: MFMA tile (dtype, [nks][256][32]) or fp32 padded [NQ][dpad]; qinfo[q*2] = ||q_hat||,
 // qinfo[q*2+1] = ||q_hat - q|| (upper bounds, fp32)
 hipError_t launch_pack_qtile(int dt, const float* q, int nqb, int d, int dpad, uint8_t* qt, float* qinfo, int* gcnt,
-                             hipStream_t st);
+                             u64* drop, hipStream_t st);
 hipError_t launch_pack_qf32(const float* q, int nqb, int nqpad, int d, int dpad, float* qp, float* qinfo,
                             hipStream_t st, int* ctr = nullptr);  // ctr: zeroed (a screen's tile queue)
 

@@ -437,11 +437,12 @@ __global__ void __launch_bounds__(256) k_gather_rows(const uint8_t* __restrict__
 template <int DT>
 __global__ void __launch_bounds__(256) k_pack_qtile(const float* __restrict__ q, int nqb, int d, int dpad,
                                                      uint8_t* __restrict__ qt, float* __restrict__ qinfo,
-                                                     int* __restrict__ gcnt) {
+                                                     int* __restrict__ gcnt, u64* __restrict__ drop) {
     const int lane = threadIdx.x & 63;
     const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= MFMA_QB) return;
-    if (gcnt && lane == 0) gcnt[r] = 0;  // survivor-list lengths of the screen that follows
+    if (gcnt && lane == 0) gcnt[r] = 0;  // survivor-list lengths of the screen that follows ...
+    if (drop && lane == 0) drop[r] = 0ull;  // ... and its workgroups' drop bounds
     double n2 = 0.0, e2 = 0.0;
 #pragma unroll 8
     for (int i = lane; i < dpad; i += 64) {
@@ -1572,7 +1573,8 @@ __global__ void __launch_bounds__(256) k_ivf_scan(IvfScanArgs a) {
 // ------------------------------------------------------------------------------------------------
 // K3: merge of partial candidate lists (block-wide selection)
 // ------------------------------------------------------------------------------------------------
-constexpr int MERGE_E = 16;  // 4096 keys per block
+// MERGE_E keys per thread: 4096 keys per block (16) or 8192 (32, screening depths above 2048)
+template <int MERGE_E>
 __global__ void __launch_bounds__(256) k_merge(const u64* __restrict__ in, int nseg, int qstride, int nq, int Kp,
                                                int spb, u64* __restrict__ out) {
     __shared__ int red[8];
@@ -1830,10 +1832,16 @@ __global__ void __launch_bounds__(RF_THREADS) k_refine(RefineArgs a, int KP2) {
     }
     // exactness certificate: every non-candidate row has exact transformed score <= smin + eps
     if (tid == 0) {
+        // rows outside the candidate set scored at most: the Kp-th best listed key (when the list
+        // was cut to Kp), or a workgroup's compaction bound (deep searches keep MFMA_KP_MAX per
+        // workgroup), whichever is larger
+        u64 th = nv >= a.Kp ? minkey_s : 0ull;
+        if (a.drop && a.drop[q] > th) th = a.drop[q];
         int cert = 1;
         if (a.optimistic && nv < a.Kp) cert = 0;  // an optimistic seed may have cut real candidates
-        else if (nv >= a.Kp && a.k <= nv) {
-            const double smin = (double)key_score(minkey_s);
+        else if (th != 0ull && a.k > nv) cert = 0;
+        else if (th != 0ull) {
+            const double smin = (double)key_score(th);
             const double qh = (double)a.qinfo[2 * q], dq = (double)a.qinfo[2 * q + 1];
             const double xm = (double)a.xmax;
             double eps = ((double)a.gamma * qh + dq) * xm * 1.01 + 1e-30;
@@ -2320,13 +2328,13 @@ hipError_t launch_gather_rows(int dt, const uint8_t* data, const int64_t* ids, i
 }
 
 hipError_t launch_pack_qtile(int dt, const float* q, int nqb, int d, int dpad, uint8_t* qt, float* qinfo, int* gcnt,
-                             hipStream_t st) {
+                             u64* drop, hipStream_t st) {
     if (dt == DT_BF16)
         hipLaunchKernelGGL(k_pack_qtile<DT_BF16>, dim3(MFMA_QB / 4), dim3(256), 0, st, q, nqb, d, dpad, qt, qinfo,
-                           gcnt);
+                           gcnt, drop);
     else
         hipLaunchKernelGGL(k_pack_qtile<DT_F16>, dim3(MFMA_QB / 4), dim3(256), 0, st, q, nqb, d, dpad, qt, qinfo,
-                           gcnt);
+                           gcnt, drop);
     return hipGetLastError();
 }
 
@@ -2425,9 +2433,12 @@ hipError_t launch_screen_gemv(int dt, const ScreenArgs& a, const float* qp, int 
 
 hipError_t launch_merge(const u64* in, int nseg, int qstride, int nq, int Kp, u64* out, int* nseg_out,
                         hipStream_t st) {
-    const int spb = (256 * MERGE_E) / Kp;  // segments per block (Kp <= 4096)
+    // >= 2 segments per block, so every stage shrinks the list count (Kp <= KP_MAX = 4096)
+    const bool wide = Kp > 2048;
+    const int spb = (256 * (wide ? 32 : 16)) / Kp;
     const int nb = (nseg + spb - 1) / spb;
-    hipLaunchKernelGGL(k_merge, dim3(nb, nq), dim3(256), 0, st, in, nseg, qstride, nq, Kp, spb, out);
+    if (wide) hipLaunchKernelGGL(k_merge<32>, dim3(nb, nq), dim3(256), 0, st, in, nseg, qstride, nq, Kp, spb, out);
+    else hipLaunchKernelGGL(k_merge<16>, dim3(nb, nq), dim3(256), 0, st, in, nseg, qstride, nq, Kp, spb, out);
     *nseg_out = nb;
     return hipGetLastError();
 }

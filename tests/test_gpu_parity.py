@@ -360,3 +360,32 @@ def test_single_query_device_api_s64(FlatIndex, dtype):
     np.testing.assert_array_equal(I.cpu().numpy(), Ie + 11)
     np.testing.assert_array_equal(S.cpu().numpy(), Se)
     np.testing.assert_array_equal(D.cpu().numpy(), Se.astype(np.float32))
+
+
+@pytest.mark.parametrize("k", [1000, 2048])
+def test_mfma_large_k_batches_stay_on_mfma(FlatIndex, k):
+    # the product's relaxed candidate_k (core/searcher.py:807-817) batched: k up to 2048 at nq > 8
+    # stays on the MFMA screen (512 per workgroup, drop-bounded certificate), bit-exact
+    N, d, nq = 150_000, 1536, 64
+    ix = FlatIndex(d, "ip", "bf16")
+    ix.add_synthetic(O.SEED_CORPUS, 0, N, True)
+    q = O.synth_rows(O.SEED_QUERIES, 0, nq, d, True, "bf16")
+    ix.set_timing(True)
+    D, I = ix.search(q, k)
+    ix.set_timing(False)
+    ms, kind = ix.timing_fetch()
+    assert kind == "mfma" and len(ms) == 1  # one MFMA launch for the whole batch, no GEMV passes
+    S, Ie = O.knn_exact(ix.reconstruct_n(0, N), q, k, "ip")
+    np.testing.assert_array_equal(I, Ie)
+    np.testing.assert_array_equal(D, S.astype(np.float32))
+    assert ix.uncertified_count() == 0
+    ix.close()
+
+
+def test_k_3000_single_query_and_batch(FlatIndex):
+    # depths above 2048 (k up to 3276): the wide merge on the GEMV path, the 4096-key refine
+    ix = FlatIndex(64, "ip", "f32")
+    ix.add_synthetic(O.SEED_CORPUS, 0, 200_000, True)
+    for nq in (1, 12):
+        q = O.synth_rows(O.SEED_QUERIES, 3, nq, 64, True, "f32")
+        _check_exact(ix, q, 3000, "ip")
