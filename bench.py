@@ -42,7 +42,7 @@ SEED_CENTROIDS = 20260419
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 MFMA_BF16_PEAK_TF = 2500.0
 MFMA_I8_PEAK_TOPS = 5000.0  # MI355X_MICROARCH.md: I8 16x16x64 runs at 2x the BF16 rate per clock
-DEFAULT_SCREEN = {"cfg3": "int8"}  # flat workloads not listed: the native screen
+DEFAULT_SCREEN = {"cfg3": "int8", "cfg2": "int8"}  # flat workloads not listed: the native screen
 METRICS = {
     "cfg3": "kNN queries/sec + recall@10 vs FAISS, N=10M d=1536 batch=256",
     "cfg2": "kNN queries/sec vs FAISS, N=1M d=1536 fp32 batch=1 top-10",
@@ -183,9 +183,10 @@ def main():
     ms_per_step = elapsed * 1e3 / args.steps
     qps = nq * args.steps / elapsed
     kavg = float(np.mean(kms)) if kms else float("nan")
-    if kind == "mfma_i8":
-        # streamed per launch: the int8 codes + per-row (scale, error norm) + int8 queries + lists
-        alg_bytes = n_local * d + n_local * 4 + nq * d + nq * k * 12
+    if kind in ("mfma_i8", "gemv_i8"):
+        # streamed per launch: the int8 codes + per-row (scale, error norm) + the queries (int8 for
+        # the MFMA screen, fp32 for the GEMV) + the candidate lists
+        alg_bytes = n_local * d + n_local * 4 + nq * d * (1 if kind == "mfma_i8" else 4) + nq * k * 12
         peak_flops = MFMA_I8_PEAK_TOPS
     else:
         alg_bytes = n_local * d * es + nq * d * es + nq * k * 12
@@ -207,7 +208,7 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "int8" if kind == "mfma_i8" else dtype,
+            "dtype": "int8" if kind in ("mfma_i8", "gemv_i8") else dtype,
             "data": "synthetic (counter-hash N(0,1) rows, L2-normalised, seeds 20260417/20260418)",
             "config": {"workload": args.workload, "desc": desc, "N": N, "d": d, "batch": nq, "k": k,
                        "n_local": n_local, "stored_rows": dtype, "screen": screen,
@@ -232,7 +233,7 @@ def main():
             "uncertified_first_pass": uncert,
             "build_s": round(t_build, 2),
         }
-        if kind == "mfma_i8":
+        if kind in ("mfma_i8", "gemv_i8"):
             out["int8_copy"] = {"hbm_bytes": n_local * (d + 4), "build_s": round(t_switch, 2),
                                 "note": "int8 codes + bf16 (scale, error norm) per row, on top of the stored rows"}
         if alt is not None:

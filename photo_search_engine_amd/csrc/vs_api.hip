@@ -361,6 +361,10 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
     }
     const int64_t tiles = (ix->ntotal + TR - 1) / TR;
     const bool use_mfma = ix->dtype != DT_F32 && nqb > GEMV_NQ_MAX;
+    // int8 screen, few queries: the GEMV streams the int8 copy (1 B per element) with the fp32
+    // query; its keys carry the row error bound, so it screens deeper (first passes only)
+    const bool gemv_i8 = !use_mfma && seed_rank > 0 && ix->screen == VS_SCREEN_I8 && ix->data8 != nullptr;
+    if (gemv_i8) Kp = (int)std::min<int64_t>(KP_MAX, round_up(std::max(8 * k, k + 64), 16));
     ScreenArgs a{};
     a.corpus = ix->data;
     a.n_valid = ix->ntotal;
@@ -386,15 +390,23 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
     } else {
         QB = nqb <= 1 ? 1 : nqb <= 2 ? 2 : nqb <= 4 ? 4 : 8;
         a.cap = (int)round_up(Kp + 2 * TR, 256);
+        const int sdt = gemv_i8 ? DT_I8 : ix->dtype;
+        const int dpadq = gemv_i8 ? ix->dpad8 : ix->dpad;
         // work-queue tiles over exactly the resident blocks (VS_GEMV_DYN=0: static ranges, 8 per CU)
-        a.G = (int)std::min<int64_t>(tiles, (int64_t)ix->num_cu * (gemv_dyn() ? gemv_blocks_per_cu(ix->dtype, QB) : 8));
-        c->qpad.ensure((size_t)QB * ix->dpad * sizeof(float));
+        a.G = (int)std::min<int64_t>(tiles, (int64_t)ix->num_cu * (gemv_dyn() ? gemv_blocks_per_cu(sdt, QB) : 8));
+        c->qpad.ensure((size_t)QB * dpadq * sizeof(float));
         int* ctr = nullptr;
         if (gemv_dyn()) {  // the work-queue counter is zeroed by the query pack (no separate memset)
             c->tilectr.ensure(sizeof(int));
             ctr = c->tilectr.as<int>();
         }
-        HIP_CHECK(launch_pack_qf32(q, nqb, QB, ix->d, ix->dpad, c->qpad.as<float>(), c->qinfo.as<float>(), st, ctr));
+        HIP_CHECK(launch_pack_qf32(q, nqb, QB, ix->d, dpadq, c->qpad.as<float>(), c->qinfo.as<float>(), st, ctr));
+        if (gemv_i8) {
+            a.corpus = ix->data8;
+            a.dpad = ix->dpad8;
+            a.rsb = ix->rsb;
+            a.qinfo = c->qinfo.as<float>();
+        }
     }
     a.G = std::max(a.G, 1);
     c->cand.ensure((size_t)a.G * QB * a.cap * sizeof(u64));
@@ -477,12 +489,12 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
         HIP_CHECK(hipEventRecord(e0, st));
     }
     if (use_mfma) HIP_CHECK(launch_screen_mfma(ix->dtype, a, c->qtile.as<uint8_t>(), nqb, st));
-    else HIP_CHECK(launch_screen_gemv(ix->dtype, a, c->qpad.as<float>(), nqb, QB, st));
+    else HIP_CHECK(launch_screen_gemv(gemv_i8 ? DT_I8 : ix->dtype, a, c->qpad.as<float>(), nqb, QB, st));
     if (timing) {
         HIP_CHECK(hipEventRecord(e1, st));
         std::lock_guard<std::mutex> g(ix->tmtx);
         ix->tev.emplace_back(e0, e1);
-        ix->last_kernel_kind = use_mfma ? 1 : 2;
+        ix->last_kernel_kind = use_mfma ? 1 : gemv_i8 ? 4 : 2;
     }
     RefineArgs r{};
     if (use_mfma) {  // the refine selects the best Kp of each query's survivor list itself
@@ -501,6 +513,7 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
     }
     r.Kp = Kp;
     r.drop = a.drop;
+    r.i8max = gemv_i8 ? ix->d_maxsq + 2 : nullptr;
     r.q = q;
     r.d = ix->d;
     r.dpad = ix->dpad;

@@ -181,6 +181,7 @@ struct ScreenArgs {
     const uint32_t* rsb;     // int8 screen, per row: bf16 scale s_x (x_hat = s_x * codes) in the low half,
                              // bf16 ||x - x_hat||_2 rounded up in the high half
     const float2* qfac;      // int8 screen: per query (t_q, ||q||), codes q_hat = t_q * int8
+    const float* qinfo;      // int8 GEMV: per query [2q] = ||q|| rounded up (k_pack_qf32)
     u64* drop;               // MFMA: per query, max over workgroups of their compaction threshold
                              // (rows below it were dropped; zeroed by the query pack), or null
 };
@@ -236,6 +237,7 @@ struct RefineArgs {
     const float* qeps;     // int8 screen (k_refine_wide): per query, true score <= key_score + qeps
     const u64* drop;       // MFMA: per query, the workgroups' largest compaction threshold (or null)
     const u64* thr0;       // the screen's starting threshold per query (or null = none)
+    const unsigned* i8max; // int8 GEMV screen: (max ||x_hat||, max beta) fp32 bits -> the certificate margin
     const uint32_t* idmap; // IVF: user id of every storage slot (keys carry slots); null = identity
 };
 hipError_t launch_refine(const RefineArgs& a, int nq, hipStream_t st);

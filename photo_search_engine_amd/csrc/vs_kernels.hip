@@ -102,7 +102,7 @@ __device__ __forceinline__ float load_elem(const uint8_t* p) {
     else if constexpr (DT == DT_BF16) return bf16_bits_to_f32(*(const uint16_t*)p);
     else return f16_bits_to_f32(*(const uint16_t*)p);
 }
-// 16 B unit -> fp32 values (4 for f32, 8 for bf16/f16)
+// 16 B unit -> fp32 values (4 for f32, 8 for bf16/f16, 16 for the int8 screen copy)
 template <int DT>
 __device__ __forceinline__ void unpack16(const uint4 r, float* v) {
     if constexpr (DT == DT_F32) {
@@ -113,6 +113,12 @@ __device__ __forceinline__ void unpack16(const uint4 r, float* v) {
         v[2] = __uint_as_float(r.y << 16); v[3] = __uint_as_float(r.y & 0xFFFF0000u);
         v[4] = __uint_as_float(r.z << 16); v[5] = __uint_as_float(r.z & 0xFFFF0000u);
         v[6] = __uint_as_float(r.w << 16); v[7] = __uint_as_float(r.w & 0xFFFF0000u);
+    } else if constexpr (DT == DT_I8) {  // 16 int8 codes
+        const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[4 * i + j] = (float)((int32_t)(w[i] << (24 - 8 * j)) >> 24);
     } else {
         v[0] = f16_bits_to_f32(r.x & 0xFFFFu); v[1] = f16_bits_to_f32(r.x >> 16);
         v[2] = f16_bits_to_f32(r.y & 0xFFFFu); v[3] = f16_bits_to_f32(r.y >> 16);
@@ -1104,12 +1110,17 @@ __device__ __forceinline__ uint4 ld_nt16(const uint8_t* p) {
 // ------------------------------------------------------------------------------------------------
 // K2: GEMV screen (any dtype, up to 8 queries per launch) -- HBM streaming, fp32 FMA
 // ------------------------------------------------------------------------------------------------
-// 256 threads, persistent over a contiguous tile range.  A row's 32-element chunk is LPR 16 B
-// units, read by LPR consecutive lanes, so every wave-instruction is a contiguous 1 KiB piece.
+// 256 threads, persistent over a contiguous tile range.  A row's chunk (32 elements; 64 for the
+// int8 screen copy) is LPR 16 B units, read by LPR consecutive lanes, so every wave-instruction is
+// a contiguous 1 KiB piece.  int8: the fp32 dot of the codes with the fp32 query (no query
+// quantisation), key = s_x * dot + beta_x * ||q|| (an upper bound of the true score up to fp32
+// rounding, certified in k_refine).
 template <int DT, int NQ>
 __global__ void __launch_bounds__(256) k_screen_gemv(ScreenArgs a, const float* __restrict__ qp, int nqb) {
-    constexpr int ES = DT == DT_F32 ? 4 : 2;
-    constexpr int CB = CH * ES;
+    constexpr bool I8 = DT == DT_I8;
+    constexpr int ES = DT == DT_F32 ? 4 : I8 ? 1 : 2;
+    constexpr int CHK = I8 ? 64 : CH;  // elements per chunk
+    constexpr int CB = CHK * ES;
     constexpr int LPR = CB / 16;
     constexpr int RPI = 64 / LPR;
     constexpr int EPU = 16 / ES;
@@ -1136,7 +1147,7 @@ __global__ void __launch_bounds__(256) k_screen_gemv(ScreenArgs a, const float* 
         cnt[tid] = 0;
     }
     __syncthreads();
-    const int nch = a.dpad / CH;
+    const int nch = a.dpad / CHK;
     const int64_t tbytes = (int64_t)TR * a.dpad * ES;
     u64* cand = a.cand + (size_t)blk * NQ * a.cap;
     const int trigger = a.cap - TR;
@@ -1168,7 +1179,7 @@ __global__ void __launch_bounds__(256) k_screen_gemv(ScreenArgs a, const float* 
                 float qv[NQ][EPU];
 #pragma unroll
                 for (int qi = 0; qi < NQ; ++qi) {
-                    const float4* qs = (const float4*)(qp + (int64_t)qi * a.dpad + c * CH + unit * EPU);
+                    const float4* qs = (const float4*)(qp + (int64_t)qi * a.dpad + c * CHK + unit * EPU);
 #pragma unroll
                     for (int h = 0; h < EPU / 4; ++h) {
                         float4 t = qs[h];
@@ -1208,11 +1219,19 @@ __global__ void __launch_bounds__(256) k_screen_gemv(ScreenArgs a, const float* 
                     const int rit = wid * 64 + (gb * RB + r) * RPI + rsub;
                     const int64_t gr = rowbase + rit;
                     if (gr >= a.n_valid) continue;
-                    const float sq = a.metric == METRIC_L2 ? a.sqn[gr] : 0.0f;
+                    float sq = 0.0f, rbeta = 0.0f;
+                    if constexpr (I8) {
+                        const uint32_t w = a.rsb[gr];
+                        sq = __uint_as_float(w << 16);            // scale s_x
+                        rbeta = __uint_as_float(w & 0xFFFF0000u);  // error norm beta_x
+                    } else {
+                        sq = a.metric == METRIC_L2 ? a.sqn[gr] : 0.0f;
+                    }
 #pragma unroll
                     for (int qi = 0; qi < NQ; ++qi) {
                         float sc = acc[r][qi];
-                        if (a.metric == METRIC_L2) sc = 2.0f * sc - sq;
+                        if constexpr (I8) sc = fmaf(rbeta, a.qinfo[2 * qi], sq * sc);
+                        else if (a.metric == METRIC_L2) sc = 2.0f * sc - sq;
                         if (sc >= thr_f[qi]) {
                             const u64 key = mk_key(sc, (uint32_t)gr);
                             if (key > thr_key[qi]) {
@@ -1845,6 +1864,10 @@ __global__ void __launch_bounds__(RF_THREADS) k_refine(RefineArgs a, int KP2) {
             const double qh = (double)a.qinfo[2 * q], dq = (double)a.qinfo[2 * q + 1];
             const double xm = (double)a.xmax;
             double eps = ((double)a.gamma * qh + dq) * xm * 1.01 + 1e-30;
+            if (a.i8max) {  // int8 GEMV keys: fp32 dot of the codes (gamma) + the key's 3 roundings
+                const double X = (double)__uint_as_float(a.i8max[0]), B = (double)__uint_as_float(a.i8max[1]);
+                eps = ((double)a.gamma * X + 3.0 * 5.9604644775390625e-08 * (X + B)) * qh * 1.01 + 1e-30;
+            }
             double tk = sc[a.k - 1];
             if (a.metric == METRIC_L2) {
                 eps = 2.0 * eps + ((double)a.gamma + 4.0 * 5.9604644775390625e-08) * (xm * xm + 2.0 * xm * qh) * 1.01 +
@@ -2408,10 +2431,12 @@ static int gemv_occ(int nqpad) {
     return e == hipSuccess && n > 0 ? n : 4;
 }
 int gemv_blocks_per_cu(int dt, int nqpad) {
-    static int cache[3][9] = {};  // benign race: idempotent
+    static int cache[4][9] = {};  // benign race: idempotent
     const int q = nqpad <= 1 ? 1 : nqpad <= 2 ? 2 : nqpad <= 4 ? 4 : 8;
     int& v = cache[dt][q];
-    if (!v) v = dt == DT_F32 ? gemv_occ<DT_F32>(q) : dt == DT_BF16 ? gemv_occ<DT_BF16>(q) : gemv_occ<DT_F16>(q);
+    if (!v)
+        v = dt == DT_F32 ? gemv_occ<DT_F32>(q) : dt == DT_BF16 ? gemv_occ<DT_BF16>(q)
+            : dt == DT_I8 ? gemv_occ<DT_I8>(q) : gemv_occ<DT_F16>(q);
     return v;
 }
 
@@ -2425,8 +2450,10 @@ static void launch_gemv_dt(const ScreenArgs& a, const float* qp, int nqb, int nq
     }
 }
 hipError_t launch_screen_gemv(int dt, const ScreenArgs& a, const float* qp, int nqb, int nqpad, hipStream_t st) {
+    if (dt == DT_I8 && (a.metric != METRIC_IP || !a.rsb || !a.qinfo)) return hipErrorInvalidValue;
     if (dt == DT_F32) launch_gemv_dt<DT_F32>(a, qp, nqb, nqpad, st);
     else if (dt == DT_BF16) launch_gemv_dt<DT_BF16>(a, qp, nqb, nqpad, st);
+    else if (dt == DT_I8) launch_gemv_dt<DT_I8>(a, qp, nqb, nqpad, st);
     else launch_gemv_dt<DT_F16>(a, qp, nqb, nqpad, st);
     return hipGetLastError();
 }

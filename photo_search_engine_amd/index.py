@@ -136,7 +136,7 @@ class FlatIndex:
         buf = (ctypes.c_float * cap)()
         kind = ctypes.c_int(0)
         n = check(self._L.vs_timing_fetch(self._h, buf, cap, ctypes.byref(kind)))
-        return [float(buf[i]) for i in range(n)], {1: "mfma", 2: "gemv", 3: "mfma_i8"}.get(kind.value, "none")
+        return [float(buf[i]) for i in range(n)], {1: "mfma", 2: "gemv", 3: "mfma_i8", 4: "gemv_i8"}.get(kind.value, "none")
 
     def uncertified_count(self) -> int:
         return int(check(self._L.vs_uncertified_count(self._h)))

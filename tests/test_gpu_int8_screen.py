@@ -130,3 +130,40 @@ def test_int8_screen_argument_errors(FlatIndex):
         ix.set_screen("int8")  # inner product only
     with pytest.raises(ValueError):
         FlatIndex(32, "ip", "bf16").set_screen("fp4")
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("nq,k", [(1, 1), (1, 10), (1, 500), (3, 37), (8, 100)])
+def test_int8_gemv_screen_exact(FlatIndex, dtype, nq, k):
+    # few queries (the product's single-query call): the GEMV streams the int8 copy with the fp32
+    # query; ids and scores bit-exact, and the timed screen is the int8 GEMV
+    N, d = 120_000, 200
+    ix = FlatIndex(d, "ip", dtype)
+    ix.add_synthetic(O.SEED_CORPUS, 0, N, True)
+    ix.set_screen("int8")
+    q = O.synth_rows(O.SEED_QUERIES, 40 + nq, nq, d, True, "f32")
+    ix.set_timing(True)
+    _exact(ix, q, k)
+    ix.set_timing(False)
+    assert ix.timing_fetch()[1] == "gemv_i8"
+    assert ix.uncertified_count() == 0
+    ix.close()
+
+
+def test_int8_gemv_cfg2_shape_matches_native(FlatIndex):
+    # BASELINE cfg2 (N=1M d=1536 fp32, batch 1, top-10) through the int8 GEMV screen
+    N, d = 1_000_000, 1536
+    ix = FlatIndex(d, "ip", "f32")
+    ix.add_synthetic(O.SEED_CORPUS, 0, N, True)
+    qs = [O.synth_rows(O.SEED_QUERIES, i, 1, d, True, "f32") for i in range(4)]
+    native = [ix.search(q, 10) for q in qs]
+    ix.set_screen("int8")
+    x = ix.reconstruct_n(0, N)
+    for q, (Dn, In) in zip(qs, native):
+        D, I = ix.search(q, 10)
+        S, Ie = O.knn_exact(x, q, 10, "ip")
+        np.testing.assert_array_equal(I, Ie)
+        np.testing.assert_array_equal(I, In)
+        np.testing.assert_array_equal(D, Dn)
+    assert ix.uncertified_count() == 0
+    ix.close()
