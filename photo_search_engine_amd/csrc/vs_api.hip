@@ -95,6 +95,7 @@ struct vs_index {
     int64_t cap8 = 0;
     uint8_t* data8 = nullptr;
     uint32_t* rsb = nullptr;  // per row: bf16 scale | bf16 error norm (rounded up) << 16
+    float i8_bmax = 0.0f;     // host copy of the largest row error norm (int8 GEMV depth)
     hipStream_t own = nullptr;  // ingest stream
     DevBuf stage[2];            // add_rows_host: fp32 chunks on the device ...
     PinnedPair pin;             // ... and their pinned host sources
@@ -224,12 +225,11 @@ void quantize_rows(vs_index* ix, int64_t r0, int64_t n, hipStream_t st) {
 }
 
 void refresh_maxsq(vs_index* ix) {
-    unsigned bits = 0;
-    HIP_CHECK(hipMemcpyAsync(&bits, ix->d_maxsq, sizeof(unsigned), hipMemcpyDeviceToHost, ix->own));
+    unsigned bits[4] = {0, 0, 0, 0};
+    HIP_CHECK(hipMemcpyAsync(bits, ix->d_maxsq, sizeof(bits), hipMemcpyDeviceToHost, ix->own));
     HIP_CHECK(hipStreamSynchronize(ix->own));
-    float f;
-    std::memcpy(&f, &bits, 4);
-    ix->maxsq = f;
+    std::memcpy(&ix->maxsq, &bits[0], 4);
+    std::memcpy(&ix->i8_bmax, &bits[3], 4);  // int8 copy: the largest row error norm
 }
 
 // optimistic seed: a 16-row-group maximum of the strided tile sample, at the rank that leaves
@@ -253,6 +253,17 @@ bool gemv_dyn() {
 // VS_SCREEN_I8; a query its certificate rejects is re-searched by the caller on the native path.
 bool use_i8(const vs_index* ix, int nqb, int k) {
     return ix->screen == VS_SCREEN_I8 && nqb > GEMV_NQ_MAX && k <= I8_MAX_K;
+}
+// int8 GEMV screen depth.  Its keys carry the row error bound beta (~0.007-0.01 ||x|| ||q||), so the
+// rows it must keep are those within ~beta of the k-th best.  For unit rows the scores are roughly
+// N(0, 1/d) and the k-th best sits z = sqrt(2 ln(N / k)) deviations out, where the density grows by
+// e^(z beta sqrt(d)) per beta: keep k times twice that (+64); deeper than kI8GemvMaxDepth, the
+// native GEMV serves the query.  Data that defeat the estimate fail the certificate, not exactness.
+constexpr int kI8GemvMaxDepth = 512;
+int i8_gemv_depth(const vs_index* ix, int k) {
+    const double z = std::sqrt(2.0 * std::log(std::max(2.0, (double)ix->ntotal / k)));
+    const double g = std::exp(std::min(20.0, z * (double)ix->i8_bmax * std::sqrt((double)ix->d)));
+    return (int)std::min<double>(KP_MAX, round_up((int64_t)std::ceil(2.0 * k * g + 64.0), 16));
 }
 // union of survivors the int8 seed aims at: ~kI8UnionPerK * k rows above the seeded threshold
 // (cfg3: k = 100 -> 6,400; the refine scores ~1.3k of them)
@@ -363,8 +374,12 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
     const bool use_mfma = ix->dtype != DT_F32 && nqb > GEMV_NQ_MAX;
     // int8 screen, few queries: the GEMV streams the int8 copy (1 B per element) with the fp32
     // query; its keys carry the row error bound, so it screens deeper (first passes only)
-    const bool gemv_i8 = !use_mfma && seed_rank > 0 && ix->screen == VS_SCREEN_I8 && ix->data8 != nullptr;
-    if (gemv_i8) Kp = (int)std::min<int64_t>(KP_MAX, round_up(std::max(8 * k, k + 64), 16));
+    bool gemv_i8 = !use_mfma && seed_rank > 0 && ix->screen == VS_SCREEN_I8 && ix->data8 != nullptr;
+    if (gemv_i8) {
+        const int kp8 = i8_gemv_depth(ix, k);
+        gemv_i8 = kp8 <= kI8GemvMaxDepth;  // a single query's refine is one workgroup: deep lists cost
+        if (gemv_i8) Kp = kp8;             // more than the int8 stream saves -> native GEMV
+    }
     ScreenArgs a{};
     a.corpus = ix->data;
     a.n_valid = ix->ntotal;
@@ -746,6 +761,7 @@ int vs_reset(vs_index* ix) {
         DeviceGuard dg(ix->device);
         ix->ntotal = 0;
         ix->maxsq = 0.0f;
+        ix->i8_bmax = 0.0f;
         HIP_CHECK(hipMemsetAsync(ix->d_maxsq, 0, sizeof(unsigned), ix->own));
         HIP_CHECK(hipMemsetAsync(ix->d_maxsq + 2, 0, 2 * sizeof(unsigned), ix->own));
         HIP_CHECK(hipStreamSynchronize(ix->own));
@@ -990,6 +1006,7 @@ int vs_set_screen(vs_index* ix, int screen) {
             ensure_capacity_i8(ix);
             quantize_rows(ix, 0, ix->ntotal, ix->own);
             HIP_CHECK(hipStreamSynchronize(ix->own));
+            refresh_maxsq(ix);
         } catch (...) {
             free_i8(ix);
             ix->screen = VS_SCREEN_NATIVE;

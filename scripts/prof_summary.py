@@ -83,10 +83,11 @@ def main():
         summary["kernels"][f"{name} grid={grid}"] = flat
     # the bench's dominant screen (its roofline kernel; the seed pass's <.., true> variant excluded)
     kind = (bench_line or {}).get("roofline", {}).get("kernel", "")
-    pat = {"k_screen_mfma_i8": "k_screen_mfma<3,", "k_screen_mfma": "k_screen_mfma<", "k_screen_gemv": "k_screen_gemv"}
+    pat = {"k_screen_mfma_i8": "k_screen_mfma<3,", "k_screen_mfma": "k_screen_mfma<",
+           "k_screen_gemv_i8": "k_screen_gemv<3,", "k_screen_gemv": "k_screen_gemv<"}
     screens = {k: v for k, v in summary["kernels"].items()
                if pat.get(kind, "k_screen") in k and "true>" not in k and v.get("dur_s")
-               and not (kind == "k_screen_mfma" and "k_screen_mfma<3," in k)}
+               and not (kind in ("k_screen_mfma", "k_screen_gemv") and "<3," in k)}
     if screens and bench_line and bench_line["config"]["workload"] != "cfg5":
         top = max(screens, key=lambda k: screens[k]["dur_s"])
         t = screens[top]

@@ -136,7 +136,7 @@ def test_int8_screen_argument_errors(FlatIndex):
 @pytest.mark.parametrize("nq,k", [(1, 1), (1, 10), (1, 500), (3, 37), (8, 100)])
 def test_int8_gemv_screen_exact(FlatIndex, dtype, nq, k):
     # few queries (the product's single-query call): the GEMV streams the int8 copy with the fp32
-    # query; ids and scores bit-exact, and the timed screen is the int8 GEMV
+    # query (k <= 128); ids and scores bit-exact, and the timed screen is the int8 GEMV
     N, d = 120_000, 200
     ix = FlatIndex(d, "ip", dtype)
     ix.add_synthetic(O.SEED_CORPUS, 0, N, True)
@@ -145,7 +145,7 @@ def test_int8_gemv_screen_exact(FlatIndex, dtype, nq, k):
     ix.set_timing(True)
     _exact(ix, q, k)
     ix.set_timing(False)
-    assert ix.timing_fetch()[1] == "gemv_i8"
+    assert ix.timing_fetch()[1] == ("gemv_i8" if k <= 128 else "gemv")  # deep single queries: native
     assert ix.uncertified_count() == 0
     ix.close()
 
