@@ -631,8 +631,10 @@ constexpr int MF_DEPTH = MF_SLOTS - 1;
 constexpr int MF_THREADS = 512;
 constexpr int MF_POOL = 512;  // LDS insert pool of the loader waves (flushed by the writer waves)
 constexpr int MF_SX = 8 * 64 * 8 * 4;  // per-wave insert staging: 64 lanes x 8 fp32 (slow path only)
-constexpr int MF_QFAC = 256 * 8;       // int8 screen: (t_q, ||q||) per query
-constexpr int MF_LDS = MF_SLOTS * MF_SLOT + 256 * 8 + 256 * 4 + 256 * 4 + 16 + MF_POOL * 8 + MF_POOL * 4 + MF_SX + MF_QFAC;
+constexpr int MF_QFAC = 256 * 8;       // int8 screen: (t_q, ||q|| / t_q) per query
+constexpr int MF_ROWX = 256 * 4;       // per-row side data of the tile (int8: scale | beta; L2: ||x||^2)
+constexpr int MF_LDS = MF_SLOTS * MF_SLOT + 256 * 8 + 256 * 4 + 256 * 4 + 16 + MF_POOL * 8 + MF_POOL * 4 + MF_SX + MF_QFAC +
+                       MF_ROWX;
 static_assert(MF_LDS <= 160 * 1024, "LDS budget");
 
 typedef __attribute__((address_space(3))) uint8_t* lds_u8_t;
@@ -772,6 +774,7 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
     float* sx = (float*)(smem + MF_SLOTS * MF_SLOT + 256 * 16 + 16 + MF_POOL * 12) + (threadIdx.x >> 6) * 512 +
                 (threadIdx.x & 63) * 8;
     float2* qfac = (float2*)(smem + MF_SLOTS * MF_SLOT + 256 * 16 + 16 + MF_POOL * 12 + MF_SX);
+    uint32_t* rowx = (uint32_t*)(smem + MF_SLOTS * MF_SLOT + 256 * 16 + 16 + MF_POOL * 12 + MF_SX + MF_QFAC);
 
     // The LDS ring is written only by the inline-asm DMA: let the array escape into an asm with a
     // memory clobber, so the compiler must assume every later memory-clobbering asm (DMA issue,
@@ -829,15 +832,24 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
     }
     int ti = t0, ks = 0;
     bool check_pending = false;
-    // int8: the tile's packed per-row (scale, error norm), 16 rows per lane, loaded PF_LEAD K-steps
-    // before its epilogue so the HBM latency hides behind the MFMAs (rows past the shard read the
-    // allocation's padding; the epilogue masks them)
-    uint4 pf_rsb[4] = {};
+    // Per-row side data of a tile (int8: packed scale | error norm; L2: ||x||^2), 4 B per row, staged
+    // in LDS by the WRITER waves: one row per lane loaded 8 K-steps before the tile's epilogue and
+    // stored to LDS 2 K-steps before it.  The loader waves issue no ordinary loads at all: a
+    // compiler-placed wait for one would count their in-flight LDS-DMA stages too (the asm DMAs
+    // are invisible to it, so it waits for vmcnt(0)) and drain the stream pipeline every tile.
+    constexpr bool ROWX = I8 || METRIC == METRIC_L2;
+    uint32_t rowx_w = 0;
     const int pf_ks = nks > 8 ? nks - 8 : 0;
-    auto prefetch_rsb = [&](int tile) {
-        const uint32_t* p = a.rsb + (int64_t)tile * TR + wm * 64 + (lane >> 4) * 4;
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi) pf_rsb[mi] = *(const uint4*)(p + mi * 16);
+    const int st_ks = nks > 2 ? nks - 2 : 0;
+    auto rowx_load = [&](int tile) {
+        if (wid >= 4) {
+            const int64_t gr = (int64_t)tile * TR + wm * 64 + lane;
+            if constexpr (I8) rowx_w = gr < a.n_valid ? a.rsb[gr] : 0u;
+            else rowx_w = gr < a.n_valid ? __float_as_uint(a.sqn[gr]) : 0u;
+        }
+    };
+    auto rowx_store = [&]() {
+        if (wid >= 4) rowx[wm * 64 + lane] = rowx_w;
     };
     // tile epilogue over the accumulators of tile `ti` (shared by the K loop and the seed tile)
     auto tile_epilogue = [&](const int ti) {
@@ -870,25 +882,22 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
                 for (int r = 0; r < 4; ++r)
                     if (rowbase + rid0 + mi * 16 + r >= a.n_valid) bad |= 1u << (mi * 4 + r);
         }
-        float sq[4][4], rb[4][4];  // L2: ||x||^2; int8: the row's scale and error norm (prefetched)
-        if constexpr (I8) {
+        float sq[4][4], rb[4][4];  // L2: ||x||^2; int8: the row's scale and error norm (from LDS)
+        if constexpr (ROWX) {
 #pragma unroll
             for (int mi = 0; mi < 4; ++mi) {
-                const uint32_t w4[4] = {pf_rsb[mi].x, pf_rsb[mi].y, pf_rsb[mi].z, pf_rsb[mi].w};
+                const uint4 w = *(const uint4*)(rowx + rid0 + mi * 16);
+                const uint32_t w4[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    sq[mi][r] = __uint_as_float(w4[r] << 16);
-                    rb[mi][r] = __uint_as_float(w4[r] & 0xFFFF0000u);
+                    if constexpr (I8) {
+                        sq[mi][r] = __uint_as_float(w4[r] << 16);
+                        rb[mi][r] = __uint_as_float(w4[r] & 0xFFFF0000u);
+                    } else {
+                        sq[mi][r] = __uint_as_float(w4[r]);
+                    }
                 }
             }
-        } else if constexpr (METRIC == METRIC_L2) {
-#pragma unroll
-            for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int64_t gr = rowbase + rid0 + mi * 16 + r;
-                    sq[mi][r] = gr < a.n_valid ? a.sqn[gr] : 0.0f;
-                }
         }
 #pragma unroll
         for (int ni = 0; ni < 8; ++ni) {
@@ -1001,7 +1010,11 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
         for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
             for (int ni = 0; ni < 8; ++ni) acc[mi][ni] = src[mi * 8 + ni];
-        if constexpr (I8) prefetch_rsb(tseed);
+        if constexpr (ROWX) {
+            rowx_load(tseed);
+            rowx_store();
+            mf_barrier_lgkm();
+        }
         tile_epilogue(tseed);
     }
     for (int s = 0; s < S; ++s) {
@@ -1013,8 +1026,11 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
                      ring + (uint32_t)(((s + MF_DEPTH) % MF_SLOTS) * MF_SLOT), tid);
             if (++iks == nks) { iks = 0; ++iti; }
         }
-        if constexpr (I8)
-            if (ks == pf_ks) prefetch_rsb(ti);
+        if constexpr (ROWX) {
+            if (ks == pf_ks) rowx_load(ti);
+            if (ks == st_ks) rowx_store();  // read by the epilogue after the next barrier
+            if (nks == 1) mf_barrier_lgkm();  // (one K-step per tile: stored and read in this step)
+        }
         mf_compute<DT>(smem + (s % MF_SLOTS) * MF_SLOT, acc, wm, wn, lane_off);
         if (ks == nks - 1) tile_epilogue(ti);
         // Deferred compaction check, after the NEXT K-step's barrier: by then every wave's
