@@ -175,6 +175,11 @@ def main():
                "hbm_frac": round(bytes_n / (kn * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                "uncertified_first_pass": unc_n}
     elapsed, kms, kind, uncert, t_switch = timed(screen)
+    unresolved = ix.unresolved_count()  # queries the device fallback could not certify (must be 0)
+    if G > 1:
+        t = torch.tensor([unresolved], dtype=torch.int64, device=dev)
+        dist.all_reduce(t)
+        unresolved = int(t.item())
     if alt is not None:  # both screens return the same exact answer
         alt["identical_results"] = bool(torch.equal(result["I"], res_native["I"]) and
                                         torch.equal(result["S"], res_native["S"]))
@@ -231,6 +236,7 @@ def main():
             },
             # first-pass certificate failures; every one was re-searched exactly (search_device_exact)
             "uncertified_first_pass": uncert,
+            "unresolved": unresolved,
             "build_s": round(t_build, 2),
         }
         if kind in ("mfma_i8", "gemv_i8"):

@@ -76,6 +76,7 @@ _SIGS = {
     "vs_set_timing": (ctypes.c_int, [_vp, ctypes.c_int]),
     "vs_timing_fetch": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
     "vs_uncertified_count": (_c_i64, [_vp]),
+    "vs_unresolved_count": (_c_i64, [_vp]),
     "vs_host_staging_bytes": (_c_i64, [_vp]),
     # multi-device flat index
     "vs_multi_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp,

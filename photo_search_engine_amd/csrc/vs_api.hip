@@ -56,6 +56,7 @@ struct Ctx {
     bool pending = false;
     DevBuf qdev, qtile, qinfo, qpad, cand, part, merge_a, merge_b, outD, outI, outS, cert, thr0, seedmax, gcnt;
     DevBuf qfac, qeps, drop;  // int8 screen: per-query code scale and norm, refine margin, drop bounds
+    DevBuf fails;             // the current query block's certificate-failure count (fallback gate)
     DevBuf rows[2];  // read_rows_host: unpacked fp32 chunks
     DevBuf tilectr;  // GEMV screen: tile work-queue counter
     DevBuf seedacc;  // MFMA seed pass: raw accumulators of each workgroup's seed tile
@@ -65,7 +66,7 @@ struct Ctx {
     HostBuf hout;    // vs_search: I (int64), D (fp32) and certificates land here; search_exact_device: certificates
     ~Ctx() {
         for (DevBuf* b : {&qdev, &qtile, &qinfo, &qpad, &cand, &part, &merge_a, &merge_b, &outD, &outI, &outS, &cert, &thr0,
-                          &seedmax, &gcnt, &rows[0], &rows[1], &tilectr, &seedacc, &outAll, &qfac, &qeps, &drop})
+                          &seedmax, &gcnt, &rows[0], &rows[1], &tilectr, &seedacc, &outAll, &qfac, &qeps, &drop, &fails})
             b->release();
         pin.release();
         hq.release();
@@ -87,6 +88,7 @@ struct vs_index {
     float* sqn = nullptr;
     unsigned* d_maxsq = nullptr;
     unsigned* d_uncert = nullptr;
+    unsigned* d_unres = nullptr;  // queries the device fallback round could not certify either
     float maxsq = 0.0f;
     // int8 screen copy (VS_SCREEN_I8): codes in row tiles of 64-element chunks + per-row scale and
     // error norm; d_maxsq[2..3] = max ||x_hat||, max error norm (fp32 bits, certificate margins)
@@ -291,8 +293,10 @@ void search_block_i8(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float
     c->qeps.ensure(sizeof(float) * MFMA_QB);
     c->drop.ensure(sizeof(u64) * MFMA_QB);
     c->gcnt.ensure(sizeof(int) * MFMA_QB);
+    c->fails.ensure(sizeof(int));
     HIP_CHECK(launch_pack_qtile_i8(q, nqb, ix->d, ix->dpad8, c->qtile.as<uint8_t>(), c->qfac.as<float2>(),
-                                   c->qeps.as<float>(), ix->d_maxsq + 2, c->gcnt.as<int>(), c->drop.as<u64>(), st));
+                                   c->qeps.as<float>(), ix->d_maxsq + 2, c->gcnt.as<int>(), c->drop.as<u64>(), st,
+                                   c->fails.as<int>()));
     a.qfac = c->qfac.as<float2>();
     a.drop = c->drop.as<u64>();
     a.lcap = a.G * a.Kp;
@@ -359,19 +363,26 @@ void search_block_i8(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float
     r.qeps = c->qeps.as<float>();
     r.drop = a.drop;
     r.thr0 = a.thr0;
+    r.fails = c->fails.as<int>();
     HIP_CHECK(launch_refine_wide(r, nqb, (int)round_up(2 * k + 32, 32), st));
 }
 
 // Enqueue one query block through screen -> merge -> refine.  q: device fp32 [nqb][d].
 // seed_rank: 0 = proven (safe) seed, > 0 = optimistic seed at that sample rank (see k_seed_select)
+// redo: the device fallback round of the block just searched (MFMA dtypes, unseeded screen): its
+// three launches (pack, screen, refine) are gated on the block's failure count (c->fails) and the
+// refine rewrites only the queries whose certificate failed; a query it cannot certify either
+// counts in d_unres
 void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, float* D, int64_t* I, double* S64,
-                  int* cert, int64_t id_offset, hipStream_t st, int seed_rank) {
+                  int* cert, int64_t id_offset, hipStream_t st, int seed_rank, bool redo = false) {
     if (seed_rank > 0 && use_i8(ix, nqb, k)) {
         search_block_i8(ix, c, q, nqb, k, D, I, S64, cert, id_offset, st);
         return;
     }
     const int64_t tiles = (ix->ntotal + TR - 1) / TR;
-    const bool use_mfma = ix->dtype != DT_F32 && nqb > GEMV_NQ_MAX;
+    const bool use_mfma = ix->dtype != DT_F32 && (nqb > GEMV_NQ_MAX || redo);
+    const int* gate = redo ? c->fails.as<int>() : nullptr;
+    if (!redo) c->fails.ensure(sizeof(int));
     // int8 screen, few queries: the GEMV streams the int8 copy (1 B per element) with the fp32
     // query; its keys carry the row error bound, so it screens deeper (first passes only)
     bool gemv_i8 = !use_mfma && seed_rank > 0 && ix->screen == VS_SCREEN_I8 && ix->data8 != nullptr;
@@ -401,7 +412,8 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
         c->gcnt.ensure(sizeof(int) * MFMA_QB);
         c->drop.ensure(sizeof(u64) * MFMA_QB);
         HIP_CHECK(launch_pack_qtile(ix->dtype, q, nqb, ix->d, ix->dpad, c->qtile.as<uint8_t>(), c->qinfo.as<float>(),
-                                    c->gcnt.as<int>(), c->drop.as<u64>(), st));
+                                    c->gcnt.as<int>(), c->drop.as<u64>(), st, redo ? nullptr : c->fails.as<int>(),
+                                    gate));
     } else {
         QB = nqb <= 1 ? 1 : nqb <= 2 ? 2 : nqb <= 4 ? 4 : 8;
         a.cap = (int)round_up(Kp + 2 * TR, 256);
@@ -415,7 +427,8 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
             c->tilectr.ensure(sizeof(int));
             ctr = c->tilectr.as<int>();
         }
-        HIP_CHECK(launch_pack_qf32(q, nqb, QB, ix->d, dpadq, c->qpad.as<float>(), c->qinfo.as<float>(), st, ctr));
+        HIP_CHECK(launch_pack_qf32(q, nqb, QB, ix->d, dpadq, c->qpad.as<float>(), c->qinfo.as<float>(), st, ctr,
+                                   c->fails.as<int>()));
         if (gemv_i8) {
             a.corpus = ix->data8;
             a.dpad = ix->dpad8;
@@ -424,6 +437,7 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
         }
     }
     a.G = std::max(a.G, 1);
+    a.gate = gate;
     c->cand.ensure((size_t)a.G * QB * a.cap * sizeof(u64));
     c->part.ensure((size_t)a.G * QB * a.Kp * sizeof(u64));  // GEMV: [G][QB][Kp]; MFMA: [QB][G*Kp] survivor lists
     a.cand = c->cand.as<u64>();
@@ -463,7 +477,8 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
     a.tile_stride = 0;
     a.thr0 = nullptr;
     bool optimistic = false;
-    if (use_mfma && tiles >= 4 * (int64_t)a.G) {
+    // (not in a fallback round: its launches cost their dispatch on every call, and it rarely runs)
+    if (use_mfma && !redo && tiles >= 4 * (int64_t)a.G) {
         ScreenArgs sa = a;
         sa.G = std::min(sa.G, 512);  // k_seed_select holds up to 8192 maxima per query
         sa.tile_stride = (int)(tiles / sa.G);
@@ -496,7 +511,7 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
         optimistic = rank < Kp;
     }
 
-    const bool timing = ix->timing.load();
+    const bool timing = ix->timing.load() && !redo;  // (a fallback round is not the timed screen)
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (timing) {
         HIP_CHECK(hipEventCreate(&e0));
@@ -545,14 +560,22 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
     r.I = I;
     r.S64 = S64;
     r.cert = cert;
-    r.uncert = ix->d_uncert;
+    r.uncert = redo ? ix->d_unres : ix->d_uncert;
+    r.fails = redo ? nullptr : c->fails.as<int>();
+    r.redo = redo ? 1 : 0;
+    r.gate = gate;
     r.optimistic = optimistic ? 1 : 0;
     HIP_CHECK(launch_refine(r, nqb, st));
 }
 
-// Full search of nq device queries; outputs device [nq][k].
+// Depth of the device fallback round: the end of vs_search's host escalation (KP_MAX), within
+// the shard.
+int fallback_depth(const vs_index* ix) { return (int)std::min<int64_t>(KP_MAX, round_up(ix->ntotal, 16)); }
+
+// Full search of nq device queries; outputs device [nq][k].  device_fallback: every block's first
+// pass is followed by its gated fallback round (no host round trip; MFMA dtypes only).
 void search_all(vs_index* ix, Ctx* c, const float* q, int64_t nq, int k, int Kp, float* D, int64_t* I, double* S64,
-                int* cert, int64_t id_offset, hipStream_t st, int seed_rank) {
+                int* cert, int64_t id_offset, hipStream_t st, int seed_rank, bool device_fallback = false) {
     const int64_t tiles = (ix->ntotal + TR - 1) / TR;
     (void)tiles;
     const bool mfma_ok = (seed_rank > 0 && ix->screen == VS_SCREEN_I8 && k <= I8_MAX_K) || ix->dtype != DT_F32;
@@ -564,6 +587,9 @@ void search_all(vs_index* ix, Ctx* c, const float* q, int64_t nq, int k, int Kp,
         else nqb = (int)std::min<int64_t>(rem, GEMV_NQ_MAX);
         search_block(ix, c, q + done * ix->d, nqb, k, Kp, D ? D + done * k : nullptr, I + done * k,
                      S64 ? S64 + done * k : nullptr, cert ? cert + done : nullptr, id_offset, st, seed_rank);
+        if (device_fallback)
+            search_block(ix, c, q + done * ix->d, nqb, k, std::max(Kp, fallback_depth(ix)), D ? D + done * k : nullptr,
+                         I + done * k, S64 ? S64 + done * k : nullptr, cert + done, id_offset, st, 0, true);
         done += nqb;
     }
 }
@@ -575,9 +601,14 @@ void check_index(const vs_index* ix) {
 }  // namespace
 
 // exact device search (vs_search_device_exact; the IVF coarse quantizer): like vs_search_device,
-// but certificate failures are re-searched with deeper screens, as vs_search does
+// but certificate failures are re-searched.  bf16 / f16 indexes: on the device, by each query
+// block's gated fallback round at the deepest screen (KP_MAX, where vs_search's escalation ends).
+// async: no host round trip at all, the call returns with the work queued and a query even the
+// fallback cannot certify counts in vs_unresolved_count; otherwise the certificates are read back
+// and such a query raises VS_ERR_UNCERTIFIED, as in vs_search.  fp32 indexes (GEMV re-search):
+// read back the certificates and re-search with deeper screens, as vs_search does.
 void vs::search_exact_device(vs_index* ix, const float* q_dev, int64_t nq, int k, int64_t* I_dev, double* S64_dev,
-                             hipStream_t st, float* D_dev, int64_t id_offset) {
+                             hipStream_t st, float* D_dev, int64_t id_offset, bool async) {
     check_index(ix);
     if (nq <= 0) return;
     std::shared_lock<std::shared_mutex> lk(ix->rw);
@@ -588,12 +619,19 @@ void vs::search_exact_device(vs_index* ix, const float* q_dev, int64_t nq, int k
     c->outD.ensure((size_t)nq * k * sizeof(float));
     c->cert.ensure((size_t)nq * sizeof(int));
     const int Kp = screen_depth(k);
+    const bool on_device = ix->dtype != DT_F32;
     search_all(ix, c, q_dev, nq, k, Kp, D_dev ? D_dev : c->outD.as<float>(), I_dev, S64_dev, c->cert.as<int>(),
-               id_offset, st, kOptimisticSeedRank);
+               id_offset, st, kOptimisticSeedRank, on_device);
+    if (on_device && async) return;
     c->hout.ensure((size_t)nq * sizeof(int));
     int* cert_h = (int*)c->hout.p;
     HIP_CHECK(hipMemcpyAsync(cert_h, c->cert.p, (size_t)nq * sizeof(int), hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));
+    if (on_device) {
+        for (int64_t qi = 0; qi < nq; ++qi)
+            if (!cert_h[qi]) throw VsError(VS_ERR_UNCERTIFIED, "exactness certificate failed at maximum screening depth");
+        return;
+    }
     for (int64_t qi = 0; qi < nq; ++qi) {
         int Kr = Kp;
         while (!cert_h[qi]) {
@@ -607,6 +645,8 @@ void vs::search_exact_device(vs_index* ix, const float* q_dev, int64_t nq, int k
         }
     }
 }
+
+unsigned* vs::unresolved_counter(vs_index* ix) { return ix->d_unres; }
 
 int64_t vs::stream_chunk_rows(int d) { return std::max<int64_t>(1, (int64_t)(32 << 20) / ((int64_t)d * 4)); }
 
@@ -712,7 +752,7 @@ int vs_create(int d, int metric, int dtype, int device, vs_index** out) {
         ix->d = d;
         // >= 2 K-steps per tile: the MFMA screen's deferred compaction check runs on the K-step
         // after a tile's epilogue, so a one-step tile would never compact its candidate buffers
-        ix->dpad = (int)std::max<int64_t>(round_up(d, CH), 2 * CH);
+        ix->dpad = pad_dim(d, dtype);
         ix->metric = metric;
         ix->dtype = dtype;
         ix->device = device;
@@ -720,10 +760,12 @@ int vs_create(int d, int metric, int dtype, int device, vs_index** out) {
         ix->num_cu = prop.multiProcessorCount;
         try {
             HIP_CHECK(hipStreamCreateWithFlags(&ix->own, hipStreamNonBlocking));
-            // [0] max ||x||^2, [1] uncertified counter, [2..3] int8 screen maxima (fp32 bits)
-            HIP_CHECK(hipMalloc(&ix->d_maxsq, sizeof(unsigned) * 4));
-            HIP_CHECK(hipMemset(ix->d_maxsq, 0, sizeof(unsigned) * 4));
+            // [0] max ||x||^2, [1] uncertified counter, [2..3] int8 screen maxima (fp32 bits),
+            // [4] unresolved counter (device fallback)
+            HIP_CHECK(hipMalloc(&ix->d_maxsq, sizeof(unsigned) * 8));
+            HIP_CHECK(hipMemset(ix->d_maxsq, 0, sizeof(unsigned) * 8));
             ix->d_uncert = ix->d_maxsq + 1;
+            ix->d_unres = ix->d_maxsq + 4;
         } catch (...) {
             delete ix;
             throw;
@@ -865,7 +907,7 @@ int vs_search_device_exact(vs_index* ix, const float* q_dev, int64_t nq, int32_t
         if (nq == 0) return;
         if (!q_dev || !I_dev) throw VsError(VS_ERR_ARG, "null device buffer");
         if (ix->ntotal == 0) throw VsError(VS_ERR_ARG, "index is empty");
-        search_exact_device(ix, q_dev, nq, k, I_dev, S64_dev, (hipStream_t)stream, D_dev, id_offset);
+        search_exact_device(ix, q_dev, nq, k, I_dev, S64_dev, (hipStream_t)stream, D_dev, id_offset, /*async*/ true);
     });
 }
 
@@ -1051,6 +1093,19 @@ int64_t vs_host_staging_bytes(vs_index* ix) {
     int64_t b = 0;
     for (const Ctx* c : ix->pool_all) b += (int64_t)(c->hq.bytes + c->hout.bytes);
     return b;
+}
+
+int64_t vs_unresolved_count(vs_index* ix) {
+    int64_t v = -1;
+    int rc = guarded([&] {
+        check_index(ix);
+        DeviceGuard dg(ix->device);
+        HIP_CHECK(hipDeviceSynchronize());
+        unsigned u = 0;
+        HIP_CHECK(hipMemcpy(&u, ix->d_unres, sizeof(unsigned), hipMemcpyDeviceToHost));
+        v = u;
+    });
+    return rc == VS_OK ? v : rc;
 }
 
 int64_t vs_uncertified_count(vs_index* ix) {

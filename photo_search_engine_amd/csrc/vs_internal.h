@@ -1,13 +1,14 @@
 // vs_internal.h -- shared constants, HBM layout and kernel launchers of libvs (gfx950 only).
 //
 // HBM layout of a corpus shard ("row tiles"):
-//   rows are grouped in tiles of TR = 256; d is padded to dpad = roundup(d, 32);
-//   inside a tile the matrix is stored chunk-major: [chunk c = i / 32][row r in tile][32 elements]
-//   so element (r, i) of a tile lives at  c*(TR*CB) + (r % TR)*CB + (i % 32)*es,
-//   CB = 32*es bytes (64 B bf16/f16, 128 B f32).
-// One K-step of the MFMA screen (256 rows x 32 elements) is therefore one contiguous 16 KiB
-// (bf16) block, every global load is a full 16 B/lane coalesced piece, and a row's chunk is a
-// 64 B / 128 B contiguous piece for the exact-rescoring gather.
+//   rows are grouped in tiles of TR = 256; a chunk is CE = CHB / es elements (32 fp32, 64 bf16 /
+//   f16), one 128 B line per row; d is padded to dpad = roundup(d, CE) (>= 64);
+//   inside a tile the matrix is stored chunk-major: [chunk c = i / CE][row r in tile][CE elements]
+//   so element (r, i) of a tile lives at  c*(TR*CHB) + (r % TR)*CHB + (i % CE)*es.
+// A row's piece of a chunk fills one 128 B line, so the exact-rescoring gather of a candidate row
+// fetches only that row's bytes.  One MFMA K-step (256 rows x 32 bf16 elements) reads the
+// 64 B half of every row's line (the next K-step the other half, from L2); every global load is
+// a 16 B/lane piece of a 64 B run.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -21,7 +22,8 @@
 namespace vs {
 
 constexpr int TR = 256;        // rows per tile
-constexpr int CH = 32;         // elements per chunk (= one MFMA K-step)
+constexpr int CH = 32;         // elements per MFMA K-step (bf16 / f16: half a chunk)
+constexpr int CHB = 128;       // bytes of a row's piece of one chunk: one 128 B line
 constexpr int DT_F32 = 0, DT_BF16 = 1, DT_F16 = 2;
 constexpr int DT_I8 = 3;        // internal: the int8 screen copy (per-row scale, exact int32 MFMA)
 constexpr int METRIC_IP = 0, METRIC_L2 = 1;
@@ -38,6 +40,12 @@ constexpr int KP_MAX = 4096;   // largest screening depth (k <= 3276; k_refine s
 constexpr int SELECT_E = 16;   // keys per thread in block selection (256 threads -> 4096 keys)
 
 inline int es_of(int dt) { return dt == DT_F32 ? 4 : 2; }
+// padded dimension of the tiled layout: whole chunks, >= 2 MFMA K-steps per tile (the screen's
+// deferred compaction check runs on the K-step after a tile's epilogue)
+inline int pad_dim(int d, int dt) {
+    const int ce = CHB / es_of(dt);
+    return (int)std::max<int64_t>(((int64_t)d + ce - 1) / ce * ce, 2 * CH);
+}
 inline int64_t tile_bytes(int dpad, int dt) { return (int64_t)TR * dpad * es_of(dt); }
 inline int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
 
@@ -184,6 +192,8 @@ struct ScreenArgs {
     const float* qinfo;      // int8 GEMV: per query [2q] = ||q|| rounded up (k_pack_qf32)
     u64* drop;               // MFMA: per query, max over workgroups of their compaction threshold
                              // (rows below it were dropped; zeroed by the query pack), or null
+    const int* gate;         // device fallback round: the launch does nothing while *gate == 0 (no
+                             // query of the block failed its certificate), or null = always run
 };
 int gemv_blocks_per_cu(int dt, int nqpad);  // resident k_screen_gemv blocks per CU (occupancy API)
 
@@ -201,10 +211,13 @@ hipError_t launch_gather_rows(int dt, const uint8_t* data, const int64_t* ids, i
 
 // queries: MFMA tile (dtype, [nks][256][32]) or fp32 padded [NQ][dpad]; qinfo[q*2] = ||q_hat||,
 // qinfo[q*2+1] = ||q_hat - q|| (upper bounds, fp32)
+// fails (optional): zeroed -- the query block's certificate-failure count (RefineArgs::fails);
+// gate (optional): as ScreenArgs::gate
 hipError_t launch_pack_qtile(int dt, const float* q, int nqb, int d, int dpad, uint8_t* qt, float* qinfo, int* gcnt,
-                             u64* drop, hipStream_t st);
+                             u64* drop, hipStream_t st, int* fails = nullptr, const int* gate = nullptr);
 hipError_t launch_pack_qf32(const float* q, int nqb, int nqpad, int d, int dpad, float* qp, float* qinfo,
-                            hipStream_t st, int* ctr = nullptr);  // ctr: zeroed (a screen's tile queue)
+                            hipStream_t st, int* ctr = nullptr,  // ctr: zeroed (a screen's tile queue)
+                            int* fails = nullptr);
 
 hipError_t launch_screen_mfma(int dt, const ScreenArgs& a, const uint8_t* qt, int nqb, hipStream_t st);
 hipError_t launch_screen_gemv(int dt, const ScreenArgs& a, const float* qp, int nqb, int nqpad, hipStream_t st);
@@ -239,6 +252,9 @@ struct RefineArgs {
     const u64* thr0;       // the screen's starting threshold per query (or null = none)
     const unsigned* i8max; // int8 GEMV screen: (max ||x_hat||, max beta) fp32 bits -> the certificate margin
     const uint32_t* idmap; // IVF: user id of every storage slot (keys carry slots); null = identity
+    int* fails;            // first pass: count of the block's uncertified queries (the fallback's gate)
+    int redo;              // device fallback round: only queries with cert[q] == 0 are refined (and
+    const int* gate;       //  their outputs rewritten), nothing at all while *gate == 0
 };
 hipError_t launch_refine(const RefineArgs& a, int nq, hipStream_t st);
 // exact refine behind the int8 screen: adaptive two-phase depth (KA keys first), IP only
@@ -248,7 +264,7 @@ constexpr int I8_MAX_K = 1024;  // largest k the int8 screen serves (k_refine_wi
 hipError_t launch_quant_rows(int dt, const uint8_t* data, int dpad, int64_t r0, int64_t n, int d, uint8_t* data8,
                              int dpad8, uint32_t* rsb, unsigned* maxes, hipStream_t st);
 hipError_t launch_pack_qtile_i8(const float* q, int nqb, int d, int dpad8, uint8_t* qt, float2* qfac, float* qeps,
-                                const unsigned* maxes, int* gcnt, u64* drop, hipStream_t st);
+                                const unsigned* maxes, int* gcnt, u64* drop, hipStream_t st, int* fails = nullptr);
 
 // ---- IVF-Flat (vs_ivf.hip) ---------------------------------------------------------------------
 // Inverted lists are chains of pages: a page is one row tile (TR rows, the flat layout above) of
@@ -299,10 +315,12 @@ void read_rows_host(vs_index* ix, int64_t i0, int64_t n,
                     const std::function<void(int64_t, int64_t, const float*)>& sink);
 int64_t stream_chunk_rows(int d);  // rows per pinned chunk (32 MiB of fp32)
 
-// Exact top-k of device queries over a flat index, certificate failures re-searched (host-
-// synchronising).  I_dev [nq][k] (k <= ntotal), S64_dev optional.
+// Exact top-k of device queries over a flat index, certificate failures re-searched (bf16/f16: by
+// a gated fallback round on the device; async = no host sync, unresolved queries counted in
+// vs_unresolved_count instead of raising).  I_dev [nq][k], S64_dev optional.
 void search_exact_device(vs_index* ix, const float* q_dev, int64_t nq, int k, int64_t* I_dev, double* S64_dev,
-                         hipStream_t st, float* D_dev = nullptr, int64_t id_offset = 0);
+                         hipStream_t st, float* D_dev = nullptr, int64_t id_offset = 0, bool async = false);
+unsigned* unresolved_counter(vs_index* ix);  // device word behind vs_unresolved_count
 // seed pass: screen one tile per workgroup (tile_stride) and write per-query 16-row-group maxima
 hipError_t launch_seed_mfma(int dt, const ScreenArgs& a, const uint8_t* qt, int nqb, hipStream_t st);
 // thr0[q] = key just below the rank-th largest of the M group maxima of query q (0 if none)

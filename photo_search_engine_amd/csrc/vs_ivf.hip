@@ -412,7 +412,7 @@ int vs_ivf_create(int d, int nlist, int metric, int dtype, int device, vs_ivf** 
         vs_ivf* ix = new vs_ivf();
         ix->coarse = coarse;
         ix->d = d;
-        ix->dpad = (int)std::max<int64_t>(round_up(d, CH), 2 * CH);
+        ix->dpad = pad_dim(d, dtype);
         ix->nlist = nlist;
         ix->metric = metric;
         ix->dtype = dtype;

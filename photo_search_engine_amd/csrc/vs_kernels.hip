@@ -290,8 +290,9 @@ __device__ __forceinline__ int block_compact_mem(const u64* src, u64* dst, int n
 // ingest: pack host/device fp32 rows into the tiled layout; synthetic rows; unpack
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ int64_t tiled_off(int64_t row, int i, int dpad, int es) {
-    return (row / TR) * (int64_t)TR * dpad * es + (int64_t)(i >> 5) * TR * CH * es + (row % TR) * CH * es +
-           (int64_t)(i & 31) * es;
+    const int ce = CHB / es;  // (es is a compile-time constant at every call)
+    return (row / TR) * (int64_t)TR * dpad * es + (int64_t)(i / ce) * TR * CHB + (row % TR) * CHB +
+           (int64_t)(i % ce) * es;
 }
 
 // one wave per row; element i handled by lane i & 63 (the canonical fp32 order for sqn)
@@ -443,10 +444,13 @@ __global__ void __launch_bounds__(256) k_gather_rows(const uint8_t* __restrict__
 template <int DT>
 __global__ void __launch_bounds__(256) k_pack_qtile(const float* __restrict__ q, int nqb, int d, int dpad,
                                                      uint8_t* __restrict__ qt, float* __restrict__ qinfo,
-                                                     int* __restrict__ gcnt, u64* __restrict__ drop) {
+                                                     int* __restrict__ gcnt, u64* __restrict__ drop,
+                                                     int* __restrict__ fails, const int* __restrict__ gate) {
+    if (gate && *gate == 0) return;  // device fallback round with nothing to re-search
     const int lane = threadIdx.x & 63;
     const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= MFMA_QB) return;
+    if (fails && r == 0 && lane == 0) *fails = 0;  // the block's certificate-failure count
     if (gcnt && lane == 0) gcnt[r] = 0;  // survivor-list lengths of the screen that follows ...
     if (drop && lane == 0) drop[r] = 0ull;  // ... and its workgroups' drop bounds
     double n2 = 0.0, e2 = 0.0;
@@ -544,10 +548,12 @@ __global__ void __launch_bounds__(256) k_quant_rows(const uint8_t* __restrict__ 
 __global__ void __launch_bounds__(256) k_pack_qtile_i8(const float* __restrict__ q, int nqb, int d, int dpad8,
                                                         uint8_t* __restrict__ qt, float2* __restrict__ qfac,
                                                         float* __restrict__ qeps, const unsigned* __restrict__ maxes,
-                                                        int* __restrict__ gcnt, u64* __restrict__ drop) {
+                                                        int* __restrict__ gcnt, u64* __restrict__ drop,
+                                                        int* __restrict__ fails) {
     const int lane = threadIdx.x & 63;
     const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= MFMA_QB) return;
+    if (fails && r == 0 && lane == 0) *fails = 0;
     if (lane == 0) {
         gcnt[r] = 0;
         drop[r] = 0ull;
@@ -589,10 +595,11 @@ __global__ void __launch_bounds__(256) k_pack_qtile_i8(const float* __restrict__
 // GEMV queries: fp32, [nqpad][dpad] zero padded; q_hat = q
 __global__ void __launch_bounds__(256) k_pack_qf32(const float* __restrict__ q, int nqb, int nqpad, int d, int dpad,
                                                     float* __restrict__ qp, float* __restrict__ qinfo,
-                                                    int* __restrict__ ctr) {
+                                                    int* __restrict__ ctr, int* __restrict__ fails) {
     const int lane = threadIdx.x & 63;
     const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (ctr && blockIdx.x == 0 && threadIdx.x == 0) *ctr = 0;  // the GEMV screen's tile queue that follows
+    if (fails && blockIdx.x == 0 && threadIdx.x == 0) *fails = 0;  // the block's certificate-failure count
     if (r >= nqpad) return;
     double n2 = 0.0;
     for (int i = lane; i < dpad; i += 64) {
@@ -632,7 +639,7 @@ constexpr int MF_THREADS = 512;
 constexpr int MF_POOL = 512;  // LDS insert pool of the loader waves (flushed by the writer waves)
 constexpr int MF_SX = 8 * 64 * 8 * 4;  // per-wave insert staging: 64 lanes x 8 fp32 (slow path only)
 constexpr int MF_QFAC = 256 * 8;       // int8 screen: (t_q, ||q|| / t_q) per query
-constexpr int MF_ROWX = 256 * 4;       // per-row side data of the tile (int8: scale | beta; L2: ||x||^2)
+constexpr int MF_ROWX = 2 * 256 * 4;   // per-row side data of two tiles (int8: scale | beta; L2: ||x||^2)
 constexpr int MF_LDS = MF_SLOTS * MF_SLOT + 256 * 8 + 256 * 4 + 256 * 4 + 16 + MF_POOL * 8 + MF_POOL * 4 + MF_SX + MF_QFAC +
                        MF_ROWX;
 static_assert(MF_LDS <= 160 * 1024, "LDS budget");
@@ -659,35 +666,43 @@ __device__ __forceinline__ int mf_swz(int r) { return (0x78 >> (2 * ((r >> 2) & 
 // issue one K-step stage: waves 0-3 (the loader waves) issue 8 LDS-DMA instructions per thread
 // (4 corpus + 4 query); waves 4-7 issue none.  Loader waves never store to global memory and the
 // writer waves never load, so each wave's in-order vmcnt holds one kind of traffic: counted waits
-// on the stage ring are never held up behind candidate stores.
+// on the stage ring are never held up behind candidate stores.  Corpus rows are 1 << RS bytes
+// apart (bf16 / f16: 128, the K-step reads the first or second 64 B of each row's line; int8: 64,
+// contiguous); the LDS block is [row][64 B] either way.
+template <int RS, int NLW>
 __device__ __forceinline__ void mf_stage(const uint8_t* __restrict__ gA, const uint8_t* __restrict__ gB,
                                          uint32_t slot_base, int tid) {
+    constexpr int NIT = 16 / NLW;  // DMA instructions per loader wave per operand
     const int w = tid >> 6, lane = tid & 63;
-    if (w >= 4) return;
+    if (w >= NLW) return;
     const uint32_t base = __builtin_amdgcn_readfirstlane(slot_base + (uint32_t)(w * 64 * 16));
 #pragma unroll
-    for (int it = 0; it < 4; ++it) {
-        const int g = it * 256 + w * 64 + lane;
+    for (int it = 0; it < NIT; ++it) {
+        const int g = it * (NLW * 64) + w * 64 + lane;
         const int row = g >> 2, pos = g & 3;
-        const int src = (row << 2) + (pos ^ mf_swz(row));
-        glds16_nt(gA + (size_t)src * 16, base + it * 256 * 16);
+        // int8: each 64 B row piece is read once -> non-temporal; bf16 / f16: the line's other
+        // half is read by the next K-step, so it must stay in L2 (default policy)
+        if constexpr (RS == 6) glds16_nt(gA + ((size_t)row << RS) + (size_t)(pos ^ mf_swz(row)) * 16, base + it * NLW * 1024);
+        else glds16(gA + ((size_t)row << RS) + (size_t)(pos ^ mf_swz(row)) * 16, base + it * NLW * 1024);
     }
 #pragma unroll
-    for (int it = 0; it < 4; ++it) {  // the query tile is re-read by every CU: default policy (L2)
-        const int g = it * 256 + w * 64 + lane;
+    for (int it = 0; it < NIT; ++it) {  // the query tile is re-read by every CU: default policy (L2)
+        const int g = it * (NLW * 64) + w * 64 + lane;
         const int row = g >> 2, pos = g & 3;
         const int src = (row << 2) + (pos ^ mf_swz(row));
-        glds16(gB + (size_t)src * 16, base + it * 256 * 16 + 16384);
+        glds16(gB + (size_t)src * 16, base + it * NLW * 1024 + 16384);
     }
 }
 
-// wait until at most `ahead` younger stages (8 LDS-DMA each) of a loader wave are in flight, then
-// barrier; writer waves only drain their LDS traffic
+// wait until at most `ahead` younger stages (32 / NLW LDS-DMA each) of a loader wave are in
+// flight, then barrier; other waves only drain their LDS traffic
+template <int NLW>
 __device__ __forceinline__ void mf_wait_barrier(int ahead, bool loader) {
+    constexpr int P = 32 / NLW;
     if (!loader) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    else if (ahead >= 3) asm volatile("s_waitcnt vmcnt(24) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    else if (ahead == 2) asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if (ahead >= 3) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(3 * P) : "memory");
+    else if (ahead == 2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(2 * P) : "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(P) : "memory");
     else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 __device__ __forceinline__ void mf_barrier_lgkm() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
@@ -761,7 +776,7 @@ __device__ __forceinline__ void mf_wave_compact(u64* __restrict__ buf, int n, in
 // s_x t_q <c_x, c_q> + ||e_x|| ||q|| of the true inner product (the query-side error term is
 // uniform over rows and sits in the refine's margin).
 template <int DT, int METRIC, bool SEED>
-__global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
+__device__ __forceinline__ void screen_mfma(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
     constexpr bool I8 = DT == DT_I8;
     static_assert(!I8 || METRIC == METRIC_IP, "the int8 screen serves inner-product indexes");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -808,8 +823,17 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
         flag[2] = 0;
         flag[3] = 0;
     }
-    const int nks = a.dpad / (I8 ? 64 : CH);  // K-steps per tile (one 16 KiB block each)
+    const int nks = a.dpad / (I8 ? 64 : CH);  // K-steps per tile (16 KiB each)
     const int64_t tbytes = (int64_t)TR * a.dpad * (I8 ? 1 : 2);
+    constexpr int RS = I8 ? 6 : 7;  // log2 of the corpus row stride within a chunk (see mf_stage)
+    // waves issuing the stage DMAs (8 each per K-step): the loader waves.  Spreading them over all
+    // 8 waves (4 each) measured slower for both screens (int8 K1 4.39 -> 4.54 ms, bf16 7.60 -> 7.94)
+    constexpr int NLW = 4;
+    // K-step ks of tile ti: int8 -> chunk ks (64 B per row); bf16 / f16 -> half (ks & 1) of chunk ks / 2
+    auto kblock = [&](int ti, int ks) -> const uint8_t* {
+        if constexpr (I8) return a.corpus + (int64_t)ti * tbytes + (int64_t)ks * 16384;
+        else return a.corpus + (int64_t)ti * tbytes + (int64_t)(ks >> 1) * (TR * CHB) + (ks & 1) * 64;
+    };
     const int S = (t1 - t0) * nks;
     u64* cand = a.cand + (size_t)blk * MFMA_QB * a.cap;
     const int trigger = a.cap - TR;
@@ -823,34 +847,43 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
 #pragma unroll
         for (int ni = 0; ni < 8; ++ni) acc[mi][ni] = floatx4{0.f, 0.f, 0.f, 0.f};
 
+    // Per-row side data of a tile (int8: packed scale | error norm; L2: ||x||^2), 4 B per row = one
+    // 1 KiB LDS-DMA by wave 0 into buffer (tile & 1), issued 3 K-steps before the tile's epilogue
+    // (after the previous reader of that buffer, two tiles back): the counted wait of the
+    // epilogue's K-step covers it, like a stage.  No ordinary global load in the K loop, so no
+    // compiler-placed wait ever drains the in-flight stages.
+    constexpr bool ROWX = I8 || METRIC == METRIC_L2;
+    const uint32_t* rowsrc = I8 ? a.rsb : (const uint32_t*)a.sqn;
+    auto rowx_issue = [&](int tile) {
+        const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_addr((const uint8_t*)(rowx + (tile & 1) * TR)));
+        glds16(rowsrc + (int64_t)tile * TR + lane * 4, dst);
+    };
+    // the DMA for the epilogue at loop step j (if j ends a tile)
+    auto rowx_rule = [&](int j) {
+        if (j >= S) return;
+        const int tile = t0 + j / nks;
+        if (j % nks == nks - 1) rowx_issue(tile);
+    };
+    if constexpr (ROWX) {
+        if (wid == 0) {
+            if (reuse) {  // the seed tile's epilogue runs before the loop (below)
+                rowx_issue(tseed);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            for (int j = 0; j < 3; ++j) rowx_rule(j);  // epilogues at loop steps 0..2
+        }
+        if (reuse) mf_barrier_lgkm();
+    }
+
     // prologue: stages 0 .. DEPTH-1
     int iti = t0, iks = 0;  // (tile, k-step) of the next stage to issue
     for (int j = 0; j < MF_DEPTH && j < S; ++j) {
-        mf_stage(a.corpus + (int64_t)iti * tbytes + (int64_t)iks * 16384, qt + (int64_t)iks * 16384,
+        mf_stage<RS, NLW>(kblock(iti, iks), qt + (int64_t)iks * 16384,
                  ring + (uint32_t)(j * MF_SLOT), tid);
         if (++iks == nks) { iks = 0; ++iti; }
     }
     int ti = t0, ks = 0;
     bool check_pending = false;
-    // Per-row side data of a tile (int8: packed scale | error norm; L2: ||x||^2), 4 B per row, staged
-    // in LDS by the WRITER waves: one row per lane loaded 8 K-steps before the tile's epilogue and
-    // stored to LDS 2 K-steps before it.  The loader waves issue no ordinary loads at all: a
-    // compiler-placed wait for one would count their in-flight LDS-DMA stages too (the asm DMAs
-    // are invisible to it, so it waits for vmcnt(0)) and drain the stream pipeline every tile.
-    constexpr bool ROWX = I8 || METRIC == METRIC_L2;
-    uint32_t rowx_w = 0;
-    const int pf_ks = nks > 8 ? nks - 8 : 0;
-    const int st_ks = nks > 2 ? nks - 2 : 0;
-    auto rowx_load = [&](int tile) {
-        if (wid >= 4) {
-            const int64_t gr = (int64_t)tile * TR + wm * 64 + lane;
-            if constexpr (I8) rowx_w = gr < a.n_valid ? a.rsb[gr] : 0u;
-            else rowx_w = gr < a.n_valid ? __float_as_uint(a.sqn[gr]) : 0u;
-        }
-    };
-    auto rowx_store = [&]() {
-        if (wid >= 4) rowx[wm * 64 + lane] = rowx_w;
-    };
     // tile epilogue over the accumulators of tile `ti` (shared by the K loop and the seed tile)
     auto tile_epilogue = [&](const int ti) {
         // ---- fused top-k epilogue: threshold filter, rare inserts ----
@@ -886,7 +919,7 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
         if constexpr (ROWX) {
 #pragma unroll
             for (int mi = 0; mi < 4; ++mi) {
-                const uint4 w = *(const uint4*)(rowx + rid0 + mi * 16);
+                const uint4 w = *(const uint4*)(rowx + (ti & 1) * TR + rid0 + mi * 16);
                 const uint32_t w4[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
@@ -1010,27 +1043,19 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint
         for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
             for (int ni = 0; ni < 8; ++ni) acc[mi][ni] = src[mi * 8 + ni];
-        if constexpr (ROWX) {
-            rowx_load(tseed);
-            rowx_store();
-            mf_barrier_lgkm();
-        }
-        tile_epilogue(tseed);
+        tile_epilogue(tseed);  // (its side data landed before the prologue stages were issued)
     }
     for (int s = 0; s < S; ++s) {
         const int left = S - 1 - s;
-        mf_wait_barrier(left < MF_DEPTH - 1 ? left : MF_DEPTH - 1, wid < 4);
+        mf_wait_barrier<NLW>(left < MF_DEPTH - 1 ? left : MF_DEPTH - 1, wid < NLW);
         const bool do_issue = s + MF_DEPTH < S;  // stage issued at step s: s + DEPTH
         if (do_issue) {
-            mf_stage(a.corpus + (int64_t)iti * tbytes + (int64_t)iks * 16384, qt + (int64_t)iks * 16384,
+            mf_stage<RS, NLW>(kblock(iti, iks), qt + (int64_t)iks * 16384,
                      ring + (uint32_t)(((s + MF_DEPTH) % MF_SLOTS) * MF_SLOT), tid);
             if (++iks == nks) { iks = 0; ++iti; }
         }
-        if constexpr (ROWX) {
-            if (ks == pf_ks) rowx_load(ti);
-            if (ks == st_ks) rowx_store();  // read by the epilogue after the next barrier
-            if (nks == 1) mf_barrier_lgkm();  // (one K-step per tile: stored and read in this step)
-        }
+        if constexpr (ROWX)
+            if (wid == 0) rowx_rule(s + 3);
         mf_compute<DT>(smem + (s % MF_SLOTS) * MF_SLOT, acc, wm, wn, lane_off);
         if (ks == nks - 1) tile_epilogue(ti);
         // Deferred compaction check, after the NEXT K-step's barrier: by then every wave's
@@ -1123,19 +1148,31 @@ __device__ __forceinline__ uint4 ld_nt16(const uint8_t* p) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+template <int DT, int METRIC, bool SEED>
+__global__ void __launch_bounds__(512, 2) k_screen_mfma(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
+    screen_mfma<DT, METRIC, SEED>(a, qt, nqb);
+}
+// the device fallback round's screen (gated on the block's failure count): its own symbol, so a
+// profile never averages its (almost always empty) launches with the main screen's
+template <int DT, int METRIC>
+__global__ void __launch_bounds__(512, 2) k_screen_mfma_redo(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
+    if (*a.gate == 0) return;
+    screen_mfma<DT, METRIC, false>(a, qt, nqb);
+}
+
 // ------------------------------------------------------------------------------------------------
 // K2: GEMV screen (any dtype, up to 8 queries per launch) -- HBM streaming, fp32 FMA
 // ------------------------------------------------------------------------------------------------
-// 256 threads, persistent over a contiguous tile range.  A row's chunk (32 elements; 64 for the
-// int8 screen copy) is LPR 16 B units, read by LPR consecutive lanes, so every wave-instruction is
-// a contiguous 1 KiB piece.  int8: the fp32 dot of the codes with the fp32 query (no query
+// 256 threads, persistent over a contiguous tile range.  A row's piece of a chunk (one 128 B line;
+// 64 B in the int8 screen copy) is LPR 16 B units, read by LPR consecutive lanes, so every
+// wave-instruction is a contiguous 1 KiB piece.  int8: the fp32 dot of the codes with the fp32 query (no query
 // quantisation), key = s_x * dot + beta_x * ||q|| (an upper bound of the true score up to fp32
 // rounding, certified in k_refine).
 template <int DT, int NQ>
 __global__ void __launch_bounds__(256) k_screen_gemv(ScreenArgs a, const float* __restrict__ qp, int nqb) {
     constexpr bool I8 = DT == DT_I8;
     constexpr int ES = DT == DT_F32 ? 4 : I8 ? 1 : 2;
-    constexpr int CHK = I8 ? 64 : CH;  // elements per chunk
+    constexpr int CHK = I8 ? 64 : CHB / ES;  // elements per chunk
     constexpr int CB = CHK * ES;
     constexpr int LPR = CB / 16;
     constexpr int RPI = 64 / LPR;
@@ -1305,7 +1342,8 @@ template <int DT, int NQ>
 __device__ __forceinline__ void ivf_scan_item(const IvfScanArgs& a, const int* itm, u64* cand, u64* thr_key,
                                               float* thr_f, int* cnt, int* qid, int* red, int* off_s) {
     constexpr int ES = DT == DT_F32 ? 4 : 2;
-    constexpr int CB = CH * ES;
+    constexpr int CE = CHB / ES;  // elements per chunk
+    constexpr int CB = CHB;
     constexpr int LPR = CB / 16;
     constexpr int RPI = 64 / LPR;
     constexpr int EPU = 16 / ES;
@@ -1315,7 +1353,7 @@ __device__ __forceinline__ void ivf_scan_item(const IvfScanArgs& a, const int* i
     static_assert(RG % RB == 0, "row groups");
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int unit = lane % LPR, rsub = lane / LPR;
-    const int nch = a.dpad / CH;
+    const int nch = a.dpad / CE;
     const int64_t tbytes = (int64_t)TR * a.dpad * ES;
     const int trigger = a.cap - TR;
     const int l = itm[0], p0 = itm[1], p1 = itm[2], nqi = itm[3];
@@ -1345,7 +1383,7 @@ __device__ __forceinline__ void ivf_scan_item(const IvfScanArgs& a, const int* i
                 float qv[NQ][EPU];
 #pragma unroll
                 for (int qi = 0; qi < NQ; ++qi) {
-                    const float4* qs = (const float4*)(a.qp + (int64_t)qid[qi] * a.dpad + c * CH + unit * EPU);
+                    const float4* qs = (const float4*)(a.qp + (int64_t)qid[qi] * a.dpad + c * CE + unit * EPU);
 #pragma unroll
                     for (int h = 0; h < EPU / 4; ++h) {
                         float4 t = qs[h];
@@ -1463,7 +1501,8 @@ __global__ void __launch_bounds__(256, 3) k_ivf_scan_dyn(IvfScanArgs a) {
 template <int DT, int NQ>
 __global__ void __launch_bounds__(256) k_ivf_scan(IvfScanArgs a) {
     constexpr int ES = DT == DT_F32 ? 4 : 2;
-    constexpr int CB = CH * ES;
+    constexpr int CE = CHB / ES;  // elements per chunk
+    constexpr int CB = CHB;
     constexpr int LPR = CB / 16;
     constexpr int RPI = 64 / LPR;
     constexpr int EPU = 16 / ES;
@@ -1481,7 +1520,7 @@ __global__ void __launch_bounds__(256) k_ivf_scan(IvfScanArgs a) {
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int unit = lane % LPR, rsub = lane / LPR;
-    const int nch = a.dpad / CH;
+    const int nch = a.dpad / CE;
     const int64_t tbytes = (int64_t)TR * a.dpad * ES;
     u64* cand = a.cand + (size_t)blockIdx.x * NQ * a.cap;
     const int trigger = a.cap - TR;
@@ -1516,7 +1555,7 @@ __global__ void __launch_bounds__(256) k_ivf_scan(IvfScanArgs a) {
                     float qv[NQ][EPU];
 #pragma unroll
                     for (int qi = 0; qi < NQ; ++qi) {
-                        const float4* qs = (const float4*)(a.qp + (int64_t)qid[qi] * a.dpad + c * CH + unit * EPU);
+                        const float4* qs = (const float4*)(a.qp + (int64_t)qid[qi] * a.dpad + c * CE + unit * EPU);
 #pragma unroll
                         for (int h = 0; h < EPU / 4; ++h) {
                             float4 t = qs[h];
@@ -1665,9 +1704,10 @@ __device__ __forceinline__ void exact_score_q2(const uint8_t* __restrict__ corpu
     constexpr int NV = DT == DT_F32 ? 2 : 1;
     constexpr int RU = 3;
     const bool two = row1 >= 0;
-    const uint8_t* rb0 = corpus + (row0 / TR) * (int64_t)TR * dpad * ES + (row0 % TR) * (CH * ES);
+    constexpr int CE = CHB / ES;  // elements per chunk: a row's piece is one 128 B line
+    const uint8_t* rb0 = corpus + (row0 / TR) * (int64_t)TR * dpad * ES + (row0 % TR) * CHB;
     const int64_t r1 = two ? row1 : row0;
-    const uint8_t* rb1 = corpus + (r1 / TR) * (int64_t)TR * dpad * ES + (r1 % TR) * (CH * ES);
+    const uint8_t* rb1 = corpus + (r1 / TR) * (int64_t)TR * dpad * ES + (r1 % TR) * CHB;
     const int ng = (d + 7) >> 3;
     double acc0 = 0.0, acc1 = 0.0;
     for (int g0 = lane; g0 < ng; g0 += 64 * RU) {
@@ -1677,7 +1717,7 @@ __device__ __forceinline__ void exact_score_q2(const uint8_t* __restrict__ corpu
             const int g = g0 + 64 * u;
             if (g < ng) {
                 const int e0 = 8 * g;
-                const int64_t off = (int64_t)(e0 >> 5) * TR * CH * ES + (e0 & 31) * ES;
+                const int64_t off = (int64_t)(e0 / CE) * TR * CHB + (e0 % CE) * ES;
 #pragma unroll
                 for (int v = 0; v < NV; ++v) {
                     raw0[u][v] = *(const uint4*)(rb0 + off + 16 * v);
@@ -1742,7 +1782,7 @@ constexpr int RF_WE = 32;         // lists up to 64 * RF_WE keys: threshold foun
 static_assert(64 * RF_WE == kRefineOneWaveKeys, "one-wave selection size");
 
 template <int DT, int METRIC, bool QLDS>
-__global__ void __launch_bounds__(RF_THREADS) k_refine(RefineArgs a, int KP2) {
+__device__ __forceinline__ void refine(const RefineArgs& a, int KP2) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     double* sc = (double*)smem;
     uint32_t* ids = (uint32_t*)(smem + (size_t)KP2 * 8);
@@ -1894,6 +1934,7 @@ __global__ void __launch_bounds__(RF_THREADS) k_refine(RefineArgs a, int KP2) {
         }
         if (a.cert) a.cert[q] = cert;
         if (!cert && a.uncert) atomicAdd(a.uncert, 1u);
+        if (!cert && a.fails) atomicAdd(a.fails, 1);
     }
     for (int j = tid; j < a.k; j += RF_THREADS) {
         const size_t o = (size_t)q * a.k + j;
@@ -1907,6 +1948,18 @@ __global__ void __launch_bounds__(RF_THREADS) k_refine(RefineArgs a, int KP2) {
             if (a.S64) a.S64[o] = a.metric == METRIC_IP ? -1.7976931348623157e308 : 1.7976931348623157e308;
         }
     }
+}
+
+template <int DT, int METRIC, bool QLDS>
+__global__ void __launch_bounds__(RF_THREADS) k_refine(RefineArgs a, int KP2) {
+    refine<DT, METRIC, QLDS>(a, KP2);
+}
+// the device fallback round's refine: only queries the first pass left uncertified (own symbol,
+// as k_screen_mfma_redo)
+template <int DT, int METRIC, bool QLDS>
+__global__ void __launch_bounds__(RF_THREADS) k_refine_redo(RefineArgs a, int KP2) {
+    if (*a.gate == 0 || a.cert[blockIdx.x] != 0) return;
+    refine<DT, METRIC, QLDS>(a, KP2);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2140,6 +2193,7 @@ __global__ void __launch_bounds__(RF_THREADS) k_refine_wide(RefineArgs a, int KA
         }
         if (a.cert) a.cert[q] = cert;
         if (!cert && a.uncert) atomicAdd(a.uncert, 1u);
+        if (!cert && a.fails) atomicAdd(a.fails, 1);
     }
     for (int j = tid; j < a.k; j += RF_THREADS) {
         const size_t o = (size_t)q * a.k + j;
@@ -2367,13 +2421,13 @@ hipError_t launch_gather_rows(int dt, const uint8_t* data, const int64_t* ids, i
 }
 
 hipError_t launch_pack_qtile(int dt, const float* q, int nqb, int d, int dpad, uint8_t* qt, float* qinfo, int* gcnt,
-                             u64* drop, hipStream_t st) {
+                             u64* drop, hipStream_t st, int* fails, const int* gate) {
     if (dt == DT_BF16)
         hipLaunchKernelGGL(k_pack_qtile<DT_BF16>, dim3(MFMA_QB / 4), dim3(256), 0, st, q, nqb, d, dpad, qt, qinfo,
-                           gcnt, drop);
+                           gcnt, drop, fails, gate);
     else
         hipLaunchKernelGGL(k_pack_qtile<DT_F16>, dim3(MFMA_QB / 4), dim3(256), 0, st, q, nqb, d, dpad, qt, qinfo,
-                           gcnt, drop);
+                           gcnt, drop, fails, gate);
     return hipGetLastError();
 }
 
@@ -2392,15 +2446,16 @@ hipError_t launch_quant_rows(int dt, const uint8_t* data, int dpad, int64_t r0, 
 }
 
 hipError_t launch_pack_qtile_i8(const float* q, int nqb, int d, int dpad8, uint8_t* qt, float2* qfac, float* qeps,
-                                const unsigned* maxes, int* gcnt, u64* drop, hipStream_t st) {
+                                const unsigned* maxes, int* gcnt, u64* drop, hipStream_t st, int* fails) {
     hipLaunchKernelGGL(k_pack_qtile_i8, dim3(MFMA_QB / 4), dim3(256), 0, st, q, nqb, d, dpad8, qt, qfac, qeps, maxes,
-                       gcnt, drop);
+                       gcnt, drop, fails);
     return hipGetLastError();
 }
 
 hipError_t launch_pack_qf32(const float* q, int nqb, int nqpad, int d, int dpad, float* qp, float* qinfo,
-                            hipStream_t st, int* ctr) {
-    hipLaunchKernelGGL(k_pack_qf32, dim3(blocks4(nqpad)), dim3(256), 0, st, q, nqb, nqpad, d, dpad, qp, qinfo, ctr);
+                            hipStream_t st, int* ctr, int* fails) {
+    hipLaunchKernelGGL(k_pack_qf32, dim3(blocks4(nqpad)), dim3(256), 0, st, q, nqb, nqpad, d, dpad, qp, qinfo, ctr,
+                       fails);
     return hipGetLastError();
 }
 
@@ -2410,12 +2465,22 @@ static void launch_mfma_one(const ScreenArgs& a, const uint8_t* qt, int nqb, hip
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void*)k_screen_mfma<DT, METRIC, SEED>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, MF_LDS);
+        if constexpr (!SEED && DT != DT_I8)
+            (void)hipFuncSetAttribute((const void*)k_screen_mfma_redo<DT, METRIC>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, MF_LDS);
         attr_set = true;
+    }
+    if constexpr (!SEED && DT != DT_I8) {
+        if (a.gate) {
+            hipLaunchKernelGGL((k_screen_mfma_redo<DT, METRIC>), dim3(a.G), dim3(MF_THREADS), MF_LDS, st, a, qt, nqb);
+            return;
+        }
     }
     hipLaunchKernelGGL((k_screen_mfma<DT, METRIC, SEED>), dim3(a.G), dim3(MF_THREADS), MF_LDS, st, a, qt, nqb);
 }
 template <bool SEED>
 static hipError_t launch_mfma_dt(int dt, const ScreenArgs& a, const uint8_t* qt, int nqb, hipStream_t st) {
+    if (a.gate && (SEED || dt == DT_I8)) return hipErrorInvalidValue;  // fallback rounds: native main screen
     if (dt == DT_I8) {
         if (a.metric != METRIC_IP || !a.rsb || !a.qfac) return hipErrorInvalidValue;
         launch_mfma_one<DT_I8, METRIC_IP, SEED>(a, qt, nqb, st);
@@ -2492,8 +2557,17 @@ static void launch_refine_one(const RefineArgs& a, int nq, int KP2, size_t lds, 
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)k_refine<DT, METRIC, QLDS>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   152 * 1024);
+        if constexpr (DT != DT_F32)
+            (void)hipFuncSetAttribute((const void*)k_refine_redo<DT, METRIC, QLDS>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 152 * 1024);
         (void)hipGetLastError();  // an attribute failure must not surface as the launch's error
         attr = true;
+    }
+    if constexpr (DT != DT_F32) {
+        if (a.redo) {
+            hipLaunchKernelGGL((k_refine_redo<DT, METRIC, QLDS>), dim3(nq), dim3(RF_THREADS), lds, st, a, KP2);
+            return;
+        }
     }
     hipLaunchKernelGGL((k_refine<DT, METRIC, QLDS>), dim3(nq), dim3(RF_THREADS), lds, st, a, KP2);
 }
@@ -2510,6 +2584,7 @@ static void launch_refine_dt(const RefineArgs& a, int nq, int KP2, size_t lds, b
 }
 
 hipError_t launch_refine(const RefineArgs& a, int nq, hipStream_t st) {
+    if (a.redo && (a.dt == DT_F32 || !a.gate || !a.cert)) return hipErrorInvalidValue;  // fallback: bf16 / f16
     int KP2 = 1;
     while (KP2 < a.Kp) KP2 <<= 1;
     const size_t base = (size_t)KP2 * 12 + 8 + (size_t)KP2 * 8;  // scores, ids, (query), kept keys

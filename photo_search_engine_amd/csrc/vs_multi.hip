@@ -117,6 +117,8 @@ struct vs_multi {
     std::vector<DevBuf> qdev, S, I;  // per device: queries, per-shard fp64 scores / global ids
     DevBuf gS, gI, oS, oI, oD;       // device 0: gathered [G][nq][k] lists, merged outputs
     hipEvent_t* ready = nullptr;     // per device: its lists landed on device 0
+    unsigned* unres_h = nullptr;     // pinned, per device: the shard's unresolved-query counter ...
+    std::vector<unsigned> unres_seen;  // ... and its value after the previous search
     int64_t ntotal = 0;
     std::mutex mu;                   // searches and adds are serialised on a multi-device handle
     Pool* pool = nullptr;
@@ -188,6 +190,9 @@ int vs_multi_create(int d, int metric, int dtype, int n_dev, const int* dev_ids,
                 DeviceGuard dg(dev_ids[g]);
                 HIP_CHECK(hipEventCreateWithFlags(&m->ready[g], hipEventDisableTiming));
             }
+            HIP_CHECK(hipHostMalloc((void**)&m->unres_h, sizeof(unsigned) * n_dev, hipHostMallocDefault));
+            std::memset(m->unres_h, 0, sizeof(unsigned) * n_dev);
+            m->unres_seen.assign(n_dev, 0u);
             m->pool = new Pool(n_dev);
         } catch (...) {
             vs_multi_destroy(m);
@@ -200,6 +205,7 @@ int vs_multi_create(int d, int metric, int dtype, int n_dev, const int* dev_ids,
 void vs_multi_destroy(vs_multi* m) {
     if (!m) return;
     delete m->pool;
+    if (m->unres_h) (void)hipHostFree(m->unres_h);
     for (int g = 0; g < (int)m->ix.size(); ++g) {
         DeviceGuard dg(m->dev[g]);
         (void)hipDeviceSynchronize();
@@ -305,8 +311,12 @@ int vs_multi_search(vs_multi* m, const float* q, int64_t nq, int32_t k, float* D
             int64_t* Ig = m->I[g].as<int64_t>();
             HIP_CHECK(hipMemcpyAsync(m->qdev[g].p, q, (size_t)nq * m->d * sizeof(float), hipMemcpyHostToDevice, s));
             if (vs_ntotal(m->ix[g]) > 0) {
-                // exact per shard (uncertified screens re-searched on this device before it returns)
+                // exact per shard: uncertified screens are re-searched on this device, queued behind
+                // the first pass (no host round trip); the shard's count of queries even that
+                // round could not certify travels back with the results
                 throw_rc(vs_search_device_exact(m->ix[g], m->qdev[g].as<float>(), nq, kk, nullptr, Ig, Sg, 0, s));
+                HIP_CHECK(hipMemcpyAsync(&m->unres_h[g], unresolved_counter(m->ix[g]), sizeof(unsigned),
+                                         hipMemcpyDeviceToHost, s));
                 hipLaunchKernelGGL(k_local_to_global, dim3((unsigned)((lb + 255) / 256)), dim3(256), 0, s, Ig,
                                    (int64_t)lb, G, g);
                 HIP_CHECK(hipGetLastError());
@@ -331,7 +341,12 @@ int vs_multi_search(vs_multi* m, const float* q, int64_t nq, int32_t k, float* D
         std::vector<int64_t> Ik(lb);
         HIP_CHECK(hipMemcpyAsync(Dk.data(), m->oD.p, lb * sizeof(float), hipMemcpyDeviceToHost, s0));
         HIP_CHECK(hipMemcpyAsync(Ik.data(), m->oI.p, lb * sizeof(int64_t), hipMemcpyDeviceToHost, s0));
-        HIP_CHECK(hipStreamSynchronize(s0));
+        HIP_CHECK(hipStreamSynchronize(s0));  // (s0 waited for every shard's ready event)
+        for (int g = 0; g < G; ++g)
+            if (vs_ntotal(m->ix[g]) > 0 && m->unres_h[g] != m->unres_seen[g]) {
+                m->unres_seen[g] = m->unres_h[g];
+                throw VsError(VS_ERR_UNCERTIFIED, "exactness certificate failed at maximum screening depth");
+            }
         for (int64_t a = 0; a < nq; ++a)
             for (int j = 0; j < k; ++j) {
                 D[a * k + j] = j < kk ? Dk[a * kk + j] : fillD;

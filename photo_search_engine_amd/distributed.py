@@ -60,7 +60,8 @@ def _device_local_search(index, q: torch.Tensor, k: int, row0: int):
     I = torch.empty((nq, k), dtype=torch.int64, device=q.device)
     D = torch.empty((nq, k), dtype=torch.float32, device=q.device)
     stream = torch.cuda.current_stream(q.device).cuda_stream
-    # exact for every query: uncertified screens are re-searched before the exchange
+    # exact for every query: uncertified screens are re-searched by a fallback round queued on the
+    # device behind the first pass (bf16/f16; no host sync before the exchange)
     index.search_device_exact(q.data_ptr(), nq, k, D.data_ptr(), I.data_ptr(), S.data_ptr(), row0, stream)
     return S, I, D
 
@@ -121,6 +122,12 @@ class ShardedFlatIndex:
     @property
     def n_local(self) -> int:
         return int(self.index.ntotal)
+
+    def unresolved_count(self) -> int:
+        """Queries this rank's device fallback could not certify so far (synchronising; 0 unless
+        more than KP_MAX rows tie within the screen's error margin -- see vs_unresolved_count)."""
+        f = getattr(self.index, "unresolved_count", None)
+        return int(f()) if f else 0
 
     # -- search --------------------------------------------------------------------------------
     def _gather(self, t: torch.Tensor) -> torch.Tensor:

@@ -125,7 +125,9 @@ class FlatIndex:
 
     def search_device_exact(self, q_ptr: int, nq: int, k: int, D_ptr: Optional[int], I_ptr: int,
                             S64_ptr: Optional[int] = None, id_offset: int = 0, stream: Optional[int] = None) -> None:
-        """``search_device`` with certificate failures re-searched (one host sync per call)."""
+        """``search_device`` with certificate failures re-searched.  bf16/f16: by a fallback round
+        queued on the device (no host sync); a query it cannot certify counts in
+        :meth:`unresolved_count`.  fp32: certificates read back, host-driven re-search."""
         check(self._L.vs_search_device_exact(self._h, q_ptr, int(nq), int(k), D_ptr or None, I_ptr, S64_ptr or None,
                                              int(id_offset), stream or None))
 
@@ -139,7 +141,12 @@ class FlatIndex:
         return [float(buf[i]) for i in range(n)], {1: "mfma", 2: "gemv", 3: "mfma_i8", 4: "gemv_i8"}.get(kind.value, "none")
 
     def uncertified_count(self) -> int:
+        """First-pass certificate failures so far (each one was re-searched)."""
         return int(check(self._L.vs_uncertified_count(self._h)))
+
+    def unresolved_count(self) -> int:
+        """Queries ``search_device_exact``'s device fallback could not certify either (must stay 0)."""
+        return int(check(self._L.vs_unresolved_count(self._h)))
 
     def host_staging_bytes(self) -> int:
         """Pinned host bytes held for ``search``'s query / result staging (bounded per context)."""

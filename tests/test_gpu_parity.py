@@ -232,16 +232,19 @@ def test_optimistic_seed_failure_falls_back_exactly(FlatIndex):
     assert ix.uncertified_count() > 0  # the optimistic pass was rejected (and then redone exactly)
 
 
-def test_device_exact_search_re_searches_uncertified_queries(FlatIndex):
-    # the adversarial corpus above through the device API used by the multi-GPU layer: the
-    # optimistic pass is rejected on the device and re-searched before the call returns
+@pytest.mark.parametrize("nq", [16, 300])
+def test_device_exact_search_re_searches_uncertified_queries(FlatIndex, nq):
+    # the adversarial corpus above through the device API used by the multi-GPU layers: the
+    # optimistic pass is rejected on the device and the failed queries are re-searched by the
+    # fallback round queued behind it (no host round trip).  nq = 300: two query blocks, only the
+    # first holds adversarial queries, so the second block's fallback kernels are gated off.
     import torch
     d, k = 64, 10
     cu = _num_cu()
     tiles = 32 * cu + 3
     N = tiles * 256
     x = O.synth_rows(O.SEED_CORPUS, 0, N, d, True, "f32")
-    q = O.synth_rows(O.SEED_QUERIES, 0, 16, d, True, "f32")
+    q = O.synth_rows(O.SEED_QUERIES, 0, nq, d, True, "f32")
     rng = np.random.default_rng(11)
     for j in range(cu):  # the sampled tile of workgroup j: the first of its range
         x[(tiles * j // cu) * 256 + 5] = q[j % 16] + 0.01 * rng.standard_normal(d).astype(np.float32)
@@ -249,15 +252,47 @@ def test_device_exact_search_re_searches_uncertified_queries(FlatIndex):
     ix.add(x)
     qb = O.round_dtype(q, "bf16")
     qd = torch.from_numpy(qb).cuda()
-    S = torch.empty((16, k), dtype=torch.float64, device="cuda")
-    I = torch.empty((16, k), dtype=torch.int64, device="cuda")
-    D = torch.empty((16, k), dtype=torch.float32, device="cuda")
-    ix.search_device_exact(qd.data_ptr(), 16, k, D.data_ptr(), I.data_ptr(), S.data_ptr(), 1000, 0)
+    S = torch.empty((nq, k), dtype=torch.float64, device="cuda")
+    I = torch.empty((nq, k), dtype=torch.int64, device="cuda")
+    D = torch.empty((nq, k), dtype=torch.float32, device="cuda")
+    ix.search_device_exact(qd.data_ptr(), nq, k, D.data_ptr(), I.data_ptr(), S.data_ptr(), 1000, 0)
     Se, Ie = O.knn_exact(ix.reconstruct_n(0, N), qb, k, "ip")
     np.testing.assert_array_equal(I.cpu().numpy(), Ie + 1000)
     np.testing.assert_array_equal(S.cpu().numpy(), Se)
     np.testing.assert_array_equal(D.cpu().numpy(), Se.astype(np.float32))
     assert ix.uncertified_count() > 0
+    assert ix.unresolved_count() == 0
+
+
+@pytest.mark.parametrize("nq", [1, 20])
+def test_ties_beyond_max_depth_are_reported(FlatIndex, nq):
+    # 5000 identical rows tie with the query's best score: no screen of KP_MAX = 4096 rows can
+    # certify that no unlisted copy wins.  vs_search raises VS_ERR_UNCERTIFIED; the device API (no
+    # host sync) counts the query in unresolved_count; the multi-device handle raises.
+    import torch
+    from photo_search_engine_amd._lib import VsError
+    from photo_search_engine_amd.index import MultiDeviceFlatIndex
+    d, k = 64, 10
+    x = O.synth_rows(O.SEED_CORPUS, 0, 25_000, d, True, "bf16")
+    v = x[123].copy()
+    x[np.random.default_rng(3).choice(25_000, 5000, replace=False)] = v
+    q = np.repeat(v[None], nq, axis=0)
+    ix = FlatIndex(d, "ip", "bf16")
+    ix.add(x)
+    with pytest.raises(VsError) as e:
+        ix.search(q, k)
+    assert e.value.code == -4
+    qd = torch.from_numpy(q).cuda()
+    I = torch.empty((nq, k), dtype=torch.int64, device="cuda")
+    ix.search_device_exact(qd.data_ptr(), nq, k, None, I.data_ptr(), None, 0, 0)
+    assert ix.unresolved_count() == nq
+    m = MultiDeviceFlatIndex(d, "ip", "bf16", devices=[0, 0])
+    m.add(x)
+    with pytest.raises(VsError) as e:
+        m.search(q, k)
+    assert e.value.code == -4
+    m.close()
+    ix.close()
 
 
 def test_device_exact_search_k_beyond_shard_rows(FlatIndex):
