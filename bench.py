@@ -42,7 +42,7 @@ SEED_CENTROIDS = 20260419
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 MFMA_BF16_PEAK_TF = 2500.0
 MFMA_I8_PEAK_TOPS = 5000.0  # MI355X_MICROARCH.md: I8 16x16x64 runs at 2x the BF16 rate per clock
-DEFAULT_SCREEN = {"cfg3": "int8", "cfg2": "int8"}  # flat workloads not listed: the native screen
+DEFAULT_SCREEN = {"cfg3": "int8", "cfg2": "int8", "cfg4": "int8"}  # (all flat workloads: inner product)
 METRICS = {
     "cfg3": "kNN queries/sec + recall@10 vs FAISS, N=10M d=1536 batch=256",
     "cfg2": "kNN queries/sec vs FAISS, N=1M d=1536 fp32 batch=1 top-10",
@@ -58,7 +58,7 @@ def parse():
     ap.add_argument("--workload", default="cfg3", choices=sorted(WORKLOADS) + sorted(IVF_WORKLOADS))
     ap.add_argument("--rows", type=int, default=0, help="override corpus rows (testing)")
     ap.add_argument("--screen", default=None, choices=["native", "int8"],
-                    help="flat workloads: the screen of the timed steps (default: int8 for cfg3, else native); "
+                    help="flat workloads: the screen of the timed steps (default: int8); "
                          "with int8 the native screen is timed too and reported beside it")
     ap.add_argument("--cpu-sample-rows", type=int, default=0,
                     help="rows of the corpus the CPU baseline scans (default: the whole corpus if host memory allows)")

@@ -8,8 +8,8 @@ through the C ABI and checked against the oracle at its own (N, d, dtype, batch,
   size) with the tie-tolerant rule below, plus a d=1536 case with >= 4 tiles per CU bit-exact
   against ``knn_exact``.
 * cfg4  d=768 fp16, batch 256, top-10, row-sharded: ``ShardedFlatIndex`` over 4 ranks (gloo, all on
-  the box's one GPU) at a reduced N of 4M rows; the merged answer checked like cfg3, and the first
-  16 queries bit-exact against ``knn_exact``.
+  the box's one GPU) at a reduced N of 4M rows; the merged answer checked like cfg3, the first
+  16 queries bit-exact against ``knn_exact``, and the int8 screen's answer identical.
 * cfg5  IVF-Flat nlist=4096 nprobe=32 d=1536 bf16, batch 256, top-10, at a reduced N of 500k rows
   of a Gaussian mixture with Zipf-sized clusters: bit-exact against ``oracle/ivf_oracle.py``.
 
@@ -152,9 +152,11 @@ def _cfg4_worker(rank, world, port, N, d, nq, k, outdir):
         synthesize_device(0, O.SEED_QUERIES, 0, nq, d, q.data_ptr(), True, "f16",
                           torch.cuda.current_stream().cuda_stream)
         D, I, S = sh.search(q, k)
+        sh.index.set_screen("int8")  # the bench's default screen for cfg4: the same exact answer
+        D8, I8, S8 = sh.search(q, k)
         torch.cuda.synchronize()
         np.savez(os.path.join(outdir, f"r{rank}.npz"), D=D.cpu().numpy(), I=I.cpu().numpy(), S=S.cpu().numpy(),
-                 n=sh.n_local)
+                 I8=I8.cpu().numpy(), S8=S8.cpu().numpy(), n=sh.n_local, unres=sh.unresolved_count())
         sh.close()
     finally:
         dist.destroy_process_group()
@@ -170,6 +172,10 @@ def test_cfg4_shape_sharded_four_ranks(tmp_path):
         np.testing.assert_array_equal(o["I"], outs[0]["I"])
         np.testing.assert_array_equal(o["S"], outs[0]["S"])
     D, I, S = outs[0]["D"], outs[0]["I"], outs[0]["S"]
+    for o in outs:  # int8 screen on every shard: identical merged answer, nothing unresolved
+        np.testing.assert_array_equal(o["I8"], I)
+        np.testing.assert_array_equal(o["S8"], S)
+        assert int(o["unres"]) == 0
     x = O.synth_rows(O.SEED_CORPUS, 0, N, d, True, "f16")
     q = O.synth_rows(O.SEED_QUERIES, 0, nq, d, True, "f16")
     np.testing.assert_array_equal(D, S.astype(np.float32))
