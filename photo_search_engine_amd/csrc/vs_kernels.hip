@@ -1689,29 +1689,35 @@ __device__ __forceinline__ bool better_exact(double sa, uint32_t ia, double sb, 
     return ia < ib;
 }
 
-// Exact canonical fp64 scores of stored rows, query staged in LDS as fp64 (QLDS) or read from
-// global fp32.  Lane l owns 8-element groups g = l, l+64, ... in ascending order and accumulates
-// them sequentially, then an xor-butterfly 32..1 -- the expression tree of the oracle's
-// orc_canon_scores (oracle/vs_oracle.c), so scores are bit-identical.
-// Two rows at once (row1 < 0: only row0): both rows' gathers are issued before either is
-// consumed, halving the serialized HBM latency per wave.  Same expression tree per row.
-template <int DT, int METRIC, bool QLDS>
-__device__ __forceinline__ void exact_score_q2(const uint8_t* __restrict__ corpus, int64_t row0, int64_t row1,
-                                               const double* __restrict__ qs, const float* __restrict__ qg, int d,
-                                               int dpad, int lane, double& s0, double& s1) {
+// Exact canonical fp64 scores of R stored rows at once (row[i] < 0: absent), query staged in LDS as
+// fp64 (QLDS) or read from global fp32.  Lane l owns 8-element groups g = l, l+64, ... in ascending
+// order and accumulates them sequentially, then an xor-butterfly 32..1 -- the expression tree of the
+// oracle's orc_canon_scores (oracle/vs_oracle.c), so scores are bit-identical.  All R rows' gathers
+// are issued before any is consumed (R rows of d x es bytes in flight per wave); a row's piece of a
+// chunk is one 128 B line.
+template <int DT>
+constexpr int refine_rows() { return DT == DT_F32 ? 2 : 4; }  // (fp32 rows: twice the registers)
+template <int DT, int METRIC, bool QLDS, int R>
+__device__ __forceinline__ void exact_score_rows(const uint8_t* __restrict__ corpus, const int64_t (&row)[R],
+                                                 const double* __restrict__ qs, const float* __restrict__ qg, int d,
+                                                 int dpad, int lane, double (&out)[R]) {
 #pragma clang fp contract(off)
     constexpr int ES = DT == DT_F32 ? 4 : 2;
     constexpr int NV = DT == DT_F32 ? 2 : 1;
     constexpr int RU = 3;
-    const bool two = row1 >= 0;
-    constexpr int CE = CHB / ES;  // elements per chunk: a row's piece is one 128 B line
-    const uint8_t* rb0 = corpus + (row0 / TR) * (int64_t)TR * dpad * ES + (row0 % TR) * CHB;
-    const int64_t r1 = two ? row1 : row0;
-    const uint8_t* rb1 = corpus + (r1 / TR) * (int64_t)TR * dpad * ES + (r1 % TR) * CHB;
+    constexpr int CE = CHB / ES;
+    const uint8_t* rb[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        const int64_t r = row[i] >= 0 ? row[i] : row[0];
+        rb[i] = corpus + (r / TR) * (int64_t)TR * dpad * ES + (r % TR) * CHB;
+    }
     const int ng = (d + 7) >> 3;
-    double acc0 = 0.0, acc1 = 0.0;
+    double acc[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) acc[i] = 0.0;
     for (int g0 = lane; g0 < ng; g0 += 64 * RU) {
-        uint4 raw0[RU][NV], raw1[RU][NV];
+        uint4 raw[RU][R][NV];
 #pragma unroll
         for (int u = 0; u < RU; ++u) {
             const int g = g0 + 64 * u;
@@ -1719,45 +1725,35 @@ __device__ __forceinline__ void exact_score_q2(const uint8_t* __restrict__ corpu
                 const int e0 = 8 * g;
                 const int64_t off = (int64_t)(e0 / CE) * TR * CHB + (e0 % CE) * ES;
 #pragma unroll
-                for (int v = 0; v < NV; ++v) {
-                    raw0[u][v] = *(const uint4*)(rb0 + off + 16 * v);
-                    if (two) raw1[u][v] = *(const uint4*)(rb1 + off + 16 * v);
-                }
+                for (int i = 0; i < R; ++i)
+                    if (i == 0 || row[i] >= 0)
+#pragma unroll
+                        for (int v = 0; v < NV; ++v) raw[u][i][v] = *(const uint4*)(rb[i] + off + 16 * v);
             }
         }
 #pragma unroll
         for (int u = 0; u < RU; ++u) {
             const int g = g0 + 64 * u;
             if (g < ng) {
-                float x0[8], x1[8];
 #pragma unroll
-                for (int v = 0; v < NV; ++v) {
-                    unpack16<DT>(raw0[u][v], x0 + 4 * v);
-                    if (two) unpack16<DT>(raw1[u][v], x1 + 4 * v);
-                }
+                for (int i = 0; i < R; ++i) {
+                    if (i > 0 && row[i] < 0) continue;
+                    float x[8];
 #pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    const int i = 8 * g + e;
-                    if (i < d) {
-                        const double qq = QLDS ? qs[e * ng + g] : (double)qg[i];
-                        const double xa = (double)x0[e];
-                        if constexpr (METRIC == METRIC_IP) {
-                            const double pa = xa * qq;
-                            acc0 = acc0 + pa;
-                        } else {
-                            const double da = xa - qq;
-                            const double pa = da * da;
-                            acc0 = acc0 + pa;
-                        }
-                        if (two) {
-                            const double xb = (double)x1[e];
+                    for (int v = 0; v < NV; ++v) unpack16<DT>(raw[u][i][v], x + 4 * v);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        const int ie = 8 * g + e;
+                        if (ie < d) {
+                            const double qq = QLDS ? qs[e * ng + g] : (double)qg[ie];
+                            const double xa = (double)x[e];
                             if constexpr (METRIC == METRIC_IP) {
-                                const double pb = xb * qq;
-                                acc1 = acc1 + pb;
+                                const double pa = xa * qq;
+                                acc[i] = acc[i] + pa;
                             } else {
-                                const double db = xb - qq;
-                                const double pb = db * db;
-                                acc1 = acc1 + pb;
+                                const double da = xa - qq;
+                                const double pa = da * da;
+                                acc[i] = acc[i] + pa;
                             }
                         }
                     }
@@ -1766,14 +1762,14 @@ __device__ __forceinline__ void exact_score_q2(const uint8_t* __restrict__ corpu
         }
     }
 #pragma unroll
-    for (int sft = 32; sft > 0; sft >>= 1) {
-        const double o0 = __shfl_xor(acc0, sft, 64);
-        const double o1 = __shfl_xor(acc1, sft, 64);
-        acc0 = acc0 + o0;
-        acc1 = acc1 + o1;
-    }
-    s0 = acc0;
-    s1 = acc1;
+    for (int sft = 32; sft > 0; sft >>= 1)
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            const double o = __shfl_xor(acc[i], sft, 64);
+            acc[i] = acc[i] + o;
+        }
+#pragma unroll
+    for (int i = 0; i < R; ++i) out[i] = acc[i];
 }
 
 constexpr int RF_THREADS = 1024;  // 16 waves per query: Kp / 16 candidates per wave
@@ -1865,19 +1861,20 @@ __device__ __forceinline__ void refine(const RefineArgs& a, int KP2) {
     }
     __syncthreads();
     const int nv = nv_s;
-    for (int j = wid; j < nv; j += 2 * NW) {
-        const int j2 = j + NW;
-        const uint32_t id0 = key_id(cq[j]);
-        const uint32_t id1 = j2 < nv ? key_id(cq[j2]) : 0u;
-        double s0, s1;
-        exact_score_q2<DT, METRIC, QLDS>(a.corpus, id0, j2 < nv ? (int64_t)id1 : -1, qs, qv, a.d, a.dpad, lane, s0, s1);
+    constexpr int RR = refine_rows<DT>();
+    for (int j = wid; j < nv; j += RR * NW) {
+        int64_t rr[RR];
+#pragma unroll
+        for (int i = 0; i < RR; ++i) rr[i] = j + i * NW < nv ? (int64_t)key_id(cq[j + i * NW]) : -1;
+        double s4[RR];
+        exact_score_rows<DT, METRIC, QLDS, RR>(a.corpus, rr, qs, qv, a.d, a.dpad, lane, s4);
         if (lane == 0) {  // keys carry storage slots; IVF maps them to user ids (sort + output)
-            sc[j] = s0;
-            ids[j] = a.idmap ? a.idmap[id0] : id0;
-            if (j2 < nv) {
-                sc[j2] = s1;
-                ids[j2] = a.idmap ? a.idmap[id1] : id1;
-            }
+#pragma unroll
+            for (int i = 0; i < RR; ++i)
+                if (rr[i] >= 0) {
+                    sc[j + i * NW] = s4[i];
+                    ids[j + i * NW] = a.idmap ? a.idmap[rr[i]] : (uint32_t)rr[i];
+                }
         }
     }
     const double worst = METRIC == METRIC_IP ? -INFINITY : INFINITY;
@@ -2013,14 +2010,17 @@ __device__ __forceinline__ void rfw_score(const RefineArgs& a, const uint32_t* i
                                           const double* qs, const float* qv) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     constexpr int NW = RF_THREADS / 64;
-    for (int j = lo + wid; j < hi; j += 2 * NW) {
-        const int j2 = j + NW;
-        double s0, s1;
-        exact_score_q2<DT, METRIC_IP, QLDS>(a.corpus, ids[j], j2 < hi ? (int64_t)ids[j2] : -1, qs, qv, a.d, a.dpad,
-                                            lane, s0, s1);
+    constexpr int RR = refine_rows<DT>();
+    for (int j = lo + wid; j < hi; j += RR * NW) {
+        int64_t rr[RR];
+#pragma unroll
+        for (int i = 0; i < RR; ++i) rr[i] = j + i * NW < hi ? (int64_t)ids[j + i * NW] : -1;
+        double s4[RR];
+        exact_score_rows<DT, METRIC_IP, QLDS, RR>(a.corpus, rr, qs, qv, a.d, a.dpad, lane, s4);
         if (lane == 0) {
-            sc[j] = s0;
-            if (j2 < hi) sc[j2] = s1;
+#pragma unroll
+            for (int i = 0; i < RR; ++i)
+                if (rr[i] >= 0) sc[j + i * NW] = s4[i];
         }
     }
 }
