@@ -267,10 +267,27 @@ int i8_gemv_depth(const vs_index* ix, int k) {
     const double g = std::exp(std::min(20.0, z * (double)ix->i8_bmax * std::sqrt((double)ix->d)));
     return (int)std::min<double>(KP_MAX, round_up((int64_t)std::ceil(2.0 * k * g + 64.0), 16));
 }
-// union of survivors the int8 seed aims at: ~kI8UnionPerK * k rows above the seeded threshold
-// (cfg3: k = 100 -> 6,400; the refine scores ~1.3k of them)
-constexpr double kI8UnionPerK = 64.0;
+// Union of survivors the int8 seed aims at (rows above the seeded threshold).  It must cover the
+// refine's window -- every key within the int8 error budget of T', measured at ~7.5-10 k rows for
+// unit-norm data -- or the certificate fails and the query is re-searched.  The seed is
+// the rank-r maximum over S sampled rows, r = U S / N, so the count above it is U (1 +- ~1/sqrt r):
+// take the smallest U whose 3-sigma low count still covers kI8Window * k rows, within
+// [kI8UnionMin, kI8UnionMaxPerK * k].  Large shards need more margin (few sampled maxima per union
+// row): cfg3's 10M rows -> ~41 k, the 8-GPU shard of 1.25M rows -> ~25 k (union sweep).
+constexpr double kI8Window = 15.0;
+constexpr double kI8UnionMaxPerK = 64.0;
 constexpr double kI8UnionMin = 1024.0;
+double i8_union_target(int k, double sampled, double n) {
+    const double need = kI8Window * k;
+    double u = std::max(need, kI8UnionMin);
+    const double umax = std::max(kI8UnionMaxPerK * k, kI8UnionMin);
+    while (u < umax) {
+        const double r = u * sampled / n;
+        if (r >= 9.0 && u * (1.0 - 3.0 / std::sqrt(r)) >= need) break;
+        u *= 1.1;
+    }
+    return std::min(u, umax);
+}
 
 // int8 pre-screen of one query block: pack int8 query codes -> seed pass -> int8 MFMA screen with
 // upper-bound keys -> adaptive exact refine (k_refine_wide).  q: device fp32 [nqb][d].
@@ -319,8 +336,9 @@ void search_block_i8(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float
         sa.seedmax = c->seedmax.as<float>();
         HIP_CHECK(launch_seed_mfma(DT_I8, sa, c->qtile.as<uint8_t>(), nqb, st));
         c->thr0.ensure(sizeof(u64) * MFMA_QB);
-        static const double per_k = getenv("VS_I8_UNION") ? atof(getenv("VS_I8_UNION")) : kI8UnionPerK;  // A/B knob
-        const double target = std::max(per_k * k, kI8UnionMin);
+        static const double per_k = getenv("VS_I8_UNION") ? atof(getenv("VS_I8_UNION")) : 0.0;  // A/B knob
+        const double target = per_k > 0.0 ? std::max(per_k * k, kI8UnionMin)
+                                           : i8_union_target(k, (double)sa.G * TR, (double)ix->ntotal);
         const double r = std::ceil(target * (double)sa.G * TR / (double)ix->ntotal);
         const int rank = (int)std::min<double>(std::max<double>(r, (double)kOptimisticMinRank), (double)M);
         HIP_CHECK(launch_seed_select(sa.seedmax, M, nqb, rank, c->thr0.as<u64>(), st));
