@@ -558,21 +558,44 @@ __global__ void __launch_bounds__(256) k_pack_qtile_i8(const float* __restrict__
         gcnt[r] = 0;
         drop[r] = 0ull;
     }
+    // The codes need not be the nearest (the error norm below is measured from the codes chosen), so
+    // v * (1 / t) replaces the division; d <= 2048 (the common case): the lane's values are loaded
+    // once, in one burst, and kept in registers for the second pass.
+    constexpr int PL = 32;
+    float vv[PL];
     float mx = 0.0f;
-    if (r < nqb)
+    const bool cached = dpad8 <= 64 * PL;
+    if (cached) {
+#pragma unroll
+        for (int j = 0; j < PL; ++j) {
+            const int i = lane + 64 * j;
+            vv[j] = (r < nqb && i < d) ? q[(int64_t)r * d + i] : 0.0f;
+            mx = fmaxf(mx, fabsf(vv[j]));
+        }
+    } else if (r < nqb) {
         for (int i = lane; i < d; i += 64) mx = fmaxf(mx, fabsf(q[(int64_t)r * d + i]));
+    }
 #pragma unroll
     for (int s = 32; s > 0; s >>= 1) mx = fmaxf(mx, __shfl_xor(mx, s, 64));
     const float t = mx / 127.0f;
+    const float inv = t > 0.0f ? 1.0f / t : 0.0f;
     double e2 = 0.0, n2 = 0.0, c2 = 0.0;
-    for (int i = lane; i < dpad8; i += 64) {
-        const float v = (r < nqb && i < d) ? q[(int64_t)r * d + i] : 0.0f;
-        const int c = t > 0.0f ? max(-127, min(127, (int)rintf(v / t))) : 0;
+    auto one = [&](int i, float v) {
+        const int c = max(-127, min(127, (int)rintf(v * inv)));
         qt[(int64_t)(i >> 6) * MFMA_QB * 64 + (int64_t)r * 64 + (i & 63)] = (uint8_t)(int8_t)c;
         const double e = (double)v - (double)t * (double)c;
         e2 += e * e;
         n2 += (double)v * v;
         c2 += (double)(c * c);
+    };
+    if (cached) {
+#pragma unroll
+        for (int j = 0; j < PL; ++j) {
+            const int i = lane + 64 * j;
+            if (i < dpad8) one(i, vv[j]);
+        }
+    } else {
+        for (int i = lane; i < dpad8; i += 64) one(i, (r < nqb && i < d) ? q[(int64_t)r * d + i] : 0.0f);
     }
     e2 = wave_sum_f64(e2);
     n2 = wave_sum_f64(n2);
