@@ -205,6 +205,29 @@ int vs_ivf_nlist(const vs_ivf* ivf);
 int vs_ivf_set_timing(vs_ivf* ivf, int enable);
 int vs_ivf_timing_fetch(vs_ivf* ivf, float* ms, double* bytes_scanned, int cap);
 
+/* ==== HNSW graph search ===================================================
+ * Replaces the search of faiss.IndexHNSWFlat, which the reference builds for
+ * index_type="hnsw" (utils/vector_store.py:73-78: IndexHNSWFlat(d, M, metric), hnsw.efSearch) and
+ * searches at utils/vector_store.py:191.  A vs_hnsw is a graph in faiss's HNSW layout (the arrays
+ * of an IHNf file: node levels, per-node offsets into the neighbour array, cumulative neighbour
+ * counts per level, entry point, max level) over the rows of a flat vs_index (graph node i = row
+ * i); the graph is copied to the index's device and validated (ids in range, neighbours present
+ * on their level, offsets matching the levels); a later duplicate in a neighbour list is dropped,
+ * which changes no search.  vs_hnsw_search runs faiss HNSW::search (greedy descent on the upper
+ * levels, then efSearch-bounded best-first search on level 0; oracle/hnsw_oracle.py) on the GPU,
+ * one workgroup per query, with the flat path's exact canonical scores as distances: D = scores
+ * (IP) / squared distances (L2) best first, I = row ids, -1 padded.  The index must hold exactly
+ * the graph's rows when searched (VS_ERR_ARG otherwise); max(ef_search, k) <= 2048. */
+typedef struct vs_hnsw vs_hnsw;
+
+int vs_hnsw_create(vs_index* index, int64_t n, const int32_t* levels, const uint64_t* offsets,
+                   const int32_t* neighbors, const int32_t* cum_nneighbor_per_level, int32_t n_cum,
+                   int32_t entry_point, int32_t max_level, vs_hnsw** out);
+void vs_hnsw_destroy(vs_hnsw* graph);
+int vs_hnsw_search(vs_hnsw* graph, const float* q, int64_t nq, int32_t k, int32_t ef_search, float* D,
+                   int64_t* I);
+int64_t vs_hnsw_ntotal(const vs_hnsw* graph);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,327 @@
+"""TEST INFRASTRUCTURE ONLY -- CPU oracle for HNSW graph search.
+
+Only ``tests/`` may import this module, and only as the checker.  The product
+(``photo_search_engine_amd``) never does.
+
+The reference builds ``faiss.IndexHNSWFlat(d, M, metric)`` for ``index_type="hnsw"`` and sets
+``hnsw.efConstruction`` / ``hnsw.efSearch`` (/root/reference/utils/vector_store.py:73-78), then
+calls ``index.search`` (``:191``).  faiss is third-party (``faiss-cpu>=1.7.0``,
+/root/reference/requirements.txt:5), neither vendored nor installed, so its published search
+algorithm is restated here (faiss/impl/HNSW.cpp ``HNSW::search``, ``greedy_update_nearest``,
+``search_from_candidates``, ``MinimaxHeap``; faiss/utils/Heap.h ``heap_push`` / ``heap_pop`` /
+``heap_replace_top`` with the ``CMax::cmp2`` id tie-break; faiss/IndexHNSW.cpp: inner-product
+distances are negated so that smaller is better, and negated back on output):
+
+1. ``nearest = entry_point``; on every level ``max_level .. 1`` the greedy descent moves to the
+   first strictly closer neighbour until none is (no visited table);
+2. level 0: a ``MinimaxHeap`` of capacity ``ef = max(efSearch, k)`` seeded with ``nearest``;
+   repeatedly pop its closest valid entry ``v0`` (distance ``d0``), stop when at least
+   ``efSearch`` heap entries -- popped ones included -- are closer than ``d0``, else every
+   unvisited neighbour of ``v0`` (list order, up to the first -1) is marked visited, scored,
+   offered to the result max-heap (size k, admission ``d < D[0]``) and pushed on the candidates
+   (when full: rejected if ``d >= max``, else the max is evicted);
+3. results sorted best first (``heap_reorder``: ascending distance, ties by id), padded with
+   id -1 and the worst distance.
+
+Distances here are the flat path's canonical fp64 scores (``oracle.canon_scores``: IP -> -score,
+L2 -> squared distance), not faiss's fp32 SIMD sums -- the same exactness contract as the flat
+search.  ``search_faiss`` restates the array heaps literally; ``search`` states the same procedure
+with the heaps as ordered multisets under the total order (distance, id), which is what the HIP
+kernel implements.  The two take identical decisions whenever no two distinct rows are at exactly
+equal distance from a query (faiss's choice among exact ties depends on its heap array layout);
+tests/test_hnsw_oracle.py checks that they agree.  Parity with faiss itself is unpinned (faiss is
+absent); the reference's own HNSW file (tests/golden/ref_photo_search.index, 77 rows, M=48) is
+searched by both.
+"""
+from __future__ import annotations
+
+import bisect
+import math
+from typing import Tuple
+
+import numpy as np
+
+from . import oracle as O
+
+
+# ---------------------------------------------------------------------------------------------
+# graph layout helpers (faiss HNSW: neighbors of node i on level l are
+# neighbors[offsets[i] + cum[l] : offsets[i] + cum[l + 1]], -1 padded)
+# ---------------------------------------------------------------------------------------------
+def neighbor_list(graph: dict, node: int, level: int):
+    off = int(graph["offsets"][node])
+    cum = graph["cum_nneighbor_per_level"]
+    out = []
+    for j in range(off + int(cum[level]), off + int(cum[level + 1])):
+        v = int(graph["neighbors"][j])
+        if v < 0:
+            break
+        out.append(v)
+    return out
+
+
+def _distances(x_stored, q, metric) -> np.ndarray:
+    """faiss HNSW distance of every (query, row): IP -> -canonical score, L2 -> canonical."""
+    S = O.canon_scores(x_stored, q, metric)
+    return -S if O._metric(metric) == O.METRIC_IP else S
+
+
+def _output(res, k: int, metric):
+    """Sorted (distance, id) pairs -> faiss layout (D fp64 score, I) padded with -1 / worst."""
+    ip = O._metric(metric) == O.METRIC_IP
+    S = np.full(k, -np.inf if ip else np.inf, dtype=np.float64)
+    I = np.full(k, -1, dtype=np.int64)
+    for j, (dv, v) in enumerate(res[:k]):
+        S[j] = -dv if ip else dv
+        I[j] = v
+    return S, I
+
+
+def _greedy_upper(graph, dist_row, nearest: int):
+    d_nearest = dist_row[nearest]
+    for level in range(int(graph["max_level"]), 0, -1):
+        while True:
+            prev = nearest
+            for v in neighbor_list(graph, nearest, level):
+                dv = dist_row[v]
+                if dv < d_nearest:
+                    nearest, d_nearest = v, dv
+            if nearest == prev:
+                break
+    return nearest, d_nearest
+
+
+# ---------------------------------------------------------------------------------------------
+# literal restatement: faiss array heaps
+# ---------------------------------------------------------------------------------------------
+def _cmp2(a, b, ia, ib) -> bool:  # CMax<T, TI>::cmp2
+    return a > b or (a == b and ia > ib)
+
+
+def _heap_push(k, val, ids, v, i):  # k = size after the push (faiss passes ++k); 1-based inside
+    j = k
+    while j > 1:
+        f = j >> 1
+        if not _cmp2(v, val[f - 1], i, ids[f - 1]):
+            break
+        val[j - 1], ids[j - 1] = val[f - 1], ids[f - 1]
+        j = f
+    val[j - 1], ids[j - 1] = v, i
+
+
+def _sift_down(k, val, ids, v, i):
+    j = 1
+    while True:
+        j1 = j << 1
+        j2 = j1 + 1
+        if j1 > k:
+            break
+        if j2 == k + 1 or _cmp2(val[j1 - 1], val[j2 - 1], ids[j1 - 1], ids[j2 - 1]):
+            if _cmp2(v, val[j1 - 1], i, ids[j1 - 1]):
+                break
+            val[j - 1], ids[j - 1] = val[j1 - 1], ids[j1 - 1]
+            j = j1
+        else:
+            if _cmp2(v, val[j2 - 1], i, ids[j2 - 1]):
+                break
+            val[j - 1], ids[j - 1] = val[j2 - 1], ids[j2 - 1]
+            j = j2
+    return j
+
+
+def _heap_pop(k, val, ids):  # k = size before the pop
+    v, i = val[k - 1], ids[k - 1]
+    j = _sift_down(k, val, ids, v, i)
+    val[j - 1], ids[j - 1] = val[k - 1], ids[k - 1]
+
+
+def _heap_replace_top(k, val, ids, v, i):
+    j = _sift_down(k, val, ids, v, i)
+    val[j - 1], ids[j - 1] = v, i
+
+
+class _MinimaxHeap:
+    def __init__(self, n: int):
+        self.n, self.k, self.nvalid = n, 0, 0
+        self.ids = [-1] * n
+        self.dis = [math.inf] * n
+
+    def push(self, i, v):
+        if self.k == self.n:
+            if v >= self.dis[0]:
+                return
+            if self.ids[0] != -1:
+                self.nvalid -= 1
+            _heap_pop(self.k, self.dis, self.ids)
+            self.k -= 1
+        self.k += 1
+        _heap_push(self.k, self.dis, self.ids, v, i)
+        self.nvalid += 1
+
+    def pop_min(self):
+        i = self.k - 1
+        while i >= 0 and self.ids[i] == -1:
+            i -= 1
+        if i < 0:
+            return -1, math.inf
+        imin, vmin = i, self.dis[i]
+        i -= 1
+        while i >= 0:
+            if self.ids[i] != -1 and self.dis[i] < vmin:
+                vmin, imin = self.dis[i], i
+            i -= 1
+        ret = self.ids[imin]
+        self.ids[imin] = -1
+        self.nvalid -= 1
+        return ret, vmin
+
+    def count_below(self, t) -> int:
+        return sum(1 for i in range(self.k) if self.dis[i] < t)
+
+
+def _search_one_faiss(graph, dist_row, k: int, ef_search: int):
+    n = len(dist_row)
+    if int(graph["entry_point"]) < 0 or n == 0:
+        return []
+    nearest, d_nearest = _greedy_upper(graph, dist_row, int(graph["entry_point"]))
+    cand = _MinimaxHeap(max(ef_search, k))
+    cand.push(nearest, d_nearest)
+    D = [math.inf] * k
+    I = [-1] * k
+    nres = 0
+    visited = np.zeros(n, dtype=bool)
+    for i in range(cand.k):  # search_from_candidates: the seeds enter the results
+        v1, dv = cand.ids[i], cand.dis[i]
+        if nres < k:
+            nres += 1
+            _heap_push(nres, D, I, dv, v1)
+        elif dv < D[0]:
+            _heap_replace_top(nres, D, I, dv, v1)
+        visited[v1] = True
+    while cand.nvalid > 0:
+        v0, d0 = cand.pop_min()
+        if cand.count_below(d0) >= ef_search:
+            break
+        for v1 in neighbor_list(graph, v0, 0):
+            if visited[v1]:
+                continue
+            visited[v1] = True
+            dv = dist_row[v1]
+            if nres < k:
+                nres += 1
+                _heap_push(nres, D, I, dv, v1)
+            elif dv < D[0]:
+                _heap_replace_top(nres, D, I, dv, v1)
+            cand.push(v1, dv)
+    # heap_reorder: pops in cmp2 order -> ascending (distance, id)
+    return sorted((D[j], I[j]) for j in range(nres))
+
+
+def search_faiss(x_stored, graph: dict, q, k: int, ef_search: int, metric="ip") -> Tuple[np.ndarray, np.ndarray]:
+    """faiss ``IndexHNSWFlat.search`` restated with its array heaps: (S fp64 nq x k, I nq x k)."""
+    q = np.atleast_2d(np.asarray(q, dtype=np.float32))
+    Dm = _distances(x_stored, q, metric)
+    S = np.empty((q.shape[0], k), dtype=np.float64)
+    I = np.empty((q.shape[0], k), dtype=np.int64)
+    for r in range(q.shape[0]):
+        S[r], I[r] = _output(_search_one_faiss(graph, Dm[r], k, ef_search), k, metric)
+    return S, I
+
+
+# ---------------------------------------------------------------------------------------------
+# ordered-multiset statement (the HIP kernel's): heaps as sorted lists under (distance, id)
+# ---------------------------------------------------------------------------------------------
+def _search_one(graph, dist_row, k: int, ef_search: int):
+    n = len(dist_row)
+    if int(graph["entry_point"]) < 0 or n == 0:
+        return []
+    nearest, d_nearest = _greedy_upper(graph, dist_row, int(graph["entry_point"]))
+    ef = max(ef_search, k)
+    cand = [(d_nearest, nearest, True)]  # sorted by (distance, id); popped entries stay (valid False)
+    res = [(d_nearest, nearest)]
+    visited = np.zeros(n, dtype=bool)
+    visited[nearest] = True
+    while any(c[2] for c in cand):
+        j = next(i for i, c in enumerate(cand) if c[2])
+        d0, v0, _ = cand[j]
+        cand[j] = (d0, v0, False)
+        if bisect.bisect_left([c[0] for c in cand], d0) >= ef_search:
+            break
+        for v1 in neighbor_list(graph, v0, 0):
+            if visited[v1]:
+                continue
+            visited[v1] = True
+            e = (dist_row[v1], v1)
+            bisect.insort(res, e)
+            del res[k:]
+            bisect.insort(cand, (e[0], e[1], True))
+            del cand[ef:]
+    return res
+
+
+def search(x_stored, graph: dict, q, k: int, ef_search: int, metric="ip") -> Tuple[np.ndarray, np.ndarray]:
+    """HNSW search with ordered-multiset heaps (the HIP kernel's statement): (S fp64, I)."""
+    q = np.atleast_2d(np.asarray(q, dtype=np.float32))
+    Dm = _distances(x_stored, q, metric)
+    S = np.empty((q.shape[0], k), dtype=np.float64)
+    I = np.empty((q.shape[0], k), dtype=np.int64)
+    for r in range(q.shape[0]):
+        S[r], I[r] = _output(_search_one(graph, Dm[r], k, ef_search), k, metric)
+    return S, I
+
+
+# ---------------------------------------------------------------------------------------------
+# test graphs
+# ---------------------------------------------------------------------------------------------
+def _default_probas(M: int):
+    """faiss ``HNSW::set_default_probas(M, 1 / log(M))``: level probabilities and cumulative
+    neighbour counts (2M on level 0, M above)."""
+    lm = 1.0 / math.log(M)
+    probas, cum, level = [], [0], 0
+    while True:
+        p = math.exp(-level / lm) * (1.0 - math.exp(-1.0 / lm))
+        if p < 1e-9:
+            break
+        probas.append(p)
+        cum.append(cum[-1] + (2 * M if level == 0 else M))
+        level += 1
+    return np.array(probas, dtype="<f8"), np.array(cum, dtype="<i4")
+
+
+def layered_knn_graph(x_stored, M: int, metric="ip", seed: int = 1, level_mult=None) -> dict:
+    """A multi-level graph in faiss's HNSW layout for exercising the search (test-only): node
+    levels drawn as faiss does (``-log(U) * 1/ln(M)``, seeded numpy RNG -- not faiss's generator),
+    and on every level each node's neighbours are its exact nearest nodes of that level (2M on
+    level 0, M above), best first, -1 padded."""
+    x = np.asarray(x_stored, dtype=np.float32)
+    n = x.shape[0]
+    probas, cum = _default_probas(M)
+    rng = np.random.default_rng(seed)
+    lm = (1.0 / math.log(M)) if level_mult is None else level_mult
+    lev = np.minimum((-np.log(rng.random(n)) * lm).astype(np.int64), len(cum) - 2)
+    levels = lev + 1
+    offsets = np.zeros(n + 1, dtype=np.uint64)
+    offsets[1:] = np.cumsum(cum[levels].astype(np.uint64))
+    nb = np.full(int(offsets[-1]), -1, dtype=np.int32)
+    S = O.canon_scores(x, x, metric)
+    ip = O._metric(metric) == O.METRIC_IP
+    for level in range(int(lev.max()) + 1):
+        members = np.nonzero(lev >= level)[0]
+        width = int(cum[level + 1] - cum[level])
+        for i in members:
+            others = members[members != i]
+            s = S[i, others]
+            order = np.lexsort((others, -s if ip else s))[:width]
+            base = int(offsets[i]) + int(cum[level])
+            nb[base:base + len(order)] = others[order]
+    top = int(lev.max())
+    entry = int(np.nonzero(lev == top)[0][0])
+    return {"assign_probas": probas, "cum_nneighbor_per_level": cum, "levels": levels.astype(np.int32),
+            "offsets": offsets, "neighbors": nb, "entry_point": entry, "max_level": top,
+            "efConstruction": 40, "efSearch": 16, "upper_beam": 1}
+
+
+def has_exact_ties(x_stored, q, metric="ip") -> bool:
+    """True if some query is at exactly equal distance from two distinct rows."""
+    Dm = _distances(x_stored, np.atleast_2d(np.asarray(q, dtype=np.float32)), metric)
+    return any(len(np.unique(r)) != len(r) for r in Dm)

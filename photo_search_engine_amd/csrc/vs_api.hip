@@ -112,6 +112,11 @@ struct vs_index {
     int last_kernel_kind = 0;  // 1 = mfma, 2 = gemv, 3 = int8 mfma
 };
 
+vs::FlatView vs::flat_view(vs_index* ix) {
+    return {ix->data, ix->d, ix->dpad, ix->dtype, ix->metric, ix->device, ix->ntotal};
+}
+std::shared_mutex& vs::flat_lock(vs_index* ix) { return ix->rw; }
+
 namespace {
 
 Ctx* acquire_ctx(vs_index* ix) {

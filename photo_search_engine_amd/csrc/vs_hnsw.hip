@@ -1,0 +1,194 @@
+// vs_hnsw.hip -- HNSW graph search of libvs (include/vs.h "HNSW graph search").
+//
+// The reference's index_type="hnsw" is faiss.IndexHNSWFlat (/root/reference/utils/vector_store.py
+// :73-78), searched at :191.  A vs_hnsw holds a graph in faiss's HNSW layout over the rows of a
+// flat vs_index on that index's device; vs_hnsw_search runs k_hnsw_search (vs_kernels.hip: faiss
+// HNSW::search with the flat path's exact canonical distances, one workgroup per query) in chunks
+// of queries, each with its own zeroed visited bitmap.  Results equal oracle/hnsw_oracle.py.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <shared_mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/vs.h"
+#include "vs_internal.h"
+
+using namespace vs;
+
+struct vs_hnsw {
+    vs_index* ix = nullptr;  // not owned
+    int device = 0;
+    int64_t n = 0;
+    int entry = -1, max_level = -1, nbmax = 1;
+    DevBuf offsets, neighbors, cum, vis, qdev, outD, outI;
+    hipStream_t st = nullptr;
+    std::mutex mtx;  // searches on one handle are serialised (shared workspaces)
+};
+
+namespace {
+
+constexpr size_t kVisitedBytes = 256u << 20;  // visited bitmaps of one query chunk
+
+void fail(const std::string& m) { throw VsError(VS_ERR_ARG, "hnsw graph: " + m); }
+
+// validate a faiss-layout graph and return its neighbour array with every list cut at its first
+// -1 and later duplicates dropped (-1 padded): both leave every faiss search unchanged
+std::vector<int32_t> checked_neighbors(int64_t n, const int32_t* levels, const uint64_t* offsets,
+                                       const int32_t* neighbors, const int32_t* cum, int n_cum, int entry,
+                                       int max_level, int* nbmax) {
+    if (n_cum < 2 || cum[0] != 0) fail("cum_nneighbor_per_level must start at 0 and cover a level");
+    const int nlev = n_cum - 1;
+    *nbmax = 1;
+    for (int l = 0; l < nlev; ++l) {
+        if (cum[l + 1] < cum[l]) fail("cum_nneighbor_per_level must not decrease");
+        *nbmax = std::max(*nbmax, cum[l + 1] - cum[l]);
+    }
+    if (*nbmax > HN_NB_MAX) fail("a level holds more than " + std::to_string(HN_NB_MAX) + " neighbours");
+    if (n == 0) {
+        if (entry != -1) fail("an empty graph has entry point -1");
+        return {};
+    }
+    if (entry < 0 || entry >= n) fail("entry point out of range");
+    if (offsets[0] != 0) fail("offsets[0] must be 0");
+    for (int64_t i = 0; i < n; ++i) {
+        if (levels[i] < 1 || levels[i] > nlev) fail("node level out of range");
+        if (offsets[i + 1] < offsets[i] || offsets[i + 1] - offsets[i] != (uint64_t)cum[levels[i]])
+            fail("offsets do not match the node levels");
+    }
+    if (max_level != levels[entry] - 1) fail("max_level must be the entry point's top level");
+    std::vector<int32_t> out(offsets[n], -1);
+    std::vector<int64_t> seen(n, -1);  // last (node, level) stamp that listed each id
+    for (int64_t i = 0; i < n; ++i)
+        for (int l = 0; l < levels[i]; ++l) {
+            const uint64_t b = offsets[i] + cum[l], e = offsets[i] + cum[l + 1];
+            const int64_t stamp = i * nlev + l;
+            uint64_t w = b;
+            for (uint64_t j = b; j < e; ++j) {
+                const int32_t v = neighbors[j];
+                if (v < 0) break;
+                if (v >= n) fail("neighbour id out of range");
+                if (levels[v] <= l) fail("a neighbour is listed on a level above its own");
+                if (seen[v] == stamp) continue;
+                seen[v] = stamp;
+                out[w++] = v;
+            }
+        }
+    return out;
+}
+
+}  // namespace
+
+extern "C" {
+
+int vs_hnsw_create(vs_index* index, int64_t n, const int32_t* levels, const uint64_t* offsets,
+                   const int32_t* neighbors, const int32_t* cum, int32_t n_cum, int32_t entry_point,
+                   int32_t max_level, vs_hnsw** out) {
+    return guarded([&] {
+        if (!index || !out || n < 0 || !cum || (n > 0 && (!levels || !offsets || !neighbors)))
+            throw VsError(VS_ERR_ARG, "vs_hnsw_create: bad arguments");
+        *out = nullptr;
+        const FlatView fv = flat_view(index);
+        int nbmax = 1;
+        const std::vector<int32_t> nb =
+            checked_neighbors(n, levels, offsets, neighbors, cum, n_cum, entry_point, max_level, &nbmax);
+        DeviceGuard g(fv.device);
+        vs_hnsw* h = new vs_hnsw();
+        try {
+            h->ix = index;
+            h->device = fv.device;
+            h->n = n;
+            h->entry = n ? entry_point : -1;
+            h->max_level = n ? max_level : -1;
+            h->nbmax = nbmax;
+            HIP_CHECK(hipStreamCreateWithFlags(&h->st, hipStreamNonBlocking));
+            if (n > 0) {
+                h->offsets.ensure((size_t)(n + 1) * 8);
+                h->neighbors.ensure(std::max<size_t>(nb.size(), 1) * 4);
+                HIP_CHECK(hipMemcpyAsync(h->offsets.p, offsets, (size_t)(n + 1) * 8, hipMemcpyHostToDevice, h->st));
+                if (!nb.empty())
+                    HIP_CHECK(hipMemcpyAsync(h->neighbors.p, nb.data(), nb.size() * 4, hipMemcpyHostToDevice, h->st));
+            }
+            h->cum.ensure((size_t)n_cum * 4);
+            HIP_CHECK(hipMemcpyAsync(h->cum.p, cum, (size_t)n_cum * 4, hipMemcpyHostToDevice, h->st));
+            HIP_CHECK(hipStreamSynchronize(h->st));
+        } catch (...) {
+            vs_hnsw_destroy(h);
+            throw;
+        }
+        *out = h;
+    });
+}
+
+void vs_hnsw_destroy(vs_hnsw* h) {
+    if (!h) return;
+    {
+        DeviceGuard g(h->device);
+        if (h->st) (void)hipStreamSynchronize(h->st);
+        for (DevBuf* b : {&h->offsets, &h->neighbors, &h->cum, &h->vis, &h->qdev, &h->outD, &h->outI}) b->release();
+        if (h->st) (void)hipStreamDestroy(h->st);
+    }
+    delete h;
+}
+
+int64_t vs_hnsw_ntotal(const vs_hnsw* h) { return h ? h->n : -1; }
+
+int vs_hnsw_search(vs_hnsw* h, const float* q, int64_t nq, int32_t k, int32_t ef_search, float* D, int64_t* I) {
+    return guarded([&] {
+        if (!h || nq < 0 || k < 1 || ef_search < 1 || (nq > 0 && (!q || !D || !I)))
+            throw VsError(VS_ERR_ARG, "vs_hnsw_search: bad arguments");
+        const int ef = std::max(ef_search, k);
+        if (ef > HN_EF_MAX) throw VsError(VS_ERR_ARG, "vs_hnsw_search: max(ef_search, k) > 2048");
+        if (nq == 0) return;
+        std::lock_guard<std::mutex> lk(h->mtx);
+        std::shared_lock<std::shared_mutex> rl(flat_lock(h->ix));
+        const FlatView fv = flat_view(h->ix);
+        if (fv.ntotal != h->n)
+            throw VsError(VS_ERR_ARG, "vs_hnsw_search: the graph covers " + std::to_string(h->n) +
+                                          " rows, the index holds " + std::to_string(fv.ntotal));
+        if (hnsw_lds_bytes(fv.d, k, ef, h->nbmax) > 160 * 1024 - 512)
+            throw VsError(VS_ERR_ARG, "vs_hnsw_search: k / ef_search too large for one workgroup's LDS");
+        DeviceGuard g(h->device);
+        const int64_t words = std::max<int64_t>(1, (h->n + 31) / 32);
+        const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>({nq, 4096, (int64_t)(kVisitedBytes / (words * 4))}));
+        h->vis.ensure((size_t)(chunk * words * 4));
+        h->qdev.ensure((size_t)(chunk * fv.d * 4));
+        h->outD.ensure((size_t)(chunk * k * 4));
+        h->outI.ensure((size_t)(chunk * k * 8));
+        HnswArgs a{};
+        a.corpus = fv.data;
+        a.d = fv.d;
+        a.dpad = fv.dpad;
+        a.dt = fv.dtype;
+        a.metric = fv.metric;
+        a.n = h->n;
+        a.offsets = h->offsets.as<uint64_t>();
+        a.neighbors = h->neighbors.as<int>();
+        a.cum = h->cum.as<int>();
+        a.entry = h->entry;
+        a.max_level = h->max_level;
+        a.nbmax = h->nbmax;
+        a.k = k;
+        a.ef_search = ef_search;
+        a.ef = ef;
+        a.vis = h->vis.as<uint32_t>();
+        a.vis_words = words;
+        a.q = h->qdev.as<float>();
+        a.D = h->outD.as<float>();
+        a.I = h->outI.as<int64_t>();
+        for (int64_t q0 = 0; q0 < nq; q0 += chunk) {
+            const int64_t m = std::min(chunk, nq - q0);
+            HIP_CHECK(hipMemcpyAsync(h->qdev.p, q + q0 * fv.d, (size_t)(m * fv.d * 4), hipMemcpyHostToDevice, h->st));
+            HIP_CHECK(hipMemsetAsync(h->vis.p, 0, (size_t)(m * words * 4), h->st));
+            HIP_CHECK(launch_hnsw_search(a, (int)m, h->st));
+            HIP_CHECK(hipMemcpyAsync(D + q0 * k, h->outD.p, (size_t)(m * k * 4), hipMemcpyDeviceToHost, h->st));
+            HIP_CHECK(hipMemcpyAsync(I + q0 * k, h->outI.p, (size_t)(m * k * 8), hipMemcpyDeviceToHost, h->st));
+            HIP_CHECK(hipStreamSynchronize(h->st));
+        }
+    });
+}
+
+}  // extern "C"

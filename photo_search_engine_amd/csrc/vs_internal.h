@@ -300,9 +300,20 @@ hipError_t launch_pack_rows_map(int dt, const float* src, int64_t n, int d, int 
 }  // namespace vs
 
 #include <functional>
+#include <shared_mutex>
 
 struct vs_index;
 namespace vs {
+// the stored rows of a flat index as the kernels see them; read it (and launch on it) while holding
+// flat_lock(ix) shared, the lock adds and resets take exclusively
+struct FlatView {
+    const uint8_t* data;
+    int d, dpad, dtype, metric, device;
+    int64_t ntotal;
+};
+FlatView flat_view(vs_index* ix);
+std::shared_mutex& flat_lock(vs_index* ix);
+
 // Host <-> HBM row streaming through two pinned host chunks (bulk add, persistence).
 // add_rows_host appends n rows: fill(r0, m, dst) writes rows r0..r0+m-1 (fp32, row-major) into a
 // pinned chunk while the copy engine and the pack kernel work on the previous one.  Takes the
@@ -328,5 +339,32 @@ hipError_t launch_seed_select(const float* seedmax, int M, int nq, int rank, u64
 
 hipError_t launch_merge_shards(int metric, const double* S_in, const int64_t* I_in, int G, int64_t nq, int k,
                                double* S_out, int64_t* I_out, float* D_out, hipStream_t st);
+
+// ---- HNSW graph search (vs_hnsw.hip) ---------------------------------------------
+// faiss HNSW::search over a graph in faiss's layout (neighbors of node i on level l:
+// neighbors[offsets[i] + cum[l] .. offsets[i] + cum[l + 1]), -1 padded), rows of a flat index,
+// canonical fp64 distances.  One workgroup per query; the candidate and result heaps are sorted
+// LDS arrays under (distance, id).
+constexpr int HN_THREADS = 256;
+constexpr int HN_EF_MAX = 2048;  // largest max(efSearch, k)
+constexpr int HN_NB_MAX = 1024;  // largest neighbour list of one level
+struct HnswArgs {
+    const uint8_t* corpus;       // flat index rows (tiled layout)
+    int d, dpad, dt, metric;
+    int64_t n;                   // rows (= graph nodes)
+    const uint64_t* offsets;     // [n + 1]
+    const int* neighbors;        // [offsets[n]]
+    const int* cum;              // [max_level + 2] cumulative neighbour counts per level
+    int entry, max_level;
+    int nbmax;                   // widest level's neighbour count
+    const float* q;              // [nq][d] fp32
+    int k, ef_search, ef;        // ef = max(ef_search, k)
+    uint32_t* vis;               // [nq][vis_words] visited bitmaps, zeroed before the launch
+    int64_t vis_words;
+    float* D;                    // [nq][k] scores (IP) / squared distances (L2), best first
+    int64_t* I;                  // [nq][k] row ids, -1 padded
+};
+size_t hnsw_lds_bytes(int d, int k, int ef, int nbmax);  // dynamic LDS of one search workgroup
+hipError_t launch_hnsw_search(const HnswArgs& a, int nq, hipStream_t st);
 
 }  // namespace vs

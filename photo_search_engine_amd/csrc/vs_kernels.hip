@@ -2720,4 +2720,354 @@ hipError_t launch_merge_shards(int metric, const double* S_in, const int64_t* I_
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------------------------------------------
+// K7: HNSW graph search (host side vs_hnsw.hip) -- faiss HNSW::search restated
+// (oracle/hnsw_oracle.py): greedy descent on the upper levels, then level 0 with a candidate set of
+// capacity ef (popped entries stay and count in the stop test) and a result set of k.  One
+// 256-thread workgroup per query.  Distances are exact_score_rows' canonical fp64 scores (IP:
+// -score).  Both sets are sorted LDS arrays under (distance, id) and take a whole neighbour list
+// per step: the new rows are scored by all four waves, rank-sorted, and merged (an element's new
+// position = its index in its own list + its rank in the other, one binary search) -- the same
+// decisions as faiss's array heaps whenever no two rows tie in distance.
+// ------------------------------------------------------------------------------------------------
+struct HnLds {
+    double* qs;
+    double* cd[2];
+    int* ci[2];
+    int* cv[2];
+    double* rd[2];
+    int* ri[2];
+    double* bd;  // new rows: distances, ids (list order) ...
+    int* bi;
+    double* sd;  // ... rank-sorted
+    int* si;
+    int* bl;     // the raw neighbour list
+};
+__host__ __device__ inline size_t hn_layout(int d, int k, int ef, int nbmax, bool qlds, uint8_t* base, HnLds* L) {
+    size_t off = 0;
+    uint8_t* p[16];
+    const size_t sz[16] = {qlds ? (size_t)((d + 7) >> 3) * 64 : 0,
+                           (size_t)ef * 8, (size_t)ef * 8, (size_t)ef * 4, (size_t)ef * 4, (size_t)ef * 4, (size_t)ef * 4,
+                           (size_t)k * 8, (size_t)k * 8, (size_t)k * 4, (size_t)k * 4,
+                           (size_t)nbmax * 8, (size_t)nbmax * 4, (size_t)nbmax * 8, (size_t)nbmax * 4,
+                           (size_t)nbmax * 4};
+    for (int i = 0; i < 16; ++i) {
+        p[i] = base + off;
+        off += (sz[i] + 15) & ~(size_t)15;
+    }
+    if (L) {
+        L->qs = (double*)p[0];
+        L->cd[0] = (double*)p[1];
+        L->cd[1] = (double*)p[2];
+        L->ci[0] = (int*)p[3];
+        L->ci[1] = (int*)p[4];
+        L->cv[0] = (int*)p[5];
+        L->cv[1] = (int*)p[6];
+        L->rd[0] = (double*)p[7];
+        L->rd[1] = (double*)p[8];
+        L->ri[0] = (int*)p[9];
+        L->ri[1] = (int*)p[10];
+        L->bd = (double*)p[11];
+        L->bi = (int*)p[12];
+        L->sd = (double*)p[13];
+        L->si = (int*)p[14];
+        L->bl = (int*)p[15];
+    }
+    return off;
+}
+constexpr size_t HN_LDS_CAP = 160 * 1024 - 512;  // dynamic LDS left beside the kernel's static words
+size_t hnsw_lds_bytes(int d, int k, int ef, int nbmax) {
+    const size_t with_q = hn_layout(d, k, ef, nbmax, true, nullptr, nullptr);
+    return with_q <= HN_LDS_CAP ? with_q : hn_layout(d, k, ef, nbmax, false, nullptr, nullptr);
+}
+
+__device__ __forceinline__ bool hn_less(double da, int ia, double db, int ib) {
+    return da < db || (da == db && ia < ib);
+}
+// entries of the sorted (distance, id) list [0, n) that precede (dv, iv)
+__device__ __forceinline__ int hn_rank(const double* d, const int* id, int n, double dv, int iv) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (hn_less(d[mid], id[mid], dv, iv)) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+// entries of the sorted list [0, n) strictly closer than t (faiss MinimaxHeap::count_below)
+__device__ __forceinline__ int hn_count_below(const double* d, int n, double t) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (d[mid] < t) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+template <int DT, int METRIC, bool QLDS>
+__global__ void __launch_bounds__(HN_THREADS) k_hnsw_search(HnswArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr int NW = HN_THREADS / 64;
+    constexpr bool IP = METRIC == METRIC_IP;
+    __shared__ int s_m, s_imin, s_valid;
+    __shared__ int s_new[NW], s_wj[NW];
+    __shared__ double s_wd[NW];
+    HnLds L;
+    hn_layout(a.d, a.k, a.ef, a.nbmax, QLDS, smem, &L);
+    const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int ng = (a.d + 7) >> 3;
+    const float* qv = a.q + (int64_t)q * a.d;
+    uint32_t* vis = a.vis + (int64_t)q * a.vis_words;
+    float* Dq = a.D + (int64_t)q * a.k;
+    int64_t* Iq = a.I + (int64_t)q * a.k;
+    if (a.entry < 0 || a.n == 0) {
+        for (int j = tid; j < a.k; j += HN_THREADS) {
+            Dq[j] = IP ? -INFINITY : INFINITY;
+            Iq[j] = -1;
+        }
+        return;
+    }
+    if constexpr (QLDS)
+        for (int i = tid; i < a.d; i += HN_THREADS) L.qs[(i & 7) * ng + (i >> 3)] = (double)qv[i];
+
+    // faiss distances of the rows bi[0 .. m) into bd (all waves, refine_rows rows per wave-step)
+    auto score = [&](int m) {
+        constexpr int RR = refine_rows<DT>();
+        for (int j0 = wid * RR; j0 < m; j0 += NW * RR) {
+            int64_t rr[RR];
+#pragma unroll
+            for (int i = 0; i < RR; ++i) rr[i] = j0 + i < m ? (int64_t)L.bi[j0 + i] : -1;
+            double s[RR];
+            exact_score_rows<DT, METRIC, QLDS, RR>(a.corpus, rr, L.qs, qv, a.d, a.dpad, lane, s);
+            if (lane == 0)
+#pragma unroll
+                for (int i = 0; i < RR; ++i)
+                    if (j0 + i < m) L.bd[j0 + i] = IP ? -s[i] : s[i];
+        }
+        __syncthreads();
+    };
+    // neighbour list of node v on level l into bl, up to its first -1; returns its length (uniform)
+    auto load_list = [&](int v, int l) -> int {
+        const int w = a.cum[l + 1] - a.cum[l];
+        const int* src = a.neighbors + a.offsets[v] + a.cum[l];
+        __syncthreads();
+        if (tid == 0) s_m = w;
+        __syncthreads();
+        for (int t = tid; t < w; t += HN_THREADS) {
+            const int u = src[t];
+            L.bl[t] = u;
+            if (u < 0) atomicMin(&s_m, t);
+        }
+        __syncthreads();
+        return s_m;
+    };
+
+    // ---- upper levels: greedy descent (faiss greedy_update_nearest) ----
+    int near = a.entry;
+    if (tid == 0) L.bi[0] = near;
+    __syncthreads();
+    score(1);
+    double dn = L.bd[0];
+    for (int l = a.max_level; l >= 1; --l) {
+        for (int64_t guard = 0; guard <= a.n; ++guard) {  // the distance strictly decreases
+            const int m = load_list(near, l);
+            for (int t = tid; t < m; t += HN_THREADS) L.bi[t] = L.bl[t];
+            __syncthreads();
+            score(m);
+            // the first neighbour at the smallest distance (faiss: first strictly closer, in order)
+            double bd = INFINITY;
+            int bj = 0x7FFFFFFF;
+            for (int t = tid; t < m; t += HN_THREADS) {
+                const double v = L.bd[t];
+                if (v < bd) {
+                    bd = v;
+                    bj = t;
+                }
+            }
+#pragma unroll
+            for (int sft = 32; sft > 0; sft >>= 1) {
+                const double od = __shfl_xor(bd, sft, 64);
+                const int oj = __shfl_xor(bj, sft, 64);
+                if (od < bd || (od == bd && oj < bj)) {
+                    bd = od;
+                    bj = oj;
+                }
+            }
+            if (lane == 0) {
+                s_wd[wid] = bd;
+                s_wj[wid] = bj;
+            }
+            __syncthreads();
+            bd = s_wd[0];
+            bj = s_wj[0];
+            for (int w = 1; w < NW; ++w)
+                if (s_wd[w] < bd || (s_wd[w] == bd && s_wj[w] < bj)) {
+                    bd = s_wd[w];
+                    bj = s_wj[w];
+                }
+            if (!(bj < m && bd < dn)) break;
+            near = L.bi[bj];
+            dn = bd;
+        }
+    }
+
+    // ---- level 0 (faiss search_from_candidates) ----
+    int cur = 0;
+    __syncthreads();
+    if (tid == 0) {
+        L.cd[0][0] = dn;
+        L.ci[0][0] = near;
+        L.cv[0][0] = 1;
+        L.rd[0][0] = dn;
+        L.ri[0][0] = near;
+        atomicOr(vis + (near >> 5), 1u << (near & 31));
+    }
+    int nc = 1, nres = 1, nvalid = 1;  // uniform
+    for (int64_t step = 0; nvalid > 0 && step <= a.n; ++step) {
+        // pop the closest valid candidate: the first valid entry of the sorted set
+        if (tid == 0) {
+            s_imin = 0x7FFFFFFF;
+            s_valid = 0;
+        }
+        __syncthreads();
+        for (int i = tid; i < nc; i += HN_THREADS)
+            if (L.cv[cur][i]) {
+                atomicMin(&s_imin, i);
+                break;
+            }
+        __syncthreads();
+        const int imin = s_imin;
+        const double d0 = L.cd[cur][imin];
+        const int v0 = L.ci[cur][imin];
+        const int below = hn_count_below(L.cd[cur], nc, d0);  // popped entries included
+        __syncthreads();
+        if (tid == 0) L.cv[cur][imin] = 0;
+        --nvalid;
+        if (below >= a.ef_search) break;
+        const int m = load_list(v0, 0);
+        // visited test-and-set; the new neighbours compacted in list order into bi
+        int nn = 0;
+        for (int t0 = 0; t0 < m; t0 += HN_THREADS) {
+            const int t = t0 + tid;
+            bool isnew = false;
+            int v = -1;
+            if (t < m) {
+                v = L.bl[t];
+                const uint32_t bit = 1u << (v & 31);
+                isnew = (atomicOr(vis + (v >> 5), bit) & bit) == 0u;
+            }
+            const u64 bal = __ballot(isnew);
+            if (lane == 0) s_new[wid] = __popcll(bal);
+            __syncthreads();
+            int pre = 0, tot = 0;
+            for (int w = 0; w < NW; ++w) {
+                const int c = s_new[w];
+                pre += w < wid ? c : 0;
+                tot += c;
+            }
+            if (isnew) L.bi[nn + pre + lane_prefix(bal)] = v;
+            nn += tot;
+            __syncthreads();
+        }
+        if (nn == 0) continue;
+        score(nn);
+        for (int j = tid; j < nn; j += HN_THREADS) {  // rank sort by (distance, id)
+            const double dj = L.bd[j];
+            const int ij = L.bi[j];
+            int r = 0;
+            for (int i = 0; i < nn; ++i) r += hn_less(L.bd[i], L.bi[i], dj, ij) ? 1 : 0;
+            L.sd[r] = dj;
+            L.si[r] = ij;
+        }
+        __syncthreads();
+        const int nxt = cur ^ 1;
+        for (int i = tid; i < nres; i += HN_THREADS) {  // results: the best k of the union
+            const int p = i + hn_rank(L.sd, L.si, nn, L.rd[cur][i], L.ri[cur][i]);
+            if (p < a.k) {
+                L.rd[nxt][p] = L.rd[cur][i];
+                L.ri[nxt][p] = L.ri[cur][i];
+            }
+        }
+        for (int j = tid; j < nn; j += HN_THREADS) {
+            const int p = j + hn_rank(L.rd[cur], L.ri[cur], nres, L.sd[j], L.si[j]);
+            if (p < a.k) {
+                L.rd[nxt][p] = L.sd[j];
+                L.ri[nxt][p] = L.si[j];
+            }
+        }
+        int myvalid = 0;  // candidates: the best ef of the union, popped entries included
+        for (int i = tid; i < nc; i += HN_THREADS) {
+            const int p = i + hn_rank(L.sd, L.si, nn, L.cd[cur][i], L.ci[cur][i]);
+            if (p < a.ef) {
+                L.cd[nxt][p] = L.cd[cur][i];
+                L.ci[nxt][p] = L.ci[cur][i];
+                L.cv[nxt][p] = L.cv[cur][i];
+                myvalid += L.cv[cur][i];
+            }
+        }
+        for (int j = tid; j < nn; j += HN_THREADS) {
+            const int p = j + hn_rank(L.cd[cur], L.ci[cur], nc, L.sd[j], L.si[j]);
+            if (p < a.ef) {
+                L.cd[nxt][p] = L.sd[j];
+                L.ci[nxt][p] = L.si[j];
+                L.cv[nxt][p] = 1;
+                ++myvalid;
+            }
+        }
+        myvalid = wave_sum_i(myvalid);
+        if (lane == 0) atomicAdd(&s_valid, myvalid);
+        __syncthreads();
+        nvalid = s_valid;
+        nres = min(nres + nn, a.k);
+        nc = min(nc + nn, a.ef);
+        cur = nxt;
+        __syncthreads();  // s_valid read by every thread before the next step resets it
+    }
+    __syncthreads();
+    for (int j = tid; j < a.k; j += HN_THREADS) {
+        if (j < nres) {
+            const double dv = L.rd[cur][j];
+            Dq[j] = (float)(IP ? -dv : dv);
+            Iq[j] = L.ri[cur][j];
+        } else {
+            Dq[j] = IP ? -INFINITY : INFINITY;
+            Iq[j] = -1;
+        }
+    }
+}
+
+template <int DT, int METRIC, bool QLDS>
+static void launch_hnsw_one(const HnswArgs& a, int nq, size_t lds, hipStream_t st) {
+    static bool attr_set = false;  // benign race: idempotent attribute
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)k_hnsw_search<DT, METRIC, QLDS>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)HN_LDS_CAP);
+        attr_set = true;
+    }
+    hipLaunchKernelGGL((k_hnsw_search<DT, METRIC, QLDS>), dim3(nq), dim3(HN_THREADS), lds, st, a);
+}
+template <int DT>
+static void launch_hnsw_dt(const HnswArgs& a, int nq, size_t lds, bool qlds, hipStream_t st) {
+    if (a.metric == METRIC_IP) {
+        if (qlds) launch_hnsw_one<DT, METRIC_IP, true>(a, nq, lds, st);
+        else launch_hnsw_one<DT, METRIC_IP, false>(a, nq, lds, st);
+    } else {
+        if (qlds) launch_hnsw_one<DT, METRIC_L2, true>(a, nq, lds, st);
+        else launch_hnsw_one<DT, METRIC_L2, false>(a, nq, lds, st);
+    }
+}
+hipError_t launch_hnsw_search(const HnswArgs& a, int nq, hipStream_t st) {
+    if (nq <= 0) return hipSuccess;
+    if (a.k < 1 || a.ef < a.k || a.ef > HN_EF_MAX || a.nbmax > HN_NB_MAX || a.nbmax < 1) return hipErrorInvalidValue;
+    const size_t lds = hnsw_lds_bytes(a.d, a.k, a.ef, a.nbmax);
+    if (lds > HN_LDS_CAP) return hipErrorInvalidValue;
+    const bool qlds = hn_layout(a.d, a.k, a.ef, a.nbmax, true, nullptr, nullptr) <= HN_LDS_CAP;
+    if (a.dt == DT_F32) launch_hnsw_dt<DT_F32>(a, nq, lds, qlds, st);
+    else if (a.dt == DT_BF16) launch_hnsw_dt<DT_BF16>(a, nq, lds, qlds, st);
+    else if (a.dt == DT_F16) launch_hnsw_dt<DT_F16>(a, nq, lds, qlds, st);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
 }  // namespace vs
