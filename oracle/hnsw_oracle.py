@@ -21,7 +21,7 @@ distances are negated so that smaller is better, and negated back on output):
    offered to the result max-heap (size k, admission ``d < D[0]``) and pushed on the candidates
    (when full: rejected if ``d >= max``, else the max is evicted);
 3. results sorted best first (``heap_reorder``: ascending distance, ties by id), padded with
-   id -1 and the worst distance.
+   id -1 and -FLT_MAX (IP) / FLT_MAX (L2), the flat path's padding.
 
 Distances here are the flat path's canonical fp64 scores (``oracle.canon_scores``: IP -> -score,
 L2 -> squared distance), not faiss's fp32 SIMD sums -- the same exactness contract as the flat
@@ -66,10 +66,13 @@ def _distances(x_stored, q, metric) -> np.ndarray:
     return -S if O._metric(metric) == O.METRIC_IP else S
 
 
+_FLT_MAX = float(np.finfo(np.float32).max)  # faiss heap neutral (Limits<float>::max), as the flat path
+
+
 def _output(res, k: int, metric):
-    """Sorted (distance, id) pairs -> faiss layout (D fp64 score, I) padded with -1 / worst."""
+    """Sorted (distance, id) pairs -> faiss layout (D fp64 score, I) padded with -1 / -+FLT_MAX."""
     ip = O._metric(metric) == O.METRIC_IP
-    S = np.full(k, -np.inf if ip else np.inf, dtype=np.float64)
+    S = np.full(k, -_FLT_MAX if ip else _FLT_MAX, dtype=np.float64)
     I = np.full(k, -1, dtype=np.int64)
     for j, (dv, v) in enumerate(res[:k]):
         S[j] = -dv if ip else dv

@@ -2823,7 +2823,7 @@ __global__ void __launch_bounds__(HN_THREADS) k_hnsw_search(HnswArgs a) {
     int64_t* Iq = a.I + (int64_t)q * a.k;
     if (a.entry < 0 || a.n == 0) {
         for (int j = tid; j < a.k; j += HN_THREADS) {
-            Dq[j] = IP ? -INFINITY : INFINITY;
+            Dq[j] = IP ? -__FLT_MAX__ : __FLT_MAX__;
             Iq[j] = -1;
         }
         return;
@@ -3031,7 +3031,7 @@ __global__ void __launch_bounds__(HN_THREADS) k_hnsw_search(HnswArgs a) {
             Dq[j] = (float)(IP ? -dv : dv);
             Iq[j] = L.ri[cur][j];
         } else {
-            Dq[j] = IP ? -INFINITY : INFINITY;
+            Dq[j] = IP ? -__FLT_MAX__ : __FLT_MAX__;
             Iq[j] = -1;
         }
     }

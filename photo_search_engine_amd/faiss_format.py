@@ -118,19 +118,31 @@ def hnsw_default_probas(M: int):
 
 def read_hnsw_graph(path: str) -> dict:
     """The graph arrays of an ``IHNf`` file (faiss ``write_index`` of an IndexHNSWFlat)."""
+    # reads the header and the graph arrays only (they precede the storage's row payload)
     with open(path, "rb") as f:
-        raw = f.read()
-    fourcc, d, ntotal, _trained, metric_type, off = _header(memoryview(raw), 0)
-    if fourcc != FOURCC_HNSW_FLAT:
-        raise FaissFormatError(f"not an HNSW file: {fourcc!r}")
-    g = {"d": d, "ntotal": ntotal, "metric_type": metric_type}
-    for name, dt in (("assign_probas", "<f8"), ("cum_nneighbor_per_level", "<i4"), ("levels", "<i4"),
-                     ("offsets", "<u8"), ("neighbors", "<i4")):
-        (n,) = struct.unpack_from("<Q", raw, off)
-        g[name] = np.frombuffer(raw, dtype=dt, count=n, offset=off + 8).copy()
-        off += 8 + n * np.dtype(dt).itemsize
-    (g["entry_point"], g["max_level"], g["efConstruction"], g["efSearch"],
-     g["upper_beam"]) = struct.unpack_from("<5i", raw, off)
+        head = f.read(41)
+        fourcc, d, ntotal, _trained, metric_type, off = _header(memoryview(head), 0)
+        if fourcc != FOURCC_HNSW_FLAT:
+            raise FaissFormatError(f"not an HNSW file: {fourcc!r}")
+        f.seek(off)
+        g = {"d": d, "ntotal": ntotal, "metric_type": metric_type}
+        for name, dt in (("assign_probas", "<f8"), ("cum_nneighbor_per_level", "<i4"), ("levels", "<i4"),
+                         ("offsets", "<u8"), ("neighbors", "<i4")):
+            raw = f.read(8)
+            if len(raw) != 8:
+                raise FaissFormatError("truncated HNSW graph")
+            (n,) = struct.unpack("<Q", raw)
+            nbytes = n * np.dtype(dt).itemsize
+            body = f.read(nbytes)
+            if len(body) != nbytes:
+                raise FaissFormatError("truncated HNSW graph")
+            g[name] = np.frombuffer(body, dtype=dt, count=n).copy()
+            off += 8 + nbytes
+        raw = f.read(20)
+        if len(raw) != 20:
+            raise FaissFormatError("truncated HNSW graph")
+        (g["entry_point"], g["max_level"], g["efConstruction"], g["efSearch"],
+         g["upper_beam"]) = struct.unpack("<5i", raw)
     g["storage_offset"] = off + 20
     return g
 

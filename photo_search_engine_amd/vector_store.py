@@ -10,8 +10,12 @@ What changes underneath:
   * ``self.index`` is a :class:`~photo_search_engine_amd.index.FlatIndex` (HBM-resident shard on
     one GPU) instead of a faiss CPU index; searches are exact (see include/vs.h).
   * ``index_type="hnsw"`` is accepted, validated and recorded in the sidecar exactly as before,
-    but served by exact flat search (recall 1.0 >= HNSW); ``save()`` writes an IHNf file (the exact
-    k-NN graph on one level + the flat storage) that the reference's faiss can load back, up to
+    and served by exact flat search by default (recall 1.0 >= HNSW); ``VECTOR_HNSW_SEARCH=graph``
+    runs faiss's HNSW search instead, on the GPU (:class:`~photo_search_engine_amd.hnsw.HNSWGraph`)
+    with ``efSearch = hnsw_ef_search`` as the reference sets it (utils/vector_store.py:77,135), over
+    the graph of the loaded IHNf file or the one ``save()`` writes.  ``save()`` writes an IHNf file
+    (a multi-level graph -- faiss's level draw, each level's exact k-NN among its nodes, built by
+    the GPU flat search -- + the flat storage) that the reference's faiss can load back, up to
     ``VECTOR_HNSW_GRAPH_MAX_ROWS`` rows (flat IxFI/IxF2 above).  ``load()`` reads both.
   * ``_embeddings`` caches only rows added in this process (a dict), not one Python list per row.
   * Bulk additions: :meth:`add` (n x d array) and :meth:`search_batch` (faiss (D, I) layout).
@@ -21,8 +25,9 @@ Normalisation stays on the host in numpy, bit-identical to the reference
 
 Environment knobs (new, optional): ``VECTOR_DEVICE`` (GPU ordinal, default 0), ``VECTOR_DEVICES``
 (e.g. ``0,1,2,3,4,5,6,7``: one index over those GPUs of this process, include/vs.h vs_multi_*),
-``VECTOR_DTYPE`` (f32 | bf16 | f16 storage, default f32 = the reference's storage precision) and
-``VECTOR_SCREEN`` (native | int8: the batched-search screen of an inner-product index).
+``VECTOR_DTYPE`` (f32 | bf16 | f16 storage, default f32 = the reference's storage precision),
+``VECTOR_SCREEN`` (native | int8: the batched-search screen of an inner-product index) and
+``VECTOR_HNSW_SEARCH`` (exact | graph: how an ``index_type="hnsw"`` store searches).
 """
 from __future__ import annotations
 
@@ -33,6 +38,7 @@ from typing import Any, Dict, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import faiss_format
+from .hnsw import HNSWGraph
 from .index import FlatIndex, MultiDeviceFlatIndex
 
 METRIC_INNER_PRODUCT = 0
@@ -62,6 +68,13 @@ def _hnsw_graph_max_rows() -> int:
     """Largest index saved as an HNSW (IHNf) file under ``index_type="hnsw"``; above it the
     exact k-NN graph build is skipped and a flat file is written (this backend loads both)."""
     return int(os.environ.get("VECTOR_HNSW_GRAPH_MAX_ROWS", "200000") or 200000)
+
+
+_HNSW_EF_MAX = 2048  # largest max(efSearch, k) of the GPU graph search (include/vs.h)
+
+
+def _hnsw_graph_search() -> bool:
+    return (os.environ.get("VECTOR_HNSW_SEARCH", "exact") or "exact").strip().lower() == "graph"
 
 
 class VectorStore:
@@ -108,6 +121,9 @@ class VectorStore:
         # what the index file on disk holds, when it is known to be a prefix of this index
         # (set by save() / load(); None after clear()): lets save() append instead of rewriting
         self._persisted: Optional[Dict[str, Any]] = None
+        # VECTOR_HNSW_SEARCH=graph: the graph arrays last loaded or saved, and its GPU copy
+        self._graph_arrays: Optional[Dict[str, Any]] = None
+        self._hnsw: Optional[HNSWGraph] = None
 
     # ------------------------------------------------------------------ internals
     def _rebuild_path_index(self) -> None:
@@ -223,7 +239,7 @@ class VectorStore:
             raise ValueError(f"向量维度不匹配: {len(query_embedding)} != {self.dimension}")
 
         k = min(top_k, self.index.ntotal)
-        distances, indices = self.index.search(self._normalize_query(query_embedding), k)
+        distances, indices = self._search_rows(self._normalize_query(query_embedding), k)
 
         results: List[Dict] = []
         for distance, index in zip(distances[0].tolist(), indices[0].tolist()):
@@ -268,10 +284,13 @@ class VectorStore:
         n, d, mt = int(self.index.ntotal), int(self.index.d), int(self.index.metric_type)
         old = self._appendable_rows(d, mt)
         if self.index_type == "hnsw" and n <= _hnsw_graph_max_rows():
-            # an IHNf file the reference's faiss can load (rollback): one-level exact k-NN graph
-            graph = faiss_format.single_level_graph(self._knn_graph(n), self.hnsw_m, self.hnsw_ef_construction,
-                                                    self.hnsw_ef_search)
+            # an IHNf file the reference's faiss can load (rollback); a graph loaded from file is
+            # kept, with efSearch as configured (the reference sets hnsw.efSearch after every load,
+            # utils/vector_store.py:135, and faiss writes it back)
+            graph = (dict(self._graph_arrays, efSearch=self.hnsw_ef_search) if self._graph_covers(n) else
+                     self._build_graph(n))
             faiss_format.write_hnsw(self.index_path, graph, d, n, mt, lambda path, off: self.index.write_rows(path, off, 0, n))
+            self._graph_arrays = graph
             self._persisted = None
             self._write_index_meta()
             with open(self.metadata_path, "w", encoding="utf-8") as file:
@@ -297,9 +316,12 @@ class VectorStore:
         index = self._create_index_with_metric(loaded.d, loaded.metric_type)
         if loaded.ntotal:  # payload streamed file -> pinned chunks -> HBM (no host copy of the matrix)
             index.add_from_file(self.index_path, loaded.payload_offset, loaded.ntotal)
+        self._drop_graph()
         self.index = index
         self._persisted = (self._file_state(loaded.ntotal, loaded.d, loaded.metric_type)
                            if loaded.kind == "flat" else None)
+        if loaded.kind == "hnsw" and self.index_type == "hnsw" and _hnsw_graph_search():
+            self._graph_arrays = faiss_format.read_hnsw_graph(self.index_path)
         payload = self._load_index_meta()
         self._validate_loaded_index(payload, loaded)
 
@@ -324,23 +346,107 @@ class VectorStore:
 
     def clear(self) -> None:
         """清空索引与元数据."""
+        self._drop_graph()
         self.index = self._create_index(self.dimension) if self.dimension else None
         self.metadata = []
         self._embeddings = {}
         self._path_to_index = {}
         self._persisted = None
 
-    def _knn_graph(self, n: int) -> np.ndarray:
-        """Exact top-2M neighbours of every stored row (itself excluded), on the GPU index."""
-        m2 = 2 * self.hnsw_m
-        out = np.full((n, m2), -1, dtype=np.int32)
-        kk = min(n, m2 + 1)
-        for r0 in range(0, n, 4096):
-            rows = self.index.reconstruct_n(r0, min(4096, n - r0))
-            _, I = self.index.search(rows, kk)
-            for j in range(I.shape[0]):
-                ids = [int(x) for x in I[j] if x >= 0 and x != r0 + j][:m2]
-                out[r0 + j, :len(ids)] = ids
+    # ------------------------------------------------------------------ HNSW graph search
+    def _graph_covers(self, n: int) -> bool:
+        g = self._graph_arrays
+        return g is not None and int(np.asarray(g["levels"]).shape[0]) == n
+
+    def _drop_graph(self) -> None:
+        if self._hnsw is not None:
+            self._hnsw.close()
+        self._hnsw = None
+        self._graph_arrays = None
+
+    def _search_rows(self, q: np.ndarray, k: int) -> Tuple[np.ndarray, np.ndarray]:
+        """``index.search``, or with ``VECTOR_HNSW_SEARCH=graph`` on an HNSW store, faiss's HNSW
+        search on the GPU over the graph of the loaded file (while it still covers every row) or
+        the graph ``save()`` writes (:meth:`_build_graph`), rebuilt after adds.  Beams wider
+        than the GPU search takes (max(efSearch, k) > 2048) and multi-GPU indexes search exactly."""
+        if (self.index_type != "hnsw" or not _hnsw_graph_search() or not isinstance(self.index, FlatIndex)
+                or max(k, self.hnsw_ef_search) > _HNSW_EF_MAX):
+            return self.index.search(q, k)
+        n = int(self.index.ntotal)
+        if self._hnsw is None or self._hnsw.ntotal != n or self._hnsw.index is not self.index:
+            if self._hnsw is not None:
+                self._hnsw.close()
+                self._hnsw = None
+            if not self._graph_covers(n):
+                self._graph_arrays = self._build_graph(n)
+            self._hnsw = HNSWGraph(self.index, self._graph_arrays, self.hnsw_ef_search)
+        return self._hnsw.search(q, k, self.hnsw_ef_search)
+
+    def _build_graph(self, n: int) -> Dict[str, Any]:
+        """A faiss-layout HNSW graph over the n stored rows: node levels drawn as faiss's
+        ``HNSW::random_level`` does (``set_default_probas(M, 1/ln M)``; numpy's generator, seed
+        12345, not faiss's), and on every level each node's neighbours are its exact nearest nodes
+        of that level (2M on level 0, M above; the flat search, ties -> lower id), best first; the
+        entry point is the first node of the top level.  The sparse upper levels give the greedy
+        descent links between clusters that a one-level k-NN graph lacks (on clustered rows whose
+        clusters hold more than 2M rows a one-level graph never leaves the entry's cluster)."""
+        M = self.hnsw_m
+        probas, cum = faiss_format.hnsw_default_probas(M)
+        f = np.random.default_rng(12345).random(n)
+        lev = np.full(n, len(probas) - 1, dtype=np.int64)
+        open_ = np.ones(n, dtype=bool)
+        for level, p in enumerate(probas):
+            hit = open_ & (f < p)
+            lev[hit] = level
+            open_ &= ~hit
+            f[open_] -= p
+        levels = (lev + 1).astype(np.int32)
+        offsets = np.zeros(n + 1, dtype=np.uint64)
+        offsets[1:] = np.cumsum(cum[levels].astype(np.uint64))
+        nb = np.full(int(offsets[-1]), -1, dtype=np.int32)
+        top = int(lev.max()) if n else -1
+        for level in range(top + 1):
+            members = np.nonzero(lev >= level)[0]
+            width = int(cum[level + 1] - cum[level])
+            knn = self._knn_graph(width, None if level == 0 else members)
+            base = offsets[members].astype(np.int64) + int(cum[level])
+            for j in range(members.shape[0]):
+                row = knn[j][knn[j] >= 0]
+                nb[base[j]:base[j] + len(row)] = row
+        return {"assign_probas": probas, "cum_nneighbor_per_level": cum, "levels": levels, "offsets": offsets,
+                "neighbors": nb, "entry_point": int(np.nonzero(lev == top)[0][0]) if n else -1, "max_level": top,
+                "efConstruction": int(self.hnsw_ef_construction), "efSearch": int(self.hnsw_ef_search),
+                "upper_beam": 1}
+
+    def _knn_graph(self, width: int, members: Optional[np.ndarray] = None) -> np.ndarray:
+        """Exact top-``width`` neighbours (itself excluded, -1 padded) of every stored row, or of
+        every row of ``members`` among ``members`` only (global ids; a temporary index over their
+        stored values), by the GPU flat search."""
+        n = int(self.index.ntotal)
+        index, ids = self.index, None
+        if members is not None:
+            ids = np.asarray(members, dtype=np.int64)
+            index = self._create_index(self.dimension)
+            for r0 in range(0, n, 65536):
+                rows = self.index.reconstruct_n(r0, min(65536, n - r0))
+                sel = ids[(ids >= r0) & (ids < r0 + rows.shape[0])] - r0
+                if sel.size:
+                    index.add(np.ascontiguousarray(rows[sel]))
+        m = int(index.ntotal)
+        out = np.full((m, width), -1, dtype=np.int32)
+        kk = min(m, width + 1)
+        try:
+            for r0 in range(0, m, 4096):
+                rows = index.reconstruct_n(r0, min(4096, m - r0))
+                _, I = index.search(rows, kk)
+                for j in range(I.shape[0]):
+                    nbr = [int(x) for x in I[j] if x >= 0 and x != r0 + j][:width]
+                    if ids is not None:
+                        nbr = [int(ids[x]) for x in nbr]
+                    out[r0 + j, :len(nbr)] = nbr
+        finally:
+            if ids is not None and hasattr(index, "close"):
+                index.close()
         return out
 
     # ------------------------------------------------------------------ persistence state
@@ -401,4 +507,4 @@ class VectorStore:
         if q.shape[1] != self.dimension:
             raise ValueError(f"向量维度不匹配: {q.shape[1]} != {self.dimension}")
         k = min(top_k, self.index.ntotal)
-        return self.index.search(self._normalize_rows(q), k)
+        return self._search_rows(self._normalize_rows(q), k)

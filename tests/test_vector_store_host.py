@@ -144,10 +144,11 @@ def test_save_rewrites_when_file_changed_or_cleared(VS, tmp_path, monkeypatch):
     assert np.array_equal(ff.vectors, store.index.reconstruct_n(0, 15))
 
 
-def test_hnsw_store_saves_ihnf_with_exact_knn_graph(VS, tmp_path):
+def test_hnsw_store_saves_ihnf_with_layered_knn_graph(VS, tmp_path):
     # index_type="hnsw" (the env templates' setting, .env.example:82-83): save() writes an IHNf file
     # the reference's faiss can read back -- same header/array layout as the reference's own
-    # fixture, storage = the stored rows, graph = exact top-2M neighbours on one level
+    # fixture, storage = the stored rows, graph = faiss's level draw with every level's exact
+    # k-NN among its nodes (2M on level 0, M above)
     import json
     import shutil
     from oracle import oracle as O
@@ -157,23 +158,33 @@ def test_hnsw_store_saves_ihnf_with_exact_knn_graph(VS, tmp_path):
     shutil.copy(os.path.join(GOLDEN, "ref_photo_search.index.meta.json"), str(idx) + ".meta.json")
     (tmp_path / "metadata.json").write_text(json.dumps([{"photo_path": f"/p/{i}"} for i in range(77)]))
     store = VS(dimension=4096, index_path=str(idx), metadata_path=str(tmp_path / "metadata.json"),
-               index_type="hnsw", hnsw_m=8, hnsw_ef_construction=320, hnsw_ef_search=192)
+               index_type="hnsw", hnsw_m=4, hnsw_ef_construction=320, hnsw_ef_search=192)
     assert store.load()
     ref = F.read_index(str(idx)).vectors.copy()
     store.save()
     ff = F.read_index(str(idx))
     assert ff.kind == "hnsw" and np.array_equal(ff.vectors, ref)
     g = F.read_hnsw_graph(str(idx))
-    probas, cum = F.hnsw_default_probas(8)
+    probas, cum = F.hnsw_default_probas(4)
     assert np.array_equal(g["assign_probas"], probas) and np.array_equal(g["cum_nneighbor_per_level"], cum)
-    assert (g["levels"] == 1).all() and (g["efConstruction"], g["efSearch"], g["entry_point"]) == (320, 192, 0)
-    nb = g["neighbors"].reshape(77, 16)
-    _, I = O.knn_exact(ref, ref, 17, "ip")
-    for i in range(77):
-        assert nb[i].tolist() == [int(j) for j in I[i] if j != i][:16]
-    # and it loads back (graph ignored, exact search)
+    assert (g["efConstruction"], g["efSearch"], g["upper_beam"]) == (320, 192, 1)
+    lev = g["levels"].astype(np.int64) - 1
+    assert g["max_level"] == lev.max() >= 1 and lev[g["entry_point"]] == g["max_level"]
+    assert g["entry_point"] == int(np.nonzero(lev == lev.max())[0][0])
+    assert np.array_equal(np.diff(g["offsets"].astype(np.int64)), cum[g["levels"]])
+    S = O.canon_scores(ref, ref, "ip")
+    for level in range(int(lev.max()) + 1):
+        members = np.nonzero(lev >= level)[0]
+        width = int(cum[level + 1] - cum[level])
+        for i in members:
+            others = members[members != i]
+            want = others[np.lexsort((others, -S[i, others]))][:width].tolist()
+            b = int(g["offsets"][i]) + int(cum[level])
+            got = g["neighbors"][b:b + width]
+            assert got[got >= 0].tolist() == want, (level, i)
+    # and it loads back (graph kept on disk, exact search by default)
     s2 = VS(dimension=4096, index_path=str(idx), metadata_path=str(tmp_path / "metadata.json"),
-            index_type="hnsw", hnsw_m=8, hnsw_ef_construction=320, hnsw_ef_search=192)
+            index_type="hnsw", hnsw_m=4, hnsw_ef_construction=320, hnsw_ef_search=192)
     assert s2.load() and s2.get_total_items() == 77
 
 
