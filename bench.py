@@ -71,6 +71,9 @@ def parse():
     ap.add_argument("--no-recall", action="store_true", help="cfg5: skip the exact ground truth (profiling runs)")
     ap.add_argument("--skew", type=float, default=0.0,
                     help="cfg5: Zipf exponent of the cluster sizes (0 = equal-sized clusters; 1.1 = a heavy head)")
+    ap.add_argument("--ivf-scan", default="auto", choices=["auto", "gemv", "mfma"],
+                    help="cfg5: list-scan kernels (auto: MFMA screen for lists probed by many queries; "
+                         "with auto the GEMV-only scan is timed too and reported beside it)")
     ap.add_argument("--iso-data", action="store_true",
                     help="cfg5: isotropic rows (the flat bench's data) instead of the Gaussian mixture")
     ap.add_argument("--traffic-file", default=None,
@@ -471,6 +474,7 @@ def run_ivf(args):
     def step():
         ix.search_device(q.data_ptr(), nq, k, D.data_ptr(), I.data_ptr(), S.data_ptr(), nprobe, stream)
 
+    ix.set_scan(args.ivf_scan)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -489,6 +493,26 @@ def run_ivf(args):
     achieved = alg_bytes / (kavg * 1e-3) / 1e9
     sizes = ix.list_sizes()
     Ig = I.cpu().numpy()
+    mfma_lists, uncert = ix.last_search_stats()
+    gemv_beside = None
+    if args.ivf_scan == "auto" and mfma_lists > 0:  # the GEMV-only scan on the same batch, beside
+        Sg0 = S.cpu().numpy()
+        ix.set_scan("gemv")
+        step()
+        torch.cuda.synchronize()
+        ix.set_timing(True)
+        t1 = time.perf_counter()
+        for _ in range(max(2, args.steps // 2)):
+            step()
+        torch.cuda.synchronize()
+        el1 = time.perf_counter() - t1
+        ix.set_timing(False)
+        kms1, _ = ix.timing_fetch()
+        gemv_beside = {"ms_per_step": round(el1 * 1e3 / max(2, args.steps // 2), 4),
+                       "scan_ms": round(float(np.mean(kms1)), 4),
+                       "identical_results": bool(np.array_equal(I.cpu().numpy(), Ig) and
+                                                 np.array_equal(S.cpu().numpy(), Sg0))}
+        ix.set_scan(args.ivf_scan)
 
     # probes (exact coarse top-nprobe) and per-batch scan volume, for the CPU baseline
     cf = FlatIndex(d, "ip", dtype, device=0)
@@ -575,6 +599,7 @@ def run_ivf(args):
         "config": {"workload": args.workload, "desc": desc, "N": N, "d": d, "batch": nq, "k": k, "nlist": nlist,
                    "nprobe": nprobe, "list_rows_min_max": [int(sizes.min()), int(sizes.max())],
                    "list_rows_median": int(np.median(sizes)), "skew": args.skew,
+                   "list_scan": args.ivf_scan, "mfma_list_scans": mfma_lists,
                    "parallelism": "1 GPU"},
         "roofline": {
             "kernel": "k_ivf_scan",
@@ -587,7 +612,8 @@ def run_ivf(args):
             "kernel_ms": round(kavg, 4),
             "alg_bytes_per_launch": alg_bytes,
         },
-        "uncertified_first_pass": None,
+        "uncertified_first_pass": uncert,
+        "gemv_scan": gemv_beside,
         "build_s": round(t_build, 2),
         "recall@10": round(hit / (nq * 10.0), 6) if parts_S else None,
         "probed_recall@10": round(got / max(need, 1), 6) if parts_S else None,

@@ -194,7 +194,11 @@ struct ScreenArgs {
                              // (rows below it were dropped; zeroed by the query pack), or null
     const int* gate;         // device fallback round: the launch does nothing while *gate == 0 (no
                              // query of the block failed its certificate), or null = always run
+    const int* tile_map;     // mapped screen (IVF list scan): page of logical tile t; keys carry
+                             // storage slots page * TR + row, n_valid counts the list's rows
+    const int* qmap;         // mapped screen: glist / gcnt row of block query q
 };
+constexpr int MFMA_MAP_TILES = 256;  // mapped screen: logical tiles per workgroup (its LDS page table)
 int gemv_blocks_per_cu(int dt, int nqpad);  // resident k_screen_gemv blocks per CU (occupancy API)
 
 // ---- launchers (vs_kernels.hip) -------------------------------------------------------------
@@ -213,13 +217,21 @@ hipError_t launch_gather_rows(int dt, const uint8_t* data, const int64_t* ids, i
 // qinfo[q*2+1] = ||q_hat - q|| (upper bounds, fp32)
 // fails (optional): zeroed -- the query block's certificate-failure count (RefineArgs::fails);
 // gate (optional): as ScreenArgs::gate
+// qidx (optional): tile row r packs query qidx[r] of q; qinfo is then indexed by qidx and max-combined
 hipError_t launch_pack_qtile(int dt, const float* q, int nqb, int d, int dpad, uint8_t* qt, float* qinfo, int* gcnt,
-                             u64* drop, hipStream_t st, int* fails = nullptr, const int* gate = nullptr);
+                             u64* drop, hipStream_t st, int* fails = nullptr, const int* gate = nullptr,
+                             const int* qidx = nullptr);
 hipError_t launch_pack_qf32(const float* q, int nqb, int nqpad, int d, int dpad, float* qp, float* qinfo,
                             hipStream_t st, int* ctr = nullptr,  // ctr: zeroed (a screen's tile queue)
                             int* fails = nullptr);
 
 hipError_t launch_screen_mfma(int dt, const ScreenArgs& a, const uint8_t* qt, int nqb, hipStream_t st);
+// the same screen over the pages a.tile_map lists (bf16 / f16, unseeded, a.Kp <= MFMA_KP_MAX,
+// at most MFMA_MAP_TILES tiles per workgroup), on a split query tile of <= 128 queries
+// (launch_pack_qtile_split); survivors appended to glist rows a.qmap[q]
+hipError_t launch_screen_mfma_mapped(int dt, const ScreenArgs& a, const uint8_t* qt, int nqb, hipStream_t st);
+hipError_t launch_pack_qtile_split(int dt, const float* q, const int* qidx, int nqb, int d, int dpad, uint8_t* qt,
+                                   float* qinfo, hipStream_t st);
 hipError_t launch_screen_gemv(int dt, const ScreenArgs& a, const float* qp, int nqb, int nqpad, hipStream_t st);
 
 // one merge stage: in[(s*qstride + q)*Kp + j], s < nseg  ->  out[(b*nq + q)*Kp + j]

@@ -44,10 +44,17 @@ struct vs_ivf {
     int64_t ntotal = 0;
     // device copy of the page tables (CSR), refreshed lazily after adds
     DevBuf d_page_off, d_list_pages, d_list_n;
+    std::vector<int> page_off_h;  // host copy of d_page_off
     bool csr_dirty = true;
     // workspaces (add: exclusive lock; search / reconstruct: search_mtx)
     DevBuf tmp_rows, slots, assign_ids;
     DevBuf qdev, probes, items, qp, qinfo, cand, glist, gcnt, cert, outD, outI, rec, next_item;
+    DevBuf mqidx, mqtile, mcand;
+    DevBuf rq, rD, rI, rS;  // re-search of uncertified queries: gathered queries and their outputs  // MFMA list scans: query indices, query tile, workspaces
+    int scan_mode = VS_IVF_SCAN_AUTO;
+    int last_mfma_lists = 0;  // first pass of the last search: MFMA list scans ...
+    int last_uncert = 0;      // ... and queries its certificate rejected (re-searched deeper)
+    int cur_mfma_lists = 0;
     std::vector<int64_t> probes_h;
     std::vector<int> cert_h;
     hipStream_t own = nullptr;
@@ -64,6 +71,20 @@ constexpr int kPagesPerItem = 16;  // scan work item: up to 16 pages (4096 rows)
 
 void check_ivf(const vs_ivf* ix) {
     if (!ix) throw VsError(VS_ERR_ARG, "null IVF index");
+}
+
+// A list probed by nql queries costs the GEMV scan ceil(nql / IVF_QG) reads of its pages (items of
+// <= 8 queries, each re-reading the list from HBM); the MFMA screen reads them once per 256
+// queries, one workgroup per CU over the list's pages.  Rates measured on MI355X: GEMV scan ~76%
+// of HBM peak on evenly probed lists, bf16 MFMA screen ~50% plus ~20 us of launches per scan.
+bool mfma_scan_pays(const vs_ivf* ix, int64_t np, int nql) {
+    if (ix->dtype == DT_F32 || nql <= 1 || ix->scan_mode == VS_IVF_SCAN_GEMV) return false;
+    if (ix->scan_mode == VS_IVF_SCAN_MFMA) return true;
+    const double B = (double)tile_bytes(ix->dpad, ix->dtype), cu = (double)ix->num_cu;
+    const double t_gemv = (double)((nql + IVF_QG - 1) / IVF_QG) * (double)np * B / 6.0e12;
+    const double waves = std::ceil((double)np / cu);  // tiles per workgroup
+    const double t_mfma = (double)((nql + MFMA_QB / 2 - 1) / (MFMA_QB / 2)) * (waves * cu * B / 4.0e12 + 20e-6);
+    return t_mfma < t_gemv;
 }
 
 int64_t rows_per_chunk(int d) { return std::max<int64_t>(1, (int64_t)(256 << 20) / ((int64_t)d * 4)); }
@@ -112,7 +133,9 @@ void refresh_maxsq(vs_ivf* ix) {
 
 void upload_csr(vs_ivf* ix, hipStream_t st) {
     if (!ix->csr_dirty) return;
-    std::vector<int> off(ix->nlist + 1, 0), flat;
+    std::vector<int>& off = ix->page_off_h;
+    std::vector<int> flat;
+    off.assign(ix->nlist + 1, 0);
     for (int l = 0; l < ix->nlist; ++l) {
         off[l + 1] = off[l] + (int)ix->pages[l].size();
         flat.insert(flat.end(), ix->pages[l].begin(), ix->pages[l].end());
@@ -193,7 +216,7 @@ void add_rows(vs_ivf* ix, int64_t n, Fill&& fill) {
 
 // one search pass at screening depth Kp; outputs device [nq][k]; cert_dev [nq]
 void search_core(vs_ivf* ix, const float* q_dev, int64_t nq, int k, int nprobe, int Kp, float* D, int64_t* I,
-                 double* S64, int* cert_dev, hipStream_t st) {
+                 double* S64, int* cert_dev, hipStream_t st, bool first_pass) {
     // 1. probes: exact top-nprobe centroids of every query
     ix->probes.ensure((size_t)nq * nprobe * sizeof(int64_t));
     search_exact_device(ix->coarse, q_dev, nq, nprobe, ix->probes.as<int64_t>(), nullptr, st);
@@ -211,12 +234,34 @@ void search_core(vs_ivf* ix, const float* q_dev, int64_t nq, int k, int nprobe, 
         }
     const int classes[4] = {1, 2, 4, IVF_QG};
     std::vector<int> cls_items[4];
-    std::vector<int> per_q((size_t)nq, 0);
+    std::vector<int64_t> per_q((size_t)nq, 0);  // candidate keys each query's list can receive
     double bytes = 0.0;
+    // MFMA list scans: (list, first page, pages, query block offset into mq, queries, workgroups)
+    struct MScan { int l, p0, np, q0, nqb, G; };
+    std::vector<MScan> mscans;
+    std::vector<int> mq;  // query indices of every MFMA scan's block
+    const bool mfma_ok = Kp <= MFMA_KP_MAX;
     for (int l = 0; l < ix->nlist; ++l) {
         const int nql = (int)lq[l].size();
         const int np = (int)ix->pages[l].size();
         if (nql == 0 || np == 0) continue;
+        bytes += (double)ix->list_n[l] * ix->d * ix->es;
+        if (mfma_ok && mfma_scan_pays(ix, np, nql)) {
+            // segments of <= num_cu * MFMA_MAP_TILES pages (the workgroups' LDS page tables)
+            const int seg = ix->num_cu * MFMA_MAP_TILES;
+            for (int b0 = 0; b0 < nql; b0 += MFMA_QB / 2) {  // split query tiles: 128 queries
+                const int nb = std::min(MFMA_QB / 2, nql - b0);
+                const int q0 = (int)mq.size();
+                mq.insert(mq.end(), lq[l].begin() + b0, lq[l].begin() + b0 + nb);
+                for (int p0 = 0; p0 < np; p0 += seg) {
+                    const int nps = std::min(seg, np - p0);
+                    const int G = std::min(nps, ix->num_cu);
+                    mscans.push_back({l, p0, nps, q0, nb, G});
+                    for (int j = 0; j < nb; ++j) per_q[lq[l][b0 + j]] += (int64_t)G * Kp;
+                }
+            }
+            continue;
+        }
         for (int g0 = 0; g0 < nql; g0 += IVF_QG) {
             const int gq = std::min(IVF_QG, nql - g0);
             const int c = gq <= 1 ? 0 : gq <= 2 ? 1 : gq <= 4 ? 2 : 3;
@@ -228,16 +273,17 @@ void search_core(vs_ivf* ix, const float* q_dev, int64_t nq, int k, int nprobe, 
                 v.push_back(pe);
                 v.push_back(gq);
                 for (int j = 0; j < IVF_QG; ++j) v.push_back(j < gq ? lq[l][g0 + j] : -1);
-                for (int j = 0; j < gq; ++j) ++per_q[lq[l][g0 + j]];
+                for (int j = 0; j < gq; ++j) per_q[lq[l][g0 + j]] += Kp;
             }
         }
-        // algorithmic bytes: every probed list read once (a list probed by more than IVF_QG
-        // queries is re-read per query group; that extra traffic is not algorithmic)
-        bytes += (double)ix->list_n[l] * ix->d * ix->es;
     }
-    int max_items = 1;
-    for (int v : per_q) max_items = std::max(max_items, v);
-    const int lcap = max_items * Kp;
+    // (algorithmic bytes above: every probed list read once; the GEMV scan re-reads a list per
+    // query group, the MFMA scan per 256-query block -- that extra traffic is not algorithmic)
+    int64_t max_keys = Kp;
+    for (int64_t v : per_q) max_keys = std::max(max_keys, v);
+    if (max_keys > (int64_t)1 << 30) throw VsError(VS_ERR_ARG, "IVF candidate lists exceed 2^30 keys per query");
+    const int lcap = (int)max_keys;
+    ix->cur_mfma_lists = (int)mscans.size();
     size_t total_ints = 0;
     for (auto& v : cls_items) total_ints += v.size();
     ix->items.ensure(std::max<size_t>(total_ints, 1) * sizeof(int));
@@ -253,7 +299,11 @@ void search_core(vs_ivf* ix, const float* q_dev, int64_t nq, int k, int nprobe, 
             for (auto& v : cls_items) all.insert(all.end(), v.begin(), v.end());
         if (!all.empty())
             HIP_CHECK(hipMemcpyAsync(ix->items.p, all.data(), all.size() * sizeof(int), hipMemcpyHostToDevice, st));
-        upload_csr(ix, st);  // synchronises the stream, so `all` may go out of scope
+        if (!mq.empty()) {
+            ix->mqidx.ensure(mq.size() * sizeof(int));
+            HIP_CHECK(hipMemcpyAsync(ix->mqidx.p, mq.data(), mq.size() * sizeof(int), hipMemcpyHostToDevice, st));
+        }
+        upload_csr(ix, st);  // synchronises the stream, so `all` and `mq` may go out of scope
     }
     // 3. queries fp32 padded, ||q|| for the certificate
     ix->qp.ensure((size_t)nq * ix->dpad * sizeof(float));
@@ -282,12 +332,45 @@ void search_core(vs_ivf* ix, const float* q_dev, int64_t nq, int k, int nprobe, 
     const int max_grid = ix->num_cu * grid_per_cu;
     ix->cand.ensure((size_t)max_grid * IVF_QG * a.cap * sizeof(u64));
     a.cand = ix->cand.as<u64>();
-    const bool timing = ix->timing.load();
+    const bool timing = first_pass && ix->timing.load();  // (re-search rounds are not the timed scan)
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (timing) {
         HIP_CHECK(hipEventCreate(&e0));
         HIP_CHECK(hipEventCreate(&e1));
         HIP_CHECK(hipEventRecord(e0, st));
+    }
+    // lists probed by many queries: the MFMA screen over their pages (unseeded; every workgroup
+    // appends its best Kp per query to the query's list, which the refine cuts to Kp)
+    if (!mscans.empty()) {
+        ix->mqtile.ensure((size_t)MFMA_QB * ix->dpad * 2);
+        ix->mcand.ensure((size_t)ix->num_cu * MFMA_QB * MFMA_CAP * sizeof(u64));
+        int packed_q0 = -1;
+        for (const MScan& m : mscans) {
+            const int* qidx = ix->mqidx.as<int>() + m.q0;
+            if (m.q0 != packed_q0) {  // the block's query tile (and its queries' bf16 margin in qinfo)
+                HIP_CHECK(launch_pack_qtile_split(ix->dtype, q_dev, qidx, m.nqb, ix->d, ix->dpad,
+                                                  ix->mqtile.as<uint8_t>(), ix->qinfo.as<float>(), st));
+                packed_q0 = m.q0;
+            }
+            ScreenArgs sa{};
+            sa.corpus = ix->data;
+            sa.tiles = m.np;
+            sa.n_valid = std::min<int64_t>((int64_t)m.np * TR, ix->list_n[m.l] - (int64_t)m.p0 * TR);
+            sa.dpad = ix->dpad;
+            sa.d = ix->d;
+            sa.metric = ix->metric;
+            sa.sqn = ix->sqn;
+            sa.Kp = Kp;
+            sa.cap = MFMA_CAP;
+            sa.cand = ix->mcand.as<u64>();
+            sa.G = m.G;
+            sa.glist = ix->glist.as<u64>();
+            sa.gcnt = ix->gcnt.as<int>();
+            sa.lcap = lcap;
+            sa.tile_map = ix->d_list_pages.as<int>() + ix->page_off_h[m.l] + m.p0;
+            sa.qmap = qidx;
+            HIP_CHECK(launch_screen_mfma_mapped(ix->dtype, sa, ix->mqtile.as<uint8_t>(), m.nqb, st));
+        }
     }
     size_t off = 0;
     if (dyn) {
@@ -364,23 +447,49 @@ void search_locked(vs_ivf* ix, const float* q_dev, int64_t nq, int k, int nprobe
         return;
     }
     nprobe = std::min(nprobe, ix->nlist);
-    const int Kp = screen_depth(k);
+    static const int kp_min = getenv("VS_IVF_KP_MIN") ? atoi(getenv("VS_IVF_KP_MIN")) : 0;  // experiments
+    const int Kp = std::max(screen_depth(k), std::min(kp_min, KP_MAX));
     ix->cert.ensure((size_t)nq * sizeof(int));
-    search_core(ix, q_dev, nq, k, nprobe, Kp, D, I, S64, ix->cert.as<int>(), st);
+    search_core(ix, q_dev, nq, k, nprobe, Kp, D, I, S64, ix->cert.as<int>(), st, true);
     ix->cert_h.resize((size_t)nq);
     HIP_CHECK(hipMemcpyAsync(ix->cert_h.data(), ix->cert.p, (size_t)nq * sizeof(int), hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));
-    std::vector<int> cert = ix->cert_h;
-    for (int64_t qi = 0; qi < nq; ++qi) {
-        int Kr = Kp;
-        while (!cert[qi]) {
-            if (Kr >= KP_MAX) throw VsError(VS_ERR_UNCERTIFIED, "exactness certificate failed at maximum screening depth");
-            Kr = std::min(Kr * 4, KP_MAX);
-            search_core(ix, q_dev + qi * ix->d, 1, k, nprobe, Kr, D ? D + qi * k : nullptr, I + qi * k,
-                        S64 ? S64 + qi * k : nullptr, ix->cert.as<int>(), st);
-            HIP_CHECK(hipMemcpyAsync(&cert[qi], ix->cert.p, sizeof(int), hipMemcpyDeviceToHost, st));
-            HIP_CHECK(hipStreamSynchronize(st));
+    std::vector<int> fail;
+    for (int64_t qi = 0; qi < nq; ++qi)
+        if (!ix->cert_h[qi]) fail.push_back((int)qi);
+    ix->last_mfma_lists = ix->cur_mfma_lists;
+    ix->last_uncert = (int)fail.size();
+    // uncertified queries: re-searched together, 4x deeper per round (their probed lists scanned
+    // once per round for all of them, on the MFMA screen where that pays)
+    const size_t ko = (size_t)k;
+    int Kr = Kp;
+    while (!fail.empty()) {
+        if (Kr >= KP_MAX) throw VsError(VS_ERR_UNCERTIFIED, "exactness certificate failed at maximum screening depth");
+        Kr = std::min(Kr * 4, KP_MAX);
+        const int nf = (int)fail.size();
+        ix->rq.ensure((size_t)nf * ix->d * sizeof(float));
+        ix->rI.ensure((size_t)nf * ko * sizeof(int64_t));
+        if (D) ix->rD.ensure((size_t)nf * ko * sizeof(float));
+        if (S64) ix->rS.ensure((size_t)nf * ko * sizeof(double));
+        for (int j = 0; j < nf; ++j)
+            HIP_CHECK(hipMemcpyAsync(ix->rq.as<float>() + (size_t)j * ix->d, q_dev + (size_t)fail[j] * ix->d,
+                                     (size_t)ix->d * sizeof(float), hipMemcpyDeviceToDevice, st));
+        search_core(ix, ix->rq.as<float>(), nf, k, nprobe, Kr, D ? ix->rD.as<float>() : nullptr, ix->rI.as<int64_t>(),
+                    S64 ? ix->rS.as<double>() : nullptr, ix->cert.as<int>(), st, false);
+        for (int j = 0; j < nf; ++j) {
+            const size_t o = (size_t)fail[j] * ko, r = (size_t)j * ko;
+            HIP_CHECK(hipMemcpyAsync(I + o, ix->rI.as<int64_t>() + r, ko * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
+            if (D) HIP_CHECK(hipMemcpyAsync(D + o, ix->rD.as<float>() + r, ko * sizeof(float), hipMemcpyDeviceToDevice, st));
+            if (S64)
+                HIP_CHECK(hipMemcpyAsync(S64 + o, ix->rS.as<double>() + r, ko * sizeof(double), hipMemcpyDeviceToDevice, st));
         }
+        ix->cert_h.resize((size_t)nf);
+        HIP_CHECK(hipMemcpyAsync(ix->cert_h.data(), ix->cert.p, (size_t)nf * sizeof(int), hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+        std::vector<int> still;
+        for (int j = 0; j < nf; ++j)
+            if (!ix->cert_h[j]) still.push_back(fail[j]);
+        fail.swap(still);
     }
 }
 
@@ -644,6 +753,24 @@ int vs_ivf_set_timing(vs_ivf* ix, int enable) {
     return guarded([&] {
         check_ivf(ix);
         ix->timing.store(enable != 0);
+    });
+}
+
+int vs_ivf_set_scan(vs_ivf* ix, int mode) {
+    return guarded([&] {
+        check_ivf(ix);
+        if (mode != VS_IVF_SCAN_AUTO && mode != VS_IVF_SCAN_GEMV && mode != VS_IVF_SCAN_MFMA)
+            throw VsError(VS_ERR_ARG, "unknown IVF scan mode");
+        std::lock_guard<std::mutex> g(ix->search_mtx);
+        ix->scan_mode = mode;
+    });
+}
+
+int vs_ivf_last_search_stats(const vs_ivf* ix, int* mfma_lists, int* uncertified) {
+    return guarded([&] {
+        check_ivf(ix);
+        if (mfma_lists) *mfma_lists = ix->last_mfma_lists;
+        if (uncertified) *uncertified = ix->last_uncert;
     });
 }
 

@@ -440,12 +440,14 @@ __global__ void __launch_bounds__(256) k_gather_rows(const uint8_t* __restrict__
 // query packing
 // ------------------------------------------------------------------------------------------------
 // MFMA query tile [nks][256][32] in the corpus dtype; qinfo = (||q_hat||, ||q_hat - q||) in fp64,
-// rounded up to fp32.
+// rounded up to fp32.  qidx (IVF list scans): tile row r is query qidx[r] of q, and its qinfo goes
+// to qinfo[2 qidx[r]] as the max with what is there (the fp32 scan's values: a bound for both).
 template <int DT>
 __global__ void __launch_bounds__(256) k_pack_qtile(const float* __restrict__ q, int nqb, int d, int dpad,
                                                      uint8_t* __restrict__ qt, float* __restrict__ qinfo,
                                                      int* __restrict__ gcnt, u64* __restrict__ drop,
-                                                     int* __restrict__ fails, const int* __restrict__ gate) {
+                                                     int* __restrict__ fails, const int* __restrict__ gate,
+                                                     const int* __restrict__ qidx) {
     if (gate && *gate == 0) return;  // device fallback round with nothing to re-search
     const int lane = threadIdx.x & 63;
     const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -454,9 +456,10 @@ __global__ void __launch_bounds__(256) k_pack_qtile(const float* __restrict__ q,
     if (gcnt && lane == 0) gcnt[r] = 0;  // survivor-list lengths of the screen that follows ...
     if (drop && lane == 0) drop[r] = 0ull;  // ... and its workgroups' drop bounds
     double n2 = 0.0, e2 = 0.0;
+    const int64_t qr = (qidx && r < nqb) ? (int64_t)qidx[r] : (int64_t)r;
 #pragma unroll 8
     for (int i = lane; i < dpad; i += 64) {
-        float v = (r < nqb && i < d) ? q[(int64_t)r * d + i] : 0.0f;
+        float v = (r < nqb && i < d) ? q[qr * d + i] : 0.0f;
         float st = round_store<DT>(v, qt + (int64_t)(i >> 5) * MFMA_QB * 64 + (int64_t)r * 64 + (i & 31) * 2);
         n2 += (double)st * st;
         double df = (double)st - (double)v;
@@ -468,8 +471,54 @@ __global__ void __launch_bounds__(256) k_pack_qtile(const float* __restrict__ q,
         e2 += __shfl_xor(e2, s, 64);
     }
     if (lane == 0 && r < nqb) {
-        qinfo[2 * r] = (float)(sqrt(n2) * (1.0 + 1e-6)) + 1e-30f;
-        qinfo[2 * r + 1] = (float)(sqrt(e2) * (1.0 + 1e-6));
+        const float nq = (float)(sqrt(n2) * (1.0 + 1e-6)) + 1e-30f, eq = (float)(sqrt(e2) * (1.0 + 1e-6));
+        if (qidx) {
+            qinfo[2 * qr] = fmaxf(qinfo[2 * qr], nq);
+            qinfo[2 * qr + 1] = fmaxf(qinfo[2 * qr + 1], eq);
+        } else {
+            qinfo[2 * r] = nq;
+            qinfo[2 * r + 1] = eq;
+        }
+    }
+}
+
+// Split query tile of the mapped (IVF list) screen: up to 128 queries, query j = wn*64 + jj (jj < 64)
+// as hi = round(q) in tile row wn*128 + (jj/16)*32 + jj%16 and lo = round(q - hi) 16 rows further,
+// so the screen sums two MFMA accumulators per query.  Query j is q[qidx[j]]; its qinfo entry
+// becomes the max of what is there and (||hi|| + ||lo||, ||q - hi - lo||) (fp64, rounded up).
+template <int DT>
+__global__ void __launch_bounds__(256) k_pack_qtile_split(const float* __restrict__ q, const int* __restrict__ qidx,
+                                                           int nqb, int d, int dpad, uint8_t* __restrict__ qt,
+                                                           float* __restrict__ qinfo) {
+    const int lane = threadIdx.x & 63;
+    const int c = blockIdx.x * 4 + (threadIdx.x >> 6);  // tile row
+    if (c >= MFMA_QB) return;
+    const int wn = c >> 7, ni = (c >> 4) & 7, part = ni & 1;
+    const int j = wn * 64 + (ni >> 1) * 16 + (c & 15);
+    const bool real = j < nqb;
+    const int64_t qr = real ? (int64_t)qidx[j] : 0;
+    double h2 = 0.0, l2 = 0.0, e2 = 0.0;
+#pragma unroll 8
+    for (int i = lane; i < dpad; i += 64) {
+        const float v = (real && i < d) ? q[qr * d + i] : 0.0f;
+        const float hi = round_only<DT>(v);
+        const float lo = round_only<DT>(v - hi);  // v - hi is exact in fp32
+        round_store<DT>(part ? lo : hi, qt + (int64_t)(i >> 5) * MFMA_QB * 64 + (int64_t)c * 64 + (i & 31) * 2);
+        h2 += (double)hi * hi;
+        l2 += (double)lo * lo;
+        const double df = (double)v - (double)hi - (double)lo;
+        e2 += df * df;
+    }
+#pragma unroll
+    for (int sh = 32; sh > 0; sh >>= 1) {
+        h2 += __shfl_xor(h2, sh, 64);
+        l2 += __shfl_xor(l2, sh, 64);
+        e2 += __shfl_xor(e2, sh, 64);
+    }
+    if (lane == 0 && real && part == 0) {
+        const float nq = (float)((sqrt(h2) + sqrt(l2)) * (1.0 + 1e-6)) + 1e-30f, eq = (float)(sqrt(e2) * (1.0 + 1e-6));
+        qinfo[2 * qr] = fmaxf(qinfo[2 * qr], nq);
+        qinfo[2 * qr + 1] = fmaxf(qinfo[2 * qr + 1], eq);
     }
 }
 
@@ -666,6 +715,8 @@ constexpr int MF_ROWX = 2 * 256 * 4;   // per-row side data of two tiles (int8: 
 constexpr int MF_LDS = MF_SLOTS * MF_SLOT + 256 * 8 + 256 * 4 + 256 * 4 + 16 + MF_POOL * 8 + MF_POOL * 4 + MF_SX + MF_QFAC +
                        MF_ROWX;
 static_assert(MF_LDS <= 160 * 1024, "LDS budget");
+constexpr int MF_LDS_MAP = MF_LDS + MFMA_MAP_TILES * 4;  // mapped screen: + the workgroup's page table
+static_assert(MF_LDS_MAP <= 160 * 1024, "LDS budget (mapped screen)");
 
 typedef __attribute__((address_space(3))) uint8_t* lds_u8_t;
 
@@ -798,7 +849,9 @@ __device__ __forceinline__ void mf_wave_compact(u64* __restrict__ buf, int n, in
 // Keys: bf16/f16 -> the fp32 MFMA score (L2: 2 x.q - ||x||^2); int8 -> the upper bound
 // s_x t_q <c_x, c_q> + ||e_x|| ||q|| of the true inner product (the query-side error term is
 // uniform over rows and sits in the refine's margin).
-template <int DT, int METRIC, bool SEED>
+// MAP: the IVF list scan -- logical tile t of the launch is page a.tile_map[t] of a page pool (the
+// workgroup's pages staged in LDS), keys carry storage slots, survivors go to glist row a.qmap[q].
+template <int DT, int METRIC, bool SEED, bool MAP = false>
 __device__ __forceinline__ void screen_mfma(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
     constexpr bool I8 = DT == DT_I8;
     static_assert(!I8 || METRIC == METRIC_IP, "the int8 screen serves inner-product indexes");
@@ -829,7 +882,19 @@ __device__ __forceinline__ void screen_mfma(ScreenArgs a, const uint8_t* __restr
         t0 = a.seed_acc ? (int)((int64_t)a.tiles * blk / a.G) : blk * a.tile_stride;
         t1 = t0 + 1 <= a.tiles ? t0 + 1 : a.tiles;
     }
-    const bool reuse = !SEED && a.seed_acc != nullptr && t1 > t0;
+    static_assert(!(MAP && SEED), "the mapped screen is unseeded");
+    int* tmap = (int*)(smem + MF_LDS);  // MAP: page of logical tile tbase + i
+    const int tbase = t0;
+    if constexpr (MAP) {
+        for (int i = tid; i < t1 - t0; i += MF_THREADS) tmap[i] = a.tile_map[t0 + i];
+        __syncthreads();
+    }
+    // storage tile of logical tile t
+    auto phys = [&](int t) -> int64_t {
+        if constexpr (MAP) return (int64_t)tmap[t - tbase];
+        else return (int64_t)t;
+    };
+    const bool reuse = !MAP && !SEED && a.seed_acc != nullptr && t1 > t0;
     const int tseed = t0;
     if (reuse) ++t0;
     if (tid < 256) {
@@ -854,8 +919,8 @@ __device__ __forceinline__ void screen_mfma(ScreenArgs a, const uint8_t* __restr
     constexpr int NLW = 4;
     // K-step ks of tile ti: int8 -> chunk ks (64 B per row); bf16 / f16 -> half (ks & 1) of chunk ks / 2
     auto kblock = [&](int ti, int ks) -> const uint8_t* {
-        if constexpr (I8) return a.corpus + (int64_t)ti * tbytes + (int64_t)ks * 16384;
-        else return a.corpus + (int64_t)ti * tbytes + (int64_t)(ks >> 1) * (TR * CHB) + (ks & 1) * 64;
+        if constexpr (I8) return a.corpus + phys(ti) * tbytes + (int64_t)ks * 16384;
+        else return a.corpus + phys(ti) * tbytes + (int64_t)(ks >> 1) * (TR * CHB) + (ks & 1) * 64;
     };
     const int S = (t1 - t0) * nks;
     u64* cand = a.cand + (size_t)blk * MFMA_QB * a.cap;
@@ -879,7 +944,7 @@ __device__ __forceinline__ void screen_mfma(ScreenArgs a, const uint8_t* __restr
     const uint32_t* rowsrc = I8 ? a.rsb : (const uint32_t*)a.sqn;
     auto rowx_issue = [&](int tile) {
         const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_addr((const uint8_t*)(rowx + (tile & 1) * TR)));
-        glds16(rowsrc + (int64_t)tile * TR + lane * 4, dst);
+        glds16(rowsrc + phys(tile) * TR + lane * 4, dst);
     };
     // the DMA for the epilogue at loop step j (if j ends a tile)
     auto rowx_rule = [&](int j) {
@@ -924,7 +989,8 @@ __device__ __forceinline__ void screen_mfma(ScreenArgs a, const uint8_t* __restr
         }
         int olane;
         asm volatile("v_mov_b32 %0, %1" : "=v"(olane) : "v"(lane));
-        const int64_t rowbase = (int64_t)ti * TR;
+        const int64_t rowbase = (int64_t)ti * TR;  // logical (the n_valid mask)
+        const int64_t idbase = MAP ? phys(ti) * TR : rowbase;  // key ids: storage slots
         const int rid0 = wm * 64 + (olane >> 4) * 4;  // + mi*16 + r
         const int q0 = wn * 128 + (olane & 15);        // + ni*16
         // padding rows of the shard's last tile never qualify: NaN, not -inf (fmaxf skips it and
@@ -955,9 +1021,12 @@ __device__ __forceinline__ void screen_mfma(ScreenArgs a, const uint8_t* __restr
                 }
             }
         }
+        // MAP: the query tile holds (hi, lo) bf16/f16 parts of each query in column pairs (ni even /
+        // odd), so a query's screen score is the sum of two accumulators (near-fp32 precision)
+        constexpr int NCOL = MAP ? 4 : 8;
 #pragma unroll
-        for (int ni = 0; ni < 8; ++ni) {
-            const int q = q0 + ni * 16;
+        for (int ni = 0; ni < NCOL; ++ni) {
+            const int q = MAP ? wn * 64 + ni * 16 + (olane & 15) : q0 + ni * 16;
             // int8: values in the query's scaled domain v = s_x <c_x, c_q> + beta_x ||q|| / t_q (one
             // convert, one multiply, one fma per value, in packed pairs); the key is t_q * v
             float tq = 1.0f;
@@ -983,7 +1052,7 @@ __device__ __forceinline__ void screen_mfma(ScreenArgs a, const uint8_t* __restr
                 for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        float sc = acc[mi][ni][r];
+                        float sc = MAP ? acc[mi][2 * ni][r] + acc[mi][2 * ni + 1][r] : acc[mi][ni][r];
                         if constexpr (METRIC == METRIC_L2) sc = 2.0f * sc - sq[mi][r];
                         v[mi][r] = sc;
                     }
@@ -1036,7 +1105,7 @@ __device__ __forceinline__ void screen_mfma(ScreenArgs a, const uint8_t* __restr
                         const int j = __builtin_ctz(mh);
                         mh &= mh - 1u;
                         const int bit = 8 * h + j;
-                        const u64 key = mk_key(sx[j], (uint32_t)(rowbase + rid0 + (bit >> 2) * 16 + (bit & 3)));
+                        const u64 key = mk_key(sx[j], (uint32_t)(idbase + rid0 + (bit >> 2) * 16 + (bit & 3)));
                         if (key <= tk) continue;  // score == threshold and not ahead of it by id
                         if (wid < 4) {
                             const int slot = atomicAdd(&flag[1], 1);
@@ -1156,10 +1225,11 @@ __device__ __forceinline__ void screen_mfma(ScreenArgs a, const uint8_t* __restr
             n = a.Kp;
         }
         if (n == 0) continue;
+        const int qg = MAP ? a.qmap[q] : q;
         int off = 0;
-        if (lane == 0) off = atomicAdd(&a.gcnt[q], n);
+        if (lane == 0) off = atomicAdd(&a.gcnt[qg], n);
         off = __shfl(off, 0, 64);
-        u64* dst = a.glist + (size_t)q * a.lcap + off;
+        u64* dst = a.glist + (size_t)qg * a.lcap + off;
         for (int j = lane; j < n; j += 64) dst[j] = cand[(size_t)q * a.cap + j];
     }
 }
@@ -1181,6 +1251,11 @@ template <int DT, int METRIC>
 __global__ void __launch_bounds__(512, 2) k_screen_mfma_redo(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
     if (*a.gate == 0) return;
     screen_mfma<DT, METRIC, false>(a, qt, nqb);
+}
+// the IVF list scan's screen (MAP): its own symbol
+template <int DT, int METRIC>
+__global__ void __launch_bounds__(512, 2) k_screen_mfma_mapped(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
+    screen_mfma<DT, METRIC, false, true>(a, qt, nqb);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2444,13 +2519,25 @@ hipError_t launch_gather_rows(int dt, const uint8_t* data, const int64_t* ids, i
 }
 
 hipError_t launch_pack_qtile(int dt, const float* q, int nqb, int d, int dpad, uint8_t* qt, float* qinfo, int* gcnt,
-                             u64* drop, hipStream_t st, int* fails, const int* gate) {
+                             u64* drop, hipStream_t st, int* fails, const int* gate, const int* qidx) {
     if (dt == DT_BF16)
         hipLaunchKernelGGL(k_pack_qtile<DT_BF16>, dim3(MFMA_QB / 4), dim3(256), 0, st, q, nqb, d, dpad, qt, qinfo,
-                           gcnt, drop, fails, gate);
+                           gcnt, drop, fails, gate, qidx);
     else
         hipLaunchKernelGGL(k_pack_qtile<DT_F16>, dim3(MFMA_QB / 4), dim3(256), 0, st, q, nqb, d, dpad, qt, qinfo,
-                           gcnt, drop, fails, gate);
+                           gcnt, drop, fails, gate, qidx);
+    return hipGetLastError();
+}
+
+hipError_t launch_pack_qtile_split(int dt, const float* q, const int* qidx, int nqb, int d, int dpad, uint8_t* qt,
+                                   float* qinfo, hipStream_t st) {
+    if (nqb <= 0 || nqb > MFMA_QB / 2 || !qidx) return hipErrorInvalidValue;
+    if (dt == DT_BF16)
+        hipLaunchKernelGGL(k_pack_qtile_split<DT_BF16>, dim3(MFMA_QB / 4), dim3(256), 0, st, q, qidx, nqb, d, dpad, qt, qinfo);
+    else if (dt == DT_F16)
+        hipLaunchKernelGGL(k_pack_qtile_split<DT_F16>, dim3(MFMA_QB / 4), dim3(256), 0, st, q, qidx, nqb, d, dpad, qt, qinfo);
+    else
+        return hipErrorInvalidValue;
     return hipGetLastError();
 }
 
@@ -2520,6 +2607,35 @@ static hipError_t launch_mfma_dt(int dt, const ScreenArgs& a, const uint8_t* qt,
 }
 hipError_t launch_screen_mfma(int dt, const ScreenArgs& a, const uint8_t* qt, int nqb, hipStream_t st) {
     return launch_mfma_dt<false>(dt, a, qt, nqb, st);
+}
+
+template <int DT, int METRIC>
+static void launch_mapped_one(const ScreenArgs& a, const uint8_t* qt, int nqb, hipStream_t st) {
+    static bool attr_set = false;  // benign race: idempotent attribute
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)k_screen_mfma_mapped<DT, METRIC>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, MF_LDS_MAP);
+        attr_set = true;
+    }
+    hipLaunchKernelGGL((k_screen_mfma_mapped<DT, METRIC>), dim3(a.G), dim3(MF_THREADS), MF_LDS_MAP, st, a, qt, nqb);
+}
+hipError_t launch_screen_mfma_mapped(int dt, const ScreenArgs& a, const uint8_t* qt, int nqb, hipStream_t st) {
+    // the launch contract the kernel relies on (checked here, on the host, before any launch)
+    if (!a.tile_map || !a.qmap || a.thr0 || a.seed_acc || a.tile_stride != 0 || a.gate || a.G <= 0 || a.tiles <= 0 ||
+        nqb <= 0 || nqb > MFMA_QB / 2 || a.Kp > MFMA_KP_MAX || a.cap != MFMA_CAP || a.lcap < a.Kp ||
+        (int64_t)a.n_valid > (int64_t)a.tiles * TR || (int64_t)a.n_valid <= (int64_t)(a.tiles - 1) * TR ||
+        ((int64_t)a.tiles + a.G - 1) / a.G > MFMA_MAP_TILES)
+        return hipErrorInvalidValue;
+    if (dt == DT_BF16) {
+        if (a.metric == METRIC_IP) launch_mapped_one<DT_BF16, METRIC_IP>(a, qt, nqb, st);
+        else launch_mapped_one<DT_BF16, METRIC_L2>(a, qt, nqb, st);
+    } else if (dt == DT_F16) {
+        if (a.metric == METRIC_IP) launch_mapped_one<DT_F16, METRIC_IP>(a, qt, nqb, st);
+        else launch_mapped_one<DT_F16, METRIC_L2>(a, qt, nqb, st);
+    } else {
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
 }
 
 template <int DT>

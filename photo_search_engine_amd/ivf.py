@@ -154,6 +154,26 @@ class IVFFlatIndex:
     def reset(self) -> None:
         check(self._L.vs_ivf_reset(self._h))
 
+    _SCANS = {"auto": 0, "gemv": 1, "mfma": 2}
+
+    def set_scan(self, mode: str) -> None:
+        """List-scan kernels: "auto" (cost model), "gemv" (never MFMA), "mfma" (every list probed by
+        more than one query, bf16/f16).  Results are identical in every mode."""
+        if mode not in self._SCANS:
+            raise ValueError(f"scan mode must be one of {sorted(self._SCANS)}")
+        check(self._L.vs_ivf_set_scan(self._h, self._SCANS[mode]))
+
+    def last_search_stats(self) -> Tuple[int, int]:
+        """First pass of the last search: (MFMA list scans, queries re-searched for their certificate)."""
+        m, u = ctypes.c_int(0), ctypes.c_int(0)
+        check(self._L.vs_ivf_last_search_stats(self._h, ctypes.byref(m), ctypes.byref(u)))
+        return int(m.value), int(u.value)
+
+    @property
+    def last_mfma_lists(self) -> int:
+        """List scans the last search's first pass ran on the MFMA screen."""
+        return self.last_search_stats()[0]
+
     # -- measurement ---------------------------------------------------------------------------
     def set_timing(self, enable: bool) -> None:
         check(self._L.vs_ivf_set_timing(self._h, int(bool(enable))))

@@ -134,3 +134,51 @@ def test_ivf_train_kmeans_then_exact(IVF):
     ix.add(x)
     q = O.synth_rows(O.SEED_QUERIES, 0, 17, d, True, "f32")
     _check(ix, x, c, q, 12, 4, "l2")
+
+
+@pytest.mark.parametrize("metric,dtype", [("ip", "bf16"), ("l2", "bf16"), ("ip", "f16")])
+def test_ivf_mfma_list_scan_matches_oracle(IVF, metric, dtype):
+    # lists probed by many queries scanned by the MFMA screen over their pages: 2 lists of ~100k
+    # rows (~390 pages: > 1 page per workgroup, a partial last page), 300 queries probing both
+    # (split query tiles of 128 + 128 + 44); identical to the oracle and to the GEMV scan, and no
+    # query needs a re-search (the (hi, lo) query split keeps the screen near fp32 precision)
+    d, N, nlist, nq, k = 64, 200_000, 2, 300, 10
+    x = O.synth_rows(O.SEED_CORPUS, 0, N, d, True, dtype)
+    ix = IVF(d, nlist, metric, dtype)
+    ix.set_centroids(IO.sample_centroids(x, nlist, 4))
+    ix.add_synthetic(O.SEED_CORPUS, 0, N, True)
+    q = O.synth_rows(O.SEED_QUERIES, 0, nq, d, True, "f32")
+    ix.set_scan("mfma")
+    D, I, _ = _check(ix, x, ix.centroids(), q, k, 2, metric)
+    assert ix.last_search_stats() == (6, 0)  # 2 lists x 3 query blocks, every query certified
+    ix.set_scan("gemv")
+    D2, I2 = ix.search(q, k, 2)
+    assert ix.last_mfma_lists == 0
+    np.testing.assert_array_equal(I2, I)
+    np.testing.assert_array_equal(D2, D)
+    ix.close()
+
+
+def test_ivf_mfma_skewed_lists_mixed_scans(IVF):
+    # Zipf-like list sizes: the head lists take the MFMA scan, the tail the GEMV items, in one
+    # search; single queries (nql = 1) always stay on the GEMV scan
+    rng = np.random.default_rng(5)
+    d, nlist = 96, 24
+    c = rng.standard_normal((nlist, d)).astype(np.float32)
+    c /= np.linalg.norm(c, axis=1, keepdims=True)
+    w = 1.0 / np.arange(1, nlist + 1) ** 1.3
+    cid = rng.choice(nlist, size=150_000, p=w / w.sum())
+    x = c[cid] + 0.6 * rng.standard_normal((cid.size, d)).astype(np.float32)
+    x /= np.linalg.norm(x, axis=1, keepdims=True)
+    ix = IVF(d, nlist, "ip", "bf16")
+    ix.set_centroids(c)
+    ix.add(x)
+    x_st = O.round_dtype(x, "bf16")
+    qc = rng.choice(nlist, size=120, p=w / w.sum())
+    q = c[qc] + 0.6 * rng.standard_normal((qc.size, d)).astype(np.float32)
+    ix.set_scan("mfma")
+    _check(ix, x_st, ix.centroids(), q, 20, 3, "ip")
+    assert ix.last_mfma_lists > 0
+    _check(ix, x_st, ix.centroids(), q[:1], 20, 3, "ip")
+    assert ix.last_mfma_lists == 0
+    ix.close()
