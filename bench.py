@@ -493,7 +493,7 @@ def run_ivf(args):
     achieved = alg_bytes / (kavg * 1e-3) / 1e9
     sizes = ix.list_sizes()
     Ig = I.cpu().numpy()
-    mfma_lists, uncert = ix.last_search_stats()
+    mfma_lists, uncert, mfma_bytes, gemv_bytes = ix.last_search_detail()
     gemv_beside = None
     if args.ivf_scan == "auto" and mfma_lists > 0:  # the GEMV-only scan on the same batch, beside
         Sg0 = S.cpu().numpy()
@@ -600,6 +600,7 @@ def run_ivf(args):
                    "nprobe": nprobe, "list_rows_min_max": [int(sizes.min()), int(sizes.max())],
                    "list_rows_median": int(np.median(sizes)), "skew": args.skew,
                    "list_scan": args.ivf_scan, "mfma_list_scans": mfma_lists,
+                   "scan_bytes_read": {"mfma": mfma_bytes, "gemv": gemv_bytes},
                    "parallelism": "1 GPU"},
         "roofline": {
             "kernel": "k_ivf_scan",

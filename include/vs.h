@@ -208,13 +208,14 @@ int vs_ivf_timing_fetch(vs_ivf* ivf, float* ms, double* bytes_scanned, int cap);
  * probed by many queries with the MFMA screen over its pages (bf16/f16, once per 256 queries) when
  * a cost model says it beats re-reading it per 8 queries with the GEMV scan; _GEMV never does;
  * _MFMA does for every list probed by > 1 query (tests).  vs_ivf_last_search_stats reports the
- * first pass of the last search: its MFMA list scans and the queries its certificate rejected
- * (re-searched together, deeper; either pointer may be NULL). */
+ * first pass of the last search: its MFMA list scans, the queries its certificate rejected
+ * (re-searched together, deeper) and the page bytes the MFMA and the GEMV scans read, re-reads
+ * included (bytes_read[0], [1]); any pointer may be NULL. */
 #define VS_IVF_SCAN_AUTO 0
 #define VS_IVF_SCAN_GEMV 1
 #define VS_IVF_SCAN_MFMA 2
 int vs_ivf_set_scan(vs_ivf* ivf, int mode);
-int vs_ivf_last_search_stats(const vs_ivf* ivf, int* mfma_lists, int* uncertified);
+int vs_ivf_last_search_stats(const vs_ivf* ivf, int* mfma_lists, int* uncertified, double* bytes_read);
 
 /* ==== HNSW graph search ===================================================
  * Replaces the search of faiss.IndexHNSWFlat, which the reference builds for

@@ -196,8 +196,12 @@ struct ScreenArgs {
                              // query of the block failed its certificate), or null = always run
     const int* tile_map;     // mapped screen (IVF list scan): page of logical tile t; keys carry
                              // storage slots page * TR + row, n_valid counts the list's rows
-    const int* qmap;         // mapped screen: glist / gcnt row of block query q
+    const int* qmap;         // mapped screen: glist / gcnt row of a query (the workgroup's slice below)
+    const int* wg_desc;      // mapped screen: per workgroup MAP_DESC ints {tile_map offset of its
+                             // first tile, tiles, logical index of the first tile in its list
+                             // segment, rows of that segment, query tile index, qmap offset, queries}
 };
+constexpr int MAP_DESC = 8;
 constexpr int MFMA_MAP_TILES = 256;  // mapped screen: logical tiles per workgroup (its LDS page table)
 int gemv_blocks_per_cu(int dt, int nqpad);  // resident k_screen_gemv blocks per CU (occupancy API)
 
@@ -226,10 +230,14 @@ hipError_t launch_pack_qf32(const float* q, int nqb, int nqpad, int d, int dpad,
                             int* fails = nullptr);
 
 hipError_t launch_screen_mfma(int dt, const ScreenArgs& a, const uint8_t* qt, int nqb, hipStream_t st);
-// the same screen over the pages a.tile_map lists (bf16 / f16, unseeded, a.Kp <= MFMA_KP_MAX,
-// at most MFMA_MAP_TILES tiles per workgroup), on a split query tile of <= 128 queries
-// (launch_pack_qtile_split); survivors appended to glist rows a.qmap[q]
-hipError_t launch_screen_mfma_mapped(int dt, const ScreenArgs& a, const uint8_t* qt, int nqb, hipStream_t st);
+// the same screen over pages of a page pool (IVF lists; bf16 / f16, unseeded, a.Kp <= MFMA_KP_MAX):
+// a.G workgroups, each with its own descriptor (a.wg_desc): <= MFMA_MAP_TILES pages of one list
+// (a.tile_map), one split query tile of <= 128 queries (qt + index * MFMA_QB * dpad * 2, made by
+// launch_pack_qtile_split); survivors appended to glist rows a.qmap[...].  Descriptors are
+// validated on the host (check_map_desc) before the launch.
+hipError_t launch_screen_mfma_mapped(int dt, const ScreenArgs& a, const uint8_t* qt, hipStream_t st);
+// host check of one descriptor against the launch (tile map length, query tiles, qmap length)
+bool check_map_desc(const int* desc, int64_t tmap_len, int n_qtiles, int64_t qmap_len);
 hipError_t launch_pack_qtile_split(int dt, const float* q, const int* qidx, int nqb, int d, int dpad, uint8_t* qt,
                                    float* qinfo, hipStream_t st);
 hipError_t launch_screen_gemv(int dt, const ScreenArgs& a, const float* qp, int nqb, int nqpad, hipStream_t st);

@@ -49,12 +49,14 @@ struct vs_ivf {
     // workspaces (add: exclusive lock; search / reconstruct: search_mtx)
     DevBuf tmp_rows, slots, assign_ids;
     DevBuf qdev, probes, items, qp, qinfo, cand, glist, gcnt, cert, outD, outI, rec, next_item;
-    DevBuf mqidx, mqtile, mcand;
+    DevBuf mqidx, mqtile, mcand, mdesc;
+    std::vector<int> desc_h;  // MFMA list scans: workgroup descriptors (MAP_DESC ints each)
     DevBuf rq, rD, rI, rS;  // re-search of uncertified queries: gathered queries and their outputs  // MFMA list scans: query indices, query tile, workspaces
     int scan_mode = VS_IVF_SCAN_AUTO;
     int last_mfma_lists = 0;  // first pass of the last search: MFMA list scans ...
     int last_uncert = 0;      // ... and queries its certificate rejected (re-searched deeper)
     int cur_mfma_lists = 0;
+    double last_bytes[2] = {0.0, 0.0}, cur_bytes[2] = {0.0, 0.0};  // pages read by the MFMA / GEMV scans
     std::vector<int64_t> probes_h;
     std::vector<int> cert_h;
     hipStream_t own = nullptr;
@@ -74,16 +76,15 @@ void check_ivf(const vs_ivf* ix) {
 }
 
 // A list probed by nql queries costs the GEMV scan ceil(nql / IVF_QG) reads of its pages (items of
-// <= 8 queries, each re-reading the list from HBM); the MFMA screen reads them once per 256
-// queries, one workgroup per CU over the list's pages.  Rates measured on MI355X: GEMV scan ~76%
-// of HBM peak on evenly probed lists, bf16 MFMA screen ~50% plus ~20 us of launches per scan.
+// <= 8 queries, each re-reading the list from HBM); the MFMA screen reads them once per 128
+// queries (split query tiles), in the one launch shared by all MFMA scans.  Rates measured on
+// MI355X: GEMV scan ~76% of HBM peak on evenly probed lists, bf16 MFMA screen ~50%.
 bool mfma_scan_pays(const vs_ivf* ix, int64_t np, int nql) {
     if (ix->dtype == DT_F32 || nql <= 1 || ix->scan_mode == VS_IVF_SCAN_GEMV) return false;
     if (ix->scan_mode == VS_IVF_SCAN_MFMA) return true;
-    const double B = (double)tile_bytes(ix->dpad, ix->dtype), cu = (double)ix->num_cu;
+    const double B = (double)tile_bytes(ix->dpad, ix->dtype);
     const double t_gemv = (double)((nql + IVF_QG - 1) / IVF_QG) * (double)np * B / 6.0e12;
-    const double waves = std::ceil((double)np / cu);  // tiles per workgroup
-    const double t_mfma = (double)((nql + MFMA_QB / 2 - 1) / (MFMA_QB / 2)) * (waves * cu * B / 4.0e12 + 20e-6);
+    const double t_mfma = (double)((nql + MFMA_QB / 2 - 1) / (MFMA_QB / 2)) * (double)np * B / 4.0e12;
     return t_mfma < t_gemv;
 }
 
@@ -224,6 +225,7 @@ void search_core(vs_ivf* ix, const float* q_dev, int64_t nq, int k, int nprobe, 
     HIP_CHECK(hipMemcpyAsync(ix->probes_h.data(), ix->probes.p, ix->probes_h.size() * sizeof(int64_t),
                              hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));
+    upload_csr(ix, st);  // page tables (and page_off_h) current
     // 2. work items (list, page range, <= IVF_QG queries), grouped by query-count class
     std::vector<std::vector<int>> lq((size_t)ix->nlist);
     for (int64_t q = 0; q < nq; ++q)
@@ -236,10 +238,11 @@ void search_core(vs_ivf* ix, const float* q_dev, int64_t nq, int k, int nprobe, 
     std::vector<int> cls_items[4];
     std::vector<int64_t> per_q((size_t)nq, 0);  // candidate keys each query's list can receive
     double bytes = 0.0;
-    // MFMA list scans: (list, first page, pages, query block offset into mq, queries, workgroups)
-    struct MScan { int l, p0, np, q0, nqb, G; };
+    // MFMA list scans: one split query tile (<= 128 queries, offset q0 into mq) over a list
+    struct MScan { int l, q0, nqb; };
     std::vector<MScan> mscans;
     std::vector<int> mq;  // query indices of every MFMA scan's block
+    int64_t mtiles = 0;   // pages all MFMA scans read
     const bool mfma_ok = Kp <= MFMA_KP_MAX;
     for (int l = 0; l < ix->nlist; ++l) {
         const int nql = (int)lq[l].size();
@@ -247,18 +250,11 @@ void search_core(vs_ivf* ix, const float* q_dev, int64_t nq, int k, int nprobe, 
         if (nql == 0 || np == 0) continue;
         bytes += (double)ix->list_n[l] * ix->d * ix->es;
         if (mfma_ok && mfma_scan_pays(ix, np, nql)) {
-            // segments of <= num_cu * MFMA_MAP_TILES pages (the workgroups' LDS page tables)
-            const int seg = ix->num_cu * MFMA_MAP_TILES;
             for (int b0 = 0; b0 < nql; b0 += MFMA_QB / 2) {  // split query tiles: 128 queries
                 const int nb = std::min(MFMA_QB / 2, nql - b0);
-                const int q0 = (int)mq.size();
+                mscans.push_back({l, (int)mq.size(), nb});
                 mq.insert(mq.end(), lq[l].begin() + b0, lq[l].begin() + b0 + nb);
-                for (int p0 = 0; p0 < np; p0 += seg) {
-                    const int nps = std::min(seg, np - p0);
-                    const int G = std::min(nps, ix->num_cu);
-                    mscans.push_back({l, p0, nps, q0, nb, G});
-                    for (int j = 0; j < nb; ++j) per_q[lq[l][b0 + j]] += (int64_t)G * Kp;
-                }
+                mtiles += np;
             }
             continue;
         }
@@ -278,12 +274,50 @@ void search_core(vs_ivf* ix, const float* q_dev, int64_t nq, int k, int nprobe, 
         }
     }
     // (algorithmic bytes above: every probed list read once; the GEMV scan re-reads a list per
-    // query group, the MFMA scan per 256-query block -- that extra traffic is not algorithmic)
+    // query group, the MFMA scan per 128-query block -- that extra traffic is not algorithmic)
+    // The MFMA scans run as ONE launch: each scan's pages are cut into workgroup chunks of about
+    // the same size (~2 workgroups per CU in all), heaviest chunks dispatched first, so small and
+    // large lists share the chip without per-list launches or an idle tail.
+    std::vector<int>& desc = ix->desc_h;
+    desc.clear();
+    if (!mscans.empty()) {
+        const int64_t chunk = std::min<int64_t>(MFMA_MAP_TILES, std::max<int64_t>(1, (mtiles + 2 * ix->num_cu - 1) /
+                                                                                         (2 * ix->num_cu)));
+        struct Wg { int nt, tm_off, t0, nvalid, qti, qoff, nqb; };
+        std::vector<Wg> wgs;
+        for (int si = 0; si < (int)mscans.size(); ++si) {
+            const MScan& m = mscans[si];
+            const int64_t np = (int64_t)ix->pages[m.l].size();
+            const int64_t G = (np + chunk - 1) / chunk;
+            for (int64_t i = 0; i < G; ++i) {
+                const int64_t t0 = np * i / G, t1 = np * (i + 1) / G;
+                wgs.push_back({(int)(t1 - t0), ix->page_off_h[m.l] + (int)t0, (int)t0, (int)ix->list_n[m.l], si, m.q0,
+                               m.nqb});
+            }
+            for (int j = 0; j < m.nqb; ++j) per_q[mq[m.q0 + j]] += G * Kp;
+        }
+        std::stable_sort(wgs.begin(), wgs.end(), [](const Wg& x, const Wg& y) { return x.nt > y.nt; });
+        const int64_t tmap_len = ix->page_off_h.back();
+        for (const Wg& w : wgs) {
+            const int g[MAP_DESC] = {w.tm_off, w.nt, w.t0, w.nvalid, w.qti, w.qoff, w.nqb, 0};
+            if (!check_map_desc(g, tmap_len, (int)mscans.size(), (int64_t)mq.size()))
+                throw VsError(VS_ERR_INTERNAL, "IVF MFMA scan: invalid workgroup descriptor");
+            desc.insert(desc.end(), g, g + MAP_DESC);
+        }
+    }
     int64_t max_keys = Kp;
     for (int64_t v : per_q) max_keys = std::max(max_keys, v);
     if (max_keys > (int64_t)1 << 30) throw VsError(VS_ERR_ARG, "IVF candidate lists exceed 2^30 keys per query");
     const int lcap = (int)max_keys;
     ix->cur_mfma_lists = (int)mscans.size();
+    {
+        const double B = (double)tile_bytes(ix->dpad, ix->dtype);
+        double gp = 0.0;
+        for (auto& v : cls_items)
+            for (size_t i = 0; i < v.size(); i += IVF_ITEM_INTS) gp += (double)(v[i + 2] - v[i + 1]);
+        ix->cur_bytes[0] = (double)mtiles * B;
+        ix->cur_bytes[1] = gp * B;
+    }
     size_t total_ints = 0;
     for (auto& v : cls_items) total_ints += v.size();
     ix->items.ensure(std::max<size_t>(total_ints, 1) * sizeof(int));
@@ -302,8 +336,10 @@ void search_core(vs_ivf* ix, const float* q_dev, int64_t nq, int k, int nprobe, 
         if (!mq.empty()) {
             ix->mqidx.ensure(mq.size() * sizeof(int));
             HIP_CHECK(hipMemcpyAsync(ix->mqidx.p, mq.data(), mq.size() * sizeof(int), hipMemcpyHostToDevice, st));
+            ix->mdesc.ensure(desc.size() * sizeof(int));
+            HIP_CHECK(hipMemcpyAsync(ix->mdesc.p, desc.data(), desc.size() * sizeof(int), hipMemcpyHostToDevice, st));
         }
-        upload_csr(ix, st);  // synchronises the stream, so `all` and `mq` may go out of scope
+        HIP_CHECK(hipStreamSynchronize(st));  // `all` and `mq` are temporaries
     }
     // 3. queries fp32 padded, ||q|| for the certificate
     ix->qp.ensure((size_t)nq * ix->dpad * sizeof(float));
@@ -342,35 +378,31 @@ void search_core(vs_ivf* ix, const float* q_dev, int64_t nq, int k, int nprobe, 
     // lists probed by many queries: the MFMA screen over their pages (unseeded; every workgroup
     // appends its best Kp per query to the query's list, which the refine cuts to Kp)
     if (!mscans.empty()) {
-        ix->mqtile.ensure((size_t)MFMA_QB * ix->dpad * 2);
-        ix->mcand.ensure((size_t)ix->num_cu * MFMA_QB * MFMA_CAP * sizeof(u64));
-        int packed_q0 = -1;
-        for (const MScan& m : mscans) {
-            const int* qidx = ix->mqidx.as<int>() + m.q0;
-            if (m.q0 != packed_q0) {  // the block's query tile (and its queries' bf16 margin in qinfo)
-                HIP_CHECK(launch_pack_qtile_split(ix->dtype, q_dev, qidx, m.nqb, ix->d, ix->dpad,
-                                                  ix->mqtile.as<uint8_t>(), ix->qinfo.as<float>(), st));
-                packed_q0 = m.q0;
-            }
-            ScreenArgs sa{};
-            sa.corpus = ix->data;
-            sa.tiles = m.np;
-            sa.n_valid = std::min<int64_t>((int64_t)m.np * TR, ix->list_n[m.l] - (int64_t)m.p0 * TR);
-            sa.dpad = ix->dpad;
-            sa.d = ix->d;
-            sa.metric = ix->metric;
-            sa.sqn = ix->sqn;
-            sa.Kp = Kp;
-            sa.cap = MFMA_CAP;
-            sa.cand = ix->mcand.as<u64>();
-            sa.G = m.G;
-            sa.glist = ix->glist.as<u64>();
-            sa.gcnt = ix->gcnt.as<int>();
-            sa.lcap = lcap;
-            sa.tile_map = ix->d_list_pages.as<int>() + ix->page_off_h[m.l] + m.p0;
-            sa.qmap = qidx;
-            HIP_CHECK(launch_screen_mfma_mapped(ix->dtype, sa, ix->mqtile.as<uint8_t>(), m.nqb, st));
-        }
+        const size_t qtb = (size_t)MFMA_QB * ix->dpad * 2;  // one query tile
+        ix->mqtile.ensure(qtb * mscans.size());
+        const int G = (int)(desc.size() / MAP_DESC);
+        ix->mcand.ensure((size_t)G * (MFMA_QB / 2) * MFMA_CAP * sizeof(u64));
+        for (size_t si = 0; si < mscans.size(); ++si)  // the query tiles (and their queries' margins in qinfo)
+            HIP_CHECK(launch_pack_qtile_split(ix->dtype, q_dev, ix->mqidx.as<int>() + mscans[si].q0, mscans[si].nqb,
+                                              ix->d, ix->dpad, ix->mqtile.as<uint8_t>() + si * qtb,
+                                              ix->qinfo.as<float>(), st));
+        ScreenArgs sa{};
+        sa.corpus = ix->data;
+        sa.dpad = ix->dpad;
+        sa.d = ix->d;
+        sa.metric = ix->metric;
+        sa.sqn = ix->sqn;
+        sa.Kp = Kp;
+        sa.cap = MFMA_CAP;
+        sa.cand = ix->mcand.as<u64>();
+        sa.G = G;
+        sa.glist = ix->glist.as<u64>();
+        sa.gcnt = ix->gcnt.as<int>();
+        sa.lcap = lcap;
+        sa.tile_map = ix->d_list_pages.as<int>();
+        sa.qmap = ix->mqidx.as<int>();
+        sa.wg_desc = ix->mdesc.as<int>();
+        HIP_CHECK(launch_screen_mfma_mapped(ix->dtype, sa, ix->mqtile.as<uint8_t>(), st));
     }
     size_t off = 0;
     if (dyn) {
@@ -458,6 +490,8 @@ void search_locked(vs_ivf* ix, const float* q_dev, int64_t nq, int k, int nprobe
     for (int64_t qi = 0; qi < nq; ++qi)
         if (!ix->cert_h[qi]) fail.push_back((int)qi);
     ix->last_mfma_lists = ix->cur_mfma_lists;
+    ix->last_bytes[0] = ix->cur_bytes[0];
+    ix->last_bytes[1] = ix->cur_bytes[1];
     ix->last_uncert = (int)fail.size();
     // uncertified queries: re-searched together, 4x deeper per round (their probed lists scanned
     // once per round for all of them, on the MFMA screen where that pays)
@@ -766,11 +800,15 @@ int vs_ivf_set_scan(vs_ivf* ix, int mode) {
     });
 }
 
-int vs_ivf_last_search_stats(const vs_ivf* ix, int* mfma_lists, int* uncertified) {
+int vs_ivf_last_search_stats(const vs_ivf* ix, int* mfma_lists, int* uncertified, double* bytes_read) {
     return guarded([&] {
         check_ivf(ix);
         if (mfma_lists) *mfma_lists = ix->last_mfma_lists;
         if (uncertified) *uncertified = ix->last_uncert;
+        if (bytes_read) {
+            bytes_read[0] = ix->last_bytes[0];
+            bytes_read[1] = ix->last_bytes[1];
+        }
     });
 }
 

@@ -884,11 +884,19 @@ __device__ __forceinline__ void screen_mfma(ScreenArgs a, const uint8_t* __restr
     }
     static_assert(!(MAP && SEED), "the mapped screen is unseeded");
     int* tmap = (int*)(smem + MF_LDS);  // MAP: page of logical tile tbase + i
-    const int tbase = t0;
-    if constexpr (MAP) {
-        for (int i = tid; i < t1 - t0; i += MF_THREADS) tmap[i] = a.tile_map[t0 + i];
+    if constexpr (MAP) {  // this workgroup's list segment, query tile and page table
+        const int* dsc = a.wg_desc + (size_t)blk * MAP_DESC;
+        const int tm_off = dsc[0], nt = dsc[1];
+        t0 = dsc[2];
+        t1 = t0 + nt;
+        a.n_valid = dsc[3];
+        qt += (size_t)dsc[4] * MFMA_QB * a.dpad * 2;
+        a.qmap += dsc[5];
+        nqb = dsc[6];
+        for (int i = tid; i < nt; i += MF_THREADS) tmap[i] = a.tile_map[tm_off + i];
         __syncthreads();
     }
+    const int tbase = t0;
     // storage tile of logical tile t
     auto phys = [&](int t) -> int64_t {
         if constexpr (MAP) return (int64_t)tmap[t - tbase];
@@ -923,7 +931,7 @@ __device__ __forceinline__ void screen_mfma(ScreenArgs a, const uint8_t* __restr
         else return a.corpus + phys(ti) * tbytes + (int64_t)(ks >> 1) * (TR * CHB) + (ks & 1) * 64;
     };
     const int S = (t1 - t0) * nks;
-    u64* cand = a.cand + (size_t)blk * MFMA_QB * a.cap;
+    u64* cand = a.cand + (size_t)blk * (MAP ? MFMA_QB / 2 : MFMA_QB) * a.cap;
     const int trigger = a.cap - TR;
     const uint32_t ring = lds_addr(smem);
     const int r16 = lane & 15;
@@ -2610,28 +2618,34 @@ hipError_t launch_screen_mfma(int dt, const ScreenArgs& a, const uint8_t* qt, in
 }
 
 template <int DT, int METRIC>
-static void launch_mapped_one(const ScreenArgs& a, const uint8_t* qt, int nqb, hipStream_t st) {
+static void launch_mapped_one(const ScreenArgs& a, const uint8_t* qt, hipStream_t st) {
     static bool attr_set = false;  // benign race: idempotent attribute
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void*)k_screen_mfma_mapped<DT, METRIC>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, MF_LDS_MAP);
         attr_set = true;
     }
-    hipLaunchKernelGGL((k_screen_mfma_mapped<DT, METRIC>), dim3(a.G), dim3(MF_THREADS), MF_LDS_MAP, st, a, qt, nqb);
+    hipLaunchKernelGGL((k_screen_mfma_mapped<DT, METRIC>), dim3(a.G), dim3(MF_THREADS), MF_LDS_MAP, st, a, qt, 0);
 }
-hipError_t launch_screen_mfma_mapped(int dt, const ScreenArgs& a, const uint8_t* qt, int nqb, hipStream_t st) {
-    // the launch contract the kernel relies on (checked here, on the host, before any launch)
-    if (!a.tile_map || !a.qmap || a.thr0 || a.seed_acc || a.tile_stride != 0 || a.gate || a.G <= 0 || a.tiles <= 0 ||
-        nqb <= 0 || nqb > MFMA_QB / 2 || a.Kp > MFMA_KP_MAX || a.cap != MFMA_CAP || a.lcap < a.Kp ||
-        (int64_t)a.n_valid > (int64_t)a.tiles * TR || (int64_t)a.n_valid <= (int64_t)(a.tiles - 1) * TR ||
-        ((int64_t)a.tiles + a.G - 1) / a.G > MFMA_MAP_TILES)
+bool check_map_desc(const int* g, int64_t tmap_len, int n_qtiles, int64_t qmap_len) {
+    const int64_t tm_off = g[0], nt = g[1], t0 = g[2], nvalid = g[3], qti = g[4], qoff = g[5], nqb = g[6];
+    // tiles [t0, t0 + nt) of a segment of nvalid rows, each holding at least one of its rows (the
+    // kernel masks rows >= nvalid); page-table, query-tile and qmap slices in range
+    return nt >= 1 && nt <= MFMA_MAP_TILES && tm_off >= 0 && tm_off + nt <= tmap_len && t0 >= 0 &&
+           (t0 + nt - 1) * TR < nvalid && nvalid <= INT32_MAX && qti >= 0 && qti < n_qtiles && nqb >= 1 &&
+           nqb <= MFMA_QB / 2 && qoff >= 0 && qoff + nqb <= qmap_len;
+}
+hipError_t launch_screen_mfma_mapped(int dt, const ScreenArgs& a, const uint8_t* qt, hipStream_t st) {
+    // the launch contract the kernel relies on (descriptors: check_map_desc, by the caller)
+    if (!a.tile_map || !a.qmap || !a.wg_desc || a.thr0 || a.seed_acc || a.tile_stride != 0 || a.gate || a.G <= 0 ||
+        a.Kp > MFMA_KP_MAX || a.cap != MFMA_CAP || a.lcap < a.Kp)
         return hipErrorInvalidValue;
     if (dt == DT_BF16) {
-        if (a.metric == METRIC_IP) launch_mapped_one<DT_BF16, METRIC_IP>(a, qt, nqb, st);
-        else launch_mapped_one<DT_BF16, METRIC_L2>(a, qt, nqb, st);
+        if (a.metric == METRIC_IP) launch_mapped_one<DT_BF16, METRIC_IP>(a, qt, st);
+        else launch_mapped_one<DT_BF16, METRIC_L2>(a, qt, st);
     } else if (dt == DT_F16) {
-        if (a.metric == METRIC_IP) launch_mapped_one<DT_F16, METRIC_IP>(a, qt, nqb, st);
-        else launch_mapped_one<DT_F16, METRIC_L2>(a, qt, nqb, st);
+        if (a.metric == METRIC_IP) launch_mapped_one<DT_F16, METRIC_IP>(a, qt, st);
+        else launch_mapped_one<DT_F16, METRIC_L2>(a, qt, st);
     } else {
         return hipErrorInvalidValue;
     }

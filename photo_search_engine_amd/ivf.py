@@ -165,9 +165,14 @@ class IVFFlatIndex:
 
     def last_search_stats(self) -> Tuple[int, int]:
         """First pass of the last search: (MFMA list scans, queries re-searched for their certificate)."""
+        return self.last_search_detail()[:2]
+
+    def last_search_detail(self) -> Tuple[int, int, float, float]:
+        """(MFMA list scans, re-searched queries, page bytes read by the MFMA scans, by the GEMV scan)."""
         m, u = ctypes.c_int(0), ctypes.c_int(0)
-        check(self._L.vs_ivf_last_search_stats(self._h, ctypes.byref(m), ctypes.byref(u)))
-        return int(m.value), int(u.value)
+        by = (ctypes.c_double * 2)()
+        check(self._L.vs_ivf_last_search_stats(self._h, ctypes.byref(m), ctypes.byref(u), by))
+        return int(m.value), int(u.value), float(by[0]), float(by[1])
 
     @property
     def last_mfma_lists(self) -> int:
