@@ -238,8 +238,10 @@ hipError_t launch_screen_mfma(int dt, const ScreenArgs& a, const uint8_t* qt, in
 hipError_t launch_screen_mfma_mapped(int dt, const ScreenArgs& a, const uint8_t* qt, hipStream_t st);
 // host check of one descriptor against the launch (tile map length, query tiles, qmap length)
 bool check_map_desc(const int* desc, int64_t tmap_len, int n_qtiles, int64_t qmap_len);
-hipError_t launch_pack_qtile_split(int dt, const float* q, const int* qidx, int nqb, int d, int dpad, uint8_t* qt,
-                                   float* qinfo, hipStream_t st);
+// every split query tile of the launch at once: tile y packs the sinfo[2y + 1] (1..128) queries
+// qidx[sinfo[2y] ..] of q (host-checked by the caller)
+hipError_t launch_pack_qtile_split(int dt, const float* q, const int* qidx, const int* sinfo, int ntiles, int d,
+                                   int dpad, uint8_t* qt, float* qinfo, hipStream_t st);
 hipError_t launch_screen_gemv(int dt, const ScreenArgs& a, const float* qp, int nqb, int nqpad, hipStream_t st);
 
 // one merge stage: in[(s*qstride + q)*Kp + j], s < nseg  ->  out[(b*nq + q)*Kp + j]

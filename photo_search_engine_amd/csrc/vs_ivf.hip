@@ -50,7 +50,8 @@ struct vs_ivf {
     DevBuf tmp_rows, slots, assign_ids;
     DevBuf qdev, probes, items, qp, qinfo, cand, glist, gcnt, cert, outD, outI, rec, next_item;
     DevBuf mqidx, mqtile, mcand, mdesc;
-    std::vector<int> desc_h;  // MFMA list scans: workgroup descriptors (MAP_DESC ints each)
+    std::vector<int> desc_h;  // MFMA list scans: workgroup descriptors (MAP_DESC ints each), then
+    int n_mdesc = 0;          // per query tile (offset into mqidx, queries)
     DevBuf rq, rD, rI, rS;  // re-search of uncertified queries: gathered queries and their outputs  // MFMA list scans: query indices, query tile, workspaces
     int scan_mode = VS_IVF_SCAN_AUTO;
     int last_mfma_lists = 0;  // first pass of the last search: MFMA list scans ...
@@ -297,12 +298,19 @@ void search_core(vs_ivf* ix, const float* q_dev, int64_t nq, int k, int nprobe, 
             for (int j = 0; j < m.nqb; ++j) per_q[mq[m.q0 + j]] += G * Kp;
         }
         std::stable_sort(wgs.begin(), wgs.end(), [](const Wg& x, const Wg& y) { return x.nt > y.nt; });
+        ix->n_mdesc = (int)wgs.size();
         const int64_t tmap_len = ix->page_off_h.back();
         for (const Wg& w : wgs) {
             const int g[MAP_DESC] = {w.tm_off, w.nt, w.t0, w.nvalid, w.qti, w.qoff, w.nqb, 0};
             if (!check_map_desc(g, tmap_len, (int)mscans.size(), (int64_t)mq.size()))
                 throw VsError(VS_ERR_INTERNAL, "IVF MFMA scan: invalid workgroup descriptor");
             desc.insert(desc.end(), g, g + MAP_DESC);
+        }
+        for (const MScan& m : mscans) {  // the query tiles' (offset into mq, queries), after the descriptors
+            if (m.nqb < 1 || m.nqb > MFMA_QB / 2 || m.q0 < 0 || m.q0 + m.nqb > (int)mq.size())
+                throw VsError(VS_ERR_INTERNAL, "IVF MFMA scan: invalid query tile");
+            desc.push_back(m.q0);
+            desc.push_back(m.nqb);
         }
     }
     int64_t max_keys = Kp;
@@ -380,12 +388,12 @@ void search_core(vs_ivf* ix, const float* q_dev, int64_t nq, int k, int nprobe, 
     if (!mscans.empty()) {
         const size_t qtb = (size_t)MFMA_QB * ix->dpad * 2;  // one query tile
         ix->mqtile.ensure(qtb * mscans.size());
-        const int G = (int)(desc.size() / MAP_DESC);
+        const int G = ix->n_mdesc;
         ix->mcand.ensure((size_t)G * (MFMA_QB / 2) * MFMA_CAP * sizeof(u64));
-        for (size_t si = 0; si < mscans.size(); ++si)  // the query tiles (and their queries' margins in qinfo)
-            HIP_CHECK(launch_pack_qtile_split(ix->dtype, q_dev, ix->mqidx.as<int>() + mscans[si].q0, mscans[si].nqb,
-                                              ix->d, ix->dpad, ix->mqtile.as<uint8_t>() + si * qtb,
-                                              ix->qinfo.as<float>(), st));
+        // the query tiles (and their queries' margins in qinfo), one launch
+        HIP_CHECK(launch_pack_qtile_split(ix->dtype, q_dev, ix->mqidx.as<int>(), ix->mdesc.as<int>() + (size_t)G * MAP_DESC,
+                                          (int)mscans.size(), ix->d, ix->dpad, ix->mqtile.as<uint8_t>(),
+                                          ix->qinfo.as<float>(), st));
         ScreenArgs sa{};
         sa.corpus = ix->data;
         sa.dpad = ix->dpad;

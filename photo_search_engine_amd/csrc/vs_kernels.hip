@@ -486,10 +486,15 @@ __global__ void __launch_bounds__(256) k_pack_qtile(const float* __restrict__ q,
 // as hi = round(q) in tile row wn*128 + (jj/16)*32 + jj%16 and lo = round(q - hi) 16 rows further,
 // so the screen sums two MFMA accumulators per query.  Query j is q[qidx[j]]; its qinfo entry
 // becomes the max of what is there and (||hi|| + ||lo||, ||q - hi - lo||) (fp64, rounded up).
+// One launch packs every tile: tile y = blockIdx.y takes queries qidx[sinfo[2y] ..] (sinfo[2y + 1]
+// of them) into qt + y * MFMA_QB * dpad * 2.
 template <int DT>
 __global__ void __launch_bounds__(256) k_pack_qtile_split(const float* __restrict__ q, const int* __restrict__ qidx,
-                                                           int nqb, int d, int dpad, uint8_t* __restrict__ qt,
-                                                           float* __restrict__ qinfo) {
+                                                           const int* __restrict__ sinfo, int d, int dpad,
+                                                           uint8_t* __restrict__ qt, float* __restrict__ qinfo) {
+    qidx += sinfo[2 * blockIdx.y];
+    const int nqb = sinfo[2 * blockIdx.y + 1];
+    qt += (size_t)blockIdx.y * MFMA_QB * dpad * 2;
     const int lane = threadIdx.x & 63;
     const int c = blockIdx.x * 4 + (threadIdx.x >> 6);  // tile row
     if (c >= MFMA_QB) return;
@@ -2537,13 +2542,14 @@ hipError_t launch_pack_qtile(int dt, const float* q, int nqb, int d, int dpad, u
     return hipGetLastError();
 }
 
-hipError_t launch_pack_qtile_split(int dt, const float* q, const int* qidx, int nqb, int d, int dpad, uint8_t* qt,
-                                   float* qinfo, hipStream_t st) {
-    if (nqb <= 0 || nqb > MFMA_QB / 2 || !qidx) return hipErrorInvalidValue;
+hipError_t launch_pack_qtile_split(int dt, const float* q, const int* qidx, const int* sinfo, int ntiles, int d,
+                                   int dpad, uint8_t* qt, float* qinfo, hipStream_t st) {
+    if (ntiles <= 0 || ntiles > 65535 || !qidx || !sinfo) return hipErrorInvalidValue;
+    const dim3 grid(MFMA_QB / 4, ntiles);
     if (dt == DT_BF16)
-        hipLaunchKernelGGL(k_pack_qtile_split<DT_BF16>, dim3(MFMA_QB / 4), dim3(256), 0, st, q, qidx, nqb, d, dpad, qt, qinfo);
+        hipLaunchKernelGGL(k_pack_qtile_split<DT_BF16>, grid, dim3(256), 0, st, q, qidx, sinfo, d, dpad, qt, qinfo);
     else if (dt == DT_F16)
-        hipLaunchKernelGGL(k_pack_qtile_split<DT_F16>, dim3(MFMA_QB / 4), dim3(256), 0, st, q, qidx, nqb, d, dpad, qt, qinfo);
+        hipLaunchKernelGGL(k_pack_qtile_split<DT_F16>, grid, dim3(256), 0, st, q, qidx, sinfo, d, dpad, qt, qinfo);
     else
         return hipErrorInvalidValue;
     return hipGetLastError();
