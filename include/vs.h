@@ -64,6 +64,11 @@ int vs_add_device(vs_index* index, const float* x_dev, int64_t n, void* stream);
 /* Fill rows [ntotal, ntotal+n) with synthetic rows global_row0.. of the counter-hash generator
  * (bench / tests; bit-identical to oracle/vs_oracle.c orc_synth_rows). */
 int vs_add_synthetic(vs_index* index, uint64_t seed, int64_t global_row0, int64_t n, int normalize);
+/* Size the row storage (and the int8 screen copy) for n more rows in one allocation: later adds up
+ * to that size never regrow (a regrow copies the rows into a 1.5x larger buffer, so the old and
+ * the new storage coexist for the copy).  vs_capacity: rows the storage holds without regrowing. */
+int vs_reserve(vs_index* index, int64_t n);
+int64_t vs_capacity(const vs_index* index);
 /* Same generator, written as row-major fp32 (values rounded to `dtype`) into device memory on
  * `device`: synthetic query batches for bench.py / tests. */
 int vs_synthesize(int device, uint64_t seed, int64_t global_row0, int64_t n, int d, int normalize, int dtype,

@@ -53,6 +53,8 @@ _SIGS = {
     "vs_add": (ctypes.c_int, [_vp, _vp, _c_i64]),
     "vs_add_device": (ctypes.c_int, [_vp, _vp, _c_i64, _vp]),
     "vs_add_synthetic": (ctypes.c_int, [_vp, ctypes.c_uint64, _c_i64, _c_i64, ctypes.c_int]),
+    "vs_reserve": (ctypes.c_int, [_vp, _c_i64]),
+    "vs_capacity": (_c_i64, [_vp]),
     "vs_synthesize": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint64, _c_i64, _c_i64, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_int, _vp, _vp]),
     "vs_search": (ctypes.c_int, [_vp, _vp, _c_i64, ctypes.c_int32, _vp, _vp]),

@@ -160,10 +160,11 @@ struct CtxLease {
 
 void ensure_capacity_i8(vs_index* ix);
 
-void ensure_capacity(vs_index* ix, int64_t rows_needed) {
+// exact: allocate exactly rows_needed (vs_reserve) instead of growing by 1.5x
+void ensure_capacity(vs_index* ix, int64_t rows_needed, bool exact = false) {
     const int64_t want = round_up(rows_needed, TR);
     if (want <= ix->cap_rows) return;
-    int64_t ncap = std::max(want, ix->cap_rows + ix->cap_rows / 2);
+    int64_t ncap = exact ? want : std::max(want, ix->cap_rows + ix->cap_rows / 2);
     ncap = round_up(ncap, TR);
     const int64_t tb = tile_bytes(ix->dpad, ix->dtype);
     uint8_t* nd = nullptr;
@@ -866,6 +867,19 @@ int vs_add_device(vs_index* ix, const float* x_dev, int64_t n, void* stream) {
         refresh_maxsq(ix);
     });
 }
+
+int vs_reserve(vs_index* ix, int64_t n) {
+    return guarded([&] {
+        check_index(ix);
+        if (n < 0) throw VsError(VS_ERR_ARG, "n must be >= 0");
+        std::unique_lock<std::shared_mutex> lk(ix->rw);
+        DeviceGuard dg(ix->device);
+        if (ix->ntotal + n > (int64_t)0xFFFFFFF0LL) throw VsError(VS_ERR_ARG, "shard exceeds 2^32 rows");
+        ensure_capacity(ix, ix->ntotal + n, true);
+    });
+}
+
+int64_t vs_capacity(const vs_index* ix) { return ix ? ix->cap_rows : -1; }
 
 int vs_add_synthetic(vs_index* ix, uint64_t seed, int64_t global_row0, int64_t n, int normalize) {
     return guarded([&] {

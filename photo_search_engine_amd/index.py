@@ -118,6 +118,14 @@ class FlatIndex:
     def add_synthetic(self, seed: int, global_row0: int, n: int, normalize: bool = True) -> None:
         check(self._L.vs_add_synthetic(self._h, int(seed), int(global_row0), int(n), int(bool(normalize))))
 
+    def reserve(self, n: int) -> None:
+        """Size the HBM row storage for ``n`` more rows in one allocation (no regrowth up to it)."""
+        check(self._L.vs_reserve(self._h, int(n)))
+
+    @property
+    def capacity(self) -> int:
+        return int(self._L.vs_capacity(self._h))
+
     def search_device(self, q_ptr: int, nq: int, k: int, D_ptr: Optional[int], I_ptr: int,
                       S64_ptr: Optional[int] = None, id_offset: int = 0, stream: Optional[int] = None) -> None:
         check(self._L.vs_search_device(self._h, q_ptr, int(nq), int(k), D_ptr or None, I_ptr, S64_ptr or None,

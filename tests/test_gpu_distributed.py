@@ -72,3 +72,44 @@ def test_four_ranks_one_gpu_match_oracle(tmp_path):
     for o in outs:
         np.testing.assert_array_equal(o["I"], Ie)
         np.testing.assert_array_equal(o["S"], Se)
+
+
+def _nccl_worker(rank, world, port, outdir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    try:
+        from photo_search_engine_amd.distributed import ShardedFlatIndex
+        N, d, nq, k = 9000, 64, 24, 12
+        sh = ShardedFlatIndex(d, "ip", "bf16", device=0)
+        sh.add_synthetic(O.SEED_CORPUS, N, True)
+        q = torch.from_numpy(O.synth_rows(O.SEED_QUERIES, 0, nq, d, True, "bf16")).cuda()
+        D, I, S = sh.search(q, k, src=0)
+        # the exchange step itself on RCCL: all_gather_into_tensor of the packed (score, id) pairs
+        # and the device merge of the gathered lists (G = 1 here)
+        SI = torch.stack([S.contiguous().view(torch.int64), I.contiguous()], dim=-1)
+        g = sh._gather(SI)
+        D2, I2, S2 = sh._merge(sh.metric, g[..., 0].contiguous().view(torch.float64), g[..., 1].contiguous(), k)
+        torch.cuda.synchronize()
+        np.savez(os.path.join(outdir, "nccl.npz"), D=D.cpu().numpy(), I=I.cpu().numpy(), S=S.cpu().numpy(),
+                 D2=D2.cpu().numpy(), I2=I2.cpu().numpy(), S2=S2.cpu().numpy(), backend=dist.get_backend())
+        sh.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_backend_one_rank_exchange_and_merge(tmp_path):
+    # the nccl (= RCCL) branch of ShardedFlatIndex._gather, which the gloo tests above never take:
+    # one rank (the box has one GPU; RCCL does not run two ranks on one device), all_gather_into_tensor
+    # + the device merge, equal to the oracle
+    mp.spawn(_nccl_worker, args=(1, _free_port(), str(tmp_path)), nprocs=1, join=True)
+    o = np.load(tmp_path / "nccl.npz")
+    assert str(o["backend"]) == "nccl"
+    x = O.synth_rows(O.SEED_CORPUS, 0, 9000, 64, True, "bf16")
+    q = O.synth_rows(O.SEED_QUERIES, 0, 24, 64, True, "bf16")
+    Se, Ie = O.knn_exact(x, q, 12, "ip")
+    for sfx in ("", "2"):
+        np.testing.assert_array_equal(o["I" + sfx], Ie)
+        np.testing.assert_array_equal(o["S" + sfx], Se)
+        np.testing.assert_array_equal(o["D" + sfx], Se.astype(np.float32))

@@ -424,3 +424,25 @@ def test_k_3000_single_query_and_batch(FlatIndex):
     for nq in (1, 12):
         q = O.synth_rows(O.SEED_QUERIES, 3, nq, 64, True, "f32")
         _check_exact(ix, q, 3000, "ip")
+
+
+def test_reserve_sizes_storage_once(FlatIndex):
+    # vs_reserve: one allocation for the rows to come; chunked adds up to it never regrow, and the
+    # search over them is exact
+    d, N = 80, 7000
+    ix = FlatIndex(d, "ip", "bf16")
+    ix.reserve(N)
+    cap = ix.capacity
+    assert cap >= N and cap < N + 256
+    for r0 in range(0, N, 1000):
+        ix.add_synthetic(O.SEED_CORPUS, r0, min(1000, N - r0), True)
+        assert ix.capacity == cap
+    ix.add_synthetic(O.SEED_CORPUS, N, 300, True)  # past the reservation: regrows
+    assert ix.capacity > cap
+    x = O.synth_rows(O.SEED_CORPUS, 0, N + 300, d, True, "bf16")
+    q = O.synth_rows(O.SEED_QUERIES, 0, 30, d, True, "f32")
+    D, I = ix.search(q, 9)
+    S, Ie = O.knn_exact(x, q, 9, "ip")
+    np.testing.assert_array_equal(I, Ie)
+    np.testing.assert_array_equal(D, S.astype(np.float32))
+    ix.close()
