@@ -90,7 +90,7 @@ def _nccl_worker(rank, world, port, outdir):
         # and the device merge of the gathered lists (G = 1 here)
         SI = torch.stack([S.contiguous().view(torch.int64), I.contiguous()], dim=-1)
         g = sh._gather(SI)
-        D2, I2, S2 = sh._merge(sh.metric, g[..., 0].contiguous().view(torch.float64), g[..., 1].contiguous(), k)
+        S2, I2, D2 = sh._merge(sh.metric, g[..., 0].contiguous().view(torch.float64), g[..., 1].contiguous(), k)
         torch.cuda.synchronize()
         np.savez(os.path.join(outdir, "nccl.npz"), D=D.cpu().numpy(), I=I.cpu().numpy(), S=S.cpu().numpy(),
                  D2=D2.cpu().numpy(), I2=I2.cpu().numpy(), S2=S2.cpu().numpy(), backend=dist.get_backend())
@@ -110,6 +110,6 @@ def test_rccl_backend_one_rank_exchange_and_merge(tmp_path):
     q = O.synth_rows(O.SEED_QUERIES, 0, 24, 64, True, "bf16")
     Se, Ie = O.knn_exact(x, q, 12, "ip")
     for sfx in ("", "2"):
-        np.testing.assert_array_equal(o["I" + sfx], Ie)
-        np.testing.assert_array_equal(o["S" + sfx], Se)
-        np.testing.assert_array_equal(o["D" + sfx], Se.astype(np.float32))
+        np.testing.assert_array_equal(o["I" + sfx], Ie, err_msg="I" + sfx)
+        np.testing.assert_array_equal(o["S" + sfx], Se, err_msg="S" + sfx)
+        np.testing.assert_array_equal(o["D" + sfx], Se.astype(np.float32), err_msg="D" + sfx)
