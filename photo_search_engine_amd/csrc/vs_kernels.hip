@@ -2232,6 +2232,13 @@ __global__ void __launch_bounds__(RF_THREADS) k_refine_wide(RefineArgs a, int KA
     int nB = 0;
     if (tB < tA) {
         if (inreg) {
+            // the keys are reloaded (L2-hot list) rather than held across phase A's scoring, where
+            // their 32 VGPRs would push the gathers' registers into scratch
+#pragma unroll
+            for (int e = 0; e < RF_E; ++e) {
+                const int j = tid + RF_THREADS * e;
+                keys[e] = j < n ? __builtin_nontemporal_load(src + j) : 0ull;
+            }
             nB = block_write_ids<RF_E>(keys, tB, tA, ids + nA2, RFW_CAP - nA2, red);
         } else {
             for (int r0 = 0; r0 < n; r0 += RF_THREADS) {
