@@ -57,6 +57,7 @@ struct Ctx {
     DevBuf qdev, qtile, qinfo, qpad, cand, part, merge_a, merge_b, outD, outI, outS, cert, thr0, seedmax, gcnt;
     DevBuf qfac, qeps, drop;  // int8 screen: per-query code scale and norm, refine margin, drop bounds
     DevBuf fails;             // the current query block's certificate-failure count (fallback gate)
+    DevBuf rsc, rdone;        // split refine: per-query scores + ids of the kept rows, done counters
     DevBuf rows[2];  // read_rows_host: unpacked fp32 chunks
     DevBuf tilectr;  // GEMV screen: tile work-queue counter
     DevBuf seedacc;  // MFMA seed pass: raw accumulators of each workgroup's seed tile
@@ -66,7 +67,7 @@ struct Ctx {
     HostBuf hout;    // vs_search: I (int64), D (fp32) and certificates land here; search_exact_device: certificates
     ~Ctx() {
         for (DevBuf* b : {&qdev, &qtile, &qinfo, &qpad, &cand, &part, &merge_a, &merge_b, &outD, &outI, &outS, &cert, &thr0,
-                          &seedmax, &gcnt, &rows[0], &rows[1], &tilectr, &seedacc, &outAll, &qfac, &qeps, &drop, &fails})
+                          &seedmax, &gcnt, &rows[0], &rows[1], &tilectr, &seedacc, &outAll, &qfac, &qeps, &drop, &fails, &rsc, &rdone})
             b->release();
         pin.release();
         hq.release();
@@ -589,6 +590,19 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
     r.redo = redo ? 1 : 0;
     r.gate = gate;
     r.optimistic = optimistic ? 1 : 0;
+    r.nsplit = redo ? 1 : refine_split(nqb, Kp, ix->dtype, ix->num_cu);
+    if (r.nsplit > 1) {
+        int KP2 = 1;
+        while (KP2 < Kp) KP2 <<= 1;
+        c->rsc.ensure((size_t)nqb * KP2 * 12);
+        r.gsc = c->rsc.as<double>();
+        r.gids = (uint32_t*)(r.gsc + (size_t)nqb * KP2);
+        if (c->rdone.bytes < sizeof(unsigned) * MFMA_QB) {  // zeroed once; the last workgroup re-zeroes
+            c->rdone.ensure(sizeof(unsigned) * MFMA_QB);
+            HIP_CHECK(hipMemsetAsync(c->rdone.p, 0, c->rdone.bytes, st));
+        }
+        r.gdone = c->rdone.as<unsigned>();
+    }
     HIP_CHECK(launch_refine(r, nqb, st));
 }
 

@@ -277,7 +277,13 @@ struct RefineArgs {
     int* fails;            // first pass: count of the block's uncertified queries (the fallback's gate)
     int redo;              // device fallback round: only queries with cert[q] == 0 are refined (and
     const int* gate;       //  their outputs rewritten), nothing at all while *gate == 0
+    int nsplit;            // k_refine, few queries with deep lists: > 1 workgroups per query each score
+    double* gsc;           //  a slice of the kept rows into gsc / gids ([nq][KP2]); the last one to
+    uint32_t* gids;        //  finish (gdone[q], zero between launches) sorts and certifies.  0/1 =
+    unsigned* gdone;       //  one workgroup per query.
 };
+// workgroups per query of k_refine for a Kp-deep refine of nq queries (1 = no split)
+int refine_split(int nq, int Kp, int dt, int num_cu);
 hipError_t launch_refine(const RefineArgs& a, int nq, hipStream_t st);
 // exact refine behind the int8 screen: adaptive two-phase depth (KA keys first), IP only
 hipError_t launch_refine_wide(const RefineArgs& a, int nq, int KA, hipStream_t st);

@@ -1973,20 +1973,48 @@ __device__ __forceinline__ void refine(const RefineArgs& a, int KP2) {
     __syncthreads();
     const int nv = nv_s;
     constexpr int RR = refine_rows<DT>();
-    for (int j = wid; j < nv; j += RR * NW) {
+    // split refine (a.nsplit > 1, blockIdx.y = slice): every workgroup of the query made the same
+    // selection above; each scores its slice of cq into the query's global rows, the last to finish
+    // gathers them and goes on alone
+    const bool split = a.nsplit > 1;
+    int jlo = 0, jhi = nv;
+    if (split) {
+        const int chunk = (nv + a.nsplit - 1) / a.nsplit;
+        jlo = min(nv, (int)blockIdx.y * chunk);
+        jhi = min(nv, jlo + chunk);
+    }
+    double* scw = split ? a.gsc + (size_t)q * KP2 : sc;
+    uint32_t* idw = split ? a.gids + (size_t)q * KP2 : ids;
+    for (int j = jlo + wid; j < jhi; j += RR * NW) {
         int64_t rr[RR];
 #pragma unroll
-        for (int i = 0; i < RR; ++i) rr[i] = j + i * NW < nv ? (int64_t)key_id(cq[j + i * NW]) : -1;
+        for (int i = 0; i < RR; ++i) rr[i] = j + i * NW < jhi ? (int64_t)key_id(cq[j + i * NW]) : -1;
         double s4[RR];
         exact_score_rows<DT, METRIC, QLDS, RR>(a.corpus, rr, qs, qv, a.d, a.dpad, lane, s4);
         if (lane == 0) {  // keys carry storage slots; IVF maps them to user ids (sort + output)
 #pragma unroll
             for (int i = 0; i < RR; ++i)
                 if (rr[i] >= 0) {
-                    sc[j + i * NW] = s4[i];
-                    ids[j + i * NW] = a.idmap ? a.idmap[rr[i]] : (uint32_t)rr[i];
+                    scw[j + i * NW] = s4[i];
+                    idw[j + i * NW] = a.idmap ? a.idmap[rr[i]] : (uint32_t)rr[i];
                 }
         }
+    }
+    if (split) {
+        __shared__ int last_s;
+        __threadfence();  // release this workgroup's scores (device scope: other XCDs' L2s)
+        __syncthreads();
+        if (tid == 0) last_s = atomicAdd(a.gdone + q, 1u) == (unsigned)(a.nsplit - 1) ? 1 : 0;
+        __syncthreads();
+        if (!last_s) return;
+        __threadfence();  // acquire the other workgroups' scores
+        const volatile double* vsc = scw;
+        const volatile uint32_t* vid = idw;
+        for (int j = tid; j < nv; j += RF_THREADS) {
+            sc[j] = vsc[j];
+            ids[j] = vid[j];
+        }
+        if (tid == 0) a.gdone[q] = 0u;  // ready for the next launch (kernel boundary orders it)
     }
     const double worst = METRIC == METRIC_IP ? -INFINITY : INFINITY;
     for (int j = nv + tid; j < KP2; j += RF_THREADS) {
@@ -2735,7 +2763,19 @@ static void launch_refine_one(const RefineArgs& a, int nq, int KP2, size_t lds, 
             return;
         }
     }
-    hipLaunchKernelGGL((k_refine<DT, METRIC, QLDS>), dim3(nq), dim3(RF_THREADS), lds, st, a, KP2);
+    const int ns = a.nsplit > 1 ? a.nsplit : 1;
+    hipLaunchKernelGGL((k_refine<DT, METRIC, QLDS>), dim3(nq, ns), dim3(RF_THREADS), lds, st, a, KP2);
+}
+
+// Split a few-query refine over several workgroups per query when its rows (Kp per query) would
+// otherwise take many serial gather rounds on one CU: >= 2 rounds (RR rows per wave x 16 waves)
+// per workgroup, at most 32 per query, the whole grid within one wave of the chip.
+int refine_split(int nq, int Kp, int dt, int num_cu) {
+    const int per_round = (dt == DT_F32 ? 2 : 4) * (RF_THREADS / 64);
+    int ns = Kp / (2 * per_round);
+    ns = std::min(ns, 32);
+    ns = std::min(ns, num_cu / std::max(nq, 1));
+    return ns >= 2 ? ns : 1;
 }
 
 template <int DT>
@@ -2751,6 +2791,7 @@ static void launch_refine_dt(const RefineArgs& a, int nq, int KP2, size_t lds, b
 
 hipError_t launch_refine(const RefineArgs& a, int nq, hipStream_t st) {
     if (a.redo && (a.dt == DT_F32 || !a.gate || !a.cert)) return hipErrorInvalidValue;  // fallback: bf16 / f16
+    if (a.nsplit > 1 && (a.redo || !a.gsc || !a.gids || !a.gdone)) return hipErrorInvalidValue;
     int KP2 = 1;
     while (KP2 < a.Kp) KP2 <<= 1;
     const size_t base = (size_t)KP2 * 12 + 8 + (size_t)KP2 * 8;  // scores, ids, (query), kept keys

@@ -446,3 +446,18 @@ def test_reserve_sizes_storage_once(FlatIndex):
     np.testing.assert_array_equal(I, Ie)
     np.testing.assert_array_equal(D, S.astype(np.float32))
     ix.close()
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16"])
+@pytest.mark.parametrize("metric", ["ip", "l2"])
+@pytest.mark.parametrize("nq,k,N", [(1, 400, 60_000), (3, 257, 40_000), (8, 700, 30_000), (1, 300, 350)])
+def test_few_query_deep_refine_split_exact(FlatIndex, dtype, metric, nq, k, N):
+    # few queries (GEMV screen) with deep lists: k_refine spreads each query's kept rows over
+    # several workgroups, the last one to finish sorts and certifies (refine_split); repeated
+    # calls check that the per-query completion counters come back to zero; N=350 leaves most
+    # slices empty (k close to the shard size)
+    ix = FlatIndex(96, metric, dtype)
+    ix.add_synthetic(O.SEED_CORPUS, 0, N, True)
+    for i in range(3):
+        q = O.synth_rows(O.SEED_QUERIES, 500 + 10 * i, nq, 96, True, "f32")
+        _check_exact(ix, q, k, metric)
