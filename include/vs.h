@@ -146,6 +146,9 @@ int64_t vs_unresolved_count(vs_index* index);
 /* pinned host bytes the index holds for vs_search's query / result staging (all contexts); each
  * context stages at most 8 MiB and loops over query chunks beyond that */
 int64_t vs_host_staging_bytes(vs_index* index);
+/* HBM bytes the screen copies hold beyond the stored rows (VS_SCREEN_I8: int8 codes, per-row scale |
+ * error norm, and for bf16/f16 rows the refine's row-major copy when it fits); 0 for native screens */
+int64_t vs_screen_copy_bytes(vs_index* index);
 
 /* ==== multi-device flat index (one process, several GPUs; SURVEY.md §8 b/e) =================
  * The reference holds ONE index in ONE process (main.py:59-68 -> utils/vector_store.py:72-81); this

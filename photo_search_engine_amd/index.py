@@ -160,6 +160,11 @@ class FlatIndex:
         """Pinned host bytes held for ``search``'s query / result staging (bounded per context)."""
         return int(check(self._L.vs_host_staging_bytes(self._h)))
 
+    def screen_copy_bytes(self) -> int:
+        """HBM bytes of the int8 screen's copies (codes, per-row scale | error norm, the refine's
+        row-major rows when they fit) on top of the stored rows; 0 on the native screen."""
+        return int(check(self._L.vs_screen_copy_bytes(self._h)))
+
     # -- lifecycle ----------------------------------------------------------------------------
     def close(self) -> None:
         if self._h is not None and self._h.value:
