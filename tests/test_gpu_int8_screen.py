@@ -167,3 +167,24 @@ def test_int8_gemv_cfg2_shape_matches_native(FlatIndex):
         np.testing.assert_array_equal(D, Dn)
     assert ix.uncertified_count() == 0
     ix.close()
+
+
+def test_int8_screen_copy_bytes(FlatIndex):
+    # vs_screen_copy_bytes: 0 on the native screen; with the int8 screen at least the codes and the
+    # per-row (scale | error norm) word of every row (allocated capacity, tiles of 256 rows); back to
+    # 0 when the screen is switched off again; grows with incremental adds
+    N, d = 5000, 200
+    ix = FlatIndex(d, "ip", "bf16")
+    ix.add_synthetic(O.SEED_CORPUS, 0, N, True)
+    assert ix.screen_copy_bytes() == 0
+    ix.set_screen("int8")
+    b = ix.screen_copy_bytes()
+    assert b >= N * (d + 4)
+    assert b % 4 == 0
+    ix.add_synthetic(O.SEED_CORPUS, N, 4 * N, True)
+    b2 = ix.screen_copy_bytes()
+    assert b2 >= 5 * N * (d + 4) and b2 >= b
+    q = O.synth_rows(O.SEED_QUERIES, 3, 40, d, True, "f32")
+    _exact(ix, q, 17)
+    ix.set_screen("native")
+    assert ix.screen_copy_bytes() == 0
