@@ -206,7 +206,9 @@ def main():
     out = None
     if rank == 0:
         out = {
-            "metric": METRICS[args.workload],
+            # a --rows run is a different configuration: its metric names the rows it ran on
+            "metric": METRICS[args.workload] if not args.rows else
+            METRICS[args.workload].split(",")[0] + f" (rows override: N={N}, not the BASELINE config)",
             "value": round(qps, 2),
             "unit": "queries/s",
             "n_gpus": G,
@@ -216,7 +218,10 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "int8" if kind in ("mfma_i8", "gemv_i8") else dtype,
+            # the stored rows' precision: every returned score is the canonical score of the stored
+            # (dtype) row; the int8 screen only pre-selects rows for the exact refine
+            "dtype": dtype,
+            "screen": "int8" if kind in ("mfma_i8", "gemv_i8") else "native",
             "data": "synthetic (counter-hash N(0,1) rows, L2-normalised, seeds 20260417/20260418)",
             "config": {"workload": args.workload, "desc": desc, "N": N, "d": d, "batch": nq, "k": k,
                        "n_local": n_local, "stored_rows": dtype, "screen": screen,

@@ -360,7 +360,9 @@ void search_block_i8(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float
         ScreenArgs sa = a;
         sa.G = std::min(sa.G, 512);
         sa.tile_stride = (int)(tiles / sa.G);
-        if (seed_reuse() && sa.G == a.G) {
+        // the direct main pass (k_screen_i8d) screens its whole range itself; the other form reuses
+        // the seed tile's accumulators
+        if (seed_reuse() && sa.G == a.G && !i8_direct_ok(ix->dpad8)) {
             c->seedacc.ensure((size_t)a.G * 128 * MF_WG_THREADS * sizeof(float));
             sa.seed_acc = c->seedacc.as<float>();
         }

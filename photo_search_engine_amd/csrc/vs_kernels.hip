@@ -17,6 +17,10 @@
 #include <math.h>
 #include <stdlib.h>
 
+#include <mutex>
+#include <set>
+#include <utility>
+
 namespace vs {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
@@ -1243,6 +1247,321 @@ __device__ __forceinline__ void screen_mfma(ScreenArgs a, const uint8_t* __restr
         if (lane == 0) off = atomicAdd(&a.gcnt[qg], n);
         off = __shfl(off, 0, 64);
         u64* dst = a.glist + (size_t)qg * a.lcap + off;
+        for (int j = lane; j < n; j += 64) dst[j] = cand[(size_t)q * a.cap + j];
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// K1 int8, direct form (k_screen_i8d): the main pass of the int8 screen when the K-steps per tile
+// are a multiple of 4 (every d that is a multiple of 256, cfg3's 1536 included).  Same input,
+// keys, candidate buffers and survivor lists as screen_mfma<DT_I8> (whose seed pass still seeds
+// it); the operands move differently:
+//   * each of the 8 waves owns 32 rows of the 256-row tile and all 256 query columns (2 x 16 MFMA
+//     16x16 tiles, 128 accumulators);
+//   * its corpus fragments go HBM -> VGPRs directly (global_load_dwordx4 nt, one 1 KiB fragment
+//     per instruction), I8D_P K-steps ahead, into I8D_U rotating register sets: no LDS staging,
+//     no LDS reads, no barrier wait on the corpus;
+//   * only the query block (16 KiB per K-step, L2-resident, shared by every wave) goes through
+//     an I8D_U-slot LDS ring by LDS-DMA, 2 instructions per wave, issued with the corpus loads;
+//   * a K-step is one asm block (vs_i8_asm.h): 16 query-fragment reads kept 4 ahead of their
+//     MFMA pairs, 32 MFMAs; the first K-step of a tile writes the accumulators (src2 = 0);
+//   * one s_waitcnt vmcnt(2 * I8D_OPS) + s_barrier per K-step (the same count for every wave and
+//     step: past the end the issue loads clamped dummy steps);
+//   * tile epilogue: per lane 8 rows x 16 query columns; a column is tested by one upper bound of
+//     its 8 keys (integer max, then the row scales' max / min and the error norms' max, all monotone
+//     in fp32), and only a column whose bound reaches the query's threshold computes its 8 keys.
+// Measured (scripts/k1_micro.hip, cfg3 shape): the loop alone runs at the HBM rate (2.53 ms,
+// 6.1 TB/s) on all-zero operands; on random int8 codes the board holds ~1.6 GHz under the MFMA
+// load and the loop takes ~3.5 ms (DESIGN §5 "power").
+// ------------------------------------------------------------------------------------------------
+}  // namespace vs
+#include "vs_i8_asm.h"
+namespace vs {
+constexpr int I8D_P = 3;            // K-steps of lead (measured: 3, 5 and 7 run at the same rate)
+constexpr int I8D_U = I8D_P + 1;    // corpus register sets = query ring slots (nks % I8D_U == 0)
+constexpr int I8D_OPS = 4;          // vector-memory ops per wave and K-step: 2 query DMAs + 2 corpus loads
+constexpr int I8D_RING = I8D_U * 16384;
+constexpr int I8D_LDS = I8D_RING + 256 * 8 + 256 * 4 + 256 * 4 + 16 + MF_POOL * 8 + MF_POOL * 4 + MF_SX + MF_QFAC +
+                        MF_ROWX;
+static_assert(I8D_LDS <= 160 * 1024, "LDS budget (direct int8 screen)");
+static_assert(I8D_U == 4, "the K loop body and the vmcnt count are written for 4 slots");
+
+bool i8_direct_ok(int dpad8) { return dpad8 % (64 * I8D_U) == 0 && dpad8 >= 2 * 64 * I8D_U; }
+
+// corpus fragment load: 16 B per lane into VGPRs, counted by the kernel's own s_waitcnt (inline
+// asm: the compiler neither waits for it nor may read the registers before the wait below)
+__device__ __forceinline__ void gld16_nt(intx4& v, const void* p) {
+    asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(v) : "v"(p) : "memory");
+}
+// 4 B per lane LDS-DMA (a tile's per-row side data: 64 rows per instruction)
+__device__ __forceinline__ void glds4(const void* gptr, uint32_t lds_base) {
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(gptr), "s"(lds_base)
+                 : "memory", "m0");
+}
+// wait until at most 2 K-steps of this wave's loads are younger than the step's own, then barrier;
+// the step's fragments are tied through the wait so nothing reads them before it
+__device__ __forceinline__ void i8d_wait_barrier(intx4& a0, intx4& a1) {
+    asm volatile("s_waitcnt vmcnt(%2)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" : "+v"(a0), "+v"(a1) : "n"(2 * I8D_OPS)
+                 : "memory");
+}
+
+__global__ void __launch_bounds__(512, 2) k_screen_i8d(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint8_t* const sm = smem + I8D_RING;
+    u64* thr_key = (u64*)sm;
+    float* thr_f = (float*)(sm + 256 * 8);
+    int* cnt = (int*)(sm + 256 * 12);
+    int* flag = (int*)(sm + 256 * 16);  // [1] pool count, [2 + tile parity] inserted
+    u64* pool_key = (u64*)(sm + 256 * 16 + 16);
+    int* pool_q = (int*)(sm + 256 * 16 + 16 + MF_POOL * 8);
+    float* sx = (float*)(sm + 256 * 16 + 16 + MF_POOL * 12) + (threadIdx.x >> 6) * 512 + (threadIdx.x & 63) * 8;
+    float2* qfac = (float2*)(sm + 256 * 16 + 16 + MF_POOL * 12 + MF_SX);
+    uint32_t* rowx = (uint32_t*)(sm + 256 * 16 + 16 + MF_POOL * 12 + MF_SX + MF_QFAC);
+    asm volatile("; lds ring escapes: %0" ::"v"(smem) : "memory");
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int blk = blockIdx.x;
+    const int t0 = (int)((int64_t)a.tiles * blk / a.G);
+    const int t1 = (int)((int64_t)a.tiles * (blk + 1) / a.G);
+    if (tid < 256) {
+        const bool real = tid < nqb;
+        const u64 k0 = real ? (a.thr0 ? a.thr0[tid] : 0ull) : ~0ull;
+        thr_key[tid] = k0;
+        thr_f[tid] = !real ? INFINITY : (k0 == 0ull ? -INFINITY : key_score(k0));
+        cnt[tid] = 0;
+        qfac[tid] = real ? a.qfac[tid] : make_float2(0.0f, 0.0f);
+    }
+    if (tid == 0) {
+        flag[0] = 0;
+        flag[1] = 0;
+        flag[2] = 0;
+        flag[3] = 0;
+    }
+    __syncthreads();
+    const int nks = a.dpad / 64;
+    const int64_t tbytes = (int64_t)TR * a.dpad;
+    u64* cand = a.cand + (size_t)blk * MFMA_QB * a.cap;
+    const int trigger = a.cap - TR;
+    const uint32_t ring = lds_addr(smem);
+    const uint32_t rowx_lds = lds_addr((const uint8_t*)rowx);
+    const int r16 = lane & 15;
+    const uint32_t lane_off = (uint32_t)(r16 * 64 + (((lane >> 4) ^ mf_swz(r16)) << 4));
+    const int a_off = wid * 2048 + r16 * 64 + (lane >> 4) * 16;  // lane's 16 B of the wave's first fragment
+
+    intx4 A[I8D_U][2];  // corpus fragments of the K-steps in flight (set = K-step & 3)
+    intx4 acc[2][16];   // acc[m][n][r]: row wid*32 + 16m + 4(lane >> 4) + r, query 16n + (lane & 15)
+    intx4 bt[4];        // query fragments in flight (inside the asm block)
+
+    // issue K-step (iti, iks) into register set SET = iks & 3 and ring slot SET: the tile's side
+    // data first when it is the tile's last K-step, then the query block, then the corpus
+    // fragments (dummy steps past the range reload the last tile: same op count every step)
+    int iti = t0, iks = 0;
+#define I8D_ISSUE(SET)                                                                                   \
+    do {                                                                                                 \
+        if (iks == nks - 1 && iti < t1) /* 4 waves cover the 1 KiB; waves 4-7 rewrite the same bytes */ \
+            glds4(a.rsb + (int64_t)iti * TR + (wid & 3) * 64 + lane,                                     \
+                  __builtin_amdgcn_readfirstlane(rowx_lds + (uint32_t)((iti & 1) * 1024 + (wid & 3) * 256))); \
+        const uint32_t qbase = __builtin_amdgcn_readfirstlane(ring + (uint32_t)((SET) * 16384 + wid * 1024)); \
+        _Pragma("unroll") for (int it = 0; it < 2; ++it) {                                               \
+            const int g = it * 512 + wid * 64 + lane;                                                    \
+            const int row = g >> 2, pos = g & 3;                                                         \
+            glds16(qt + (int64_t)iks * 16384 + (row << 6) + ((pos ^ mf_swz(row)) << 4), qbase + it * 8192); \
+        }                                                                                                \
+        const uint8_t* ab = a.corpus + (int64_t)(iti < t1 ? iti : t1 - 1) * tbytes + (int64_t)iks * 16384 + a_off; \
+        gld16_nt(A[SET][0], ab);                                                                         \
+        gld16_nt(A[SET][1], ab + 1024);                                                                  \
+        if (++iks == nks) { iks = 0; ++iti; }                                                            \
+    } while (0)
+
+    if (t1 > t0) {
+        I8D_ISSUE(0);
+        I8D_ISSUE(1);
+        I8D_ISSUE(2);
+    }
+    bool check_pending = false;
+    // one K-step: wait for its fragments + query block, barrier, issue the step 3 ahead, then the
+    // MFMA block STEP_ (a static choice per call site: a runtime choice between asm variants makes
+    // the register allocator shuffle the 128 accumulators)
+#define I8D_BODY(U_, STEP_)                                                          \
+    do {                                                                             \
+        i8d_wait_barrier(A[U_][0], A[U_][1]);                                        \
+        I8D_ISSUE(((U_) + I8D_P) & 3);                                               \
+        const uint32_t slot_lds = ring + (uint32_t)((U_) * 16384) + lane_off;        \
+        STEP_(A[U_][0], A[U_][1]);                                                   \
+    } while (0)
+    for (int ti = t0; ti < t1; ++ti) {
+        // K-steps 0..3: the first writes the accumulators; the deferred compaction check of the
+        // previous tile runs after step 0's barrier (every wave's inserts of that tile complete)
+        i8d_wait_barrier(A[0][0], A[0][1]);
+        I8D_ISSUE(I8D_P);
+        if (check_pending) {
+            check_pending = false;
+            if (flag[2 + ((ti - 1) & 1)] != 0) {  // skipped when the tile inserted nothing
+                int np = flag[1];
+                np = np < MF_POOL ? np : MF_POOL;
+                for (int j = tid; j < np; j += MF_THREADS) {  // the LDS pool -> candidate buffers
+                    const int q = pool_q[j];
+                    const int slot = atomicAdd(&cnt[q], 1);
+                    if (slot < a.cap) cand[(size_t)q * a.cap + slot] = pool_key[j];
+                }
+                // every wave has read the pool and the flag and done its counter atomics; the stores
+                // stay in flight (vmcnt counts them in issue order behind the corpus loads, so the
+                // counted corpus waits stay exact -- MI355X_MICROARCH.md, s_waitcnt)
+                mf_barrier_lgkm();
+                if (tid == 0) {
+                    flag[1] = 0;
+                    flag[2 + ((ti - 1) & 1)] = 0;
+                }
+                int need = 0;
+#pragma unroll
+                for (int i = 0; i < 256 / 64; ++i) {
+                    const int q = lane + 64 * i;
+                    need |= (q < nqb && cnt[q] > trigger) ? 1 : 0;
+                }
+                if (__any(need)) {       // (uniform: every wave read the same counters)
+                    mf_barrier_drain();  // all candidate stores complete before a wave compacts a buffer
+                    for (int q = wid; q < nqb; q += 8) {
+                        const int n = cnt[q];
+                        if (n > trigger) {
+                            mf_wave_compact<MFMA_CAP / 64>(cand + (size_t)q * a.cap, n < a.cap ? n : a.cap, a.Kp,
+                                                           &thr_key[q], &thr_f[q], a.drop ? a.drop + q : nullptr,
+                                                           lane);
+                            if (lane == 0) cnt[q] = a.Kp;
+                        }
+                    }
+                    mf_barrier_drain();  // counters / thresholds / compacted buffers published
+                }
+            }
+        }
+        {
+            const uint32_t slot_lds = ring + lane_off;
+            I8D_STEP0(A[0][0], A[0][1]);
+        }
+        I8D_BODY(1, I8D_STEP);
+        I8D_BODY(2, I8D_STEP);
+        I8D_BODY(3, I8D_STEP);
+        for (int ks0 = I8D_U; ks0 < nks; ks0 += I8D_U) {
+            I8D_BODY(0, I8D_STEP);
+            I8D_BODY(1, I8D_STEP);
+            I8D_BODY(2, I8D_STEP);
+            I8D_BODY(3, I8D_STEP);
+        }
+        // the epilogue reads the last MFMAs' results (the hazard recognizer does not see the asm)
+        asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+        // ---- tile epilogue ----
+        int olane;  // asm-opaque lane id: lane-derived indices are not hoisted out of the K loop
+        asm volatile("v_mov_b32 %0, %1" : "=v"(olane) : "v"(lane));
+        const int64_t rowbase = (int64_t)ti * TR;
+        const int rw0 = wid * 32 + (olane >> 4) * 4;  // + 16 m + r
+        const int qlane = olane & 15;                  // + 16 n
+        float sq[2][4], rb[2][4];                      // the rows' scale and error norm
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+            const uint4 w = *(const uint4*)(rowx + (ti & 1) * TR + rw0 + m * 16);
+            const uint32_t w4[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                sq[m][r] = __uint_as_float(w4[r] << 16);
+                rb[m][r] = __uint_as_float(w4[r] & 0xFFFF0000u);
+            }
+        }
+        // the shard's last tile: rows >= n_valid (garbage side data) never qualify -> no bound test,
+        // every column takes the per-row path, which makes those rows NaN
+        const bool edge = rowbase + TR > a.n_valid;
+        uint32_t bad = 0;
+        float smax = sq[0][0], smin = sq[0][0], bmax = rb[0][0];
+        if (edge) {
+#pragma unroll
+            for (int m = 0; m < 2; ++m)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if (rowbase + rw0 + m * 16 + r >= a.n_valid) bad |= 1u << (m * 4 + r);
+        } else {
+#pragma unroll
+            for (int m = 0; m < 2; ++m)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    smax = fmaxf(smax, sq[m][r]);
+                    smin = fminf(smin, sq[m][r]);
+                    bmax = fmaxf(bmax, rb[m][r]);
+                }
+        }
+#pragma unroll
+        for (int n = 0; n < 16; ++n) {
+            const int q = 16 * n + qlane;
+            const float2 f = qfac[q];  // (t_q, ||q|| / t_q): key = t_q * (s_x acc + beta_x ||q|| / t_q)
+            const float tf = thr_f[q];
+            bool go = true;
+            if (!edge) {
+                // bound of the column's 8 keys: max acc (exact int) -> fp32, times the rows' largest
+                // (acc >= 0) or smallest (acc < 0) scale, plus the largest error norm; each step is
+                // monotone, so a key that would pass implies a bound that passes
+                const int mi = max(max(max(acc[0][n][0], acc[0][n][1]), max(acc[0][n][2], acc[0][n][3])),
+                                   max(max(acc[1][n][0], acc[1][n][1]), max(acc[1][n][2], acc[1][n][3])));
+                const float fm = (float)mi;
+                go = __builtin_fmaf(bmax, f.y, fmaxf(smax * fm, smin * fm)) * f.x >= tf;
+            }
+            if (!go) continue;
+            float v[8];
+#pragma unroll
+            for (int m = 0; m < 2; ++m)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float x = __builtin_fmaf(rb[m][r], f.y, (float)acc[m][n][r] * sq[m][r]) * f.x;
+                    v[m * 4 + r] = (bad >> (m * 4 + r)) & 1u ? __builtin_nanf("") : x;
+                }
+            uint32_t mh = 0;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) mh |= (v[j] >= tf ? 1u : 0u) << j;  // (ties resolved by key below)
+            if (!mh) continue;
+            flag[2 + (ti & 1)] = 1;
+            const u64 tk = thr_key[q];
+            *(float4*)(sx) = make_float4(v[0], v[1], v[2], v[3]);
+            *(float4*)(sx + 4) = make_float4(v[4], v[5], v[6], v[7]);
+            while (mh) {  // compact insert loop: the LDS pool, a direct store when it is full
+                const int j = __builtin_ctz(mh);
+                mh &= mh - 1u;
+                const u64 key = mk_key(sx[j], (uint32_t)(rowbase + rw0 + (j >> 2) * 16 + (j & 3)));
+                if (key <= tk) continue;  // score == threshold and not ahead of it by id
+                const int ps = atomicAdd(&flag[1], 1);
+                if (ps < MF_POOL) {
+                    pool_key[ps] = key;
+                    pool_q[ps] = q;
+                    continue;
+                }
+                const int slot = atomicAdd(&cnt[q], 1);
+                if (slot < a.cap) cand[(size_t)q * a.cap + slot] = key;
+            }
+        }
+        check_pending = true;
+    }
+#undef I8D_ISSUE
+#undef I8D_BODY
+    // ---- flush: pool -> buffers, then the best <= Kp per query -> the query's survivor list ----
+    mf_barrier_drain();  // (also drains the dummy steps' loads)
+    {
+        int np = flag[1];
+        np = np < MF_POOL ? np : MF_POOL;
+        for (int j = tid; j < np; j += MF_THREADS) {
+            const int q = pool_q[j];
+            const int slot = atomicAdd(&cnt[q], 1);
+            if (slot < a.cap) cand[(size_t)q * a.cap + slot] = pool_key[j];
+        }
+    }
+    mf_barrier_drain();
+    for (int q = wid; q < nqb; q += 8) {
+        int n = cnt[q];
+        if (n > a.cap) n = a.cap;
+        if (n > a.Kp) {
+            mf_wave_compact<MFMA_CAP / 64>(cand + (size_t)q * a.cap, n, a.Kp, &thr_key[q], &thr_f[q],
+                                           a.drop ? a.drop + q : nullptr, lane);
+            n = a.Kp;
+        }
+        if (n == 0) continue;
+        int off = 0;
+        if (lane == 0) off = atomicAdd(&a.gcnt[q], n);
+        off = __shfl(off, 0, 64);
+        u64* dst = a.glist + (size_t)q * a.lcap + off;
         for (int j = lane; j < n; j += 64) dst[j] = cand[(size_t)q * a.cap + j];
     }
 }
@@ -2653,17 +2972,23 @@ hipError_t launch_pack_qf32(const float* q, int nqb, int nqpad, int d, int dpad,
     return hipGetLastError();
 }
 
+// Dynamic-LDS limit of a kernel, set once per (kernel, device) -- the attribute is per device, and
+// several threads may launch at once (vs_multi runs one worker per device); thread-safe.
+static void set_lds_attr(const void* fn, int bytes) {
+    static std::mutex mu;
+    static std::set<std::pair<const void*, int>> done;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(mu);
+    if (!done.insert({fn, dev}).second) return;
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    (void)hipGetLastError();  // an attribute failure must not surface as the launch's error
+}
+
 template <int DT, int METRIC, bool SEED>
 static void launch_mfma_one(const ScreenArgs& a, const uint8_t* qt, int nqb, hipStream_t st) {
-    static bool attr_set = false;  // benign race: idempotent attribute
-    if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)k_screen_mfma<DT, METRIC, SEED>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, MF_LDS);
-        if constexpr (!SEED && DT != DT_I8)
-            (void)hipFuncSetAttribute((const void*)k_screen_mfma_redo<DT, METRIC>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, MF_LDS);
-        attr_set = true;
-    }
+    set_lds_attr((const void*)k_screen_mfma<DT, METRIC, SEED>, MF_LDS);
+    if constexpr (!SEED && DT != DT_I8) set_lds_attr((const void*)k_screen_mfma_redo<DT, METRIC>, MF_LDS);
     if constexpr (!SEED && DT != DT_I8) {
         if (a.gate) {
             hipLaunchKernelGGL((k_screen_mfma_redo<DT, METRIC>), dim3(a.G), dim3(MF_THREADS), MF_LDS, st, a, qt, nqb);
@@ -2677,6 +3002,12 @@ static hipError_t launch_mfma_dt(int dt, const ScreenArgs& a, const uint8_t* qt,
     if (a.gate && (SEED || dt == DT_I8)) return hipErrorInvalidValue;  // fallback rounds: native main screen
     if (dt == DT_I8) {
         if (a.metric != METRIC_IP || !a.rsb || !a.qfac) return hipErrorInvalidValue;
+        if (!SEED && i8_direct_ok(a.dpad)) {  // the main pass: direct form (no seed-tile reuse)
+            if (a.seed_acc || a.tile_stride != 0) return hipErrorInvalidValue;
+            set_lds_attr((const void*)k_screen_i8d, I8D_LDS);
+            hipLaunchKernelGGL(k_screen_i8d, dim3(a.G), dim3(MF_THREADS), I8D_LDS, st, a, qt, nqb);
+            return hipGetLastError();
+        }
         launch_mfma_one<DT_I8, METRIC_IP, SEED>(a, qt, nqb, st);
     } else if (dt == DT_BF16) {
         if (a.metric == METRIC_IP) launch_mfma_one<DT_BF16, METRIC_IP, SEED>(a, qt, nqb, st);
@@ -2695,12 +3026,7 @@ hipError_t launch_screen_mfma(int dt, const ScreenArgs& a, const uint8_t* qt, in
 
 template <int DT, int METRIC>
 static void launch_mapped_one(const ScreenArgs& a, const uint8_t* qt, hipStream_t st) {
-    static bool attr_set = false;  // benign race: idempotent attribute
-    if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)k_screen_mfma_mapped<DT, METRIC>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, MF_LDS_MAP);
-        attr_set = true;
-    }
+    set_lds_attr((const void*)k_screen_mfma_mapped<DT, METRIC>, MF_LDS_MAP);
     hipLaunchKernelGGL((k_screen_mfma_mapped<DT, METRIC>), dim3(a.G), dim3(MF_THREADS), MF_LDS_MAP, st, a, qt, 0);
 }
 bool check_map_desc(const int* g, int64_t tmap_len, int n_qtiles, int64_t qmap_len) {
@@ -2782,16 +3108,8 @@ hipError_t launch_merge(const u64* in, int nseg, int qstride, int nq, int Kp, u6
 
 template <int DT, int METRIC, bool QLDS>
 static void launch_refine_one(const RefineArgs& a, int nq, int KP2, size_t lds, hipStream_t st) {
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_refine<DT, METRIC, QLDS>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  152 * 1024);
-        if constexpr (DT != DT_F32)
-            (void)hipFuncSetAttribute((const void*)k_refine_redo<DT, METRIC, QLDS>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 152 * 1024);
-        (void)hipGetLastError();  // an attribute failure must not surface as the launch's error
-        attr = true;
-    }
+    set_lds_attr((const void*)k_refine<DT, METRIC, QLDS>, 152 * 1024);
+    if constexpr (DT != DT_F32) set_lds_attr((const void*)k_refine_redo<DT, METRIC, QLDS>, 152 * 1024);
     if constexpr (DT != DT_F32) {
         if (a.redo) {
             hipLaunchKernelGGL((k_refine_redo<DT, METRIC, QLDS>), dim3(nq), dim3(RF_THREADS), lds, st, a, KP2);
@@ -2841,13 +3159,7 @@ hipError_t launch_refine(const RefineArgs& a, int nq, hipStream_t st) {
 
 template <int DT, bool QLDS>
 static void launch_refine_wide_one(const RefineArgs& a, int nq, int KA, size_t lds, hipStream_t st) {
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_refine_wide<DT, QLDS>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  152 * 1024);
-        (void)hipGetLastError();
-        attr = true;
-    }
+    set_lds_attr((const void*)k_refine_wide<DT, QLDS>, 152 * 1024);
     hipLaunchKernelGGL((k_refine_wide<DT, QLDS>), dim3(nq), dim3(RF_THREADS), lds, st, a, KA);
 }
 
@@ -3258,12 +3570,7 @@ __global__ void __launch_bounds__(HN_THREADS) k_hnsw_search(HnswArgs a) {
 
 template <int DT, int METRIC, bool QLDS>
 static void launch_hnsw_one(const HnswArgs& a, int nq, size_t lds, hipStream_t st) {
-    static bool attr_set = false;  // benign race: idempotent attribute
-    if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)k_hnsw_search<DT, METRIC, QLDS>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)HN_LDS_CAP);
-        attr_set = true;
-    }
+    set_lds_attr((const void*)k_hnsw_search<DT, METRIC, QLDS>, (int)HN_LDS_CAP);
     hipLaunchKernelGGL((k_hnsw_search<DT, METRIC, QLDS>), dim3(nq), dim3(HN_THREADS), lds, st, a);
 }
 template <int DT>

@@ -1,0 +1,91 @@
+"""ISA check of the direct int8 screen (k_screen_i8d): build-time evidence that the inline-asm
+corpus loads are only ever read by the MFMAs, i.e. that hipcc inserted no copy, spill or other
+read of a fragment register that could run before the kernel's own s_waitcnt.
+
+    python scripts/check_i8d_isa.py [vs_kernels.s]   (default: compiles vs_kernels.hip to asm)
+
+Checks, for the kernel's code: no scratch (spill) traffic; every register written by a corpus load
+(`global_load_dwordx4 ... nt`) is read only by v_mfma instructions; one s_barrier per K-step body.
+Exit status 0 = pass.
+"""
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SRC = os.path.join(HERE, "..", "photo_search_engine_amd", "csrc", "vs_kernels.hip")
+
+
+def regs(spec: str):
+    m = re.fullmatch(r"v\[(\d+):(\d+)\]", spec)
+    if m:
+        return set(range(int(m.group(1)), int(m.group(2)) + 1))
+    m = re.fullmatch(r"v(\d+)", spec)
+    return {int(m.group(1))} if m else set()
+
+
+def operands(line: str):
+    body = line.split(";")[0].strip()
+    parts = body.split(None, 1)
+    if len(parts) < 2:
+        return parts[0] if parts else "", []
+    return parts[0], [o.strip() for o in parts[1].split(",")]
+
+
+def main() -> int:
+    if len(sys.argv) > 1:
+        asm = open(sys.argv[1]).read()
+    else:
+        with tempfile.TemporaryDirectory() as td:
+            out = os.path.join(td, "k.s")
+            subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "--cuda-device-only",
+                            "-S", "-Wno-inline-asm", "-o", out, SRC], check=True)
+            asm = open(out).read()
+    start = asm.index("_ZN2vs12k_screen_i8dENS_10ScreenArgsEPKhi:")
+    end = asm.index(".Lfunc_end", start)
+    raw = asm[start:end].split("\n")
+    code = [f"{l}  ;#L{i}" for i, l in enumerate(raw) if l.strip() and not l.strip().startswith((";", "."))]
+    bad = []
+    if any("scratch_" in l for l in code):
+        bad.append("scratch (spill) instructions present")
+    # Forward scan from every corpus load (in layout order, the load's fall-through path) to the
+    # first MFMA that reads its registers or the first redefinition of them: no other instruction
+    # may READ them in between (a copy or spill there would read the register before the kernel's
+    # s_waitcnt lets the load land).  The compiler never writes a register it believes live, so
+    # writes need no check.
+    def split(l):
+        op, ops = operands(l)
+        if not ops:
+            return op, set(), set()
+        if op.startswith(("global_load_lds", "s_")) or op.startswith(("global_store", "ds_write")):
+            return op, set(), set().union(*[regs(o) for o in ops])
+        return op, regs(ops[0]), set().union(*[regs(o) for o in ops[1:]]) if len(ops) > 1 else set()
+    parsed = [split(l) for l in code]
+    loaded = set()
+    for i, l in enumerate(code):
+        op, dst, _ = parsed[i]
+        if not (op == "global_load_dwordx4" and l.split(";")[0].rstrip().endswith("nt")):
+            continue
+        loaded |= dst
+        for j in range(i + 1, len(code)):
+            op2, dst2, src2 = parsed[j]
+            if op2.startswith("v_mfma") and src2 & dst:
+                break
+            if src2 & dst:
+                bad.append(f"corpus fragment {sorted(dst)[0]}.. read before its MFMA by: {code[j].strip()}")
+                break
+            if dst2 & dst:
+                break
+    nmfma = sum(1 for l in code if l.strip().startswith("v_mfma"))
+    nbar = sum(1 for l in code if l.strip().startswith("s_barrier"))
+    print(f"k_screen_i8d: {len(code)} instructions, {nmfma} MFMA, {nbar} s_barrier, "
+          f"{len(loaded)} corpus-fragment VGPRs")
+    for b in bad[:20]:
+        print("FAIL:", b)
+    return 1 if bad else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -52,6 +52,22 @@ def test_int8_screen_exact(FlatIndex, dtype, nq, k, N, d):
     ix.close()
 
 
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("nq,k,N,d", [(40, 10, 9000, 512), (256, 100, 20000, 768), (300, 7, 3001, 1024),
+                                     (64, 1000, 150000, 512), (17, 1, 5000, 512), (200, 50, 70000, 1536)])
+def test_int8_direct_screen_exact(FlatIndex, dtype, nq, k, N, d):
+    """d a multiple of 256 (K-steps per tile a multiple of 4): the main pass is the direct form
+    k_screen_i8d (corpus fragments straight to registers).  Unseeded and seeded corpora, a partial
+    last tile, k = 1000 (candidate compaction in the K loop), two query blocks."""
+    ix = FlatIndex(d, "ip", dtype)
+    ix.add_synthetic(O.SEED_CORPUS + 5, 0, N, True)
+    ix.set_screen("int8")
+    q = O.synth_rows(O.SEED_QUERIES + 5, 0, nq, d, True, "f32")
+    _exact(ix, q, k)
+    assert ix.uncertified_count() == 0
+    ix.close()
+
+
 @pytest.mark.parametrize("k", [10, 100])
 def test_int8_screen_seeded_matches_native(FlatIndex, k):
     # >= 4 tiles per CU: the int8 seed pass, optimistic union and adaptive refine depth
@@ -68,11 +84,12 @@ def test_int8_screen_seeded_matches_native(FlatIndex, k):
     ix.close()
 
 
-def test_int8_screen_ties_zero_rows_and_incremental_adds(FlatIndex):
+@pytest.mark.parametrize("d", [64, 512])
+def test_int8_screen_ties_zero_rows_and_incremental_adds(FlatIndex, d):
     rng = np.random.default_rng(5)
-    base = rng.standard_normal((60, 64)).astype(np.float32)
-    x = np.concatenate([base, np.repeat(base[7:8], 300, axis=0), np.zeros((40, 64), np.float32), base], axis=0)
-    ix = FlatIndex(64, "ip", "bf16")
+    base = rng.standard_normal((60, d)).astype(np.float32)
+    x = np.concatenate([base, np.repeat(base[7:8], 300, axis=0), np.zeros((40, d), np.float32), base], axis=0)
+    ix = FlatIndex(d, "ip", "bf16")
     ix.add(x[:100])
     ix.set_screen("int8")
     ix.add(x[100:])  # the int8 copy follows later adds
