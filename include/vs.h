@@ -236,8 +236,9 @@ int vs_ivf_last_search_stats(const vs_ivf* ivf, int* mfma_lists, int* uncertifie
  * which changes no search.  vs_hnsw_search runs faiss HNSW::search (greedy descent on the upper
  * levels, then efSearch-bounded best-first search on level 0; oracle/hnsw_oracle.py) on the GPU,
  * one workgroup per query, with the flat path's exact canonical scores as distances: D = scores
- * (IP) / squared distances (L2) best first, I = row ids, -1 padded.  The index must hold exactly
- * the graph's rows when searched (VS_ERR_ARG otherwise); max(ef_search, k) <= 2048. */
+ * (IP) / squared distances (L2) best first, I = row ids, -1 padded.  The graph covers the first
+ * n rows of the index: rows added behind it are not reachable (the caller searches them exactly
+ * and merges); an index holding fewer than n rows is VS_ERR_ARG; max(ef_search, k) <= 2048. */
 typedef struct vs_hnsw vs_hnsw;
 
 int vs_hnsw_create(vs_index* index, int64_t n, const int32_t* levels, const uint64_t* offsets,

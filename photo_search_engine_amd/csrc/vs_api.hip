@@ -65,6 +65,7 @@ struct Ctx {
     PinnedPair pin;  // read_rows_host: pinned landing chunks
     HostBuf hq;      // vs_search: the query batch, staged for the H2D copy
     HostBuf hout;    // vs_search: I (int64), D (fp32) and certificates land here; search_exact_device: certificates
+    unsigned* unres = nullptr;  // this call's unresolved-query counter (device), instead of the index's
     ~Ctx() {
         for (DevBuf* b : {&qdev, &qtile, &qinfo, &qpad, &cand, &part, &merge_a, &merge_b, &outD, &outI, &outS, &cert, &thr0,
                           &seedmax, &gcnt, &rows[0], &rows[1], &tilectr, &seedacc, &outAll, &qfac, &qeps, &drop, &fails, &rsc, &rdone})
@@ -615,7 +616,7 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
     r.I = I;
     r.S64 = S64;
     r.cert = cert;
-    r.uncert = redo ? ix->d_unres : ix->d_uncert;
+    r.uncert = redo ? (c->unres ? c->unres : ix->d_unres) : ix->d_uncert;
     r.fails = redo ? nullptr : c->fails.as<int>();
     r.redo = redo ? 1 : 0;
     r.gate = gate;
@@ -676,7 +677,7 @@ void check_index(const vs_index* ix) {
 // and such a query raises VS_ERR_UNCERTIFIED, as in vs_search.  fp32 indexes (GEMV re-search):
 // read back the certificates and re-search with deeper screens, as vs_search does.
 void vs::search_exact_device(vs_index* ix, const float* q_dev, int64_t nq, int k, int64_t* I_dev, double* S64_dev,
-                             hipStream_t st, float* D_dev, int64_t id_offset, bool async) {
+                             hipStream_t st, float* D_dev, int64_t id_offset, bool async, unsigned* unres) {
     check_index(ix);
     if (nq <= 0) return;
     std::shared_lock<std::shared_mutex> lk(ix->rw);
@@ -688,6 +689,11 @@ void vs::search_exact_device(vs_index* ix, const float* q_dev, int64_t nq, int k
     c->cert.ensure((size_t)nq * sizeof(int));
     const int Kp = screen_depth(k);
     const bool on_device = ix->dtype != DT_F32;
+    struct UnresScope {  // the caller's counter for this call only (the Ctx goes back to the pool)
+        Ctx* c;
+        ~UnresScope() { c->unres = nullptr; }
+    } us{c};
+    c->unres = unres;
     search_all(ix, c, q_dev, nq, k, Kp, D_dev ? D_dev : c->outD.as<float>(), I_dev, S64_dev, c->cert.as<int>(),
                id_offset, st, kOptimisticSeedRank, on_device);
     if (on_device && async) return;
@@ -715,6 +721,14 @@ void vs::search_exact_device(vs_index* ix, const float* q_dev, int64_t nq, int k
 }
 
 unsigned* vs::unresolved_counter(vs_index* ix) { return ix->d_unres; }
+
+void vs::truncate_rows(vs_index* ix, int64_t n) {
+    check_index(ix);
+    std::unique_lock<std::shared_mutex> lk(ix->rw);
+    if (n < 0 || n > ix->ntotal) throw VsError(VS_ERR_ARG, "truncate_rows: n outside [0, ntotal]");
+    ix->ntotal = n;  // the rows behind stay allocated and are never read again (appends overwrite them)
+}
+
 
 int64_t vs::stream_chunk_rows(int d) { return std::max<int64_t>(1, (int64_t)(32 << 20) / ((int64_t)d * 4)); }
 

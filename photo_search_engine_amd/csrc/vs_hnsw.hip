@@ -146,9 +146,11 @@ int vs_hnsw_search(vs_hnsw* h, const float* q, int64_t nq, int32_t k, int32_t ef
         std::lock_guard<std::mutex> lk(h->mtx);
         std::shared_lock<std::shared_mutex> rl(flat_lock(h->ix));
         const FlatView fv = flat_view(h->ix);
-        if (fv.ntotal != h->n)
+        // rows are append-only, so a graph over the first h->n rows stays valid while rows are
+        // added behind it (the host searches those exactly and merges); fewer rows = a reset index
+        if (fv.ntotal < h->n)
             throw VsError(VS_ERR_ARG, "vs_hnsw_search: the graph covers " + std::to_string(h->n) +
-                                          " rows, the index holds " + std::to_string(fv.ntotal));
+                                          " rows, the index holds only " + std::to_string(fv.ntotal));
         if (hnsw_lds_bytes(fv.d, k, ef, h->nbmax) > 160 * 1024 - 512)
             throw VsError(VS_ERR_ARG, "vs_hnsw_search: k / ef_search too large for one workgroup's LDS");
         DeviceGuard g(h->device);

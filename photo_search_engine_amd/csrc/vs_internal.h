@@ -365,8 +365,14 @@ int64_t stream_chunk_rows(int d);  // rows per pinned chunk (32 MiB of fp32)
 // Exact top-k of device queries over a flat index, certificate failures re-searched (bf16/f16: by
 // a gated fallback round on the device; async = no host sync, unresolved queries counted in
 // vs_unresolved_count instead of raising).  I_dev [nq][k], S64_dev optional.
+// unres (optional): a device counter of this call's queries even the fallback round could not
+// certify (default: the index's counter behind vs_unresolved_count)
 void search_exact_device(vs_index* ix, const float* q_dev, int64_t nq, int k, int64_t* I_dev, double* S64_dev,
-                         hipStream_t st, float* D_dev = nullptr, int64_t id_offset = 0, bool async = false);
+                         hipStream_t st, float* D_dev = nullptr, int64_t id_offset = 0, bool async = false,
+                         unsigned* unres = nullptr);
+// drop rows [n, ntotal) of a flat index (rows are append-only: a failed multi-device add rolls back
+// the shards that took their rows); the running maxima stay (they only widen certificate margins)
+void truncate_rows(vs_index* ix, int64_t n);
 unsigned* unresolved_counter(vs_index* ix);  // device word behind vs_unresolved_count
 // seed pass: screen one tile per workgroup (tile_stride) and write per-query 16-row-group maxima
 hipError_t launch_seed_mfma(int dt, const ScreenArgs& a, const uint8_t* qt, int nqb, hipStream_t st);

@@ -11,6 +11,10 @@
 //     and copies its (fp64 score, id) lists to device 0 over xGMI (peer copies); device 0 merges
 //     the G sorted lists (k_merge_shards: score, then lower global id) and returns D / I.
 // The merged order is total, so the result equals one index over all rows, bit for bit.
+// Concurrency (the reference serves from Flask's threaded server, /root/reference/main.py:353):
+// searches hold the handle's lock shared and lease a per-call context (streams, buffers, events,
+// counters and one worker per device), so concurrent searches run concurrently on every device;
+// adds, resets and screen switches take it exclusively.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -18,6 +22,7 @@
 #include <cstring>
 #include <functional>
 #include <mutex>
+#include <shared_mutex>
 #include <thread>
 #include <vector>
 
@@ -109,19 +114,26 @@ void throw_rc(int rc) {
 
 }  // namespace
 
+// one search's resources on every device, leased per call
+struct MCtx {
+    std::vector<hipStream_t> st;
+    std::vector<DevBuf> qdev, S, I, unres_d;  // per device: queries, per-shard lists, unresolved count
+    std::vector<hipEvent_t> ready;            // per device: its lists landed on device 0
+    unsigned* unres_h = nullptr;              // pinned, per device: this call's unresolved queries
+    DevBuf gS, gI, oS, oI, oD;                // device 0: gathered [G][nq][k] lists, merged outputs
+    Pool* pool = nullptr;                     // one worker per device (fp32 shards wait on the host)
+};
+
 struct vs_multi {
     int d = 0, metric = 0, dtype = 0, G = 0;
     std::vector<int> dev;
     std::vector<vs_index*> ix;
-    std::vector<hipStream_t> st;
-    std::vector<DevBuf> qdev, S, I;  // per device: queries, per-shard fp64 scores / global ids
-    DevBuf gS, gI, oS, oI, oD;       // device 0: gathered [G][nq][k] lists, merged outputs
-    hipEvent_t* ready = nullptr;     // per device: its lists landed on device 0
-    unsigned* unres_h = nullptr;     // pinned, per device: the shard's unresolved-query counter ...
-    std::vector<unsigned> unres_seen;  // ... and its value after the previous search
     int64_t ntotal = 0;
-    std::mutex mu;                   // searches and adds are serialised on a multi-device handle
+    std::shared_mutex rw;   // searches / reads shared; adds, resets, screen switches exclusive
+    std::mutex pool_mu;     // the shared worker pool of the non-search jobs
     Pool* pool = nullptr;
+    std::mutex ctx_mu;      // search contexts: every one ever made, the idle ones
+    std::vector<MCtx*> ctx_all, ctx_idle;
 };
 
 namespace {
@@ -155,6 +167,76 @@ void locate(const vs_multi* m, int64_t id, int* g, int64_t* local) {
 
 extern "C" {
 
+namespace {
+
+void destroy_ctx(vs_multi* m, MCtx* c) {
+    delete c->pool;
+    for (int g = 0; g < (int)c->st.size(); ++g) {
+        DeviceGuard dg(m->dev[g]);
+        if (c->st[g]) (void)hipStreamSynchronize(c->st[g]);
+        for (DevBuf* b : {&c->qdev[g], &c->S[g], &c->I[g], &c->unres_d[g]}) b->release();
+        if (c->ready[g]) (void)hipEventDestroy(c->ready[g]);
+        if (c->st[g]) (void)hipStreamDestroy(c->st[g]);
+    }
+    if (!m->dev.empty()) {
+        DeviceGuard dg(m->dev[0]);
+        for (DevBuf* b : {&c->gS, &c->gI, &c->oS, &c->oI, &c->oD}) b->release();
+    }
+    if (c->unres_h) (void)hipHostFree(c->unres_h);
+    delete c;
+}
+
+MCtx* make_ctx(vs_multi* m) {
+    MCtx* c = new MCtx();
+    const int G = m->G;
+    c->st.assign(G, nullptr);
+    c->ready.assign(G, nullptr);
+    c->qdev.resize(G);
+    c->S.resize(G);
+    c->I.resize(G);
+    c->unres_d.resize(G);
+    try {
+        for (int g = 0; g < G; ++g) {
+            DeviceGuard dg(m->dev[g]);
+            HIP_CHECK(hipStreamCreateWithFlags(&c->st[g], hipStreamNonBlocking));
+            HIP_CHECK(hipEventCreateWithFlags(&c->ready[g], hipEventDisableTiming));
+            c->unres_d[g].ensure(sizeof(unsigned));
+        }
+        HIP_CHECK(hipHostMalloc((void**)&c->unres_h, sizeof(unsigned) * G, hipHostMallocDefault));
+        std::memset(c->unres_h, 0, sizeof(unsigned) * G);
+        c->pool = new Pool(G);
+    } catch (...) {
+        destroy_ctx(m, c);
+        throw;
+    }
+    return c;
+}
+
+// a search context for one call: an idle one, or a new one (concurrency grows the set)
+struct CtxLease {
+    vs_multi* m;
+    MCtx* c;
+    explicit CtxLease(vs_multi* mm) : m(mm), c(nullptr) {
+        {
+            std::lock_guard<std::mutex> lk(m->ctx_mu);
+            if (!m->ctx_idle.empty()) {
+                c = m->ctx_idle.back();
+                m->ctx_idle.pop_back();
+                return;
+            }
+        }
+        c = make_ctx(m);
+        std::lock_guard<std::mutex> lk(m->ctx_mu);
+        m->ctx_all.push_back(c);
+    }
+    ~CtxLease() {
+        std::lock_guard<std::mutex> lk(m->ctx_mu);
+        m->ctx_idle.push_back(c);
+    }
+};
+
+}  // namespace
+
 int vs_multi_create(int d, int metric, int dtype, int n_dev, const int* dev_ids, vs_multi** out) {
     return guarded([&] {
         if (!out) throw VsError(VS_ERR_ARG, "out is null");
@@ -171,28 +253,14 @@ int vs_multi_create(int d, int metric, int dtype, int n_dev, const int* dev_ids,
                 vs_index* x = nullptr;
                 throw_rc(vs_create(d, metric, dtype, dev_ids[g], &x));
                 m->ix.push_back(x);
-                DeviceGuard dg(dev_ids[g]);
-                hipStream_t s = nullptr;
-                HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-                m->st.push_back(s);
                 if (dev_ids[g] != dev_ids[0]) {  // xGMI peer path to device 0 (best effort: copies work either way)
+                    DeviceGuard dg(dev_ids[g]);
                     int can = 0;
                     if (hipDeviceCanAccessPeer(&can, dev_ids[g], dev_ids[0]) == hipSuccess && can)
                         (void)hipDeviceEnablePeerAccess(dev_ids[0], 0);
                     (void)hipGetLastError();
                 }
             }
-            m->qdev.resize(n_dev);
-            m->S.resize(n_dev);
-            m->I.resize(n_dev);
-            m->ready = new hipEvent_t[n_dev]();
-            for (int g = 0; g < n_dev; ++g) {
-                DeviceGuard dg(dev_ids[g]);
-                HIP_CHECK(hipEventCreateWithFlags(&m->ready[g], hipEventDisableTiming));
-            }
-            HIP_CHECK(hipHostMalloc((void**)&m->unres_h, sizeof(unsigned) * n_dev, hipHostMallocDefault));
-            std::memset(m->unres_h, 0, sizeof(unsigned) * n_dev);
-            m->unres_seen.assign(n_dev, 0u);
             m->pool = new Pool(n_dev);
         } catch (...) {
             vs_multi_destroy(m);
@@ -204,25 +272,51 @@ int vs_multi_create(int d, int metric, int dtype, int n_dev, const int* dev_ids,
 
 void vs_multi_destroy(vs_multi* m) {
     if (!m) return;
+    for (MCtx* c : m->ctx_all) destroy_ctx(m, c);
     delete m->pool;
-    if (m->unres_h) (void)hipHostFree(m->unres_h);
     for (int g = 0; g < (int)m->ix.size(); ++g) {
         DeviceGuard dg(m->dev[g]);
         (void)hipDeviceSynchronize();
-        m->qdev[g].release();
-        m->S[g].release();
-        m->I[g].release();
-        if (m->ready && m->ready[g]) hipEventDestroy(m->ready[g]);
-        if (g < (int)m->st.size() && m->st[g]) hipStreamDestroy(m->st[g]);
         vs_destroy(m->ix[g]);
     }
-    if (!m->dev.empty()) {
-        DeviceGuard dg(m->dev[0]);
-        for (DevBuf* b : {&m->gS, &m->gI, &m->oS, &m->oI, &m->oD}) b->release();
-    }
-    delete[] m->ready;
     delete m;
 }
+
+namespace {
+// append n global rows on the shards (add(g, piece) per shard piece, the devices in parallel); if
+// any shard fails, the shards that took their rows are truncated back, so the shard row counts
+// always match the chunk dealing of ntotal rows (global ids stay arithmetic); caller holds rw
+// exclusively
+void multi_append(vs_multi* m, int64_t n, const std::function<void(int, const Piece&)>& add) {
+    const auto pieces = split_rows(m->G, m->ntotal, n);
+    std::vector<int64_t> before(m->G);
+    for (int g = 0; g < m->G; ++g) before[g] = vs_ntotal(m->ix[g]);
+    try {
+        std::lock_guard<std::mutex> pl(m->pool_mu);
+        m->pool->run([&](int g) {
+            for (const Piece& p : pieces[g]) add(g, p);
+        });
+    } catch (...) {
+        for (int g = 0; g < m->G; ++g) {
+            try {
+                if (vs_ntotal(m->ix[g]) > before[g]) truncate_rows(m->ix[g], before[g]);
+            } catch (...) {
+            }
+        }
+        throw;
+    }
+    m->ntotal += n;
+    const auto want = split_rows(m->G, 0, m->ntotal);
+    for (int g = 0; g < m->G; ++g) {
+        int64_t rows = 0;
+        for (const Piece& p : want[g]) rows += p.n;
+        if (vs_ntotal(m->ix[g]) != rows)
+            throw VsError(VS_ERR_INTERNAL, "multi-device add: shard " + std::to_string(g) + " holds " +
+                                               std::to_string(vs_ntotal(m->ix[g])) + " rows, expected " +
+                                               std::to_string(rows));
+    }
+}
+}  // namespace
 
 int vs_multi_add(vs_multi* m, const float* x, int64_t n) {
     return guarded([&] {
@@ -230,12 +324,8 @@ int vs_multi_add(vs_multi* m, const float* x, int64_t n) {
         if (n < 0) throw VsError(VS_ERR_ARG, "n must be >= 0");
         if (n == 0) return;
         if (!x) throw VsError(VS_ERR_ARG, "x is null");
-        std::lock_guard<std::mutex> lk(m->mu);
-        const auto pieces = split_rows(m->G, m->ntotal, n);
-        m->pool->run([&](int g) {
-            for (const Piece& p : pieces[g]) throw_rc(vs_add(m->ix[g], x + p.src * m->d, p.n));
-        });
-        m->ntotal += n;
+        std::unique_lock<std::shared_mutex> lk(m->rw);
+        multi_append(m, n, [&](int g, const Piece& p) { throw_rc(vs_add(m->ix[g], x + p.src * m->d, p.n)); });
     });
 }
 
@@ -244,13 +334,10 @@ int vs_multi_add_from_file(vs_multi* m, const char* path, int64_t byte_offset, i
         if (!m || !path) throw VsError(VS_ERR_ARG, "null argument");
         if (n < 0 || byte_offset < 0) throw VsError(VS_ERR_ARG, "bad range");
         if (n == 0) return;
-        std::lock_guard<std::mutex> lk(m->mu);
-        const auto pieces = split_rows(m->G, m->ntotal, n);
-        m->pool->run([&](int g) {
-            for (const Piece& p : pieces[g])
-                throw_rc(vs_add_from_file(m->ix[g], path, byte_offset + p.src * m->d * (int64_t)sizeof(float), p.n));
+        std::unique_lock<std::shared_mutex> lk(m->rw);
+        multi_append(m, n, [&](int g, const Piece& p) {
+            throw_rc(vs_add_from_file(m->ix[g], path, byte_offset + p.src * m->d * (int64_t)sizeof(float), p.n));
         });
-        m->ntotal += n;
     });
 }
 
@@ -259,7 +346,8 @@ int vs_multi_write_rows_to_file(vs_multi* m, const char* path, int64_t byte_offs
         if (!m || !path) throw VsError(VS_ERR_ARG, "null argument");
         if (i0 < 0 || n < 0 || i0 + n > m->ntotal) throw VsError(VS_ERR_ARG, "row range out of bounds");
         if (n == 0) return;
-        std::lock_guard<std::mutex> lk(m->mu);
+        std::shared_lock<std::shared_mutex> lk(m->rw);
+        std::lock_guard<std::mutex> pl(m->pool_mu);
         const auto pieces = split_rows(m->G, i0, n);
         m->pool->run([&](int g) {  // disjoint file ranges: the devices write concurrently
             for (const Piece& p : pieces[g]) {
@@ -280,7 +368,7 @@ int vs_multi_search(vs_multi* m, const float* q, int64_t nq, int32_t k, float* D
         if (k <= 0) throw VsError(VS_ERR_ARG, "k must be > 0");
         if (nq == 0) return;
         if (!q || !D || !I) throw VsError(VS_ERR_ARG, "null host buffer");
-        std::lock_guard<std::mutex> lk(m->mu);
+        std::shared_lock<std::shared_mutex> lk(m->rw);  // concurrent searches; adds wait
         const float fillD = m->metric == VS_METRIC_IP ? -3.402823466e+38f : 3.402823466e+38f;
         const int kk = (int)std::min<int64_t>(k, m->ntotal);
         if (kk == 0) {
@@ -293,30 +381,35 @@ int vs_multi_search(vs_multi* m, const float* q, int64_t nq, int32_t k, float* D
         if (kk > KP_MAX * 4 / 5) throw VsError(VS_ERR_ARG, "k too large (max " + std::to_string(KP_MAX * 4 / 5) + ")");
         const int G = m->G;
         const size_t lb = (size_t)nq * kk;
+        CtxLease L(m);
+        MCtx* c = L.c;
         {
             DeviceGuard dg(m->dev[0]);
-            m->gS.ensure(lb * G * sizeof(double));
-            m->gI.ensure(lb * G * sizeof(int64_t));
-            m->oS.ensure(lb * sizeof(double));
-            m->oI.ensure(lb * sizeof(int64_t));
-            m->oD.ensure(lb * sizeof(float));
+            c->gS.ensure(lb * G * sizeof(double));
+            c->gI.ensure(lb * G * sizeof(int64_t));
+            c->oS.ensure(lb * sizeof(double));
+            c->oI.ensure(lb * sizeof(int64_t));
+            c->oD.ensure(lb * sizeof(float));
         }
-        m->pool->run([&](int g) {
+        c->pool->run([&](int g) {
             DeviceGuard dg(m->dev[g]);
-            hipStream_t s = m->st[g];
-            m->qdev[g].ensure((size_t)nq * m->d * sizeof(float));
-            m->S[g].ensure(lb * sizeof(double));
-            m->I[g].ensure(lb * sizeof(int64_t));
-            double* Sg = m->S[g].as<double>();
-            int64_t* Ig = m->I[g].as<int64_t>();
-            HIP_CHECK(hipMemcpyAsync(m->qdev[g].p, q, (size_t)nq * m->d * sizeof(float), hipMemcpyHostToDevice, s));
+            hipStream_t s = c->st[g];
+            c->qdev[g].ensure((size_t)nq * m->d * sizeof(float));
+            c->S[g].ensure(lb * sizeof(double));
+            c->I[g].ensure(lb * sizeof(int64_t));
+            double* Sg = c->S[g].as<double>();
+            int64_t* Ig = c->I[g].as<int64_t>();
+            c->unres_h[g] = 0;
+            HIP_CHECK(hipMemcpyAsync(c->qdev[g].p, q, (size_t)nq * m->d * sizeof(float), hipMemcpyHostToDevice, s));
             if (vs_ntotal(m->ix[g]) > 0) {
                 // exact per shard: uncertified screens are re-searched on this device, queued behind
-                // the first pass (no host round trip); the shard's count of queries even that
-                // round could not certify travels back with the results
-                throw_rc(vs_search_device_exact(m->ix[g], m->qdev[g].as<float>(), nq, kk, nullptr, Ig, Sg, 0, s));
-                HIP_CHECK(hipMemcpyAsync(&m->unres_h[g], unresolved_counter(m->ix[g]), sizeof(unsigned),
-                                         hipMemcpyDeviceToHost, s));
+                // the first pass (no host round trip for bf16 / f16 shards); the queries even that
+                // round could not certify are counted in THIS call's counter and travel back with
+                // the results
+                unsigned* ud = c->unres_d[g].as<unsigned>();
+                HIP_CHECK(hipMemsetAsync(ud, 0, sizeof(unsigned), s));
+                search_exact_device(m->ix[g], c->qdev[g].as<float>(), nq, kk, Ig, Sg, s, nullptr, 0, /*async*/ true, ud);
+                HIP_CHECK(hipMemcpyAsync(&c->unres_h[g], ud, sizeof(unsigned), hipMemcpyDeviceToHost, s));
                 hipLaunchKernelGGL(k_local_to_global, dim3((unsigned)((lb + 255) / 256)), dim3(256), 0, s, Ig,
                                    (int64_t)lb, G, g);
                 HIP_CHECK(hipGetLastError());
@@ -325,28 +418,27 @@ int vs_multi_search(vs_multi* m, const float* q, int64_t nq, int32_t k, float* D
                 std::vector<int64_t> wi(lb, -1);
                 HIP_CHECK(hipMemcpyAsync(Sg, ws.data(), lb * sizeof(double), hipMemcpyHostToDevice, s));
                 HIP_CHECK(hipMemcpyAsync(Ig, wi.data(), lb * sizeof(int64_t), hipMemcpyHostToDevice, s));
-                HIP_CHECK(hipStreamSynchronize(s));
+                HIP_CHECK(hipStreamSynchronize(s));  // (the host vectors go out of scope)
             }
             // this shard's lists into slot g of device 0's gather buffers (xGMI peer copy)
-            HIP_CHECK(hipMemcpyPeerAsync(m->gS.as<double>() + lb * g, m->dev[0], Sg, m->dev[g], lb * sizeof(double), s));
-            HIP_CHECK(hipMemcpyPeerAsync(m->gI.as<int64_t>() + lb * g, m->dev[0], Ig, m->dev[g], lb * sizeof(int64_t), s));
-            HIP_CHECK(hipEventRecord(m->ready[g], s));
+            HIP_CHECK(hipMemcpyPeerAsync(c->gS.as<double>() + lb * g, m->dev[0], Sg, m->dev[g], lb * sizeof(double), s));
+            HIP_CHECK(hipMemcpyPeerAsync(c->gI.as<int64_t>() + lb * g, m->dev[0], Ig, m->dev[g], lb * sizeof(int64_t), s));
+            HIP_CHECK(hipEventRecord(c->ready[g], s));
         });
         DeviceGuard dg(m->dev[0]);
-        hipStream_t s0 = m->st[0];
-        for (int g = 1; g < G; ++g) HIP_CHECK(hipStreamWaitEvent(s0, m->ready[g], 0));
-        HIP_CHECK(launch_merge_shards(m->metric, m->gS.as<double>(), m->gI.as<int64_t>(), G, nq, kk, m->oS.as<double>(),
-                                      m->oI.as<int64_t>(), m->oD.as<float>(), s0));
+        hipStream_t s0 = c->st[0];
+        for (int g = 1; g < G; ++g) HIP_CHECK(hipStreamWaitEvent(s0, c->ready[g], 0));
+        HIP_CHECK(launch_merge_shards(m->metric, c->gS.as<double>(), c->gI.as<int64_t>(), G, nq, kk, c->oS.as<double>(),
+                                      c->oI.as<int64_t>(), c->oD.as<float>(), s0));
         std::vector<float> Dk(lb);
         std::vector<int64_t> Ik(lb);
-        HIP_CHECK(hipMemcpyAsync(Dk.data(), m->oD.p, lb * sizeof(float), hipMemcpyDeviceToHost, s0));
-        HIP_CHECK(hipMemcpyAsync(Ik.data(), m->oI.p, lb * sizeof(int64_t), hipMemcpyDeviceToHost, s0));
-        HIP_CHECK(hipStreamSynchronize(s0));  // (s0 waited for every shard's ready event)
+        HIP_CHECK(hipMemcpyAsync(Dk.data(), c->oD.p, lb * sizeof(float), hipMemcpyDeviceToHost, s0));
+        HIP_CHECK(hipMemcpyAsync(Ik.data(), c->oI.p, lb * sizeof(int64_t), hipMemcpyDeviceToHost, s0));
+        HIP_CHECK(hipStreamSynchronize(s0));  // (s0 waited for every shard's ready event, which follows its
+                                              //  counter copy)
         for (int g = 0; g < G; ++g)
-            if (vs_ntotal(m->ix[g]) > 0 && m->unres_h[g] != m->unres_seen[g]) {
-                m->unres_seen[g] = m->unres_h[g];
+            if (c->unres_h[g] != 0)
                 throw VsError(VS_ERR_UNCERTIFIED, "exactness certificate failed at maximum screening depth");
-            }
         for (int64_t a = 0; a < nq; ++a)
             for (int j = 0; j < k; ++j) {
                 D[a * k + j] = j < kk ? Dk[a * kk + j] : fillD;
@@ -360,7 +452,8 @@ int vs_multi_reconstruct_n(vs_multi* m, int64_t i0, int64_t n, float* out) {
         if (!m || !out) throw VsError(VS_ERR_ARG, "null argument");
         if (i0 < 0 || n < 0 || i0 + n > m->ntotal) throw VsError(VS_ERR_ARG, "reconstruct range out of bounds");
         if (n == 0) return;
-        std::lock_guard<std::mutex> lk(m->mu);
+        std::shared_lock<std::shared_mutex> lk(m->rw);
+        std::lock_guard<std::mutex> pl(m->pool_mu);
         const auto pieces = split_rows(m->G, i0, n);
         m->pool->run([&](int g) {
             for (const Piece& p : pieces[g]) {
@@ -376,7 +469,7 @@ int vs_multi_reconstruct_n(vs_multi* m, int64_t i0, int64_t n, float* out) {
 int vs_multi_reset(vs_multi* m) {
     return guarded([&] {
         if (!m) throw VsError(VS_ERR_ARG, "null handle");
-        std::lock_guard<std::mutex> lk(m->mu);
+        std::unique_lock<std::shared_mutex> lk(m->rw);
         for (vs_index* x : m->ix) throw_rc(vs_reset(x));
         m->ntotal = 0;
     });
@@ -385,7 +478,8 @@ int vs_multi_reset(vs_multi* m) {
 int vs_multi_set_screen(vs_multi* m, int screen) {
     return guarded([&] {
         if (!m) throw VsError(VS_ERR_ARG, "null handle");
-        std::lock_guard<std::mutex> lk(m->mu);
+        std::unique_lock<std::shared_mutex> lk(m->rw);
+        std::lock_guard<std::mutex> pl(m->pool_mu);
         m->pool->run([&](int g) { throw_rc(vs_set_screen(m->ix[g], screen)); });
     });
 }

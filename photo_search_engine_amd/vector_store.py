@@ -71,6 +71,28 @@ def _hnsw_graph_max_rows() -> int:
 
 
 _HNSW_EF_MAX = 2048  # largest max(efSearch, k) of the GPU graph search (include/vs.h)
+# graph mode rebuilds the graph once the store holds this many times the rows the graph covers
+_GRAPH_REBUILD_GROWTH = 1.25
+
+
+def _merge_topk(D1: np.ndarray, I1: np.ndarray, D2: np.ndarray, I2: np.ndarray, k: int,
+                higher_is_better: bool) -> Tuple[np.ndarray, np.ndarray]:
+    """Per query, the best k of two (D, I) result lists (faiss layout, -1 padded): by score (IP:
+    larger first; L2: smaller first), ties to the lower id, padding last."""
+    D = np.concatenate([D1, D2], axis=1)
+    I = np.concatenate([I1, I2], axis=1)
+    key = -D if higher_is_better else D.copy()
+    key = np.where(I >= 0, key, np.inf)
+    order = np.lexsort((np.where(I >= 0, I, np.iinfo(np.int64).max), key), axis=1)[:, :k]
+    Do = np.take_along_axis(D, order, axis=1)
+    Io = np.take_along_axis(I, order, axis=1)
+    if Do.shape[1] < k:  # fewer candidates than k: faiss padding
+        pad = k - Do.shape[1]
+        fill = np.float32(-np.finfo(np.float32).max if higher_is_better else np.finfo(np.float32).max)
+        Do = np.concatenate([Do, np.full((Do.shape[0], pad), fill, dtype=Do.dtype)], axis=1)
+        Io = np.concatenate([Io, np.full((Io.shape[0], pad), -1, dtype=Io.dtype)], axis=1)
+    Do = np.where(Io >= 0, Do, np.float32(-np.finfo(np.float32).max if higher_is_better else np.finfo(np.float32).max))
+    return Do.astype(np.float32), Io.astype(np.int64)
 
 
 def _hnsw_graph_search() -> bool:
@@ -124,6 +146,7 @@ class VectorStore:
         # VECTOR_HNSW_SEARCH=graph: the graph arrays last loaded or saved, and its GPU copy
         self._graph_arrays: Optional[Dict[str, Any]] = None
         self._hnsw: Optional[HNSWGraph] = None
+        self._graph_tail: Optional[FlatIndex] = None  # rows added behind the graph, searched exactly
 
     # ------------------------------------------------------------------ internals
     def _rebuild_path_index(self) -> None:
@@ -359,28 +382,55 @@ class VectorStore:
         return g is not None and int(np.asarray(g["levels"]).shape[0]) == n
 
     def _drop_graph(self) -> None:
-        if self._hnsw is not None:
-            self._hnsw.close()
-        self._hnsw = None
+        self._drop_graph_search()
         self._graph_arrays = None
 
     def _search_rows(self, q: np.ndarray, k: int) -> Tuple[np.ndarray, np.ndarray]:
         """``index.search``, or with ``VECTOR_HNSW_SEARCH=graph`` on an HNSW store, faiss's HNSW
-        search on the GPU over the graph of the loaded file (while it still covers every row) or
-        the graph ``save()`` writes (:meth:`_build_graph`), rebuilt after adds.  Beams wider
-        than the GPU search takes (max(efSearch, k) > 2048) and multi-GPU indexes search exactly."""
-        if (self.index_type != "hnsw" or not _hnsw_graph_search() or not isinstance(self.index, FlatIndex)
-                or max(k, self.hnsw_ef_search) > _HNSW_EF_MAX):
-            return self.index.search(q, k)
+        search on the GPU over the graph of the loaded file or the graph ``save()`` writes
+        (:meth:`_build_graph`).  The graph is rebuilt only once the store has grown by
+        ``_GRAPH_REBUILD_GROWTH`` since it was built; rows added behind it meanwhile are searched
+        exactly (a flat index of those rows) and merged with the graph's results, so alternating
+        ``add_item`` / ``search`` does not pay a whole-graph build per search.  Stores above
+        ``VECTOR_HNSW_GRAPH_MAX_ROWS`` (no graph is saved for them either), beams wider than the GPU
+        search takes (max(efSearch, k) > 2048) and multi-GPU indexes search exactly."""
         n = int(self.index.ntotal)
-        if self._hnsw is None or self._hnsw.ntotal != n or self._hnsw.index is not self.index:
-            if self._hnsw is not None:
-                self._hnsw.close()
-                self._hnsw = None
-            if not self._graph_covers(n):
+        if (self.index_type != "hnsw" or not _hnsw_graph_search() or not isinstance(self.index, FlatIndex)
+                or max(k, self.hnsw_ef_search) > _HNSW_EF_MAX or n > _hnsw_graph_max_rows()):
+            return self.index.search(q, k)
+        if self._hnsw is not None and self._hnsw.index is not self.index:
+            self._drop_graph_search()
+        covered = self._hnsw.ntotal if self._hnsw is not None else 0
+        if self._hnsw is None or n > covered * _GRAPH_REBUILD_GROWTH:
+            self._drop_graph_search()
+            g = self._graph_arrays
+            if g is None or not 0 < int(np.asarray(g["levels"]).shape[0]) <= n or \
+                    n > int(np.asarray(g["levels"]).shape[0]) * _GRAPH_REBUILD_GROWTH:
                 self._graph_arrays = self._build_graph(n)
             self._hnsw = HNSWGraph(self.index, self._graph_arrays, self.hnsw_ef_search)
-        return self._hnsw.search(q, k, self.hnsw_ef_search)
+            covered = self._hnsw.ntotal
+        D, I = self._hnsw.search(q, k, self.hnsw_ef_search)
+        if covered == n:
+            return D, I
+        # rows [covered, n): exact search over a flat index of just those rows, then a merge
+        tail = self._graph_tail
+        if tail is None:
+            tail = self._graph_tail = self._create_index(self.dimension)
+        have = covered + int(tail.ntotal)
+        if have < n:
+            tail.add(np.ascontiguousarray(self.index.reconstruct_n(have, n - have)))
+        Dt, It = tail.search(q, min(k, n - covered))
+        It = np.where(It >= 0, It + covered, -1)
+        return _merge_topk(D, I, Dt, It, k, int(self.index.metric_type) == METRIC_INNER_PRODUCT)
+
+    def _drop_graph_search(self) -> None:
+        """Release the GPU graph and the exactly-searched tail behind it (the arrays stay)."""
+        if self._hnsw is not None:
+            self._hnsw.close()
+        self._hnsw = None
+        if self._graph_tail is not None:
+            self._graph_tail.close()
+        self._graph_tail = None
 
     def _build_graph(self, n: int) -> Dict[str, Any]:
         """A faiss-layout HNSW graph over the n stored rows: node levels drawn as faiss's

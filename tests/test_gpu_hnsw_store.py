@@ -46,14 +46,51 @@ def test_store_graph_mode_search_save_load_add(tmp_path, monkeypatch):
     assert s2.load()
     D2, I2 = s2.search_batch(q, 10)
     assert np.array_equal(I2, I) and np.array_equal(D2, D)
-    # rows added after: the graph is rebuilt over every row
+    # rows added after (+13%): the graph is kept over the first n rows, the new rows are searched
+    # exactly and merged (no whole-graph rebuild per search after an add)
     extra = O.synth_rows(O.SEED_CORPUS + 32, 0, 200, d, False)
     s2.add(extra, [{"photo_path": f"/e/{i}.jpg"} for i in range(200)])
+    built = []
+    orig_build = s2._build_graph
+    s2._build_graph = lambda m: built.append(m) or orig_build(m)
     D3, I3 = s2.search_batch(q, 10)
+    assert built == [] and int(np.asarray(s2._graph_arrays["levels"]).shape[0]) == n
     x3 = s2.index.reconstruct_n(0, n + 200)
-    assert int(np.asarray(s2._graph_arrays["levels"]).shape[0]) == n + 200
-    S3, I3r = H.search(x3, s2._graph_arrays, qn, 10, 32, "ip")
+    Sg, Ig = H.search(x3[:n], s2._graph_arrays, qn, 10, 32, "ip")
+    St, It = O.knn_exact(x3[n:], qn, 10, "ip")
+    S3, I3r = O.merge_topk(np.stack([Sg, St]), np.stack([Ig, It + n]), 10, "ip")
     assert np.array_equal(I3, I3r) and np.array_equal(D3, S3.astype(np.float32))
+    # a newly added row is found first by its own query
+    res = s2.search(extra[5].tolist(), 3)
+    assert res[0]["metadata"]["photo_path"] == "/e/5.jpg"
+    # alternating add_item / search keeps the graph until the store outgrows it by 25 %
+    for i in range(5):
+        s2.add_item(extra[i] * 0.5 + x3[i] * 0.5, {"photo_path": f"/a/{i}.jpg"})
+        s2.search(q[i].tolist(), 5)
+    assert built == []
+    more = O.synth_rows(O.SEED_CORPUS + 33, 0, 300, d, False)
+    s2.add(more, [{"photo_path": f"/m/{i}.jpg"} for i in range(300)])  # 2005 rows > 1.25 x 1500
+    D4, I4 = s2.search_batch(q, 10)
+    n4 = n + 200 + 5 + 300
+    assert built == [n4] and int(np.asarray(s2._graph_arrays["levels"]).shape[0]) == n4
+    x4 = s2.index.reconstruct_n(0, n4)
+    S4, I4r = H.search(x4, s2._graph_arrays, qn, 10, 32, "ip")
+    assert np.array_equal(I4, I4r) and np.array_equal(D4, S4.astype(np.float32))
+
+
+def test_store_graph_mode_above_row_cap_searches_exactly(tmp_path, monkeypatch):
+    """Above VECTOR_HNSW_GRAPH_MAX_ROWS the store neither saves nor searches a graph: exact search."""
+    monkeypatch.setenv("VECTOR_HNSW_SEARCH", "graph")
+    monkeypatch.setenv("VECTOR_HNSW_GRAPH_MAX_ROWS", "500")
+    n, d = 800, 32
+    rows = O.synth_rows(O.SEED_CORPUS + 41, 0, n, d, False)
+    store = _store(tmp_path, d)
+    store.add(rows, [{"photo_path": f"/p/{i}.jpg"} for i in range(n)])
+    store._build_graph = lambda m: pytest.fail("no graph build above the row cap")
+    q = O.synth_rows(O.SEED_QUERIES + 41, 0, 8, d, False)
+    D, I = store.search_batch(q, 10)
+    S_ref, I_ref = O.knn_exact(store.index.reconstruct_n(0, n), store._normalize_rows(q), 10, "ip")
+    assert np.array_equal(I, I_ref) and np.array_equal(D, S_ref.astype(np.float32))
 
 
 def test_store_graph_mode_on_the_reference_file(tmp_path, monkeypatch):

@@ -98,3 +98,59 @@ def test_vector_store_over_devices_saves_and_loads_identically(tmp_path, monkeyp
                              metadata_path=str(tmp_path / "two.json"))
     assert back.load() and back.get_total_items() == rows.shape[0]
     assert back.search(rows[5].tolist(), 5) == one.search(rows[5].tolist(), 5)
+
+
+def test_concurrent_searches_run_concurrently_and_exactly(Multi):
+    """vs_multi_search from 8 threads (the reference serves from Flask's threaded server,
+    /root/reference/main.py:353): every result exact, and calls overlap in wall-clock time (each
+    call leases its own streams / buffers / workers; the handle's lock is shared)."""
+    import threading
+    import time
+
+    N, d = 300_000, 128
+    x = O.synth_rows(O.SEED_CORPUS + 61, 0, N, d, True, "bf16")
+    ix = Multi(d, "ip", "bf16", devices=[0, 0])
+    ix.add(x)
+    qs = [O.synth_rows(O.SEED_QUERIES + 61, 64 * t, 64, d, True, "f32") for t in range(8)]
+    ref = [O.knn_exact(x, q, 20, "ip") for q in qs]
+    spans, errs = [], []
+
+    def worker(t):
+        try:
+            for _ in range(6):
+                t0 = time.perf_counter()
+                D, I = ix.search(qs[t], 20)
+                spans.append((t0, time.perf_counter()))
+                np.testing.assert_array_equal(I, ref[t][1])
+                np.testing.assert_array_equal(D, ref[t][0].astype(np.float32))
+        except Exception as e:  # pragma: no cover - reported below
+            errs.append(e)
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs[0]
+    spans.sort()
+    overlapping = sum(1 for i in range(1, len(spans)) if spans[i][0] < max(e for _, e in spans[:i]))
+    assert overlapping >= len(spans) // 2, f"only {overlapping} of {len(spans)} calls overlapped another"
+    ix.close()
+
+
+def test_failed_add_rolls_back_every_shard(Multi, tmp_path):
+    """A multi-device add that fails on one shard (its rows lie beyond the end of the file) leaves
+    no shard with extra rows: ids stay arithmetic and later adds and searches stay exact."""
+    d = 32
+    x = O.synth_rows(O.SEED_CORPUS + 62, 0, 65536 + 100, d, True, "f32")
+    path = tmp_path / "rows.f32"
+    x.tofile(path)
+    ix = Multi(d, "ip", "f32", devices=[0, 0])
+    with pytest.raises(Exception):
+        ix.add_from_file(str(path), 0, 2 * 65536)  # shard 0's chunk reads, shard 1's runs past EOF
+    assert ix.ntotal == 0 and ix.shard_rows() == [0, 0]
+    ix.add(x)
+    assert ix.shard_rows() == [65536, 100]
+    q = O.synth_rows(O.SEED_QUERIES + 62, 0, 12, d, True, "f32")
+    _exact(ix, x, q, 10, "ip")
+    ix.close()

@@ -255,3 +255,32 @@ def test_query_with_extra_axis_is_rejected_like_the_reference():
         store._normalize = normalize
         q = store._normalize_query(np.ones((8, 1), dtype=np.float32))
         assert q.ndim != 2 or q.shape[0] != 1
+
+
+def test_graph_tail_merge_matches_oracle_merge():
+    """graph mode's merge of the graph's results with the exactly searched tail (rows added behind
+    the graph): the same top-k as the oracle's shard merge, ties to the lower id, padding last."""
+    from oracle import oracle as O
+    from photo_search_engine_amd.vector_store import _merge_topk
+
+    rng = np.random.default_rng(5)
+    nq, k = 7, 6
+    for metric in ("ip", "l2"):
+        S1 = np.sort(rng.integers(0, 9, (nq, k)).astype(np.float64), axis=1)
+        S2 = np.sort(rng.integers(0, 9, (nq, k)).astype(np.float64), axis=1)
+        if metric == "ip":
+            S1, S2 = S1[:, ::-1].copy(), S2[:, ::-1].copy()
+        I1 = rng.permutation(50)[: nq * k].reshape(nq, k).astype(np.int64)
+        I2 = 50 + rng.permutation(50)[: nq * k].reshape(nq, k).astype(np.int64)
+        # keep each list sorted by (score, id) as both searches return it
+        for S, I in ((S1, I1), (S2, I2)):
+            for r in range(nq):
+                o = np.lexsort((I[r], -S[r] if metric == "ip" else S[r]))
+                S[r], I[r] = S[r][o], I[r][o]
+        Sr, Ir = O.merge_topk(np.stack([S1, S2]), np.stack([I1, I2]), k, metric)
+        D, I = _merge_topk(S1.astype(np.float32), I1, S2.astype(np.float32), I2, k, metric == "ip")
+        assert np.array_equal(I, Ir) and np.array_equal(D, Sr.astype(np.float32))
+    # a short tail (fewer rows than k) and faiss padding
+    D, I = _merge_topk(np.array([[3.0, 1.0]], np.float32), np.array([[4, -1]]), np.array([[2.0]], np.float32),
+                       np.array([[9]]), 3, True)
+    assert I.tolist() == [[4, 9, -1]] and D[0, :2].tolist() == [3.0, 2.0]
