@@ -1281,8 +1281,10 @@ constexpr int I8D_P = 3;            // K-steps of lead (measured: 3, 5 and 7 run
 constexpr int I8D_U = I8D_P + 1;    // corpus register sets = query ring slots (nks % I8D_U == 0)
 constexpr int I8D_OPS = 4;          // vector-memory ops per wave and K-step: 2 query DMAs + 2 corpus loads
 constexpr int I8D_RING = I8D_U * 16384;
-constexpr int I8D_LDS = I8D_RING + 256 * 8 + 256 * 4 + 256 * 4 + 16 + MF_POOL * 8 + MF_POOL * 4 + MF_SX + MF_QFAC +
-                        MF_ROWX;
+constexpr int I8D_REC = 64;  // per wave: staged (lane, column) records of the epilogue's per-row path
+constexpr int I8D_LDS = I8D_RING + 256 * 8 + 256 * 4 + 256 * 4 + 16 + MF_POOL * 8 + MF_POOL * 4 +
+                        8 * I8D_REC * 32 /* record accumulators */ + 256 * 16 /* qrec */ + MF_ROWX +
+                        8 * I8D_REC * 4 /* record meta */;
 static_assert(I8D_LDS <= 160 * 1024, "LDS budget (direct int8 screen)");
 static_assert(I8D_U == 4, "the K loop body and the vmcnt count are written for 4 slots");
 
@@ -1314,9 +1316,12 @@ __global__ void __launch_bounds__(512, 2) k_screen_i8d(ScreenArgs a, const uint8
     int* flag = (int*)(sm + 256 * 16);  // [1] pool count, [2 + tile parity] inserted
     u64* pool_key = (u64*)(sm + 256 * 16 + 16);
     int* pool_q = (int*)(sm + 256 * 16 + 16 + MF_POOL * 8);
-    float* sx = (float*)(sm + 256 * 16 + 16 + MF_POOL * 12) + (threadIdx.x >> 6) * 512 + (threadIdx.x & 63) * 8;
-    float2* qfac = (float2*)(sm + 256 * 16 + 16 + MF_POOL * 12 + MF_SX);
-    uint32_t* rowx = (uint32_t*)(sm + 256 * 16 + 16 + MF_POOL * 12 + MF_SX + MF_QFAC);
+    // the wave's epilogue records: 8 accumulators (int) of one (lane, query column), and its meta
+    intx4* rec = (intx4*)(sm + 256 * 16 + 16 + MF_POOL * 12) + (threadIdx.x >> 6) * I8D_REC * 2;
+    float4* qrec = (float4*)(sm + 256 * 16 + 16 + MF_POOL * 12 + 8 * I8D_REC * 32);  // (t_q, ||q|| / t_q, thr, -)
+    uint32_t* rowx = (uint32_t*)(sm + 256 * 16 + 16 + MF_POOL * 12 + 8 * I8D_REC * 32 + 256 * 16);
+    int* rmeta = (int*)(sm + 256 * 16 + 16 + MF_POOL * 12 + 8 * I8D_REC * 32 + 256 * 16 + MF_ROWX) +
+                 (threadIdx.x >> 6) * I8D_REC;
     asm volatile("; lds ring escapes: %0" ::"v"(smem) : "memory");
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -1327,9 +1332,11 @@ __global__ void __launch_bounds__(512, 2) k_screen_i8d(ScreenArgs a, const uint8
         const bool real = tid < nqb;
         const u64 k0 = real ? (a.thr0 ? a.thr0[tid] : 0ull) : ~0ull;
         thr_key[tid] = k0;
-        thr_f[tid] = !real ? INFINITY : (k0 == 0ull ? -INFINITY : key_score(k0));
+        const float tf = !real ? INFINITY : (k0 == 0ull ? -INFINITY : key_score(k0));
+        thr_f[tid] = tf;
         cnt[tid] = 0;
-        qfac[tid] = real ? a.qfac[tid] : make_float2(0.0f, 0.0f);
+        const float2 f = real ? a.qfac[tid] : make_float2(0.0f, 0.0f);
+        qrec[tid] = make_float4(f.x, f.y, tf, 0.0f);
     }
     if (tid == 0) {
         flag[0] = 0;
@@ -1426,7 +1433,10 @@ __global__ void __launch_bounds__(512, 2) k_screen_i8d(ScreenArgs a, const uint8
                             mf_wave_compact<MFMA_CAP / 64>(cand + (size_t)q * a.cap, n < a.cap ? n : a.cap, a.Kp,
                                                            &thr_key[q], &thr_f[q], a.drop ? a.drop + q : nullptr,
                                                            lane);
-                            if (lane == 0) cnt[q] = a.Kp;
+                            if (lane == 0) {  // (lane 0 wrote the new threshold)
+                                cnt[q] = a.Kp;
+                                qrec[q].z = thr_f[q];
+                            }
                         }
                     }
                     mf_barrier_drain();  // counters / thresholds / compacted buffers published
@@ -1449,90 +1459,109 @@ __global__ void __launch_bounds__(512, 2) k_screen_i8d(ScreenArgs a, const uint8
         // the epilogue reads the last MFMAs' results (the hazard recognizer does not see the asm)
         asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
         // ---- tile epilogue ----
+        // Per lane: 8 rows x 16 query columns.  A column is tested by ONE upper bound of its 8 keys;
+        // the (lane, column) pairs that pass are staged as records in the wave's LDS buffer and their
+        // keys are computed afterwards one record per lane (a column passes for a lane or two at a
+        // time: per-column key code would run for the whole wave).
         int olane;  // asm-opaque lane id: lane-derived indices are not hoisted out of the K loop
         asm volatile("v_mov_b32 %0, %1" : "=v"(olane) : "v"(lane));
         const int64_t rowbase = (int64_t)ti * TR;
-        const int rw0 = wid * 32 + (olane >> 4) * 4;  // + 16 m + r
-        const int qlane = olane & 15;                  // + 16 n
-        float sq[2][4], rb[2][4];                      // the rows' scale and error norm
+        const int qlane = olane & 15;  // + 16 n
+        const uint32_t* rx = rowx + (ti & 1) * TR;
+        // the shard's last tile: rows >= n_valid (garbage side data) never qualify -> no bound test,
+        // every pair is staged, and the per-row path makes those rows NaN
+        const bool edge = rowbase + TR > a.n_valid;
+        float smax = 0.0f, smin = 0.0f, bmax = 0.0f;
+        {
+            const int rw0 = wid * 32 + (olane >> 4) * 4;
+            const uint4 w0 = *(const uint4*)(rx + rw0), w1 = *(const uint4*)(rx + rw0 + 16);
+            const uint32_t w8[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+            smax = smin = __uint_as_float(w8[0] << 16);
+            bmax = __uint_as_float(w8[0] & 0xFFFF0000u);
 #pragma unroll
-        for (int m = 0; m < 2; ++m) {
-            const uint4 w = *(const uint4*)(rowx + (ti & 1) * TR + rw0 + m * 16);
-            const uint32_t w4[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                sq[m][r] = __uint_as_float(w4[r] << 16);
-                rb[m][r] = __uint_as_float(w4[r] & 0xFFFF0000u);
+            for (int j = 1; j < 8; ++j) {
+                smax = fmaxf(smax, __uint_as_float(w8[j] << 16));
+                smin = fminf(smin, __uint_as_float(w8[j] << 16));
+                bmax = fmaxf(bmax, __uint_as_float(w8[j] & 0xFFFF0000u));
             }
         }
-        // the shard's last tile: rows >= n_valid (garbage side data) never qualify -> no bound test,
-        // every column takes the per-row path, which makes those rows NaN
-        const bool edge = rowbase + TR > a.n_valid;
-        uint32_t bad = 0;
-        float smax = sq[0][0], smin = sq[0][0], bmax = rb[0][0];
-        if (edge) {
+        // keys of the staged records, one per lane; the record slot is reused as value staging
+        auto drain = [&](int nrec) {
+            __builtin_amdgcn_wave_barrier();
+            if (lane < nrec) {
+                const int meta = rmeta[lane];
+                const int n = meta & 15, sl = meta >> 4;
+                const int q = 16 * n + (sl & 15);
+                const int r0 = wid * 32 + (sl >> 4) * 4;  // + 16 m + r
+                const intx4 c0 = rec[2 * lane], c1 = rec[2 * lane + 1];
+                const uint4 w0 = *(const uint4*)(rx + r0), w1 = *(const uint4*)(rx + r0 + 16);
+                const int cc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+                const uint32_t w8[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+                const float4 f = qrec[q];  // key = t_q * (s_x acc + beta_x ||q|| / t_q)
+                float v[8];
+                uint32_t mh = 0;
 #pragma unroll
-            for (int m = 0; m < 2; ++m)
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    if (rowbase + rw0 + m * 16 + r >= a.n_valid) bad |= 1u << (m * 4 + r);
-        } else {
-#pragma unroll
-            for (int m = 0; m < 2; ++m)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    smax = fmaxf(smax, sq[m][r]);
-                    smin = fminf(smin, sq[m][r]);
-                    bmax = fmaxf(bmax, rb[m][r]);
+                for (int j = 0; j < 8; ++j) {
+                    const int row = r0 + (j >> 2) * 16 + (j & 3);
+                    const float x = __builtin_fmaf(__uint_as_float(w8[j] & 0xFFFF0000u), f.y,
+                                                   (float)cc[j] * __uint_as_float(w8[j] << 16)) * f.x;
+                    v[j] = rowbase + row >= a.n_valid ? __builtin_nanf("") : x;
+                    mh |= (v[j] >= f.z ? 1u : 0u) << j;  // (ties resolved by key below)
                 }
-        }
+                if (mh) {
+                    flag[2 + (ti & 1)] = 1;
+                    const u64 tk = thr_key[q];
+                    float* sv = (float*)(rec + 2 * lane);
+                    *(float4*)(sv) = make_float4(v[0], v[1], v[2], v[3]);
+                    *(float4*)(sv + 4) = make_float4(v[4], v[5], v[6], v[7]);
+                    while (mh) {  // compact insert loop: the LDS pool, a direct store when it is full
+                        const int j = __builtin_ctz(mh);
+                        mh &= mh - 1u;
+                        const u64 key = mk_key(sv[j], (uint32_t)(rowbase + r0 + (j >> 2) * 16 + (j & 3)));
+                        if (key <= tk) continue;  // score == threshold and not ahead of it by id
+                        const int ps = atomicAdd(&flag[1], 1);
+                        if (ps < MF_POOL) {
+                            pool_key[ps] = key;
+                            pool_q[ps] = q;
+                            continue;
+                        }
+                        const int slot = atomicAdd(&cnt[q], 1);
+                        if (slot < a.cap) cand[(size_t)q * a.cap + slot] = key;
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+        };
+        int nrec = 0;  // wave-uniform
 #pragma unroll
         for (int n = 0; n < 16; ++n) {
-            const int q = 16 * n + qlane;
-            const float2 f = qfac[q];  // (t_q, ||q|| / t_q): key = t_q * (s_x acc + beta_x ||q|| / t_q)
-            const float tf = thr_f[q];
             bool go = true;
             if (!edge) {
                 // bound of the column's 8 keys: max acc (exact int) -> fp32, times the rows' largest
                 // (acc >= 0) or smallest (acc < 0) scale, plus the largest error norm; each step is
                 // monotone, so a key that would pass implies a bound that passes
+                const float4 f = qrec[16 * n + qlane];
                 const int mi = max(max(max(acc[0][n][0], acc[0][n][1]), max(acc[0][n][2], acc[0][n][3])),
                                    max(max(acc[1][n][0], acc[1][n][1]), max(acc[1][n][2], acc[1][n][3])));
                 const float fm = (float)mi;
-                go = __builtin_fmaf(bmax, f.y, fmaxf(smax * fm, smin * fm)) * f.x >= tf;
+                go = __builtin_fmaf(bmax, f.y, fmaxf(smax * fm, smin * fm)) * f.x >= f.z;
             }
-            if (!go) continue;
-            float v[8];
-#pragma unroll
-            for (int m = 0; m < 2; ++m)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float x = __builtin_fmaf(rb[m][r], f.y, (float)acc[m][n][r] * sq[m][r]) * f.x;
-                    v[m * 4 + r] = (bad >> (m * 4 + r)) & 1u ? __builtin_nanf("") : x;
-                }
-            uint32_t mh = 0;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) mh |= (v[j] >= tf ? 1u : 0u) << j;  // (ties resolved by key below)
-            if (!mh) continue;
-            flag[2 + (ti & 1)] = 1;
-            const u64 tk = thr_key[q];
-            *(float4*)(sx) = make_float4(v[0], v[1], v[2], v[3]);
-            *(float4*)(sx + 4) = make_float4(v[4], v[5], v[6], v[7]);
-            while (mh) {  // compact insert loop: the LDS pool, a direct store when it is full
-                const int j = __builtin_ctz(mh);
-                mh &= mh - 1u;
-                const u64 key = mk_key(sx[j], (uint32_t)(rowbase + rw0 + (j >> 2) * 16 + (j & 3)));
-                if (key <= tk) continue;  // score == threshold and not ahead of it by id
-                const int ps = atomicAdd(&flag[1], 1);
-                if (ps < MF_POOL) {
-                    pool_key[ps] = key;
-                    pool_q[ps] = q;
-                    continue;
-                }
-                const int slot = atomicAdd(&cnt[q], 1);
-                if (slot < a.cap) cand[(size_t)q * a.cap + slot] = key;
+            const u64 bal = __ballot(go);
+            if (bal == 0ull) continue;
+            const int c = __popcll(bal);
+            if (nrec + c > I8D_REC) {
+                drain(nrec);
+                nrec = 0;
             }
+            if (go) {
+                const int slot = nrec + lane_prefix(bal);
+                rec[2 * slot] = acc[0][n];
+                rec[2 * slot + 1] = acc[1][n];
+                rmeta[slot] = n | (olane << 4);
+            }
+            nrec += c;
         }
+        if (nrec) drain(nrec);
         check_pending = true;
     }
 #undef I8D_ISSUE
