@@ -74,6 +74,11 @@ def parse():
     ap.add_argument("--ivf-scan", default="auto", choices=["auto", "gemv", "mfma"],
                     help="cfg5: list-scan kernels (auto: MFMA screen for lists probed by many queries; "
                          "with auto the GEMV-only scan is timed too and reported beside it)")
+    ap.add_argument("--data", default="iso", choices=["iso", "mixture", "mixture-sorted"],
+                    help="flat workloads: isotropic rows (default, the BASELINE data), or a Gaussian mixture "
+                         "(64 clusters, sigma --sigma) in random / cluster-sorted insertion order; the "
+                         "mixture runs report no CPU baseline (their rows are made on the GPU)")
+    ap.add_argument("--sigma", type=float, default=1.0, help="--data mixture: cluster spread")
     ap.add_argument("--iso-data", action="store_true",
                     help="cfg5: isotropic rows (the flat bench's data) instead of the Gaussian mixture")
     ap.add_argument("--traffic-file", default=None,
@@ -116,7 +121,25 @@ def main():
     t_build = time.time()
     # the product's multi-GPU layer: one row shard per rank, all-gather + device merge (G > 1)
     sh = ShardedFlatIndex(d, "ip", dtype, device=local)
-    if args.zero_corpus:
+    if args.data != "iso":
+        # clustered rows: normalise(c[cid] + sigma g) over 64 unit centroids (the cfg5 data model,
+        # `_mixture_rows`); sorted = inserted cluster by cluster (cid non-decreasing in row order)
+        C = 64
+        cen = torch.empty((C, d), dtype=torch.float32, device=dev)
+        synthesize_device(local, SEED_CENTROIDS, 0, C, d, cen.data_ptr(), True, dtype, torch.cuda.current_stream(dev).cuda_stream)
+        sh.row0, sh.n_total = row0, N
+        chunk = 1 << 18
+        for r in range(0, n_local, chunk):
+            m = min(chunk, n_local - r)
+            if args.data == "mixture":
+                xr = _mixture_rows(SEED_CORPUS, row0 + r, m, d, cen, args.sigma, dev, torch.cuda.current_stream(dev).cuda_stream)
+            else:
+                xr = _mixture_rows_sorted(SEED_CORPUS, row0 + r, m, N, d, cen, args.sigma, dev,
+                                          torch.cuda.current_stream(dev).cuda_stream)
+            sh.index.add_device(xr.data_ptr(), m, torch.cuda.current_stream(dev).cuda_stream)
+            torch.cuda.synchronize()
+            del xr
+    elif args.zero_corpus:
         zeros = torch.zeros((1 << 20, d), dtype=torch.float32, device=dev)
         sh.row0, sh.n_total = row0, N
         for r in range(0, n_local, zeros.shape[0]):
@@ -129,6 +152,8 @@ def main():
     q = torch.empty((nq, d), dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev)
     synthesize_device(local, SEED_QUERIES, 0, nq, d, q.data_ptr(), True, dtype, stream.cuda_stream)
+    if args.data != "iso":
+        q.copy_(_mixture_rows(SEED_QUERIES, 0, nq, d, cen, args.sigma, dev, stream.cuda_stream))
     torch.cuda.synchronize()
     screen = args.screen or DEFAULT_SCREEN.get(args.workload, "native")
     t_build = time.time() - t_build
@@ -145,7 +170,10 @@ def main():
         u0 = ix.uncertified_count()
         for _ in range(args.warmup):
             step()
-        torch.cuda.synchronize()
+            # (one step at a time: the index's screen-health feedback -- a batch's certificate
+            # failures read back behind it -- then reaches the next warmup step, as it does between
+            # the synchronous calls of a server; the timed steps are enqueued back to back)
+            torch.cuda.synchronize()
         ix.timing_fetch()  # drop warmup events
         ix.set_timing(True)
         if G > 1:
@@ -222,7 +250,8 @@ def main():
             # (dtype) row; the int8 screen only pre-selects rows for the exact refine
             "dtype": dtype,
             "screen": "int8" if kind in ("mfma_i8", "gemv_i8") else "native",
-            "data": "synthetic (counter-hash N(0,1) rows, L2-normalised, seeds 20260417/20260418)",
+            "data": ("synthetic (counter-hash N(0,1) rows, L2-normalised, seeds 20260417/20260418)" if args.data == "iso"
+                     else f"synthetic Gaussian mixture ({args.data}, 64 clusters, sigma {args.sigma}), L2-normalised"),
             "config": {"workload": args.workload, "desc": desc, "N": N, "d": d, "batch": nq, "k": k,
                        "n_local": n_local, "stored_rows": dtype, "screen": screen,
                        "parallelism": f"row-shard x{G}" + (
@@ -254,7 +283,7 @@ def main():
                                         "capacity)"}
         if alt is not None:
             out["native_screen"] = alt
-    if rank == 0 and G == 1 and not args.no_cpu_baseline:
+    if rank == 0 and G == 1 and not args.no_cpu_baseline and args.data == "iso":
         out["cpu_baseline"], out["recall@10"], out["parity"] = cpu_baseline_and_recall(
             args, N, d, dtype, nq, k, local, torch, (result["D"].cpu().numpy(), result["I"].cpu().numpy()))
     if rank == 0:
@@ -393,6 +422,20 @@ class _heartbeat:
         self.stop.set()
         self.t.join()
         _progress(f"{self.msg}: done")
+
+
+def _mixture_rows_sorted(seed, r0, m, n_total, d, centroids, sigma, dev, stream):
+    """As `_mixture_rows`, with row i in cluster floor(i * C / n_total): the corpus inserted cluster
+    by cluster (the int8 screen's seed sample then sees whole clusters per workgroup)."""
+    import torch
+
+    from photo_search_engine_amd.index import synthesize_device
+    g = torch.empty((m, d), dtype=torch.float32, device=dev)
+    synthesize_device(dev.index, seed, r0, m, d, g.data_ptr(), True, "f32", stream)
+    rows = torch.arange(r0, r0 + m, dtype=torch.int64, device=dev)
+    cid = torch.clamp(rows * centroids.shape[0] // n_total, max=centroids.shape[0] - 1)
+    x = centroids[cid] + sigma * g
+    return x / torch.linalg.vector_norm(x, dim=1, keepdim=True)
 
 
 def _mixture_rows(seed, r0, m, d, centroids, sigma, dev, stream, cdf=None):

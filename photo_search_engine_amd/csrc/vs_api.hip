@@ -114,6 +114,21 @@ struct vs_index {
     std::mutex tmtx;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> tev;
     int last_kernel_kind = 0;  // 1 = mfma, 2 = gemv, 3 = int8 mfma
+    // Screen health (first passes of MFMA batches): the certificate-failure count of a batch is read
+    // back without a host wait (pinned word + event, observed by a later search).  A failed query
+    // costs its block a full fallback round, so the index adapts to its corpus:
+    //  * an int8 batch with failures routes the next kI8RouteBatches searches to the native screen
+    //    (score distributions denser than the int8 error window, e.g. tight clusters);
+    //  * a native batch in which more than 1/64 of the queries failed doubles the optimistic seed's
+    //    depth (rows listed ahead of the refine), up to 2^kSeedScaleMax; kSeedRelax clean batches
+    //    halve it again.
+    std::mutex h_mu;
+    unsigned* h_fails = nullptr;  // pinned
+    hipEvent_t h_ev = nullptr;
+    int h_pending = 0;          // 0 none, 1 int8 batch, 2 native batch in flight
+    int h_nq = 0;               // queries of that batch
+    int i8_route = 0;           // searches still routed to the native screen
+    int seed_log2 = 0, seed_clean = 0;
 };
 
 vs::FlatView vs::flat_view(vs_index* ix) {
@@ -205,14 +220,12 @@ void free_i8(vs_index* ix) {
     ix->cap8 = 0;
 }
 
-// row-major copy for the int8 refine (bf16/f16 rows, opt-in VS_I8_ROWMAJOR=1): whole-row gathers
-// instead of 128 B lines 32 KiB apart.  Measured at cfg3: k_refine_wide 247 -> 235 us per batch
-// (-16 us per step) for another N * d * 2 bytes of HBM (30.7 GB), so it is off by default; skipped
-// when it does not fit (the refine then reads the tiled rows).
-bool want_rowmajor(const vs_index* ix) {
-    static const bool on = getenv("VS_I8_ROWMAJOR") && atoi(getenv("VS_I8_ROWMAJOR")) == 1;
-    return on && ix->dtype != DT_F32;
-}
+// row-major copy for the int8 refine (bf16/f16 rows): whole-row gathers instead of 128 B lines
+// 32 KiB apart.  Measured at cfg3: k_refine_wide 247 -> 235 us per batch (-16 us per step) for
+// another N * d * 2 bytes of HBM (30.7 GB), so it is off (kRowMajorCopy; the refine keeps the code
+// path: rowm == null reads the tiled rows).  No environment variable changes a product path.
+constexpr bool kRowMajorCopy = false;
+bool want_rowmajor(const vs_index* ix) { return kRowMajorCopy && ix->dtype != DT_F32; }
 
 // grow the int8 screen copy to ix->cap_rows rows (device copy of the rows present; the old and new
 // arrays coexist only for the copy, as for the primary rows)
@@ -275,20 +288,69 @@ constexpr int kOptimisticSeedRank = 1;  // seed_rank argument: > 0 selects the o
 constexpr double kOptimisticPassFactor = 8.0;
 constexpr int kOptimisticMinRank = 4;
 
-bool seed_reuse() {
-    static const bool on = !(getenv("VS_SEED_REUSE") && atoi(getenv("VS_SEED_REUSE")) == 0);
-    return on;
-}
-
-bool gemv_dyn() {
-    static const bool on = !(getenv("VS_GEMV_DYN") && atoi(getenv("VS_GEMV_DYN")) == 0);
-    return on;
-}
+// the seed pass screens each main-pass workgroup's first tile and the (native) main pass reuses
+// its accumulators; the GEMV screen takes tiles from a work queue over its resident blocks (both
+// measured faster than the alternatives they replaced)
+constexpr bool seed_reuse() { return true; }
+constexpr bool gemv_dyn() { return true; }
 
 // The int8 pre-screen serves first passes of MFMA-sized batches (k <= I8_MAX_K) of an index with
 // VS_SCREEN_I8; a query its certificate rejects is re-searched by the caller on the native path.
 bool use_i8(const vs_index* ix, int nqb, int k) {
     return ix->screen == VS_SCREEN_I8 && nqb > GEMV_NQ_MAX && k <= I8_MAX_K;
+}
+
+constexpr int kI8RouteBatches = 64;  // searches routed to the native screen after a failing int8 batch
+constexpr int kSeedScaleMax = 6;     // native optimistic seed: at most 64x the default depth
+constexpr int kSeedRelax = 64;       // clean native batches before the depth is halved again
+
+// observe a completed failure-count readback (caller holds h_mu)
+void health_poll(vs_index* ix) {
+    if (ix->h_pending && hipEventQuery(ix->h_ev) == hipSuccess) {
+        const unsigned f = *ix->h_fails;
+        if (ix->h_pending == 1) {
+            if (f > 0) ix->i8_route = kI8RouteBatches;
+        } else if (f > (unsigned)(ix->h_nq / 64)) {  // (a stray hard query does not deepen every batch)
+            ix->seed_log2 = std::min(ix->seed_log2 + 1, kSeedScaleMax);
+            ix->seed_clean = 0;
+        } else if (ix->seed_log2 > 0 && ++ix->seed_clean >= kSeedRelax) {
+            --ix->seed_log2;
+            ix->seed_clean = 0;
+        }
+        ix->h_pending = 0;
+    }
+    (void)hipGetLastError();  // (hipEventQuery's "not ready" is no error)
+}
+// May this search use the int8 screen?  Consumes the routing state (one call per search).
+bool i8_allowed(vs_index* ix) {
+    if (ix->screen != VS_SCREEN_I8) return false;
+    std::lock_guard<std::mutex> g(ix->h_mu);
+    health_poll(ix);
+    if (ix->i8_route > 0) {
+        --ix->i8_route;
+        return false;
+    }
+    return true;
+}
+// depth multiplier of the native optimistic seed
+double seed_scale(vs_index* ix) {
+    std::lock_guard<std::mutex> g(ix->h_mu);
+    health_poll(ix);
+    return (double)(1 << ix->seed_log2);
+}
+// after a first-pass batch (kind 1 int8, 2 native): read its failure count back behind it on the
+// stream (one readback in flight per index)
+void health_note(vs_index* ix, Ctx* c, hipStream_t st, int kind, int nq) {
+    std::lock_guard<std::mutex> g(ix->h_mu);
+    if (ix->h_pending) return;
+    if (!ix->h_fails) {
+        HIP_CHECK(hipHostMalloc((void**)&ix->h_fails, sizeof(unsigned), hipHostMallocDefault));
+        HIP_CHECK(hipEventCreateWithFlags(&ix->h_ev, hipEventDisableTiming));
+    }
+    HIP_CHECK(hipMemcpyAsync(ix->h_fails, c->fails.p, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipEventRecord(ix->h_ev, st));
+    ix->h_pending = kind;
+    ix->h_nq = nq;
 }
 // int8 GEMV screen depth.  Its keys carry the row error bound beta (~0.007-0.01 ||x|| ||q||), so the
 // rows it must keep are those within ~beta of the k-th best.  For unit rows the scores are roughly
@@ -372,9 +434,7 @@ void search_block_i8(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float
         sa.seedmax = c->seedmax.as<float>();
         HIP_CHECK(launch_seed_mfma(DT_I8, sa, c->qtile.as<uint8_t>(), nqb, st));
         c->thr0.ensure(sizeof(u64) * MFMA_QB);
-        static const double per_k = getenv("VS_I8_UNION") ? atof(getenv("VS_I8_UNION")) : 0.0;  // A/B knob
-        const double target = per_k > 0.0 ? std::max(per_k * k, kI8UnionMin)
-                                           : i8_union_target(k, (double)sa.G * TR, (double)ix->ntotal);
+        const double target = i8_union_target(k, (double)sa.G * TR, (double)ix->ntotal);
         const double r = std::ceil(target * (double)sa.G * TR / (double)ix->ntotal);
         const int rank = (int)std::min<double>(std::max<double>(r, (double)kOptimisticMinRank), (double)M);
         HIP_CHECK(launch_seed_select(sa.seedmax, M, nqb, rank, c->thr0.as<u64>(), st));
@@ -430,9 +490,11 @@ void search_block_i8(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float
 // refine rewrites only the queries whose certificate failed; a query it cannot certify either
 // counts in d_unres
 void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, float* D, int64_t* I, double* S64,
-                  int* cert, int64_t id_offset, hipStream_t st, int seed_rank, bool redo = false) {
-    if (seed_rank > 0 && use_i8(ix, nqb, k)) {
+                  int* cert, int64_t id_offset, hipStream_t st, int seed_rank, bool redo = false,
+                  bool allow_i8 = true) {
+    if (seed_rank > 0 && allow_i8 && use_i8(ix, nqb, k)) {
         search_block_i8(ix, c, q, nqb, k, D, I, S64, cert, id_offset, st);
+        health_note(ix, c, st, 1, nqb);
         return;
     }
     const int64_t tiles = (ix->ntotal + TR - 1) / TR;
@@ -456,8 +518,11 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
     a.metric = ix->metric;
     a.sqn = ix->sqn;
     // MFMA: each workgroup keeps its best min(Kp, MFMA_KP_MAX) per query; deeper screens certify
-    // against the workgroups' compaction bounds (drop) in the refine
-    a.Kp = use_mfma ? std::min(Kp, MFMA_KP_MAX) : Kp;
+    // against the workgroups' compaction bounds (drop) in the refine.  First passes of inner-product
+    // batches (adaptive refine below) keep MFMA_KP_MAX: a workgroup that holds many of a query's
+    // best rows (a cluster inserted contiguously) then drops only rows far below the k-th best.
+    const bool wide = use_mfma && !redo && ix->metric == METRIC_IP && k <= I8_MAX_K && refine_split(nqb, Kp, ix->dtype, ix->num_cu) <= 1;
+    a.Kp = use_mfma ? (wide ? MFMA_KP_MAX : std::min(Kp, MFMA_KP_MAX)) : Kp;
     int QB;
     c->qinfo.ensure(sizeof(float) * 2 * MFMA_QB);
     if (use_mfma) {
@@ -494,6 +559,7 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
     }
     a.G = std::max(a.G, 1);
     a.gate = gate;
+    if (redo && use_mfma) a.skip = cert;  // the fallback screens only the block's failed queries
     c->cand.ensure((size_t)a.G * QB * a.cap * sizeof(u64));
     c->part.ensure((size_t)a.G * QB * a.Kp * sizeof(u64));  // GEMV: [G][QB][Kp]; MFMA: [QB][G*Kp] survivor lists
     a.cand = c->cand.as<u64>();
@@ -554,12 +620,14 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
         if (seed_rank > 0) {
             const double sampled = (double)sa.G * TR;
             // deep screens aim lower (~12k listed rows per query), so the refine selects in registers
-            const double factor = std::min(kOptimisticPassFactor, 12288.0 / Kp);
+            const double factor = std::min(kOptimisticPassFactor, 12288.0 / Kp) * (wide ? seed_scale(ix) : 1.0);
             const double r = std::ceil(factor * Kp * sampled / (double)ix->ntotal);
             // floor: at rank 1 a sample maximum that falls inside the true top-Kp leaves fewer than
             // Kp survivors (probability ~Kp * sampled / N per query, ~2% at 100M rows); with >= 4
             // sampled rows required in the top-Kp the failure odds drop to ~(that)^4 / 24
-            rank = (int)std::min<double>(std::max<double>(r, (double)kOptimisticMinRank), (double)Kp);
+            // (the fixed-depth refine needs rank <= Kp -- the proven seed -- for its certificate; the
+            // adaptive refine's certificate checks the seed itself, so its rank may go deeper)
+            rank = (int)std::min<double>(std::max<double>(r, (double)kOptimisticMinRank), wide ? (double)M : (double)Kp);
         }
         HIP_CHECK(launch_seed_select(sa.seedmax, M, nqb, rank, c->thr0.as<u64>(), st));
         a.thr0 = c->thr0.as<u64>();
@@ -599,6 +667,7 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
     }
     r.Kp = Kp;
     r.drop = a.drop;
+    r.thr0 = a.thr0;  // (the adaptive refine's certificate: rows never listed scored <= thr0)
     r.i8max = gemv_i8 ? ix->d_maxsq + 2 : nullptr;
     r.q = q;
     r.d = ix->d;
@@ -634,6 +703,15 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
         }
         r.gdone = c->rdone.as<unsigned>();
     }
+    // native MFMA first passes (inner product): the adaptive two-phase refine -- it scores every
+    // listed row whose key is within the screen's margin of the k-th best, so dense score
+    // distributions (clustered corpora) certify without a re-search; the fixed-depth refine's
+    // certificate needs a gap of 2 margins between the k-th and the Kp-th best
+    if (wide) {
+        HIP_CHECK(launch_refine_wide(r, nqb, (int)round_up(std::max(Kp, k + 32), 32), st));
+        health_note(ix, c, st, 2, nqb);
+        return;
+    }
     HIP_CHECK(launch_refine(r, nqb, st));
 }
 
@@ -647,7 +725,8 @@ void search_all(vs_index* ix, Ctx* c, const float* q, int64_t nq, int k, int Kp,
                 int* cert, int64_t id_offset, hipStream_t st, int seed_rank, bool device_fallback = false) {
     const int64_t tiles = (ix->ntotal + TR - 1) / TR;
     (void)tiles;
-    const bool mfma_ok = (seed_rank > 0 && ix->screen == VS_SCREEN_I8 && k <= I8_MAX_K) || ix->dtype != DT_F32;
+    const bool i8 = seed_rank > 0 && i8_allowed(ix);  // (int8 screen on, and not routed away)
+    const bool mfma_ok = (i8 && k <= I8_MAX_K) || ix->dtype != DT_F32;
     int64_t done = 0;
     while (done < nq) {
         const int64_t rem = nq - done;
@@ -655,7 +734,7 @@ void search_all(vs_index* ix, Ctx* c, const float* q, int64_t nq, int k, int Kp,
         if (mfma_ok && rem > GEMV_NQ_MAX) nqb = (int)std::min<int64_t>(rem, MFMA_QB);
         else nqb = (int)std::min<int64_t>(rem, GEMV_NQ_MAX);
         search_block(ix, c, q + done * ix->d, nqb, k, Kp, D ? D + done * k : nullptr, I + done * k,
-                     S64 ? S64 + done * k : nullptr, cert ? cert + done : nullptr, id_offset, st, seed_rank);
+                     S64 ? S64 + done * k : nullptr, cert ? cert + done : nullptr, id_offset, st, seed_rank, false, i8);
         if (device_fallback)
             search_block(ix, c, q + done * ix->d, nqb, k, std::max(Kp, fallback_depth(ix)), D ? D + done * k : nullptr,
                          I + done * k, S64 ? S64 + done * k : nullptr, cert + done, id_offset, st, 0, true);
@@ -874,6 +953,8 @@ void vs_destroy(vs_index* ix) {
         if (ix->d_maxsq) hipFree(ix->d_maxsq);
         free_i8(ix);
         if (ix->own) hipStreamDestroy(ix->own);
+        if (ix->h_ev) hipEventDestroy(ix->h_ev);
+        if (ix->h_fails) hipHostFree(ix->h_fails);
     }
     delete ix;
 }

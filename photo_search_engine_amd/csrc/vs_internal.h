@@ -197,6 +197,8 @@ struct ScreenArgs {
     const int* tile_map;     // mapped screen (IVF list scan): page of logical tile t; keys carry
                              // storage slots page * TR + row, n_valid counts the list's rows
     const int* qmap;         // mapped screen: glist / gcnt row of a query (the workgroup's slice below)
+    const int* skip;         // device fallback round: queries with skip[q] != 0 (certified by the first
+                             // pass) are not screened (threshold +inf: no candidates), or null
     const int* wg_desc;      // mapped screen: per workgroup MAP_DESC ints {tile_map offset of its
                              // first tile, tiles, logical index of the first tile in its list
                              // segment, rows of that segment, query tile index, qmap offset, queries}

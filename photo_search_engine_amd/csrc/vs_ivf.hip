@@ -329,9 +329,9 @@ void search_core(vs_ivf* ix, const float* q_dev, int64_t nq, int k, int nprobe, 
     size_t total_ints = 0;
     for (auto& v : cls_items) total_ints += v.size();
     ix->items.ensure(std::max<size_t>(total_ints, 1) * sizeof(int));
-    // one dynamic launch (default) takes the items most expensive class first; VS_IVF_DYN=0 keeps
-    // one launch per class (A/B)
-    static const bool dyn = !(getenv("VS_IVF_DYN") && atoi(getenv("VS_IVF_DYN")) == 0);
+    // one dynamic launch takes the items most expensive class first (measured faster than one
+    // launch per class)
+    constexpr bool dyn = true;
     {
         std::vector<int> all;
         all.reserve(total_ints);
@@ -372,7 +372,7 @@ void search_core(vs_ivf* ix, const float* q_dev, int64_t nq, int k, int nprobe, 
     a.gcnt = ix->gcnt.as<int>();
     a.lcap = lcap;
     // persistent scan workgroups: 8 per CU (32 waves) keep enough 16 B loads in flight per CU
-    static const int grid_per_cu = getenv("VS_IVF_GRID") ? std::max(1, atoi(getenv("VS_IVF_GRID"))) : 8;
+    constexpr int grid_per_cu = 8;
     const int max_grid = ix->num_cu * grid_per_cu;
     ix->cand.ensure((size_t)max_grid * IVF_QG * a.cap * sizeof(u64));
     a.cand = ix->cand.as<u64>();
@@ -487,8 +487,7 @@ void search_locked(vs_ivf* ix, const float* q_dev, int64_t nq, int k, int nprobe
         return;
     }
     nprobe = std::min(nprobe, ix->nlist);
-    static const int kp_min = getenv("VS_IVF_KP_MIN") ? atoi(getenv("VS_IVF_KP_MIN")) : 0;  // experiments
-    const int Kp = std::max(screen_depth(k), std::min(kp_min, KP_MAX));
+    const int Kp = screen_depth(k);
     ix->cert.ensure((size_t)nq * sizeof(int));
     search_core(ix, q_dev, nq, k, nprobe, Kp, D, I, S64, ix->cert.as<int>(), st, true);
     ix->cert_h.resize((size_t)nq);

@@ -915,7 +915,8 @@ __device__ __forceinline__ void screen_mfma(ScreenArgs a, const uint8_t* __restr
     const int tseed = t0;
     if (reuse) ++t0;
     if (tid < 256) {
-        const bool real = tid < nqb;
+        // (a fallback round screens only the queries its first pass left uncertified)
+        const bool real = tid < nqb && !(a.skip && a.skip[tid] != 0);
         const u64 k0 = real ? (a.thr0 ? a.thr0[tid] : 0ull) : ~0ull;
         thr_key[tid] = k0;
         thr_f[tid] = !real ? INFINITY : (k0 == 0ull ? -INFINITY : key_score(k0));
@@ -1532,20 +1533,24 @@ __global__ void __launch_bounds__(512, 2) k_screen_i8d(ScreenArgs a, const uint8
             }
             __builtin_amdgcn_wave_barrier();
         };
+        // the bound test of all 16 columns first (straight-line VALU, one bit per column)
+        uint32_t gomask = 0;
+#pragma unroll
+        for (int n = 0; n < 16; ++n) {
+            // bound of the column's 8 keys: max acc (exact int) -> fp32, times the rows' largest
+            // (acc >= 0) or smallest (acc < 0) scale, plus the largest error norm; each step is
+            // monotone, so a key that would pass implies a bound that passes
+            const float4 f = qrec[16 * n + qlane];
+            const int mi = max(max(max(acc[0][n][0], acc[0][n][1]), max(acc[0][n][2], acc[0][n][3])),
+                               max(max(acc[1][n][0], acc[1][n][1]), max(acc[1][n][2], acc[1][n][3])));
+            const float fm = (float)mi;
+            gomask |= (__builtin_fmaf(bmax, f.y, fmaxf(smax * fm, smin * fm)) * f.x >= f.z ? 1u : 0u) << n;
+        }
+        if (edge) gomask = 0xFFFFu;
         int nrec = 0;  // wave-uniform
 #pragma unroll
         for (int n = 0; n < 16; ++n) {
-            bool go = true;
-            if (!edge) {
-                // bound of the column's 8 keys: max acc (exact int) -> fp32, times the rows' largest
-                // (acc >= 0) or smallest (acc < 0) scale, plus the largest error norm; each step is
-                // monotone, so a key that would pass implies a bound that passes
-                const float4 f = qrec[16 * n + qlane];
-                const int mi = max(max(max(acc[0][n][0], acc[0][n][1]), max(acc[0][n][2], acc[0][n][3])),
-                                   max(max(acc[1][n][0], acc[1][n][1]), max(acc[1][n][2], acc[1][n][3])));
-                const float fm = (float)mi;
-                go = __builtin_fmaf(bmax, f.y, fmaxf(smax * fm, smin * fm)) * f.x >= f.z;
-            }
+            const bool go = (gomask >> n) & 1u;
             const u64 bal = __ballot(go);
             if (bal == 0ull) continue;
             const int c = __popcll(bal);
@@ -2449,8 +2454,10 @@ __global__ void __launch_bounds__(RF_THREADS) k_refine_redo(RefineArgs a, int KP
 }
 
 // ------------------------------------------------------------------------------------------------
-// K5w: exact refine behind the int8 screen -- adaptive depth, two phases, one block per query.
-// The screen keys are upper bounds: true <x, q> <= key_score + qeps[q] (k_pack_qtile_i8).
+// K5w: exact refine behind the int8 screen and the native MFMA screen's first passes (inner
+// product) -- adaptive depth, two phases, one block per query.  The screen keys are within qeps of
+// the true score from above: int8 keys are upper bounds, true <x, q> <= key_score + qeps[q]
+// (k_pack_qtile_i8); native keys are within the native margin either way.
 //  A: the best KA keys of the query's survivor list are scored exactly (canonical fp64); T' = the
 //     k-th best of them is a lower bound of the final k-th best exact score T.
 //  B: every other key with key_score >= T' - qeps could still reach T': those rows are scored too.
@@ -2554,7 +2561,12 @@ __global__ void __launch_bounds__(RF_THREADS) k_refine_wide(RefineArgs a, int KA
     const float* qv = a.q + (int64_t)q * a.d;
     if constexpr (QLDS)
         for (int i = tid; i < a.d; i += RF_THREADS) qs[(i & 7) * ng + (i >> 3)] = (double)qv[i];
-    const double eps = (double)a.qeps[q];
+    // the key's margin: int8 keys carry theirs per query (upper bounds: true <= key + qeps); native
+    // MFMA keys (qeps == null) are within the native screen's two-sided error of the true score
+    // (the same bound as k_refine's certificate: fp32 accumulation + query rounding, times max ||x||)
+    const double eps = a.qeps ? (double)a.qeps[q]
+                              : ((double)a.gamma * (double)a.qinfo[2 * q] + (double)a.qinfo[2 * q + 1]) *
+                                        (double)a.xmax * 1.01 + 1e-30;
     const double worst = -INFINITY;
     // ---- phase A: the best KA keys ----
     u64 keys[RF_E];
@@ -3193,7 +3205,8 @@ static void launch_refine_wide_one(const RefineArgs& a, int nq, int KA, size_t l
 }
 
 hipError_t launch_refine_wide(const RefineArgs& a, int nq, int KA, hipStream_t st) {
-    if (a.metric != METRIC_IP || !a.qeps || !a.cand_n || KA <= 0 || 2 * KA > RFW_CAP) return hipErrorInvalidValue;
+    if (a.metric != METRIC_IP || !(a.qeps || a.qinfo) || !a.cand_n || KA <= 0 || 2 * KA > RFW_CAP)
+        return hipErrorInvalidValue;
     const size_t base = (size_t)RFW_CAP * 12;
     const size_t qbytes = (size_t)((a.d + 7) >> 3) * 64;
     const bool qlds = base + qbytes <= 148 * 1024;

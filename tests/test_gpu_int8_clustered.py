@@ -1,0 +1,79 @@
+"""The int8 pre-screen on non-isotropic data: clustered rows in random and in
+cluster-sorted insertion order, tight and loose clusters, and the reference's own 77 x 4096 photo
+vectors.  The screen's seed is a sample (each workgroup's first tile): on sorted clusters it is
+biased, so the certificate may reject queries -- they are re-searched -- but the answer must stay
+bit-exact against ``oracle.knn_exact`` and identical to the native screen's."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from photo_search_engine_amd import faiss_format
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _mixture(n, d, n_clusters, sigma, seed, sort):
+    """normalise(c[cid] + sigma * g): the bench's cfg5 data model (bench.py `_mixture_rows`) on the
+    host; `sort` inserts the rows cluster by cluster (a corpus indexed folder by folder)."""
+    c = O.synth_rows(O.SEED_CORPUS + 900, 0, n_clusters, d, True)
+    g = O.synth_rows(seed, 0, n, d, True)
+    cid = np.random.default_rng(seed).integers(0, n_clusters, n)
+    if sort:
+        cid = np.sort(cid)
+    x = c[cid] + np.float32(sigma) * g
+    return (x / np.linalg.norm(x, axis=1, keepdims=True)).astype(np.float32)
+
+
+@pytest.mark.parametrize("sigma,sort", [(1.0, False), (1.0, True), (0.3, False), (0.3, True)])
+@pytest.mark.parametrize("k", [10, 100])
+def test_int8_screen_clustered_rows_exact(sigma, sort, k):
+    from photo_search_engine_amd.index import FlatIndex
+
+    N, d, nq, C = 300_000, 1536, 64, 64  # 1172 tiles: the seeded int8 path (>= 4 tiles per CU)
+    x = _mixture(N, d, C, sigma, O.SEED_CORPUS + 71, sort)
+    q = _mixture(nq, d, C, sigma, O.SEED_QUERIES + 71, False)
+    ix = FlatIndex(d, "ip", "bf16")
+    ix.add(x)
+    Dn, In = ix.search(q, k)
+    ix.set_screen("int8")
+    xs = ix.reconstruct_n(0, N)
+    S, Ie = O.knn_exact(xs, q, k, "ip")
+    # the first int8 batch may fail its certificates on dense clusters (re-searched exactly); its
+    # failure count, read back behind it, routes the following batches to the native screen, whose
+    # failing batches deepen its seed (include/vs.h "screen health")
+    for rep in range(6):
+        u0 = ix.uncertified_count()
+        D8, I8 = ix.search(q, k)
+        np.testing.assert_array_equal(I8, Ie)
+        np.testing.assert_array_equal(D8, S.astype(np.float32))
+        np.testing.assert_array_equal(I8, In)
+        np.testing.assert_array_equal(D8, Dn)
+        if rep == 5:  # by then the index has adapted: re-searches are rare
+            assert ix.uncertified_count() - u0 <= nq // 8
+    ix.close()
+
+
+def test_int8_screen_reference_photo_vectors():
+    """The reference's own index (77 real 4096-d photo embeddings, tests/golden): every row as a
+    query, int8 screen == native == oracle."""
+    from photo_search_engine_amd.index import FlatIndex
+
+    x = np.ascontiguousarray(faiss_format.read_index(os.path.join(GOLDEN, "ref_photo_search.index")).vectors,
+                             dtype=np.float32)
+    assert x.shape == (77, 4096)
+    for dtype in ("f32", "bf16"):
+        ix = FlatIndex(4096, "ip", dtype)
+        ix.add(x)
+        Dn, In = ix.search(x, 10)
+        ix.set_screen("int8")
+        D8, I8 = ix.search(x, 10)
+        S, Ie = O.knn_exact(ix.reconstruct_n(0, 77), x, 10, "ip")
+        np.testing.assert_array_equal(I8, Ie)
+        np.testing.assert_array_equal(D8, S.astype(np.float32))
+        np.testing.assert_array_equal(I8, In)
+        if dtype == "f32":
+            assert (I8[:, 0] == np.arange(77)).all()  # every (unit) photo vector finds itself first
+        ix.close()

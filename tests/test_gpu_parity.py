@@ -264,18 +264,19 @@ def test_device_exact_search_re_searches_uncertified_queries(FlatIndex, nq):
     assert ix.unresolved_count() == 0
 
 
-@pytest.mark.parametrize("nq", [1, 20])
-def test_ties_beyond_max_depth_are_reported(FlatIndex, nq):
-    # 5000 identical rows tie with the query's best score: no screen of KP_MAX = 4096 rows can
-    # certify that no unlisted copy wins.  vs_search raises VS_ERR_UNCERTIFIED; the device API (no
-    # host sync) counts the query in unresolved_count; the multi-device handle raises.
+@pytest.mark.parametrize("nq,copies", [(1, 5000), (20, 12000)])
+def test_ties_beyond_max_depth_are_reported(FlatIndex, nq, copies):
+    # `copies` identical rows tie with the query's best score: more than any screen depth (KP_MAX =
+    # 4096 rows for single queries; the batch refine's 8192 scored rows) can certify that no
+    # unlisted copy wins.  vs_search raises VS_ERR_UNCERTIFIED; the device API (no host sync)
+    # counts the query in unresolved_count; the multi-device handle raises.
     import torch
     from photo_search_engine_amd._lib import VsError
     from photo_search_engine_amd.index import MultiDeviceFlatIndex
     d, k = 64, 10
     x = O.synth_rows(O.SEED_CORPUS, 0, 25_000, d, True, "bf16")
     v = x[123].copy()
-    x[np.random.default_rng(3).choice(25_000, 5000, replace=False)] = v
+    x[np.random.default_rng(3).choice(25_000, copies, replace=False)] = v
     q = np.repeat(v[None], nq, axis=0)
     ix = FlatIndex(d, "ip", "bf16")
     ix.add(x)
@@ -292,6 +293,27 @@ def test_ties_beyond_max_depth_are_reported(FlatIndex, nq):
         m.search(q, k)
     assert e.value.code == -4
     m.close()
+    ix.close()
+
+
+def test_batch_refine_certifies_ties_within_its_depth(FlatIndex):
+    """5000 exact ties (beyond KP_MAX = 4096) in a 20-query batch: the adaptive refine lists and
+    scores every copy (<= 8192 rows), so the batch certifies with the exact answer -- the lowest-id
+    copies, faiss' tie order -- where a fixed-depth screen could only report the query."""
+    d, k, nq = 64, 10, 20
+    x = O.synth_rows(O.SEED_CORPUS, 0, 25_000, d, True, "bf16")
+    v = x[123].copy()
+    dup = np.random.default_rng(3).choice(25_000, 5000, replace=False)
+    x[dup] = v
+    ix = FlatIndex(d, "ip", "bf16")
+    ix.add(x)
+    q = np.repeat(v[None], nq, axis=0)
+    D, I = ix.search(q, k)
+    S, Ie = O.knn_exact(ix.reconstruct_n(0, 25_000), q, k, "ip")
+    np.testing.assert_array_equal(I, Ie)
+    np.testing.assert_array_equal(D, S.astype(np.float32))
+    assert set(I[0].tolist()) <= set(dup.tolist()) | {123}
+    assert ix.unresolved_count() == 0
     ix.close()
 
 
