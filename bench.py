@@ -258,7 +258,8 @@ def main():
                            (" + RCCL all-gather" if args.dist_backend == "nccl" else f" + {args.dist_backend} all-gather")
                            if G > 1 else "")},
             "roofline": {
-                "kernel": f"k_screen_{kind}",
+                # the int8 main pass runs the direct form when d is a multiple of 256 (vs_kernels.hip)
+                "kernel": "k_screen_i8d" if kind == "mfma_i8" and d % 256 == 0 else f"k_screen_{kind}",
                 "bound": "hbm",
                 "achieved": round(achieved_gbs, 1),
                 "peak": HBM_PEAK_GBS,

@@ -83,10 +83,11 @@ def main():
         summary["kernels"][f"{name} grid={grid}"] = flat
     # the bench's dominant screen (its roofline kernel; the seed pass's <.., true> variant excluded)
     kind = (bench_line or {}).get("roofline", {}).get("kernel", "")
-    pat = {"k_screen_mfma_i8": "k_screen_mfma<3,", "k_screen_mfma": "k_screen_mfma<",
-           "k_screen_gemv_i8": "k_screen_gemv<3,", "k_screen_gemv": "k_screen_gemv<"}
+    pat = {"k_screen_i8d": ("k_screen_i8d",), "k_screen_mfma_i8": ("k_screen_mfma<3,", "k_screen_i8d"),
+           "k_screen_mfma": ("k_screen_mfma<",), "k_screen_gemv_i8": ("k_screen_gemv<3,",),
+           "k_screen_gemv": ("k_screen_gemv<",)}
     screens = {k: v for k, v in summary["kernels"].items()
-               if pat.get(kind, "k_screen") in k and "true>" not in k and v.get("dur_s")
+               if any(p in k for p in pat.get(kind, ("k_screen",))) and "true>" not in k and v.get("dur_s")
                and not (kind in ("k_screen_mfma", "k_screen_gemv") and "<3," in k)}
     if screens and bench_line and bench_line["config"]["workload"] != "cfg5":
         top = max(screens, key=lambda k: screens[k]["dur_s"])
@@ -100,7 +101,8 @@ def main():
                    "profiled_kernel_ms": t["dur_s"] * 1e3, "clock_ghz": t.get("clock_ghz"),
                    "source": f"profiles/{tag}_pmc.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes)"}
         suffix = "" if cfg["n_local"] == cfg.get("N") else f"_n{cfg['n_local']}"
-        with open(os.path.join(prof, f"traffic_{cfg['workload']}_{kind.replace('k_screen_', '')}{suffix}.json"), "w") as f:
+        kname = {"k_screen_i8d": "k_screen_mfma_i8"}.get(kind, kind)  # (the bench's traffic lookup key)
+        with open(os.path.join(prof, f"traffic_{cfg['workload']}_{kname.replace('k_screen_', '')}{suffix}.json"), "w") as f:
             json.dump(traffic, f, indent=1)
         summary["dominant"] = traffic
     # IVF (cfg5): one search launches k_ivf_scan once per query-count class; traffic per search =
