@@ -279,9 +279,8 @@ def main():
         }
         if kind in ("mfma_i8", "gemv_i8"):
             out["int8_copy"] = {"hbm_bytes": ix.screen_copy_bytes(), "build_s": round(t_switch, 2),
-                                "note": "int8 codes + bf16 (scale, error norm) per row, and for bf16/f16 rows the "
-                                        "refine's row-major copy when it fits, on top of the stored rows (allocated "
-                                        "capacity)"}
+                                "note": "int8 codes + bf16 (scale, error norm) per row on top of the stored rows "
+                                        "(allocated capacity)"}
         if alt is not None:
             out["native_screen"] = alt
     if rank == 0 and G == 1 and not args.no_cpu_baseline and args.data == "iso":

@@ -147,7 +147,7 @@ int64_t vs_unresolved_count(vs_index* index);
  * context stages at most 8 MiB and loops over query chunks beyond that */
 int64_t vs_host_staging_bytes(vs_index* index);
 /* HBM bytes the screen copies hold beyond the stored rows (VS_SCREEN_I8: int8 codes, per-row scale |
- * error norm, and for bf16/f16 rows the refine's row-major copy when it fits); 0 for native screens */
+ * error norm); 0 for native screens */
 int64_t vs_screen_copy_bytes(vs_index* index);
 
 /* ==== multi-device flat index (one process, several GPUs; SURVEY.md §8 b/e) =================

@@ -99,8 +99,6 @@ struct vs_index {
     int64_t cap8 = 0;
     uint8_t* data8 = nullptr;
     uint32_t* rsb = nullptr;  // per row: bf16 scale | bf16 error norm (rounded up) << 16
-    uint8_t* datar = nullptr;  // int8 screen on bf16/f16 rows: row-major copy for the refine's gathers
-    int64_t rstride = 0;       //  (opt-in VS_I8_ROWMAJOR=1; absent when it does not fit in HBM)
     float i8_bmax = 0.0f;     // host copy of the largest row error norm (int8 GEMV depth)
     hipStream_t own = nullptr;  // ingest stream
     DevBuf stage[2];            // add_rows_host: fp32 chunks on the device ...
@@ -213,19 +211,10 @@ void ensure_capacity(vs_index* ix, int64_t rows_needed, bool exact = false) {
 void free_i8(vs_index* ix) {
     if (ix->data8) (void)hipFree(ix->data8);
     if (ix->rsb) (void)hipFree(ix->rsb);
-    if (ix->datar) (void)hipFree(ix->datar);
     ix->data8 = nullptr;
     ix->rsb = nullptr;
-    ix->datar = nullptr;
     ix->cap8 = 0;
 }
-
-// row-major copy for the int8 refine (bf16/f16 rows): whole-row gathers instead of 128 B lines
-// 32 KiB apart.  Measured at cfg3: k_refine_wide 247 -> 235 us per batch (-16 us per step) for
-// another N * d * 2 bytes of HBM (30.7 GB), so it is off (kRowMajorCopy; the refine keeps the code
-// path: rowm == null reads the tiled rows).  No environment variable changes a product path.
-constexpr bool kRowMajorCopy = false;
-bool want_rowmajor(const vs_index* ix) { return kRowMajorCopy && ix->dtype != DT_F32; }
 
 // grow the int8 screen copy to ix->cap_rows rows (device copy of the rows present; the old and new
 // arrays coexist only for the copy, as for the primary rows)
@@ -241,27 +230,15 @@ void ensure_capacity_i8(vs_index* ix) {
         if (nd) hipFree(nd);
         HIP_CHECK(e);
     }
-    const int64_t rstride = (int64_t)((ix->d + 7) / 8) * 16;
-    uint8_t* ndr = nullptr;
-    if (want_rowmajor(ix) && hipMalloc(&ndr, (size_t)ncap * rstride) != hipSuccess) {
-        (void)hipGetLastError();  // no room: the refine gathers from the tiled rows
-        ndr = nullptr;
-    }
     if (ix->data8 && ix->ntotal > 0) {
         const int64_t used_tiles = (ix->ntotal + TR - 1) / TR;
         HIP_CHECK(hipMemcpyAsync(nd, ix->data8, (size_t)used_tiles * tb8, hipMemcpyDeviceToDevice, ix->own));
         HIP_CHECK(hipMemcpyAsync(nr, ix->rsb, (size_t)ix->ntotal * sizeof(uint32_t), hipMemcpyDeviceToDevice, ix->own));
-        if (ndr) {
-            if (ix->datar) HIP_CHECK(hipMemcpyAsync(ndr, ix->datar, (size_t)ix->ntotal * rstride, hipMemcpyDeviceToDevice, ix->own));
-            else HIP_CHECK(launch_rowmajor_copy(ix->dtype, ix->data, ix->dpad, 0, ix->ntotal, ix->d, ndr, rstride, ix->own));
-        }
     }
     HIP_CHECK(hipStreamSynchronize(ix->own));
     free_i8(ix);
     ix->data8 = nd;
     ix->rsb = nr;
-    ix->datar = ndr;
-    ix->rstride = rstride;
     ix->cap8 = ncap;
 }
 
@@ -270,7 +247,6 @@ void quantize_rows(vs_index* ix, int64_t r0, int64_t n, hipStream_t st) {
     if (ix->screen != VS_SCREEN_I8 || n <= 0) return;
     HIP_CHECK(launch_quant_rows(ix->dtype, ix->data, ix->dpad, r0, n, ix->d, ix->data8, ix->dpad8, ix->rsb,
                                 ix->d_maxsq + 2, st));
-    if (ix->datar) HIP_CHECK(launch_rowmajor_copy(ix->dtype, ix->data, ix->dpad, r0, n, ix->d, ix->datar, ix->rstride, st));
 }
 
 void refresh_maxsq(vs_index* ix) {
@@ -466,8 +442,6 @@ void search_block_i8(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float
     r.dt = ix->dtype;
     r.metric = METRIC_IP;
     r.corpus = ix->data;
-    r.rowm = ix->datar;
-    r.rstride = ix->rstride;
     r.k = k;
     r.n_valid = ix->ntotal;
     r.id_offset = id_offset;
@@ -540,7 +514,7 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
         a.cap = (int)round_up(Kp + 2 * TR, 256);
         const int sdt = gemv_i8 ? DT_I8 : ix->dtype;
         const int dpadq = gemv_i8 ? ix->dpad8 : ix->dpad;
-        // work-queue tiles over exactly the resident blocks (VS_GEMV_DYN=0: static ranges, 8 per CU)
+        // work-queue tiles over exactly the resident blocks
         a.G = (int)std::min<int64_t>(tiles, (int64_t)ix->num_cu * (gemv_dyn() ? gemv_blocks_per_cu(sdt, QB) : 8));
         c->qpad.ensure((size_t)QB * dpadq * sizeof(float));
         int* ctr = nullptr;
@@ -605,7 +579,7 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
         sa.G = std::min(sa.G, 512);  // k_seed_select holds up to 8192 maxima per query
         sa.tile_stride = (int)(tiles / sa.G);
         // seed tile = the first tile of each main-pass workgroup; its raw accumulators are kept so
-        // the main pass starts one tile later (VS_SEED_REUSE=0: sample strided tiles, rescreen all)
+        // the main pass starts one tile later
         if (seed_reuse() && sa.G == a.G) {
             c->seedacc.ensure((size_t)a.G * 128 * MF_WG_THREADS * sizeof(float));
             sa.seed_acc = c->seedacc.as<float>();
@@ -1275,7 +1249,7 @@ int64_t vs_screen_copy_bytes(vs_index* ix) {
     if (!ix) return -1;
     if (!ix->data8) return 0;
     const int64_t rows = ix->cap8;
-    return (rows / TR) * (int64_t)TR * ix->dpad8 + rows * (int64_t)sizeof(uint32_t) + (ix->datar ? rows * ix->rstride : 0);
+    return (rows / TR) * (int64_t)TR * ix->dpad8 + rows * (int64_t)sizeof(uint32_t);
 }
 
 int64_t vs_unresolved_count(vs_index* ix) {

@@ -282,8 +282,6 @@ struct RefineArgs {
     int* fails;            // first pass: count of the block's uncertified queries (the fallback's gate)
     int redo;              // device fallback round: only queries with cert[q] == 0 are refined (and
     const int* gate;       //  their outputs rewritten), nothing at all while *gate == 0
-    const uint8_t* rowm;   // k_refine_wide, bf16/f16: row-major copy of the stored rows (or null =
-    int64_t rstride;       //  gather from the tiled corpus), rstride bytes per row
     int nsplit;            // k_refine, few queries with deep lists: > 1 workgroups per query each score
     double* gsc;           //  a slice of the kept rows into gsc / gids ([nq][KP2]); the last one to
     uint32_t* gids;        //  finish (gdone[q], zero between launches) sorts and certifies.  0/1 =
@@ -296,9 +294,6 @@ hipError_t launch_refine(const RefineArgs& a, int nq, hipStream_t st);
 hipError_t launch_refine_wide(const RefineArgs& a, int nq, int KA, hipStream_t st);
 constexpr int I8_MAX_K = 1024;  // largest k the int8 screen serves (k_refine_wide: 2 * KA <= RFW_CAP)
 // int8 screen copy of stored rows [r0, r0 + n) (maxes[0..1]: running max ||x_hat||, max beta)
-// row-major copy (rstride bytes per row, 16-B groups of 8 elements) of tiled bf16/f16 rows [r0, r0 + n)
-hipError_t launch_rowmajor_copy(int dt, const uint8_t* data, int dpad, int64_t r0, int64_t n, int d, uint8_t* rowm,
-                                int64_t rstride, hipStream_t st);
 hipError_t launch_quant_rows(int dt, const uint8_t* data, int dpad, int64_t r0, int64_t n, int d, uint8_t* data8,
                              int dpad8, uint32_t* rsb, unsigned* maxes, hipStream_t st);
 hipError_t launch_pack_qtile_i8(const float* q, int nqb, int d, int dpad8, uint8_t* qt, float2* qfac, float* qeps,

@@ -2161,9 +2161,7 @@ __device__ __forceinline__ bool better_exact(double sa, uint32_t ia, double sb, 
 // chunk is one 128 B line.
 template <int DT>
 constexpr int refine_rows() { return DT == DT_F32 ? 2 : 4; }  // (fp32 rows: twice the registers)
-// ROWM: corpus is a row-major copy (dpad = its row stride in bytes): a row's 16-B groups are
-// contiguous, so a wave's load instruction reads 1 KiB of one row instead of 8 lines 32 KiB apart.
-template <int DT, int METRIC, bool QLDS, int R, bool ROWM = false>
+template <int DT, int METRIC, bool QLDS, int R>
 __device__ __forceinline__ void exact_score_rows(const uint8_t* __restrict__ corpus, const int64_t (&row)[R],
                                                  const double* __restrict__ qs, const float* __restrict__ qg, int d,
                                                  int dpad, int lane, double (&out)[R]) {
@@ -2176,7 +2174,7 @@ __device__ __forceinline__ void exact_score_rows(const uint8_t* __restrict__ cor
 #pragma unroll
     for (int i = 0; i < R; ++i) {
         const int64_t r = row[i] >= 0 ? row[i] : row[0];
-        rb[i] = ROWM ? corpus + r * (int64_t)dpad : corpus + (r / TR) * (int64_t)TR * dpad * ES + (r % TR) * CHB;
+        rb[i] = corpus + (r / TR) * (int64_t)TR * dpad * ES + (r % TR) * CHB;
     }
     const int ng = (d + 7) >> 3;
     double acc[R];
@@ -2189,7 +2187,7 @@ __device__ __forceinline__ void exact_score_rows(const uint8_t* __restrict__ cor
             const int g = g0 + 64 * u;
             if (g < ng) {
                 const int e0 = 8 * g;
-                const int64_t off = ROWM ? (int64_t)e0 * ES : (int64_t)(e0 / CE) * TR * CHB + (e0 % CE) * ES;
+                const int64_t off = (int64_t)(e0 / CE) * TR * CHB + (e0 % CE) * ES;
 #pragma unroll
                 for (int i = 0; i < R; ++i)
                     if (i == 0 || row[i] >= 0)
@@ -2512,10 +2510,7 @@ __device__ __forceinline__ void rfw_score(const RefineArgs& a, const uint32_t* i
 #pragma unroll
         for (int i = 0; i < RR; ++i) rr[i] = j + i * NW < hi ? (int64_t)ids[j + i * NW] : -1;
         double s4[RR];
-        if (DT != DT_F32 && a.rowm)
-            exact_score_rows<DT, METRIC_IP, QLDS, RR, true>(a.rowm, rr, qs, qv, a.d, (int)a.rstride, lane, s4);
-        else
-            exact_score_rows<DT, METRIC_IP, QLDS, RR>(a.corpus, rr, qs, qv, a.d, a.dpad, lane, s4);
+        exact_score_rows<DT, METRIC_IP, QLDS, RR>(a.corpus, rr, qs, qv, a.d, a.dpad, lane, s4);
         if (lane == 0) {
 #pragma unroll
             for (int i = 0; i < RR; ++i)
@@ -2953,36 +2948,6 @@ hipError_t launch_pack_qtile_split(int dt, const float* q, const int* qidx, cons
     else
         return hipErrorInvalidValue;
     return hipGetLastError();
-}
-
-// one thread per 16-B group (8 bf16/f16 elements): tiled chunk piece -> row-major row
-__global__ void __launch_bounds__(256) k_rowmajor_copy(const uint8_t* __restrict__ data, int dpad, int64_t r0,
-                                                       int64_t n, int ng, uint8_t* __restrict__ rowm, int64_t rstride) {
-    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (t >= n * ng) return;
-    const int64_t row = r0 + t / ng;
-    const int e0 = 8 * (int)(t % ng);
-    constexpr int CE = CHB / 2;
-    const uint8_t* src = data + (row / TR) * (int64_t)TR * dpad * 2 + (int64_t)(e0 / CE) * TR * CHB + (row % TR) * CHB +
-                         (e0 % CE) * 2;
-    *(uint4*)(rowm + row * rstride + (int64_t)e0 * 2) = *(const uint4*)src;
-}
-
-hipError_t launch_rowmajor_copy(int dt, const uint8_t* data, int dpad, int64_t r0, int64_t n, int d, uint8_t* rowm,
-                                int64_t rstride, hipStream_t st) {
-    if (n <= 0) return hipSuccess;
-    if (dt == DT_F32 || rstride < (int64_t)((d + 7) / 8) * 16) return hipErrorInvalidValue;
-    const int ng = (d + 7) / 8;
-    const int64_t CHUNK = 1 << 20;  // rows per launch (grid-size bound)
-    for (int64_t c0 = 0; c0 < n; c0 += CHUNK) {
-        const int64_t m = n - c0 < CHUNK ? n - c0 : CHUNK;
-        const int64_t th = m * ng;
-        hipLaunchKernelGGL(k_rowmajor_copy, dim3((unsigned)((th + 255) / 256)), dim3(256), 0, st, data, dpad, r0 + c0, m,
-                           ng, rowm, rstride);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-    }
-    return hipSuccess;
 }
 
 hipError_t launch_quant_rows(int dt, const uint8_t* data, int dpad, int64_t r0, int64_t n, int d, uint8_t* data8,

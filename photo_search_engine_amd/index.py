@@ -161,8 +161,8 @@ class FlatIndex:
         return int(check(self._L.vs_host_staging_bytes(self._h)))
 
     def screen_copy_bytes(self) -> int:
-        """HBM bytes of the int8 screen's copies (codes, per-row scale | error norm, the refine's
-        row-major rows when they fit) on top of the stored rows; 0 on the native screen."""
+        """HBM bytes of the int8 screen's copy (codes, per-row scale | error norm) on top of the
+        stored rows; 0 on the native screen."""
         return int(check(self._L.vs_screen_copy_bytes(self._h)))
 
     # -- lifecycle ----------------------------------------------------------------------------
