@@ -119,6 +119,11 @@ def test_hnsw_graph_validation_and_staleness():
     D, I = hg.search(q, 5, 20)
     S_ref, I_ref = H.search(x, dup, q, 5, 20, "l2")
     _check(D, I, S_ref, I_ref)
+    # rows are append-only: the graph keeps searching its own first n rows after adds (the store
+    # searches the newer rows exactly and merges, test_gpu_hnsw_store.py)
     ix.add(O.synth_rows(O.SEED_CORPUS + 99, 0, 3, d, True))
+    D, I = hg.search(q, 5, 20)
+    _check(D, I, S_ref, I_ref)
+    ix.reset()  # fewer rows than the graph covers: refused
     with pytest.raises(_lib.VsError):
-        hg.search(q, 5, 20)  # the graph no longer covers every row
+        hg.search(q, 5, 20)
