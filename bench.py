@@ -57,6 +57,14 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="cfg3", choices=sorted(WORKLOADS) + sorted(IVF_WORKLOADS))
     ap.add_argument("--rows", type=int, default=0, help="override corpus rows (testing)")
+    ap.add_argument("--shard-of", type=int, default=0,
+                    help="measure ONE rank of a G-shard step on this GPU: its N/G-row shard, the two-phase "
+                         "search and both exchanges over a one-rank process group (not the BASELINE line)")
+    ap.add_argument("--one-phase", action="store_true",
+                    help="N > 1 / --shard-of: keep the one-phase local search (A/B of the two-phase step)")
+    ap.add_argument("--metric", default="ip", choices=["ip", "l2"],
+                    help="flat workloads: the index metric (BASELINE's configs are inner product; l2 = the "
+                         "reference's metric='l2' stores, utils/vector_store.py:79-81)")
     ap.add_argument("--screen", default=None, choices=["native", "int8"],
                     help="flat workloads: the screen of the timed steps (default: int8); "
                          "with int8 the native screen is timed too and reported beside it")
@@ -110,6 +118,13 @@ def main():
             dist.init_process_group(args.dist_backend)
     else:
         torch.cuda.set_device(local)
+        if args.shard_of > 1:  # the one-rank group that carries the exchanges of --shard-of
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
+            if args.dist_backend == "nccl":
+                dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", local))
+            else:
+                dist.init_process_group(args.dist_backend, rank=0, world_size=1)
     dev = torch.device("cuda", local)
 
     N, d, dtype, nq, k, desc = WORKLOADS[args.workload]
@@ -117,10 +132,14 @@ def main():
         N = args.rows
     G = world
     row0, n_local = shard_range(N, rank, G)
+    if args.shard_of > 1:
+        row0, n_local = shard_range(N, 0, args.shard_of)
 
     t_build = time.time()
     # the product's multi-GPU layer: one row shard per rank, all-gather + device merge (G > 1)
-    sh = ShardedFlatIndex(d, "ip", dtype, device=local)
+    sh = ShardedFlatIndex(d, args.metric, dtype, device=local)
+    if args.shard_of > 1:
+        sh.shards_hint = args.shard_of
     if args.data != "iso":
         # clustered rows: normalise(c[cid] + sigma g) over 64 unit centroids (the cfg5 data model,
         # `_mixture_rows`); sorted = inserted cluster by cluster (cid non-decreasing in row order)
@@ -146,6 +165,9 @@ def main():
             m = min(zeros.shape[0], n_local - r)
             sh.index.add_device(zeros.data_ptr(), m, torch.cuda.current_stream(dev).cuda_stream)
         del zeros
+    elif args.shard_of > 1:
+        sh.row0, sh.n_total = row0, N
+        sh.index.add_synthetic(SEED_CORPUS, row0, n_local, True)
     else:
         sh.add_synthetic(SEED_CORPUS, N, True)
     ix = sh.index
@@ -156,6 +178,10 @@ def main():
         q.copy_(_mixture_rows(SEED_QUERIES, 0, nq, d, cen, args.sigma, dev, stream.cuda_stream))
     torch.cuda.synchronize()
     screen = args.screen or DEFAULT_SCREEN.get(args.workload, "native")
+    if args.one_phase:
+        sh._two_phase_ok = lambda *a_: False
+    elif args.shard_of > 1 and screen == "int8":
+        sh.floor_override = _shard_floor(args, N, d, dtype, nq, k, q, local, dev, torch)
     t_build = time.time() - t_build
     result = {}
 
@@ -200,7 +226,7 @@ def main():
         el_n, km_n, kind_n, unc_n, _ = timed("native")
         res_native = {k_: v.clone() for k_, v in result.items()}
         kn = float(np.mean(km_n)) if km_n else float("nan")
-        bytes_n = n_local * d * es + nq * d * es + nq * k * 12
+        bytes_n = n_local * d * es + nq * d * es + nq * k * 12 + (n_local * 4 if args.metric == "l2" else 0)
         alt = {"screen": "native", "kernel": f"k_screen_{kind_n}", "value": round(nq * args.steps / el_n, 2),
                "ms_per_step": round(el_n * 1e3 / args.steps, 4), "kernel_ms": round(kn, 4),
                "hbm_frac": round(bytes_n / (kn * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
@@ -212,8 +238,18 @@ def main():
         dist.all_reduce(t)
         unresolved = int(t.item())
     if alt is not None:  # both screens return the same exact answer
-        alt["identical_results"] = bool(torch.equal(result["I"], res_native["I"]) and
-                                        torch.equal(result["S"], res_native["S"]))
+        if sh.floor_override is not None:
+            # --shard-of: the two-phase rank returns its share of the GLOBAL top-k exactly (entries at
+            # least as good as the G-shard floor), the native beside it its local top-k: compare those
+            fl = sh.floor_override[:, k - 1:k]
+            m1 = result["S"] >= fl if args.metric == "ip" else result["S"] <= fl
+            m2 = res_native["S"] >= fl if args.metric == "ip" else res_native["S"] <= fl
+            alt["identical_results"] = bool(torch.equal(m1, m2) and torch.equal(result["I"][m1], res_native["I"][m2])
+                                            and torch.equal(result["S"][m1], res_native["S"][m2]))
+            alt["compared"] = "entries at least as good as the G-shard floor"
+        else:
+            alt["identical_results"] = bool(torch.equal(result["I"], res_native["I"]) and
+                                            torch.equal(result["S"], res_native["S"]))
         del res_native
 
     ms_per_step = elapsed * 1e3 / args.steps
@@ -223,9 +259,11 @@ def main():
         # streamed per launch: the int8 codes + per-row (scale, error norm) + the queries (int8 for
         # the MFMA screen, fp32 for the GEMV) + the candidate lists
         alg_bytes = n_local * d + n_local * 4 + nq * d * (1 if kind == "mfma_i8" else 4) + nq * k * 12
+        if args.metric == "l2":
+            alg_bytes += n_local * 4  # the rows' ||x||^2
         peak_flops = MFMA_I8_PEAK_TOPS
     else:
-        alg_bytes = n_local * d * es + nq * d * es + nq * k * 12
+        alg_bytes = n_local * d * es + nq * d * es + nq * k * 12 + (n_local * 4 if args.metric == "l2" else 0)
         peak_flops = MFMA_BF16_PEAK_TF
     alg_flops = 2.0 * n_local * d * nq
     achieved_gbs = alg_bytes / (kavg * 1e-3) / 1e9
@@ -235,8 +273,12 @@ def main():
     if rank == 0:
         out = {
             # a --rows run is a different configuration: its metric names the rows it ran on
-            "metric": METRICS[args.workload] if not args.rows else
-            METRICS[args.workload].split(",")[0] + f" (rows override: N={N}, not the BASELINE config)",
+            "metric": (METRICS[args.workload] if not args.rows else
+                       METRICS[args.workload].split(",")[0] + f" (rows override: N={N}, not the BASELINE config)") +
+                      ("" if args.metric == "ip" else " [L2 metric, not the BASELINE config]") +
+                      (f" [one rank of a {args.shard_of}-shard step: {n_local} rows, both exchanges over a "
+                       "one-rank group, the G-shard floor precomputed; not the BASELINE line]"
+                       if args.shard_of > 1 else ""),
             "value": round(qps, 2),
             "unit": "queries/s",
             "n_gpus": G,
@@ -252,8 +294,10 @@ def main():
             "screen": "int8" if kind in ("mfma_i8", "gemv_i8") else "native",
             "data": ("synthetic (counter-hash N(0,1) rows, L2-normalised, seeds 20260417/20260418)" if args.data == "iso"
                      else f"synthetic Gaussian mixture ({args.data}, 64 clusters, sigma {args.sigma}), L2-normalised"),
-            "config": {"workload": args.workload, "desc": desc, "N": N, "d": d, "batch": nq, "k": k,
+            "config": {"workload": args.workload, "desc": desc, "N": N, "d": d, "batch": nq, "k": k, "metric": args.metric,
                        "n_local": n_local, "stored_rows": dtype, "screen": screen,
+                       "shard_of": args.shard_of or None,
+                       "two_phase": bool(sh._two_phase_ok(sh.index, nq, k)) and (G > 1 or args.shard_of > 1),
                        "parallelism": f"row-shard x{G}" + (
                            (" + RCCL all-gather" if args.dist_backend == "nccl" else f" + {args.dist_backend} all-gather")
                            if G > 1 else "")},
@@ -283,14 +327,36 @@ def main():
                                         "(allocated capacity)"}
         if alt is not None:
             out["native_screen"] = alt
-    if rank == 0 and G == 1 and not args.no_cpu_baseline and args.data == "iso":
+    if rank == 0 and G == 1 and not args.no_cpu_baseline and args.data == "iso" and args.metric == "ip" and not args.shard_of:
         out["cpu_baseline"], out["recall@10"], out["parity"] = cpu_baseline_and_recall(
             args, N, d, dtype, nq, k, local, torch, (result["D"].cpu().numpy(), result["I"].cpu().numpy()))
     if rank == 0:
         print(json.dumps(out), flush=True)
     sh.close()
-    if G > 1:
+    if G > 1 or args.shard_of > 1:
         dist.destroy_process_group()
+
+
+def _shard_floor(args, N, d, dtype, nq, k, q, local, dev, torch):
+    """--shard-of G (untimed setup): phase A of the two-phase search on each of the G shards in turn
+    (a temporary index per shard), merged on the device -- the floor all G ranks would share after
+    the first exchange, which the measured rank then uses in place of its one-rank exchange's."""
+    from photo_search_engine_amd.distributed import METRIC_CODES, _device_merge, shard_range
+    from photo_search_engine_amd.index import FlatIndex
+    G = args.shard_of
+    Sg = torch.empty((G, nq, k), dtype=torch.float64, device=dev)
+    Ig = torch.empty((G, nq, k), dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    for s_ in range(G):
+        r0, n = shard_range(N, s_, G)
+        t = FlatIndex(d, args.metric, dtype, device=local)
+        t.add_synthetic(SEED_CORPUS, r0, n, True)
+        t.set_screen("int8")
+        pend = t.search_phase_a(q.data_ptr(), nq, k, G, Sg[s_].data_ptr(), Ig[s_].data_ptr(), r0, stream)
+        t.search_pending_free(pend)
+        torch.cuda.synchronize()
+        t.close()
+    return _device_merge(METRIC_CODES[args.metric], Sg, Ig, k)[0]
 
 
 def _host_mem_bytes() -> int:

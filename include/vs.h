@@ -95,6 +95,30 @@ int vs_search_device(vs_index* index, const float* q_dev, int64_t nq, int32_t k,
 int vs_search_device_exact(vs_index* index, const float* q_dev, int64_t nq, int32_t k, float* D_dev,
                            int64_t* I_dev, double* S64_dev, int64_t id_offset, void* stream);
 
+/* ---- two-phase exact device search: the sharded step (one shard per rank) with a global T'
+ * exchange (no faiss counterpart; replaces vs_search_device_exact inside
+ * photo_search_engine_amd/distributed.py when vs_two_phase_ok says so).
+ *  phase A: screen the shard and score each query's best keys exactly; S_a / I_a (nq x k, device,
+ *           best-first, ids + id_offset, padded with -1 / worst score) are this shard's best so far;
+ *           returns a pending search in *out that holds the index's read lock and workspace;
+ *  (the caller all-gathers every shard's (S_a, I_a) and merges them: vs_merge_shards_device)
+ *  phase B: floor_S = that merged nq x k list (device): its k-th score per query is a lower bound
+ *           of the global k-th best, so the shard scores only rows whose bound reaches it and
+ *           certifies against it; writes the shard's exact top-k as vs_search_device_exact does
+ *           (its gated device fallback round included) and frees the pending search.
+ * Results after the final all-gather + merge are identical to vs_search_device_exact's.  Every rank
+ * must take the same path: vs_two_phase_ok depends only on the index configuration (int8 screen,
+ * bf16/f16 rows) and on (nq, k) -- one int8 MFMA block, 8 < nq <= 256, k <= 1024.  world = the
+ * number of shards (sets phase A's depth).  vs_search_pending_free drops a pending search whose
+ * phase B will not run. */
+typedef struct vs_pending vs_pending;
+int vs_two_phase_ok(vs_index* index, int64_t nq, int32_t k);
+int vs_search_device_phase_a(vs_index* index, const float* q_dev, int64_t nq, int32_t k, int32_t world,
+                             int64_t id_offset, double* S_a, int64_t* I_a, void* stream, vs_pending** out);
+int vs_search_device_phase_b(vs_pending* pending, const double* floor_S, float* D_dev, int64_t* I_dev,
+                             double* S64_dev, void* stream);
+void vs_search_pending_free(vs_pending* pending);
+
 /* ---- merge of per-shard results (all-gather + K3 merge).
  * S_in/I_in: G x nq x k (device), each list sorted best-first; output nq x k best-first under
  * (score desc | asc for L2, id asc).  D_out is S_out rounded to fp32 (may be NULL). */
@@ -122,7 +146,8 @@ int vs_write_rows_to_file(vs_index* index, const char* path, int64_t byte_offset
  * screen it with int8 MFMAs under a proven per-row error bound; an adaptive exact refine then
  * scores every candidate the bound cannot exclude.  Results are identical to the native path
  * (same exact ids and scores); queries the certificate rejects are re-searched natively.
- * Inner-product indexes only. */
+ * Both metrics: L2 keys bound the transformed score 2 <x, q> - ||x||^2 from above (the fp32 row
+ * norm and its rounding inside the margin), and the refine compares canonical distances. */
 int vs_set_screen(vs_index* index, int screen);
 int vs_screen(const vs_index* index);
 

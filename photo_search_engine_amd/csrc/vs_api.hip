@@ -58,6 +58,7 @@ struct Ctx {
     DevBuf qfac, qeps, drop;  // int8 screen: per-query code scale and norm, refine margin, drop bounds
     DevBuf fails;             // the current query block's certificate-failure count (fallback gate)
     DevBuf rsc, rdone;        // split refine: per-query scores + ids of the kept rows, done counters
+    DevBuf pa;       // two-phase (sharded) search: the refine's phase-1 state between the launches
     DevBuf rows[2];  // read_rows_host: unpacked fp32 chunks
     DevBuf tilectr;  // GEMV screen: tile work-queue counter
     DevBuf seedacc;  // MFMA seed pass: raw accumulators of each workgroup's seed tile
@@ -68,7 +69,8 @@ struct Ctx {
     unsigned* unres = nullptr;  // this call's unresolved-query counter (device), instead of the index's
     ~Ctx() {
         for (DevBuf* b : {&qdev, &qtile, &qinfo, &qpad, &cand, &part, &merge_a, &merge_b, &outD, &outI, &outS, &cert, &thr0,
-                          &seedmax, &gcnt, &rows[0], &rows[1], &tilectr, &seedacc, &outAll, &qfac, &qeps, &drop, &fails, &rsc, &rdone})
+                          &seedmax, &gcnt, &rows[0], &rows[1], &tilectr, &seedacc, &outAll, &qfac, &qeps, &drop, &fails, &rsc, &rdone,
+                          &pa})
             b->release();
         pin.release();
         hq.release();
@@ -363,8 +365,11 @@ double i8_union_target(int k, double sampled, double n) {
 
 // int8 pre-screen of one query block: pack int8 query codes -> seed pass -> int8 MFMA screen with
 // upper-bound keys -> adaptive exact refine (k_refine_wide).  q: device fp32 [nqb][d].
+// phase 1 (two-phase sharded search, KA1 keys in phase A): stops after the refine's phase A and
+// returns its arguments in *keep for vs_search_device_phase_b
 void search_block_i8(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float* D, int64_t* I, double* S64,
-                     int* cert, int64_t id_offset, hipStream_t st) {
+                     int* cert, int64_t id_offset, hipStream_t st, int phase = 0, int KA1 = 0,
+                     RefineArgs* keep = nullptr) {
     const int64_t tiles = (ix->ntotal + TR - 1) / TR;
     ScreenArgs a{};
     a.corpus = ix->data8;
@@ -372,7 +377,8 @@ void search_block_i8(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float
     a.tiles = (int)tiles;
     a.dpad = ix->dpad8;
     a.d = ix->d;
-    a.metric = METRIC_IP;
+    a.metric = ix->metric;  // L2: keys 2 (upper bound of <x, q>) - ||x||^2
+    a.sqn = ix->sqn;
     a.Kp = MFMA_KP_MAX;  // per workgroup and query; the refine's depth is adaptive
     a.cap = MFMA_CAP;
     a.G = (int)std::max<int64_t>(1, std::min<int64_t>(tiles, ix->num_cu));
@@ -385,7 +391,8 @@ void search_block_i8(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float
     c->fails.ensure(sizeof(int));
     HIP_CHECK(launch_pack_qtile_i8(q, nqb, ix->d, ix->dpad8, c->qtile.as<uint8_t>(), c->qfac.as<float2>(),
                                    c->qeps.as<float>(), ix->d_maxsq + 2, c->gcnt.as<int>(), c->drop.as<u64>(), st,
-                                   c->fails.as<int>()));
+                                   c->fails.as<int>(), ix->metric == METRIC_L2 ? ix->d_maxsq : nullptr,
+                                   gamma_of(ix->d)));
     a.qfac = c->qfac.as<float2>();
     a.drop = c->drop.as<u64>();
     a.lcap = a.G * a.Kp;
@@ -440,7 +447,8 @@ void search_block_i8(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float
     r.d = ix->d;
     r.dpad = ix->dpad;
     r.dt = ix->dtype;
-    r.metric = METRIC_IP;
+    r.metric = ix->metric;
+    r.xmax = (float)(std::sqrt((double)ix->maxsq) * (1.0 + 1e-5)) + 1e-30f;
     r.corpus = ix->data;
     r.k = k;
     r.n_valid = ix->ntotal;
@@ -454,6 +462,19 @@ void search_block_i8(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float
     r.drop = a.drop;
     r.thr0 = a.thr0;
     r.fails = c->fails.as<int>();
+    if (phase == 1) {
+        const int ka = KA1;
+        c->pa.ensure((size_t)nqb * ka * 12 + (size_t)nqb * 16);
+        r.phase = 1;
+        r.pa_cap = ka;
+        r.pa_sc = c->pa.as<double>();
+        r.pa_ids = (uint32_t*)(r.pa_sc + (size_t)nqb * ka);
+        r.pa_tA = (u64*)(r.pa_ids + (size_t)nqb * ka);
+        r.pa_n = (int*)(r.pa_tA + nqb);
+        HIP_CHECK(launch_refine_wide(r, nqb, ka, st));
+        if (keep) *keep = r;
+        return;
+    }
     HIP_CHECK(launch_refine_wide(r, nqb, (int)round_up(2 * k + 32, 32), st));
 }
 
@@ -775,6 +796,105 @@ void vs::search_exact_device(vs_index* ix, const float* q_dev, int64_t nq, int k
 
 unsigned* vs::unresolved_counter(vs_index* ix) { return ix->d_unres; }
 
+// ---- two-phase exact device search (the sharded step with a global T' exchange) ----
+// Phase A of every shard scores the best KA keys of each query's survivor list; the shards exchange
+// those top-k lists, and the merged k-th best (a lower bound of the global k-th best score) is the
+// floor under which phase B scores nothing and the certificate needs nothing: each shard then
+// scores about its share of the global refine window instead of a whole window of its own.
+// Applies to one int8 MFMA block of a bf16/f16 index (static: the same answer on every rank of a
+// collective); otherwise phase A runs the whole exact search and phase B returns its result.
+struct vs_pending {
+    vs_index* ix = nullptr;
+    std::shared_lock<std::shared_mutex> lk;
+    std::unique_ptr<CtxLease> L;
+    hipStream_t st = nullptr;
+    const float* q = nullptr;
+    int64_t nq = 0;
+    int k = 0, ka = 0;
+    int64_t id_offset = 0;
+    bool two = false;
+    RefineArgs r{};
+};
+
+bool vs::two_phase_ok(const vs_index* ix, int64_t nq, int k) {
+    return ix->screen == VS_SCREEN_I8 && ix->dtype != DT_F32 && nq > GEMV_NQ_MAX && nq <= MFMA_QB && k <= I8_MAX_K;
+}
+
+vs_pending* vs::search_phase_a(vs_index* ix, const float* q_dev, int64_t nq, int k, int world, int64_t id_offset,
+                               double* S_a, int64_t* I_a, hipStream_t st) {
+    check_index(ix);
+    if (k <= 0 || nq <= 0 || world <= 0) throw VsError(VS_ERR_ARG, "nq, k and world must be > 0");
+    if (ix->ntotal == 0) throw VsError(VS_ERR_ARG, "index is empty");
+    std::unique_ptr<vs_pending> p(new vs_pending());
+    p->ix = ix;
+    p->lk = std::shared_lock<std::shared_mutex>(ix->rw);
+    DeviceGuard dg(ix->device);
+    p->L.reset(new CtxLease(ix, st, false));
+    Ctx* c = p->L->c;
+    p->st = st;
+    p->q = q_dev;
+    p->nq = nq;
+    p->k = k;
+    p->id_offset = id_offset;
+    if (!two_phase_ok(ix, nq, k)) throw VsError(VS_ERR_ARG, "two-phase search: not applicable (vs_two_phase_ok)");
+    p->two = i8_allowed(ix);  // (routed to the native screen: phase A runs the whole search)
+    c->cert.ensure((size_t)nq * sizeof(int));
+    if (p->two) {
+        // phase A's depth: twice a shard's expected share of the global top-k (+32), so the shards'
+        // lists together hold the global k-th best of what they scored
+        const int share = (k + world - 1) / world;
+        p->ka = (int)std::min<int64_t>(round_up(2 * k + 32, 32), round_up(2 * share + 32, 32));
+        search_block_i8(ix, c, q_dev, (int)nq, k, nullptr, I_a, S_a, c->cert.as<int>(), id_offset, st, 1, p->ka,
+                        &p->r);
+    } else {
+        c->outS.ensure((size_t)nq * k * sizeof(double));
+        c->outI.ensure((size_t)nq * k * sizeof(int64_t));
+        c->outD.ensure((size_t)nq * k * sizeof(float));
+        search_all(ix, c, q_dev, nq, k, screen_depth(k), c->outD.as<float>(), c->outI.as<int64_t>(),
+                   c->outS.as<double>(), c->cert.as<int>(), id_offset, st, kOptimisticSeedRank, true);
+        HIP_CHECK(hipMemcpyAsync(S_a, c->outS.p, (size_t)nq * k * sizeof(double), hipMemcpyDeviceToDevice, st));
+        HIP_CHECK(hipMemcpyAsync(I_a, c->outI.p, (size_t)nq * k * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
+    }
+    return p.release();
+}
+
+void vs::search_phase_b(vs_pending* p, const double* floor_S, float* D, int64_t* I, double* S64, hipStream_t st) {
+    std::unique_ptr<vs_pending> own(p);
+    vs_index* ix = p->ix;
+    DeviceGuard dg(ix->device);
+    Ctx* c = p->L->c;
+    if (st != p->st) {  // order the caller's stream behind phase A's work
+        hipEvent_t e;
+        HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        HIP_CHECK(hipEventRecord(e, p->st));
+        HIP_CHECK(hipStreamWaitEvent(st, e, 0));
+        (void)hipEventDestroy(e);
+        p->L->st = st;
+    }
+    const int64_t nq = p->nq;
+    const int k = p->k;
+    if (!p->two) {
+        HIP_CHECK(hipMemcpyAsync(I, c->outI.p, (size_t)nq * k * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
+        if (S64) HIP_CHECK(hipMemcpyAsync(S64, c->outS.p, (size_t)nq * k * sizeof(double), hipMemcpyDeviceToDevice, st));
+        if (D) HIP_CHECK(hipMemcpyAsync(D, c->outD.p, (size_t)nq * k * sizeof(float), hipMemcpyDeviceToDevice, st));
+        return;
+    }
+    RefineArgs r = p->r;
+    r.phase = 2;
+    r.tfloor = floor_S;
+    r.tfloor_k = k;
+    r.D = D;
+    r.I = I;
+    r.S64 = S64;
+    HIP_CHECK(launch_refine_wide(r, (int)nq, p->ka, st));
+    health_note(ix, c, st, 1, (int)nq);
+    // the block's gated fallback round (native screen, local certificate), as search_all's
+    search_block(ix, c, p->q, (int)nq, k, std::max(screen_depth(k), fallback_depth(ix)), D, I, S64,
+                 c->cert.as<int>(), p->id_offset, st, 0, true);
+}
+
+void vs::search_pending_free(vs_pending* p) { delete p; }
+
 void vs::truncate_rows(vs_index* ix, int64_t n) {
     check_index(ix);
     std::unique_lock<std::shared_mutex> lk(ix->rw);
@@ -1061,6 +1181,35 @@ int vs_search_device_exact(vs_index* ix, const float* q_dev, int64_t nq, int32_t
     });
 }
 
+int vs_two_phase_ok(vs_index* ix, int64_t nq, int32_t k) {
+    if (!ix) return VS_ERR_ARG;
+    return two_phase_ok(ix, nq, k) ? 1 : 0;
+}
+
+int vs_search_device_phase_a(vs_index* ix, const float* q_dev, int64_t nq, int32_t k, int32_t world,
+                             int64_t id_offset, double* S_a, int64_t* I_a, void* stream, vs_pending** out) {
+    return guarded([&] {
+        if (!out || !q_dev || !S_a || !I_a) throw VsError(VS_ERR_ARG, "null argument");
+        *out = nullptr;
+        if (screen_depth(k) < k) throw VsError(VS_ERR_ARG, "k too large (max " + std::to_string(KP_MAX * 4 / 5) + ")");
+        *out = search_phase_a(ix, q_dev, nq, k, world, id_offset, S_a, I_a, (hipStream_t)stream);
+    });
+}
+
+int vs_search_device_phase_b(vs_pending* p, const double* floor_S, float* D_dev, int64_t* I_dev, double* S64_dev,
+                             void* stream) {
+    return guarded([&] {
+        if (!p) throw VsError(VS_ERR_ARG, "null pending search");
+        if (!floor_S || !I_dev) {
+            search_pending_free(p);
+            throw VsError(VS_ERR_ARG, "null device buffer");
+        }
+        search_phase_b(p, floor_S, D_dev, I_dev, S64_dev, (hipStream_t)stream);
+    });
+}
+
+void vs_search_pending_free(vs_pending* p) { search_pending_free(p); }
+
 int vs_search(vs_index* ix, const float* q, int64_t nq, int32_t k, float* D, int64_t* I) {
     return guarded([&] {
         check_index(ix);
@@ -1180,8 +1329,6 @@ int vs_set_screen(vs_index* ix, int screen) {
     return guarded([&] {
         check_index(ix);
         if (screen != VS_SCREEN_NATIVE && screen != VS_SCREEN_I8) throw VsError(VS_ERR_ARG, "screen must be 0 (native) or 1 (int8)");
-        if (screen == VS_SCREEN_I8 && ix->metric != VS_METRIC_IP)
-            throw VsError(VS_ERR_ARG, "the int8 screen serves inner-product indexes");
         std::unique_lock<std::shared_mutex> lk(ix->rw);
         DeviceGuard dg(ix->device);
         if (screen == ix->screen) return;

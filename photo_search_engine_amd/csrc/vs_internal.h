@@ -286,6 +286,19 @@ struct RefineArgs {
     double* gsc;           //  a slice of the kept rows into gsc / gids ([nq][KP2]); the last one to
     uint32_t* gids;        //  finish (gdone[q], zero between launches) sorts and certifies.  0/1 =
     unsigned* gdone;       //  one workgroup per query.
+    // k_refine_wide in two launches around an exchange (the sharded step, vs_search_device_phase_a
+    // / _phase_b): phase 1 scores the best KA keys and stops -- the top-k of them go to (D, I, S64)
+    // for the exchange, the scored rows to pa_* -- and phase 2 resumes from pa_* with the floor
+    // tfloor[q * tfloor_k + tfloor_k - 1] (a lower bound of the global k-th best score, metric
+    // domain: IP score / L2 distance) raising T'.  0 = one launch (both phases).
+    int phase;
+    double* pa_sc;         // [nq][pa_cap] phase-1 scored rows (sorted, worst-padded), their ids,
+    uint32_t* pa_ids;      //  count and phase-A key threshold
+    int* pa_n;
+    u64* pa_tA;
+    int pa_cap;
+    const double* tfloor;
+    int tfloor_k;
 };
 // workgroups per query of k_refine for a Kp-deep refine of nq queries (1 = no split)
 int refine_split(int nq, int Kp, int dt, int num_cu);
@@ -297,7 +310,8 @@ constexpr int I8_MAX_K = 1024;  // largest k the int8 screen serves (k_refine_wi
 hipError_t launch_quant_rows(int dt, const uint8_t* data, int dpad, int64_t r0, int64_t n, int d, uint8_t* data8,
                              int dpad8, uint32_t* rsb, unsigned* maxes, hipStream_t st);
 hipError_t launch_pack_qtile_i8(const float* q, int nqb, int d, int dpad8, uint8_t* qt, float2* qfac, float* qeps,
-                                const unsigned* maxes, int* gcnt, u64* drop, hipStream_t st, int* fails = nullptr);
+                                const unsigned* maxes, int* gcnt, u64* drop, hipStream_t st, int* fails = nullptr,
+                                const unsigned* l2max = nullptr, float gamma = 0.0f);
 
 // ---- IVF-Flat (vs_ivf.hip) ---------------------------------------------------------------------
 // Inverted lists are chains of pages: a page is one row tile (TR rows, the flat layout above) of
@@ -371,6 +385,12 @@ void search_exact_device(vs_index* ix, const float* q_dev, int64_t nq, int k, in
 // the shards that took their rows); the running maxima stay (they only widen certificate margins)
 void truncate_rows(vs_index* ix, int64_t n);
 unsigned* unresolved_counter(vs_index* ix);  // device word behind vs_unresolved_count
+// two-phase exact device search (vs_search_device_phase_a / _b)
+bool two_phase_ok(const vs_index* ix, int64_t nq, int k);
+vs_pending* search_phase_a(vs_index* ix, const float* q_dev, int64_t nq, int k, int world, int64_t id_offset,
+                           double* S_a, int64_t* I_a, hipStream_t st);
+void search_phase_b(vs_pending* p, const double* floor_S, float* D, int64_t* I, double* S64, hipStream_t st);
+void search_pending_free(vs_pending* p);
 // seed pass: screen one tile per workgroup (tile_stride) and write per-query 16-row-group maxima
 hipError_t launch_seed_mfma(int dt, const ScreenArgs& a, const uint8_t* qt, int nqb, hipStream_t st);
 // thr0[q] = key just below the rank-th largest of the M group maxima of query q (0 if none)

@@ -607,7 +607,8 @@ __global__ void __launch_bounds__(256) k_pack_qtile_i8(const float* __restrict__
                                                         uint8_t* __restrict__ qt, float2* __restrict__ qfac,
                                                         float* __restrict__ qeps, const unsigned* __restrict__ maxes,
                                                         int* __restrict__ gcnt, u64* __restrict__ drop,
-                                                        int* __restrict__ fails) {
+                                                        int* __restrict__ fails, const unsigned* __restrict__ l2max,
+                                                        float gamma) {
     const int lane = threadIdx.x & 63;
     const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= MFMA_QB) return;
@@ -669,7 +670,17 @@ __global__ void __launch_bounds__(256) k_pack_qtile_i8(const float* __restrict__
         // the screen computes key = t_q * (s_x acc + beta_x * (||q|| / t_q)); a zero query has t_q = 0
         // and every key 0
         qfac[r] = make_float2(t, t > 0.0f ? qn / t : 0.0f);
-        qeps[r] = f32_up((X * eq + slop) * (1.0 + 1e-9));
+        double e = X * eq + slop;
+        if (l2max) {
+            // L2 keys fl(2 fl(t v) - ||x||^2_fp32) bound 2 <x, q> - ||x||^2: twice the inner-product
+            // margin, the fp32 norm's error (gamma_d ||x||^2, its canonical sum) and the key's last
+            // rounding (relative 2^-24 of 2 (X ||t_q c_q|| + B ||q||) + ||x||^2)
+            const double S = (double)__uint_as_float(l2max[0]);  // max ||x||^2 (fp32)
+            e = 2.0 * e + ((double)gamma + 2.0 * 5.9604644775390625e-08) * S +
+                2.0 * 5.9604644775390625e-08 * (X * qh + B * (double)qn);
+            e *= 1.01;
+        }
+        qeps[r] = f32_up((e) * (1.0 + 1e-9));
     }
 }
 
@@ -854,6 +865,46 @@ __device__ __forceinline__ void mf_wave_compact(u64* __restrict__ buf, int n, in
     }
 }
 
+// Flush of a workgroup's candidate buffers into the per-query survivor lists, once every buffer
+// holds at most Kp keys (cnt[q] = its length).  Wave w owns queries w, w + 8, ... (32 per wave):
+// lanes 0..31 reserve their queries' list space with one atomic each, issued together, and the
+// wave's keys are then copied by one flat loop of independent loads and stores.  (One returning
+// atomic and one dependent copy per query in turn -- with every workgroup flushing at the same
+// moment onto the same 256 counters -- cost ~0.1 ms per launch: the screens' fixed overhead.)
+template <bool MAP>
+__device__ __forceinline__ void mf_flush_wave(const ScreenArgs& a, const u64* __restrict__ cand, const int* cnt,
+                                              int nqb, int wid, int lane) {
+    int n = 0, off = 0, qg = 0;
+    const int q = wid + 8 * lane;
+    if (lane < 32 && q < nqb) {
+        n = min(cnt[q], min(a.cap, a.Kp));
+        qg = MAP ? a.qmap[q] : q;
+        if (n > 0) off = atomicAdd(&a.gcnt[qg], n);
+    }
+    int incl = n;
+#pragma unroll
+    for (int sft = 1; sft < 64; sft <<= 1) {
+        const int v = __shfl_up(incl, sft, 64);
+        if (lane >= sft) incl += v;
+    }
+    const int total = __shfl(incl, 63, 64);
+    const int excl = incl - n;
+    for (int t0 = 0; t0 < total; t0 += 64) {  // (wave-uniform trip count: every lane shuffles)
+        const int t = t0 + lane;
+        int lo = 0, hi = 31;  // the owner: the last lane whose exclusive prefix is <= t
+#pragma unroll
+        for (int step = 0; step < 5; ++step) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (__shfl(excl, mid, 64) <= t) lo = mid;
+            else hi = mid - 1;
+        }
+        const int j = t - __shfl(excl, lo, 64);
+        const int o = __shfl(off, lo, 64);
+        const int g = __shfl(qg, lo, 64);
+        if (t < total) a.glist[(size_t)g * a.lcap + o + j] = cand[(size_t)(wid + 8 * lo) * a.cap + j];
+    }
+}
+
 // SEED: the threshold-seed pass (one tile per workgroup, 16-row-group maxima of the keys only).
 // Keys: bf16/f16 -> the fp32 MFMA score (L2: 2 x.q - ||x||^2); int8 -> the upper bound
 // s_x t_q <c_x, c_q> + ||e_x|| ||q|| of the true inner product (the query-side error term is
@@ -863,7 +914,10 @@ __device__ __forceinline__ void mf_wave_compact(u64* __restrict__ buf, int n, in
 template <int DT, int METRIC, bool SEED, bool MAP = false>
 __device__ __forceinline__ void screen_mfma(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
     constexpr bool I8 = DT == DT_I8;
-    static_assert(!I8 || METRIC == METRIC_IP, "the int8 screen serves inner-product indexes");
+    // int8 + L2: keys 2 (upper bound of <x, q>) - ||x||^2, the tile's ||x||^2 read by ordinary loads
+    // in the epilogue (this form serves the seed pass and the main pass of d % 256 != 0; the direct
+    // form k_screen_i8d stages them by LDS-DMA)
+    constexpr bool I8L2 = I8 && METRIC == METRIC_L2;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     u64* thr_key = (u64*)(smem + MF_SLOTS * MF_SLOT);
     float* thr_f = (float*)(smem + MF_SLOTS * MF_SLOT + 256 * 8);
@@ -1023,6 +1077,16 @@ __device__ __forceinline__ void screen_mfma(ScreenArgs a, const uint8_t* __restr
                     if (rowbase + rid0 + mi * 16 + r >= a.n_valid) bad |= 1u << (mi * 4 + r);
         }
         float sq[4][4], rb[4][4];  // L2: ||x||^2; int8: the row's scale and error norm (from LDS)
+        float sq8[4][4];           // int8 + L2: ||x||^2
+        if constexpr (I8L2) {
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int64_t gr = rowbase + rid0 + mi * 16 + r;
+                    sq8[mi][r] = a.sqn[gr < a.n_valid ? gr : a.n_valid - 1];
+                }
+        }
         if constexpr (ROWX) {
 #pragma unroll
             for (int mi = 0; mi < 4; ++mi) {
@@ -1065,6 +1129,12 @@ __device__ __forceinline__ void screen_mfma(ScreenArgs a, const uint8_t* __restr
                         v[mi][2 * h] = vv.x;
                         v[mi][2 * h + 1] = vv.y;
                     }
+                if constexpr (I8L2) {  // the keys themselves: 2 t_q v - ||x||^2
+#pragma unroll
+                    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) v[mi][r] = __builtin_fmaf(2.0f, v[mi][r] * tq, -sq8[mi][r]);
+                }
             } else {
 #pragma unroll
                 for (int mi = 0; mi < 4; ++mi)
@@ -1087,7 +1157,7 @@ __device__ __forceinline__ void screen_mfma(ScreenArgs a, const uint8_t* __restr
             for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) mx = fmaxf(mx, v[mi][r]);
-            if constexpr (I8) mx *= tq;  // monotone: fl(t * max v) = max fl(t * v)
+            if constexpr (I8 && !I8L2) mx *= tq;  // monotone: fl(t * max v) = max fl(t * v)
             // one compare per query column; the insert path runs only where something passes,
             // and then costs one LDS atomic per lane plus predicated stores
             if constexpr (SEED) {  // group g = wm*4 + lane/16 of the tile: 16 distinct rows
@@ -1102,7 +1172,7 @@ __device__ __forceinline__ void screen_mfma(ScreenArgs a, const uint8_t* __restr
                 for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        if constexpr (I8) v[mi][r] *= tq;  // the keys' scores
+                        if constexpr (I8 && !I8L2) v[mi][r] *= tq;  // the keys' scores
                         m |= (v[mi][r] >= tf ? 1u : 0u) << (mi * 4 + r);  // ties below
                     }
                 if (m) flag[2 + (ti & 1)] = 1;
@@ -1240,16 +1310,10 @@ __device__ __forceinline__ void screen_mfma(ScreenArgs a, const uint8_t* __restr
         if (n > a.Kp) {
             mf_wave_compact<MFMA_CAP / 64>(cand + (size_t)q * a.cap, n, a.Kp, &thr_key[q], &thr_f[q],
                                            a.drop ? a.drop + q : nullptr, lane);
-            n = a.Kp;
+            if (lane == 0) cnt[q] = a.Kp;  // (read back by this wave's flush: LDS order within a wave)
         }
-        if (n == 0) continue;
-        const int qg = MAP ? a.qmap[q] : q;
-        int off = 0;
-        if (lane == 0) off = atomicAdd(&a.gcnt[qg], n);
-        off = __shfl(off, 0, 64);
-        u64* dst = a.glist + (size_t)qg * a.lcap + off;
-        for (int j = lane; j < n; j += 64) dst[j] = cand[(size_t)q * a.cap + j];
     }
+    mf_flush_wave<MAP>(a, cand, cnt, nqb, wid, lane);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1285,7 +1349,7 @@ constexpr int I8D_RING = I8D_U * 16384;
 constexpr int I8D_REC = 64;  // per wave: staged (lane, column) records of the epilogue's per-row path
 constexpr int I8D_LDS = I8D_RING + 256 * 8 + 256 * 4 + 256 * 4 + 16 + MF_POOL * 8 + MF_POOL * 4 +
                         8 * I8D_REC * 32 /* record accumulators */ + 256 * 16 /* qrec */ + MF_ROWX +
-                        8 * I8D_REC * 4 /* record meta */;
+                        8 * I8D_REC * 4 /* record meta */ + MF_ROWX /* L2: ||x||^2 of two tiles */;
 static_assert(I8D_LDS <= 160 * 1024, "LDS budget (direct int8 screen)");
 static_assert(I8D_U == 4, "the K loop body and the vmcnt count are written for 4 slots");
 
@@ -1308,7 +1372,9 @@ __device__ __forceinline__ void i8d_wait_barrier(intx4& a0, intx4& a1) {
                  : "memory");
 }
 
+template <int METRIC>
 __global__ void __launch_bounds__(512, 2) k_screen_i8d(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
+    constexpr bool L2 = METRIC == METRIC_L2;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint8_t* const sm = smem + I8D_RING;
     u64* thr_key = (u64*)sm;
@@ -1323,6 +1389,8 @@ __global__ void __launch_bounds__(512, 2) k_screen_i8d(ScreenArgs a, const uint8
     uint32_t* rowx = (uint32_t*)(sm + 256 * 16 + 16 + MF_POOL * 12 + 8 * I8D_REC * 32 + 256 * 16);
     int* rmeta = (int*)(sm + 256 * 16 + 16 + MF_POOL * 12 + 8 * I8D_REC * 32 + 256 * 16 + MF_ROWX) +
                  (threadIdx.x >> 6) * I8D_REC;
+    // L2: the tiles' ||x||^2 (fp32, two tiles), the transformed key being 2 <x, q> - ||x||^2
+    float* rowq = (float*)(sm + 256 * 16 + 16 + MF_POOL * 12 + 8 * I8D_REC * 32 + 256 * 16 + MF_ROWX + 8 * I8D_REC * 4);
     asm volatile("; lds ring escapes: %0" ::"v"(smem) : "memory");
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -1352,6 +1420,11 @@ __global__ void __launch_bounds__(512, 2) k_screen_i8d(ScreenArgs a, const uint8
     const int trigger = a.cap - TR;
     const uint32_t ring = lds_addr(smem);
     const uint32_t rowx_lds = lds_addr((const uint8_t*)rowx);
+    // this wave's side-data DMA (wave-uniform, scalar): source rows and LDS destination
+    const int wid_s = __builtin_amdgcn_readfirstlane(wid);
+    const bool sq_wave = L2 && wid_s >= 4;
+    const uint32_t* const side_src = (sq_wave ? (const uint32_t*)a.sqn : a.rsb) + (wid_s & 3) * 64;
+    const uint32_t side_dst = (sq_wave ? lds_addr((const uint8_t*)rowq) : rowx_lds) + (uint32_t)((wid_s & 3) * 256);
     const int r16 = lane & 15;
     const uint32_t lane_off = (uint32_t)(r16 * 64 + (((lane >> 4) ^ mf_swz(r16)) << 4));
     const int a_off = wid * 2048 + r16 * 64 + (lane >> 4) * 16;  // lane's 16 B of the wave's first fragment
@@ -1366,9 +1439,11 @@ __global__ void __launch_bounds__(512, 2) k_screen_i8d(ScreenArgs a, const uint8
     int iti = t0, iks = 0;
 #define I8D_ISSUE(SET)                                                                                   \
     do {                                                                                                 \
-        if (iks == nks - 1 && iti < t1) /* 4 waves cover the 1 KiB; waves 4-7 rewrite the same bytes */ \
-            glds4(a.rsb + (int64_t)iti * TR + (wid & 3) * 64 + lane,                                     \
-                  __builtin_amdgcn_readfirstlane(rowx_lds + (uint32_t)((iti & 1) * 1024 + (wid & 3) * 256))); \
+        /* 4 waves cover the tile's 1 KiB of (scale | beta); waves 4-7 load its ||x||^2 (L2) or      \
+           rewrite the same bytes (inner product): the same op count for every wave */                 \
+        if (iks == nks - 1 && iti < t1)                                                                  \
+            glds4(side_src + (int64_t)iti * TR + lane,                                                   \
+                  __builtin_amdgcn_readfirstlane(side_dst + (uint32_t)((iti & 1) * 1024)));              \
         const uint32_t qbase = __builtin_amdgcn_readfirstlane(ring + (uint32_t)((SET) * 16384 + wid * 1024)); \
         _Pragma("unroll") for (int it = 0; it < 2; ++it) {                                               \
             const int g = it * 512 + wid * 64 + lane;                                                    \
@@ -1405,9 +1480,13 @@ __global__ void __launch_bounds__(512, 2) k_screen_i8d(ScreenArgs a, const uint8
         if (check_pending) {
             check_pending = false;
             if (flag[2 + ((ti - 1) & 1)] != 0) {  // skipped when the tile inserted nothing
+                // (thread-derived LDS addresses from an asm-opaque id: not hoisted out of the K loop,
+                // where they would hold VGPRs across it)
+                int otid;
+                asm volatile("v_mov_b32 %0, %1" : "=v"(otid) : "v"(tid));
                 int np = flag[1];
                 np = np < MF_POOL ? np : MF_POOL;
-                for (int j = tid; j < np; j += MF_THREADS) {  // the LDS pool -> candidate buffers
+                for (int j = otid; j < np; j += MF_THREADS) {  // the LDS pool -> candidate buffers
                     const int q = pool_q[j];
                     const int slot = atomicAdd(&cnt[q], 1);
                     if (slot < a.cap) cand[(size_t)q * a.cap + slot] = pool_key[j];
@@ -1423,7 +1502,7 @@ __global__ void __launch_bounds__(512, 2) k_screen_i8d(ScreenArgs a, const uint8
                 int need = 0;
 #pragma unroll
                 for (int i = 0; i < 256 / 64; ++i) {
-                    const int q = lane + 64 * i;
+                    const int q = (otid & 63) + 64 * i;
                     need |= (q < nqb && cnt[q] > trigger) ? 1 : 0;
                 }
                 if (__any(need)) {       // (uniform: every wave read the same counters)
@@ -1472,7 +1551,8 @@ __global__ void __launch_bounds__(512, 2) k_screen_i8d(ScreenArgs a, const uint8
         // the shard's last tile: rows >= n_valid (garbage side data) never qualify -> no bound test,
         // every pair is staged, and the per-row path makes those rows NaN
         const bool edge = rowbase + TR > a.n_valid;
-        float smax = 0.0f, smin = 0.0f, bmax = 0.0f;
+        const float* rq = rowq + (ti & 1) * TR;  // (L2)
+        float smax = 0.0f, smin = 0.0f, bmax = 0.0f, sqmin = 0.0f;
         {
             const int rw0 = wid * 32 + (olane >> 4) * 4;
             const uint4 w0 = *(const uint4*)(rx + rw0), w1 = *(const uint4*)(rx + rw0 + 16);
@@ -1484,6 +1564,10 @@ __global__ void __launch_bounds__(512, 2) k_screen_i8d(ScreenArgs a, const uint8
                 smax = fmaxf(smax, __uint_as_float(w8[j] << 16));
                 smin = fminf(smin, __uint_as_float(w8[j] << 16));
                 bmax = fmaxf(bmax, __uint_as_float(w8[j] & 0xFFFF0000u));
+            }
+            if constexpr (L2) {
+                const float4 n0 = *(const float4*)(rq + rw0), n1 = *(const float4*)(rq + rw0 + 16);
+                sqmin = fminf(fminf(fminf(n0.x, n0.y), fminf(n0.z, n0.w)), fminf(fminf(n1.x, n1.y), fminf(n1.z, n1.w)));
             }
         }
         // keys of the staged records, one per lane; the record slot is reused as value staging
@@ -1504,8 +1588,9 @@ __global__ void __launch_bounds__(512, 2) k_screen_i8d(ScreenArgs a, const uint8
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const int row = r0 + (j >> 2) * 16 + (j & 3);
-                    const float x = __builtin_fmaf(__uint_as_float(w8[j] & 0xFFFF0000u), f.y,
-                                                   (float)cc[j] * __uint_as_float(w8[j] << 16)) * f.x;
+                    float x = __builtin_fmaf(__uint_as_float(w8[j] & 0xFFFF0000u), f.y,
+                                             (float)cc[j] * __uint_as_float(w8[j] << 16)) * f.x;
+                    if constexpr (L2) x = __builtin_fmaf(2.0f, x, -rq[row]);  // 2 <x, q> - ||x||^2
                     v[j] = rowbase + row >= a.n_valid ? __builtin_nanf("") : x;
                     mh |= (v[j] >= f.z ? 1u : 0u) << j;  // (ties resolved by key below)
                 }
@@ -1544,7 +1629,9 @@ __global__ void __launch_bounds__(512, 2) k_screen_i8d(ScreenArgs a, const uint8
             const int mi = max(max(max(acc[0][n][0], acc[0][n][1]), max(acc[0][n][2], acc[0][n][3])),
                                max(max(acc[1][n][0], acc[1][n][1]), max(acc[1][n][2], acc[1][n][3])));
             const float fm = (float)mi;
-            gomask |= (__builtin_fmaf(bmax, f.y, fmaxf(smax * fm, smin * fm)) * f.x >= f.z ? 1u : 0u) << n;
+            float b = __builtin_fmaf(bmax, f.y, fmaxf(smax * fm, smin * fm)) * f.x;
+            if constexpr (L2) b = __builtin_fmaf(2.0f, b, -sqmin);  // (monotone: >= every row's key)
+            gomask |= (b >= f.z ? 1u : 0u) << n;
         }
         if (edge) gomask = 0xFFFFu;
         int nrec = 0;  // wave-uniform
@@ -1589,15 +1676,10 @@ __global__ void __launch_bounds__(512, 2) k_screen_i8d(ScreenArgs a, const uint8
         if (n > a.Kp) {
             mf_wave_compact<MFMA_CAP / 64>(cand + (size_t)q * a.cap, n, a.Kp, &thr_key[q], &thr_f[q],
                                            a.drop ? a.drop + q : nullptr, lane);
-            n = a.Kp;
+            if (lane == 0) cnt[q] = a.Kp;  // (read back by this wave's flush: LDS order within a wave)
         }
-        if (n == 0) continue;
-        int off = 0;
-        if (lane == 0) off = atomicAdd(&a.gcnt[q], n);
-        off = __shfl(off, 0, 64);
-        u64* dst = a.glist + (size_t)q * a.lcap + off;
-        for (int j = lane; j < n; j += 64) dst[j] = cand[(size_t)q * a.cap + j];
     }
+    mf_flush_wave<false>(a, cand, cnt, nqb, wid, lane);
 }
 
 // 16 B streaming load with the non-temporal hint (corpus and list bytes are read once per pass)
@@ -1747,8 +1829,12 @@ __global__ void __launch_bounds__(256) k_screen_gemv(ScreenArgs a, const float* 
 #pragma unroll
                     for (int qi = 0; qi < NQ; ++qi) {
                         float sc = acc[r][qi];
-                        if constexpr (I8) sc = fmaf(rbeta, a.qinfo[2 * qi], sq * sc);
-                        else if (a.metric == METRIC_L2) sc = 2.0f * sc - sq;
+                        if constexpr (I8) {
+                            sc = fmaf(rbeta, a.qinfo[2 * qi], sq * sc);
+                            if (a.metric == METRIC_L2) sc = 2.0f * sc - a.sqn[gr];
+                        } else if (a.metric == METRIC_L2) {
+                            sc = 2.0f * sc - sq;
+                        }
                         if (sc >= thr_f[qi]) {
                             const u64 key = mk_key(sc, (uint32_t)gr);
                             if (key > thr_key[qi]) {
@@ -2498,8 +2584,9 @@ __device__ __forceinline__ int block_write_ids(const u64 (&keys)[E], u64 lo, u64
     return total;
 }
 
-// scores of ids[lo, hi) into sc[lo, hi): 16 waves, two rows in flight per wave
-template <int DT, bool QLDS>
+// scores of ids[lo, hi) into sc[lo, hi): 16 waves, two rows in flight per wave.  L2: sc holds the
+// negated canonical distance, so one order (higher first, ties to the lower id) serves both metrics
+template <int DT, int METRIC, bool QLDS>
 __device__ __forceinline__ void rfw_score(const RefineArgs& a, const uint32_t* ids, double* sc, int lo, int hi,
                                           const double* qs, const float* qv) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -2510,11 +2597,11 @@ __device__ __forceinline__ void rfw_score(const RefineArgs& a, const uint32_t* i
 #pragma unroll
         for (int i = 0; i < RR; ++i) rr[i] = j + i * NW < hi ? (int64_t)ids[j + i * NW] : -1;
         double s4[RR];
-        exact_score_rows<DT, METRIC_IP, QLDS, RR>(a.corpus, rr, qs, qv, a.d, a.dpad, lane, s4);
+        exact_score_rows<DT, METRIC, QLDS, RR>(a.corpus, rr, qs, qv, a.d, a.dpad, lane, s4);
         if (lane == 0) {
 #pragma unroll
             for (int i = 0; i < RR; ++i)
-                if (rr[i] >= 0) sc[j + i * NW] = s4[i];
+                if (rr[i] >= 0) sc[j + i * NW] = METRIC == METRIC_L2 ? -s4[i] : s4[i];
         }
     }
 }
@@ -2541,14 +2628,16 @@ __device__ __forceinline__ void rfw_sort(double* sc, uint32_t* ids, int n2) {
     }
 }
 
-template <int DT, bool QLDS>
+template <int DT, int METRIC, bool QLDS>
 __global__ void __launch_bounds__(RF_THREADS) k_refine_wide(RefineArgs a, int KA) {
+    constexpr bool L2 = METRIC == METRIC_L2;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     double* sc = (double*)smem;                                  // [RFW_CAP]
     uint32_t* ids = (uint32_t*)(smem + (size_t)RFW_CAP * 8);     // [RFW_CAP]
     double* qs = (double*)(smem + (size_t)RFW_CAP * 12);         // fp64 query, transposed groups
     __shared__ int red[RF_THREADS / 64];
     __shared__ int nb_s;
+    __shared__ double qq_s;
     const int q = blockIdx.x, tid = threadIdx.x;
     const int ng = (a.d + 7) >> 3;
     const u64* src = a.cand + (size_t)q * a.lcap;
@@ -2559,21 +2648,36 @@ __global__ void __launch_bounds__(RF_THREADS) k_refine_wide(RefineArgs a, int KA
     // the key's margin: int8 keys carry theirs per query (upper bounds: true <= key + qeps); native
     // MFMA keys (qeps == null) are within the native screen's two-sided error of the true score
     // (the same bound as k_refine's certificate: fp32 accumulation + query rounding, times max ||x||)
-    const double eps = a.qeps ? (double)a.qeps[q]
-                              : ((double)a.gamma * (double)a.qinfo[2 * q] + (double)a.qinfo[2 * q + 1]) *
-                                        (double)a.xmax * 1.01 + 1e-30;
+    double eps = a.qeps ? (double)a.qeps[q]
+                        : ((double)a.gamma * (double)a.qinfo[2 * q] + (double)a.qinfo[2 * q + 1]) *
+                                  (double)a.xmax * 1.01 + 1e-30;
+    // L2 (int8 keys of 2 <x, q> - ||x||^2, margin in qeps): the canonical distance D is compared with
+    // the keys as ||q||^2 - D, whose fp64 evaluation adds ~1e-16 relative (budgeted 1e-12)
+    double qq = 0.0;
+    if constexpr (L2) {
+        if (tid < 64) {
+            double s2 = 0.0;
+            for (int i = tid; i < a.d; i += 64) s2 += (double)qv[i] * (double)qv[i];
+            s2 = wave_sum_f64(s2);
+            if (tid == 0) qq_s = s2;
+        }
+        __syncthreads();
+        qq = qq_s;
+        eps += 1e-12 * (qq + (double)a.xmax * (double)a.xmax);
+    }
     const double worst = -INFINITY;
     // ---- phase A: the best KA keys ----
     u64 keys[RF_E];
     const bool inreg = n <= RF_THREADS * RF_E;
+    u64 tA = 1ull;  // keys >= tA form phase A
+    int nA, nA2 = 1;
+    if (a.phase != 2) {
 #pragma unroll
     for (int e = 0; e < RF_E; ++e) {
         const int j = tid + RF_THREADS * e;
         keys[e] = (inreg && j < n) ? src[j] : 0ull;
     }
-    u64 tA = 1ull;  // keys >= tA form phase A
     if (n > KA) tA = inreg ? block_kth<RF_E>(keys, KA, red) : block_kth_mem(src, n, KA, red);
-    int nA;
     if (inreg) {
         nA = block_write_ids<RF_E>(keys, tA, ~0ull, ids, RFW_CAP, red);
     } else {  // very long lists: the phase-A set from memory (block_compact_mem writes keys)
@@ -2598,9 +2702,8 @@ __global__ void __launch_bounds__(RF_THREADS) k_refine_wide(RefineArgs a, int KA
     }
     nA = min(nA, RFW_CAP);
     __syncthreads();
-    rfw_score<DT, QLDS>(a, ids, sc, 0, nA, qs, qv);
+    rfw_score<DT, METRIC, QLDS>(a, ids, sc, 0, nA, qs, qv);
     __syncthreads();
-    int nA2 = 1;
     while (nA2 < nA) nA2 <<= 1;
     for (int j = nA + tid; j < nA2; j += RF_THREADS) {
         sc[j] = worst;
@@ -2608,12 +2711,48 @@ __global__ void __launch_bounds__(RF_THREADS) k_refine_wide(RefineArgs a, int KA
     }
     __syncthreads();
     rfw_sort(sc, ids, nA2);  // phase A best first (nA2 <= RFW_CAP: KA <= RFW_CAP / 2)
-    const double Tp = nA >= a.k ? sc[a.k - 1] : -INFINITY;
+    } else {  // phase 2: resume from the phase-1 state
+        nA = a.pa_n[q];
+        tA = a.pa_tA[q];
+        while (nA2 < nA) nA2 <<= 1;
+        for (int j = tid; j < nA2; j += RF_THREADS) {
+            sc[j] = j < nA ? a.pa_sc[(size_t)q * a.pa_cap + j] : worst;
+            ids[j] = j < nA ? a.pa_ids[(size_t)q * a.pa_cap + j] : 0xFFFFFFFFu;
+        }
+        __syncthreads();
+    }
+    if (a.phase == 1) {  // phase 1 ends here: its state, and its top-k for the exchange
+        for (int j = tid; j < nA; j += RF_THREADS) {
+            a.pa_sc[(size_t)q * a.pa_cap + j] = sc[j];
+            a.pa_ids[(size_t)q * a.pa_cap + j] = ids[j];
+        }
+        if (tid == 0) {
+            a.pa_n[q] = nA;
+            a.pa_tA[q] = tA;
+        }
+        for (int j = tid; j < a.k; j += RF_THREADS) {
+            const size_t o = (size_t)q * a.k + j;
+            const double v = j < nA ? (L2 ? -sc[j] : sc[j]) : (L2 ? 1.7976931348623157e308 : -1.7976931348623157e308);
+            if (a.D) a.D[o] = j < nA ? (float)v : (L2 ? 3.402823466e+38f : -3.402823466e+38f);
+            a.I[o] = j < nA ? (int64_t)ids[j] + a.id_offset : -1;
+            if (a.S64) a.S64[o] = v;
+        }
+        return;
+    }
+    // the exchange's floor: a lower bound of the global k-th best score (all shards' phase-1 rows)
+    double floor_sc = -INFINITY;
+    if (a.tfloor) {
+        const double f = L2 ? -a.tfloor[(size_t)q * a.tfloor_k + a.tfloor_k - 1]
+                            : a.tfloor[(size_t)q * a.tfloor_k + a.tfloor_k - 1];
+        if (f > -1.7976931348623157e308) floor_sc = f;  // (padding -DBL_MAX / +DBL_MAX distance: none)
+    }
+    const double Tp = fmax(nA >= a.k ? sc[a.k - 1] : -INFINITY, floor_sc);
     // ---- phase B: keys in [tB, tA) whose bound reaches T' ----
     u64 tB = 1ull;
     if (Tp > -INFINITY) {
-        float f = (float)(Tp - eps);
-        if ((double)f > Tp - eps) f = nextafterf(f, -INFINITY);  // round down: keys below tB score < T' - eps
+        const double TpK = L2 ? qq + Tp : Tp;  // T' in the keys' domain
+        float f = (float)(TpK - eps);
+        if ((double)f > TpK - eps) f = nextafterf(f, -INFINITY);  // round down: keys below tB score < T' - eps
         tB = (u64)ord_f32(f) << 32;
         if (tB == 0ull) tB = 1ull;
     }
@@ -2651,7 +2790,7 @@ __global__ void __launch_bounds__(RF_THREADS) k_refine_wide(RefineArgs a, int KA
     const bool overflow = nA2 + nB > RFW_CAP;
     nB = min(nB, RFW_CAP - nA2);
     __syncthreads();
-    rfw_score<DT, QLDS>(a, ids, sc, nA2, nA2 + nB, qs, qv);
+    rfw_score<DT, METRIC, QLDS>(a, ids, sc, nA2, nA2 + nB, qs, qv);
     __syncthreads();
     // phase-B rows that beat T' join the phase-A list (order-preserving compaction in place)
     if (tid == 0) nb_s = 0;
@@ -2694,7 +2833,10 @@ __global__ void __launch_bounds__(RF_THREADS) k_refine_wide(RefineArgs a, int KA
         if (a.thr0 && a.thr0[q] > th) th = a.thr0[q];
         int cert = overflow ? 0 : 1;
         if (cert && th != 0ull) {  // some rows were never listed
-            const double T = nF >= a.k ? sc[a.k - 1] : -INFINITY;
+            // rows never listed score < T: below the k-th best of this shard's scored rows, or below
+            // the exchange's floor (<= the global k-th best): in neither case in the global top-k
+            const double Tl = fmax(nF >= a.k ? sc[a.k - 1] : -INFINITY, floor_sc);
+            const double T = Tl > -INFINITY ? (L2 ? qq + Tl : Tl) : -INFINITY;
             cert = ((double)key_score(th) + eps < T) ? 1 : 0;
         }
         if (a.cert) a.cert[q] = cert;
@@ -2704,13 +2846,14 @@ __global__ void __launch_bounds__(RF_THREADS) k_refine_wide(RefineArgs a, int KA
     for (int j = tid; j < a.k; j += RF_THREADS) {
         const size_t o = (size_t)q * a.k + j;
         if (j < nF) {
-            if (a.D) a.D[o] = (float)sc[j];
+            const double v = L2 ? -sc[j] : sc[j];
+            if (a.D) a.D[o] = (float)v;
             a.I[o] = (int64_t)ids[j] + a.id_offset;
-            if (a.S64) a.S64[o] = sc[j];
+            if (a.S64) a.S64[o] = v;
         } else {
-            if (a.D) a.D[o] = -3.402823466e+38f;
+            if (a.D) a.D[o] = L2 ? 3.402823466e+38f : -3.402823466e+38f;
             a.I[o] = -1;
-            if (a.S64) a.S64[o] = -1.7976931348623157e308;
+            if (a.S64) a.S64[o] = L2 ? 1.7976931348623157e308 : -1.7976931348623157e308;
         }
     }
 }
@@ -2794,6 +2937,72 @@ __global__ void __launch_bounds__(256) k_seed_select(const float* __restrict__ s
 // one wave per query: lane g < G holds the head of shard list g; each of the k rounds picks the
 // best head by a wave butterfly on (score, id) -- score desc (IP) / asc (L2), ties -> lower id --
 // and the winning lane advances.  Lists end at their first id -1.
+// Merge by rank (G * k <= kMergeRankMax, one 256-thread workgroup per query): the G lists go to
+// LDS; every valid entry's output position is its index in its own list plus, for every other
+// list, the number of that list's entries ahead of it -- a binary search, since each list is sorted
+// under the same total order (score, then id, then list index) -- so no entry waits on another and
+// the ~k dependent steps (each a global load) of k_merge_shards' wave-per-query merge are gone.
+constexpr int kMergeRankMax = 4096;  // G * k entries (16 B each) in LDS
+__global__ void __launch_bounds__(256) k_merge_shards_rank(int metric, const double* __restrict__ S_in,
+                                                           const int64_t* __restrict__ I_in, int G, int64_t nq, int k,
+                                                           double* __restrict__ S_out, int64_t* __restrict__ I_out,
+                                                           float* __restrict__ D_out) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    double* ss = (double*)smem;
+    int64_t* si = (int64_t*)(smem + (size_t)G * k * 8);
+    __shared__ int nval[64];
+    const int64_t q = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int n = G * k;
+    const bool ip = metric == METRIC_IP;
+    if (tid < 64) nval[tid] = 0;
+    __syncthreads();
+    for (int i = tid; i < n; i += 256) {
+        const int g = i / k, j = i - g * k;
+        const size_t o = ((size_t)g * nq + q) * k + j;
+        const int64_t id = I_in[o];
+        si[i] = id;
+        ss[i] = id >= 0 ? S_in[o] : 0.0;
+        if (id >= 0) atomicAdd(&nval[g], 1);  // (valid entries are each list's prefix)
+    }
+    __syncthreads();
+    int total = 0;
+    for (int g = 0; g < G; ++g) total += nval[g];
+    for (int i = tid; i < n; i += 256) {
+        const int g = i / k, j = i - g * k;
+        if (j >= nval[g]) continue;
+        const double s = ss[i];
+        const int64_t id = si[i];
+        int rank = j;
+        for (int g2 = 0; g2 < G && rank < k; ++g2) {
+            if (g2 == g) continue;
+            const double* s2 = ss + (size_t)g2 * k;
+            const int64_t* i2 = si + (size_t)g2 * k;
+            int lo = 0, hi = nval[g2];
+            while (lo < hi) {  // entries of list g2 ahead of (s, id, g)
+                const int mid = (lo + hi) >> 1;
+                const double sm = s2[mid];
+                const bool ahead = sm != s ? (ip ? sm > s : sm < s) : (i2[mid] != id ? i2[mid] < id : g2 < g);
+                if (ahead) lo = mid + 1;
+                else hi = mid;
+            }
+            rank += lo;
+        }
+        if (rank < k) {
+            const size_t oo = (size_t)q * k + rank;
+            S_out[oo] = s;
+            I_out[oo] = id;
+            if (D_out) D_out[oo] = (float)s;
+        }
+    }
+    for (int r = total + tid; r < k; r += 256) {  // every list exhausted: padding
+        const size_t oo = (size_t)q * k + r;
+        S_out[oo] = ip ? -1.7976931348623157e308 : 1.7976931348623157e308;
+        I_out[oo] = -1;
+        if (D_out) D_out[oo] = ip ? -3.402823466e+38f : 3.402823466e+38f;
+    }
+}
+
 __global__ void __launch_bounds__(256) k_merge_shards(int metric, const double* __restrict__ S_in,
                                                       const int64_t* __restrict__ I_in, int G, int64_t nq, int k,
                                                       double* __restrict__ S_out, int64_t* __restrict__ I_out,
@@ -2965,9 +3174,10 @@ hipError_t launch_quant_rows(int dt, const uint8_t* data, int dpad, int64_t r0, 
 }
 
 hipError_t launch_pack_qtile_i8(const float* q, int nqb, int d, int dpad8, uint8_t* qt, float2* qfac, float* qeps,
-                                const unsigned* maxes, int* gcnt, u64* drop, hipStream_t st, int* fails) {
+                                const unsigned* maxes, int* gcnt, u64* drop, hipStream_t st, int* fails,
+                                const unsigned* l2max, float gamma) {
     hipLaunchKernelGGL(k_pack_qtile_i8, dim3(MFMA_QB / 4), dim3(256), 0, st, q, nqb, d, dpad8, qt, qfac, qeps, maxes,
-                       gcnt, drop, fails);
+                       gcnt, drop, fails, l2max, gamma);
     return hipGetLastError();
 }
 
@@ -3007,14 +3217,19 @@ template <bool SEED>
 static hipError_t launch_mfma_dt(int dt, const ScreenArgs& a, const uint8_t* qt, int nqb, hipStream_t st) {
     if (a.gate && (SEED || dt == DT_I8)) return hipErrorInvalidValue;  // fallback rounds: native main screen
     if (dt == DT_I8) {
-        if (a.metric != METRIC_IP || !a.rsb || !a.qfac) return hipErrorInvalidValue;
+        if (!a.rsb || !a.qfac || (a.metric == METRIC_L2 && !a.sqn)) return hipErrorInvalidValue;
         if (!SEED && i8_direct_ok(a.dpad)) {  // the main pass: direct form (no seed-tile reuse)
             if (a.seed_acc || a.tile_stride != 0) return hipErrorInvalidValue;
-            set_lds_attr((const void*)k_screen_i8d, I8D_LDS);
-            hipLaunchKernelGGL(k_screen_i8d, dim3(a.G), dim3(MF_THREADS), I8D_LDS, st, a, qt, nqb);
+            const void* fn = a.metric == METRIC_IP ? (const void*)k_screen_i8d<METRIC_IP> : (const void*)k_screen_i8d<METRIC_L2>;
+            set_lds_attr(fn, I8D_LDS);
+            if (a.metric == METRIC_IP)
+                hipLaunchKernelGGL(k_screen_i8d<METRIC_IP>, dim3(a.G), dim3(MF_THREADS), I8D_LDS, st, a, qt, nqb);
+            else
+                hipLaunchKernelGGL(k_screen_i8d<METRIC_L2>, dim3(a.G), dim3(MF_THREADS), I8D_LDS, st, a, qt, nqb);
             return hipGetLastError();
         }
-        launch_mfma_one<DT_I8, METRIC_IP, SEED>(a, qt, nqb, st);
+        if (a.metric == METRIC_IP) launch_mfma_one<DT_I8, METRIC_IP, SEED>(a, qt, nqb, st);
+        else launch_mfma_one<DT_I8, METRIC_L2, SEED>(a, qt, nqb, st);
     } else if (dt == DT_BF16) {
         if (a.metric == METRIC_IP) launch_mfma_one<DT_BF16, METRIC_IP, SEED>(a, qt, nqb, st);
         else launch_mfma_one<DT_BF16, METRIC_L2, SEED>(a, qt, nqb, st);
@@ -3092,7 +3307,7 @@ static void launch_gemv_dt(const ScreenArgs& a, const float* qp, int nqb, int nq
     }
 }
 hipError_t launch_screen_gemv(int dt, const ScreenArgs& a, const float* qp, int nqb, int nqpad, hipStream_t st) {
-    if (dt == DT_I8 && (a.metric != METRIC_IP || !a.rsb || !a.qinfo)) return hipErrorInvalidValue;
+    if (dt == DT_I8 && (!a.rsb || !a.qinfo || (a.metric == METRIC_L2 && !a.sqn))) return hipErrorInvalidValue;
     if (dt == DT_F32) launch_gemv_dt<DT_F32>(a, qp, nqb, nqpad, st);
     else if (dt == DT_BF16) launch_gemv_dt<DT_BF16>(a, qp, nqb, nqpad, st);
     else if (dt == DT_I8) launch_gemv_dt<DT_I8>(a, qp, nqb, nqpad, st);
@@ -3165,12 +3380,19 @@ hipError_t launch_refine(const RefineArgs& a, int nq, hipStream_t st) {
 
 template <int DT, bool QLDS>
 static void launch_refine_wide_one(const RefineArgs& a, int nq, int KA, size_t lds, hipStream_t st) {
-    set_lds_attr((const void*)k_refine_wide<DT, QLDS>, 152 * 1024);
-    hipLaunchKernelGGL((k_refine_wide<DT, QLDS>), dim3(nq), dim3(RF_THREADS), lds, st, a, KA);
+    if (a.metric == METRIC_IP) {
+        set_lds_attr((const void*)k_refine_wide<DT, METRIC_IP, QLDS>, 152 * 1024);
+        hipLaunchKernelGGL((k_refine_wide<DT, METRIC_IP, QLDS>), dim3(nq), dim3(RF_THREADS), lds, st, a, KA);
+    } else {
+        set_lds_attr((const void*)k_refine_wide<DT, METRIC_L2, QLDS>, 152 * 1024);
+        hipLaunchKernelGGL((k_refine_wide<DT, METRIC_L2, QLDS>), dim3(nq), dim3(RF_THREADS), lds, st, a, KA);
+    }
 }
 
 hipError_t launch_refine_wide(const RefineArgs& a, int nq, int KA, hipStream_t st) {
-    if (a.metric != METRIC_IP || !(a.qeps || a.qinfo) || !a.cand_n || KA <= 0 || 2 * KA > RFW_CAP)
+    // L2: int8 keys only (their margin qeps covers the transformed key; native L2 uses k_refine)
+    if ((a.metric != METRIC_IP && !(a.metric == METRIC_L2 && a.qeps)) || !(a.qeps || a.qinfo) || !a.cand_n ||
+        KA <= 0 || 2 * KA > RFW_CAP)
         return hipErrorInvalidValue;
     const size_t base = (size_t)RFW_CAP * 12;
     const size_t qbytes = (size_t)((a.d + 7) >> 3) * 64;
@@ -3253,6 +3475,11 @@ hipError_t launch_ivf_scan_dyn(int dt, const IvfScanArgs& a, int grid, hipStream
 hipError_t launch_merge_shards(int metric, const double* S_in, const int64_t* I_in, int G, int64_t nq, int k,
                                double* S_out, int64_t* I_out, float* D_out, hipStream_t st) {
     if (G > 64) return hipErrorInvalidValue;
+    if ((int64_t)G * k <= kMergeRankMax) {
+        hipLaunchKernelGGL(k_merge_shards_rank, dim3((unsigned)nq), dim3(256), (size_t)G * k * 16, st, metric, S_in,
+                           I_in, G, nq, k, S_out, I_out, D_out);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(k_merge_shards, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, st, metric, S_in, I_in, G, nq, k,
                        S_out, I_out, D_out);
     return hipGetLastError();

@@ -12,6 +12,13 @@ own :class:`~photo_search_engine_amd.index.FlatIndex` (HBM-resident); a search i
   3. a merge of the G sorted lists on the device (``vs_merge_shards_device``) on every rank, so
      all ranks hold the same final (D, I) without a second collective.
 
+With the int8 screen on bf16/f16 shards (``vs_two_phase_ok``: one int8 MFMA batch), step 1 runs in
+two phases around one more exchange of the same shape: phase A scores each query's best few keys
+per shard and the shards all-gather + merge those lists; the merged k-th score is a lower bound of
+the global k-th best, so in phase B each shard exactly scores only the rows whose screen bound
+reaches it (its share of the global refine window, not a whole window of its own) and certifies
+against it.  The final exchange and merge are unchanged, and so is the result.
+
 Ordering is total (score, then lower id), so the result is identical to a single-GPU search of
 the whole corpus.  The reference has no multi-device path (faiss CPU index, utils/vector_store.py
 :72-81); this module is the MI355X scale-out of the same ``index.search`` contract (:191).
@@ -66,6 +73,32 @@ def _device_local_search(index, q: torch.Tensor, k: int, row0: int):
     return S, I, D
 
 
+def _device_phase_a(index, q: torch.Tensor, k: int, row0: int, world: int):
+    """Two-phase local search, phase A: (S_a fp64, I_a int64) device lists + the pending search."""
+    nq = q.shape[0]
+    S = torch.empty((nq, k), dtype=torch.float64, device=q.device)
+    I = torch.empty((nq, k), dtype=torch.int64, device=q.device)
+    stream = torch.cuda.current_stream(q.device).cuda_stream
+    pend = index.search_phase_a(q.data_ptr(), nq, k, world, S.data_ptr(), I.data_ptr(), row0, stream)
+    return S, I, pend
+
+
+def _device_phase_b(index, pend, floor_S: torch.Tensor, q: torch.Tensor, k: int):
+    """Phase B with the merged phase-A lists as the floor: the shard's exact top-k (S, I, D)."""
+    nq = q.shape[0]
+    S = torch.empty((nq, k), dtype=torch.float64, device=q.device)
+    I = torch.empty((nq, k), dtype=torch.int64, device=q.device)
+    D = torch.empty((nq, k), dtype=torch.float32, device=q.device)
+    stream = torch.cuda.current_stream(q.device).cuda_stream
+    index.search_phase_b(pend, floor_S.data_ptr(), D.data_ptr(), I.data_ptr(), S.data_ptr(), stream)
+    return S, I, D
+
+
+def _device_two_phase_ok(index, nq: int, k: int) -> bool:
+    f = getattr(index, "two_phase_ok", None)
+    return bool(f(nq, k)) if f else False
+
+
 class ShardedFlatIndex:
     """One shard of a row-partitioned exact flat index per rank of ``group``.
 
@@ -76,7 +109,9 @@ class ShardedFlatIndex:
 
     def __init__(self, d: int, metric: str = "ip", dtype: str = "f32", device: Optional[int] = None,
                  group=None, index=None,
-                 local_search: Optional[Callable] = None, merge: Optional[Callable] = None) -> None:
+                 local_search: Optional[Callable] = None, merge: Optional[Callable] = None,
+                 phase_a: Optional[Callable] = None, phase_b: Optional[Callable] = None,
+                 two_phase_ok: Optional[Callable] = None) -> None:
         # without an initialised process group this process is the only shard (1 GPU)
         self.group = group
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
@@ -90,8 +125,18 @@ class ShardedFlatIndex:
         self.index = index
         self._local_search = local_search or _device_local_search
         self._merge = merge or _device_merge
+        self._phase_a = phase_a or _device_phase_a
+        self._phase_b = phase_b or _device_phase_b
+        # (injected local searches without phase functions keep the one-phase protocol)
+        self._two_phase_ok = two_phase_ok or (_device_two_phase_ok if local_search is None else (lambda *a: False))
         self.row0 = 0
         self.n_total = 0
+        # measurement only (bench.py --shard-of G): a single rank runs the G-shard step on its shard,
+        # the exchanges included (over its one-rank process group)
+        self.shards_hint: Optional[int] = None
+        # ... and the floor the other shards would have contributed (the G shards' merged phase-A
+        # lists, computed beforehand), used in place of its one-rank exchange's merge
+        self.floor_override: Optional[torch.Tensor] = None
 
     # -- build ---------------------------------------------------------------------------------
     def add_shard(self, x_local, row0: int, n_total: int) -> None:
@@ -151,21 +196,56 @@ class ShardedFlatIndex:
         if src is not None and self.world > 1:
             dist.broadcast(q, src=src, group=self.group)
         nq = q.shape[0]
-        if self.n_local > 0:
+        # (every rank takes the same branch: the test depends only on the index configuration)
+        shards = self.shards_hint or self.world
+        if shards > 1 and self._two_phase_ok(self.index, nq, k):
+            S, I, D = self._two_phase_local(q, k, shards)
+        elif self.n_local > 0:
             S, I, D = self._local_search(self.index, q, k, self.row0)
         else:  # empty shard (n_total < world): contributes only padding
-            S = torch.full((nq, k), _worst(self.metric), dtype=torch.float64, device=q.device)
-            I = torch.full((nq, k), -1, dtype=torch.int64, device=q.device)
-            D = torch.full((nq, k), -3.4028234663852886e38 if self.metric == 0 else 3.4028234663852886e38,
-                           dtype=torch.float32, device=q.device)
-        if self.world == 1:
+            S, I, D = self._padding(nq, k, q.device)
+        if shards == 1:
             return D, I, S
         # ONE all-gather of interleaved (fp64 score bits, id) pairs: a second collective would add
         # its full latency to every step (the payload is only nq * k * 16 B per rank)
+        return self._exchange(S, I, k)
+
+    def _padding(self, nq: int, k: int, device):
+        S = torch.full((nq, k), _worst(self.metric), dtype=torch.float64, device=device)
+        I = torch.full((nq, k), -1, dtype=torch.int64, device=device)
+        D = torch.full((nq, k), -3.4028234663852886e38 if self.metric == 0 else 3.4028234663852886e38,
+                       dtype=torch.float32, device=device)
+        return S, I, D
+
+    def _exchange(self, S: torch.Tensor, I: torch.Tensor, k: int):
+        """all-gather of the (S, I) lists + the device merge: (D, I, S), identical on every rank."""
         SI = torch.stack([S.contiguous().view(torch.int64), I.contiguous()], dim=-1)
         g = self._gather(SI)
         S, I, D = self._merge(self.metric, g[..., 0].contiguous().view(torch.float64), g[..., 1].contiguous(), k)
         return D, I, S
+
+    def _two_phase_local(self, q: torch.Tensor, k: int, shards: int):
+        """The shard's exact top-k by the two-phase search: phase A, the exchange of the phase-A
+        lists (their merge = the floor), phase B."""
+        nq = q.shape[0]
+        pend = None
+        if self.n_local > 0:
+            Sa, Ia, pend = self._phase_a(self.index, q, k, self.row0, shards)
+        else:
+            Sa, Ia, _ = self._padding(nq, k, q.device)
+        try:
+            _, _, floor_S = self._exchange(Sa, Ia, k)
+        except BaseException:
+            if pend is not None:
+                free = getattr(self.index, "search_pending_free", None)
+                if free:
+                    free(pend)
+            raise
+        if self.floor_override is not None:
+            floor_S = self.floor_override
+        if pend is None:
+            return self._padding(nq, k, q.device)
+        return self._phase_b(self.index, pend, floor_S, q, k)
 
     def close(self) -> None:
         close = getattr(self.index, "close", None)

@@ -139,6 +139,30 @@ class FlatIndex:
         check(self._L.vs_search_device_exact(self._h, q_ptr, int(nq), int(k), D_ptr or None, I_ptr, S64_ptr or None,
                                              int(id_offset), stream or None))
 
+    # -- two-phase search (the sharded step with a global T' exchange, include/vs.h) -------------
+    def two_phase_ok(self, nq: int, k: int) -> bool:
+        """Whether :meth:`search_phase_a` applies to a batch of ``nq`` queries at ``k`` (depends only
+        on the index configuration, so every shard of a collective answers the same)."""
+        return int(check(self._L.vs_two_phase_ok(self._h, int(nq), int(k)))) == 1
+
+    def search_phase_a(self, q_ptr: int, nq: int, k: int, world: int, S_ptr: int, I_ptr: int, id_offset: int = 0,
+                       stream: Optional[int] = None) -> int:
+        """Phase A: this shard's best-so-far (S, I) lists for the exchange; returns the pending search
+        for :meth:`search_phase_b` (or :meth:`search_pending_free`)."""
+        out = ctypes.c_void_p(0)
+        check(self._L.vs_search_device_phase_a(self._h, q_ptr, int(nq), int(k), int(world), int(id_offset), S_ptr,
+                                               I_ptr, stream or None, ctypes.byref(out)))
+        return int(out.value)
+
+    def search_phase_b(self, pending: int, floor_S_ptr: int, D_ptr: Optional[int], I_ptr: int,
+                       S64_ptr: Optional[int] = None, stream: Optional[int] = None) -> None:
+        """Phase B with the merged phase-A lists as the floor; frees the pending search."""
+        check(self._L.vs_search_device_phase_b(ctypes.c_void_p(pending), floor_S_ptr, D_ptr or None, I_ptr,
+                                               S64_ptr or None, stream or None))
+
+    def search_pending_free(self, pending: int) -> None:
+        self._L.vs_search_pending_free(ctypes.c_void_p(pending))
+
     def set_timing(self, enable: bool) -> None:
         check(self._L.vs_set_timing(self._h, int(bool(enable))))
 

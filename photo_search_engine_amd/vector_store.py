@@ -26,7 +26,7 @@ Normalisation stays on the host in numpy, bit-identical to the reference
 Environment knobs (new, optional): ``VECTOR_DEVICE`` (GPU ordinal, default 0), ``VECTOR_DEVICES``
 (e.g. ``0,1,2,3,4,5,6,7``: one index over those GPUs of this process, include/vs.h vs_multi_*),
 ``VECTOR_DTYPE`` (f32 | bf16 | f16 storage, default f32 = the reference's storage precision),
-``VECTOR_SCREEN`` (native | int8: the batched-search screen of an inner-product index) and
+``VECTOR_SCREEN`` (native | int8: the batched-search screen, either metric) and
 ``VECTOR_HNSW_SEARCH`` (exact | graph: how an ``index_type="hnsw"`` store searches).
 """
 from __future__ import annotations
@@ -55,7 +55,7 @@ def _default_index_factory(dimension: int, metric: str):
         device = int(devices[0]) if devices else int(os.environ.get("VECTOR_DEVICE", "0") or 0)
         index = FlatIndex(dimension, metric=kind, dtype=dtype, device=device)
     screen = (os.environ.get("VECTOR_SCREEN", "") or "").strip().lower()
-    if screen and kind == "ip":
+    if screen:
         index.set_screen(screen)
     return index
 

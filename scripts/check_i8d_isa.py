@@ -4,6 +4,8 @@ read of a fragment register that could run before the kernel's own s_waitcnt (DE
 
     python scripts/check_i8d_isa.py [vs_kernels.s]   (default: compiles vs_kernels.hip to asm)
 
+Both instantiations are checked (inner product and L2).
+
 Checks, for the kernel's code: no scratch (spill) traffic; every register written by a corpus load
 (`global_load_dwordx4 ... nt`) is read only by v_mfma instructions; one s_barrier per K-step body.
 Exit status 0 = pass.
@@ -43,7 +45,15 @@ def main() -> int:
             subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "--cuda-device-only",
                             "-S", "-Wno-inline-asm", "-o", out, SRC], check=True)
             asm = open(out).read()
-    start = asm.index("_ZN2vs12k_screen_i8dENS_10ScreenArgsEPKhi:")
+    rc = 0
+    for metric, sym in (("ip", "_ZN2vs12k_screen_i8dILi0EEEvNS_10ScreenArgsEPKhi:"),
+                        ("l2", "_ZN2vs12k_screen_i8dILi1EEEvNS_10ScreenArgsEPKhi:")):
+        rc |= check(asm, metric, sym)
+    return rc
+
+
+def check(asm: str, metric: str, sym: str) -> int:
+    start = asm.index(sym)
     end = asm.index(".Lfunc_end", start)
     raw = asm[start:end].split("\n")
     code = [f"{l}  ;#L{i}" for i, l in enumerate(raw) if l.strip() and not l.strip().startswith((";", "."))]
@@ -80,7 +90,7 @@ def main() -> int:
                 break
     nmfma = sum(1 for l in code if l.strip().startswith("v_mfma"))
     nbar = sum(1 for l in code if l.strip().startswith("s_barrier"))
-    print(f"k_screen_i8d: {len(code)} instructions, {nmfma} MFMA, {nbar} s_barrier, "
+    print(f"k_screen_i8d<{metric}>: {len(code)} instructions, {nmfma} MFMA, {nbar} s_barrier, "
           f"{len(loaded)} corpus-fragment VGPRs")
     for b in bad[:20]:
         print("FAIL:", b)

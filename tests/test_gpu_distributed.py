@@ -22,7 +22,7 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, N, d, dtype, nq, k, metric, outdir):
+def _worker(rank, world, port, N, d, dtype, nq, k, metric, outdir, screen="native"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     torch.cuda.set_device(0)
@@ -31,13 +31,16 @@ def _worker(rank, world, port, N, d, dtype, nq, k, metric, outdir):
         from photo_search_engine_amd.distributed import ShardedFlatIndex
         sh = ShardedFlatIndex(d, metric, dtype, device=0)
         sh.add_synthetic(O.SEED_CORPUS, N, True)
+        sh.index.set_screen(screen)
         q = torch.from_numpy(O.synth_rows(O.SEED_QUERIES, 0, nq, d, True, dtype)).cuda()
         if rank != 0:
             q.zero_()  # rank 0's batch arrives by broadcast
         D, I, S = sh.search(q, k, src=0)
+        D, I, S = sh.search(q, k, src=0)  # (a second call: the pending-search state is released)
         torch.cuda.synchronize()
         np.savez(os.path.join(outdir, f"r{rank}.npz"), D=D.cpu().numpy(), I=I.cpu().numpy(), S=S.cpu().numpy(),
-                 row0=sh.row0, n=sh.n_local)
+                 row0=sh.row0, n=sh.n_local, two=sh.index.two_phase_ok(nq, k),
+                 unres=sh.unresolved_count())
         sh.close()
     finally:
         dist.destroy_process_group()
@@ -72,6 +75,77 @@ def test_four_ranks_one_gpu_match_oracle(tmp_path):
     for o in outs:
         np.testing.assert_array_equal(o["I"], Ie)
         np.testing.assert_array_equal(o["S"], Se)
+
+
+@pytest.mark.parametrize("world,metric,dtype,nq,k,N,d", [
+    (2, "ip", "bf16", 40, 25, 20011, 64),
+    (2, "l2", "f16", 64, 10, 30000, 256),
+    (4, "ip", "bf16", 256, 100, 4 * 256 * 4 * 256 + 333, 256),  # >= 4 tiles per CU per shard: seeded
+    (4, "l2", "bf16", 100, 50, 4 * 256 * 4 * 256 + 333, 512),
+    (3, "ip", "f16", 20, 30, 50, 64),                          # shards smaller than k
+])
+def test_two_phase_int8_ranks_one_gpu_match_oracle(tmp_path, world, metric, dtype, nq, k, N, d):
+    # the int8 screen on bf16/f16 shards takes the two-phase search: phase-A lists exchanged and
+    # merged into each query's floor, phase B per shard, then the final exchange -- the same exact
+    # global answer as one index
+    mp.spawn(_worker, args=(world, _free_port(), N, d, dtype, nq, k, metric, str(tmp_path), "int8"),
+             nprocs=world, join=True)
+    outs = [np.load(tmp_path / f"r{r}.npz") for r in range(world)]
+    assert all(bool(o["two"]) for o in outs)
+    assert sum(int(o["unres"]) for o in outs) == 0
+    x = O.synth_rows(O.SEED_CORPUS, 0, N, d, True, dtype)
+    q = O.synth_rows(O.SEED_QUERIES, 0, nq, d, True, dtype)
+    Se, Ie = O.knn_exact(x, q, k, metric)
+    for o in outs:
+        np.testing.assert_array_equal(o["I"], Ie)
+        valid = Ie >= 0
+        np.testing.assert_array_equal(o["S"][valid], Se[valid])
+        np.testing.assert_array_equal(o["D"][valid], Se[valid].astype(np.float32))
+
+
+@pytest.mark.parametrize("metric", ["ip", "l2"])
+def test_two_phase_single_index_with_external_floor(metric):
+    # phase B with a floor taken from the WHOLE corpus's exact answer, on an index holding only a
+    # slice of it: every row of the slice at least as good as the floor must come back exactly
+    # (rows below it may be skipped); with its own phase-A lists as the floor it equals the
+    # one-phase search
+    from photo_search_engine_amd.index import FlatIndex
+    N, d, nq, k = 300_000, 256, 64, 50
+    x = O.synth_rows(O.SEED_CORPUS, 0, N, d, True, "bf16")
+    q = O.synth_rows(O.SEED_QUERIES, 0, nq, d, True, "bf16")
+    Sg, Ig = O.knn_exact(x, q, k, metric)
+    lo, hi = 100_000, 250_000
+    ix = FlatIndex(d, metric, "bf16")
+    ix.add(x[lo:hi])
+    ix.set_screen("int8")
+    assert ix.two_phase_ok(nq, k) and not ix.two_phase_ok(8, k) and not ix.two_phase_ok(257, k)
+    qd = torch.from_numpy(q).cuda()
+    Sa = torch.empty((nq, k), dtype=torch.float64, device="cuda")
+    Ia = torch.empty((nq, k), dtype=torch.int64, device="cuda")
+    S = torch.empty((nq, k), dtype=torch.float64, device="cuda")
+    I = torch.empty((nq, k), dtype=torch.int64, device="cuda")
+    D = torch.empty((nq, k), dtype=torch.float32, device="cuda")
+    # (1) own floor
+    p = ix.search_phase_a(qd.data_ptr(), nq, k, 1, Sa.data_ptr(), Ia.data_ptr(), lo)
+    ix.search_phase_b(p, Sa.data_ptr(), D.data_ptr(), I.data_ptr(), S.data_ptr())
+    Sl, Il = O.knn_exact(x[lo:hi], q, k, metric)
+    np.testing.assert_array_equal(I.cpu().numpy(), Il + lo)
+    np.testing.assert_array_equal(S.cpu().numpy(), Sl)
+    # (2) the global floor: the slice's rows within the global top-k are all found, exactly
+    floor = torch.from_numpy(Sg).cuda()
+    p = ix.search_phase_a(qd.data_ptr(), nq, k, 4, Sa.data_ptr(), Ia.data_ptr(), lo)
+    ix.search_phase_b(p, floor.data_ptr(), D.data_ptr(), I.data_ptr(), S.data_ptr())
+    Ih, Sh = I.cpu().numpy(), S.cpu().numpy()
+    for qi in range(nq):
+        mine = [(s, i) for s, i in zip(Sg[qi], Ig[qi]) if lo <= i < hi]
+        got = list(zip(Sh[qi][:len(mine)], Ih[qi][:len(mine)]))
+        assert got == mine, qi
+    assert ix.unresolved_count() == 0
+    # (3) a pending search dropped without phase B releases the index (an add must not block)
+    p = ix.search_phase_a(qd.data_ptr(), nq, k, 2, Sa.data_ptr(), Ia.data_ptr(), lo)
+    ix.search_pending_free(p)
+    ix.add(x[hi:hi + 10])
+    ix.close()
 
 
 def _nccl_worker(rank, world, port, outdir):

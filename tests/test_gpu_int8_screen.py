@@ -27,13 +27,13 @@ def _num_cu():
     return torch.cuda.get_device_properties(0).multi_processor_count
 
 
-def _exact(ix, q, k):
+def _exact(ix, q, k, metric="ip"):
     x = ix.reconstruct_n(0, ix.ntotal)
     D, I = ix.search(q, k)
-    S, Ie = O.knn_exact(x, q, k, "ip")
+    S, Ie = O.knn_exact(x, q, k, metric)
     np.testing.assert_array_equal(I, Ie)
     Dexp = S.astype(np.float32)
-    Dexp[Ie < 0] = -3.4028235e38
+    Dexp[Ie < 0] = -3.4028235e38 if metric == "ip" else 3.4028235e38
     np.testing.assert_array_equal(D, Dexp)
     return D, I
 
@@ -141,12 +141,107 @@ def test_int8_screen_device_api_with_offset(FlatIndex):
 
 
 def test_int8_screen_argument_errors(FlatIndex):
-    from photo_search_engine_amd._lib import VsError
-    ix = FlatIndex(32, "l2", "bf16")
-    with pytest.raises(VsError):
-        ix.set_screen("int8")  # inner product only
     with pytest.raises(ValueError):
         FlatIndex(32, "ip", "bf16").set_screen("fp4")
+
+
+# ---- L2 indexes: keys 2 (upper bound of <x, q>) - ||x||^2 in the int8 screens, the canonical
+# distance in the refine; same ids and distances as the native path and knn_exact ----
+
+def _l2_rows(N, d, seed, unit):
+    x = O.synth_rows(O.SEED_CORPUS + seed, 0, N, d, True, "f32")
+    if not unit:  # row norms spread over [0.25, 4): ||x||^2 decides as much as the angle
+        rng = np.random.default_rng(seed)
+        x *= rng.uniform(0.25, 4.0, size=(N, 1)).astype(np.float32)
+    return x
+
+
+@pytest.mark.parametrize("unit", [True, False])
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16"])
+@pytest.mark.parametrize("nq,k,N,d", [(40, 10, 9000, 128), (256, 100, 20000, 192), (300, 7, 3001, 72),
+                                     (200, 50, 70000, 1536), (64, 1000, 150000, 512)])
+def test_int8_screen_l2_exact(FlatIndex, dtype, unit, nq, k, N, d):
+    """Both K1 forms (tiled: d % 256 != 0; direct k_screen_i8d: d % 256 == 0), unseeded and seeded
+    corpora, partial tiles, k = 1000, unit and spread row norms."""
+    x = _l2_rows(N, d, 21, unit)
+    ix = FlatIndex(d, "l2", dtype)
+    ix.add(x)
+    ix.set_screen("int8")
+    assert ix.screen == "int8"
+    q = O.synth_rows(O.SEED_QUERIES + 21, 0, nq, d, True, "f32") * (1.0 if unit else 1.7)
+    _exact(ix, q.astype(np.float32), k, "l2")
+    assert ix.uncertified_count() == 0
+    ix.close()
+
+
+@pytest.mark.parametrize("k", [10, 100])
+@pytest.mark.parametrize("d", [1536, 320])
+def test_int8_screen_l2_seeded_matches_native(FlatIndex, k, d):
+    # >= 4 tiles per CU: the int8 seed pass and union target on L2 keys
+    N, nq = 256 * 4 * _num_cu() + 777, 64
+    ix = FlatIndex(d, "l2", "bf16")
+    ix.add_synthetic(O.SEED_CORPUS, 0, N, True)
+    q = O.synth_rows(O.SEED_QUERIES, 0, nq, d, True, "bf16")
+    Dn, In = ix.search(q, k)
+    ix.set_screen("int8")
+    ix.set_timing(True)
+    D8, I8 = _exact(ix, q, k, "l2")
+    ix.set_timing(False)
+    assert ix.timing_fetch()[1] == "mfma_i8"
+    np.testing.assert_array_equal(I8, In)
+    np.testing.assert_array_equal(D8, Dn)
+    assert ix.uncertified_count() == 0
+    ix.close()
+
+
+@pytest.mark.parametrize("d", [64, 512])
+def test_int8_screen_l2_ties_zero_rows_and_adds(FlatIndex, d):
+    rng = np.random.default_rng(7)
+    base = rng.standard_normal((60, d)).astype(np.float32)
+    x = np.concatenate([base, np.repeat(base[7:8], 300, axis=0), np.zeros((40, d), np.float32), base], axis=0)
+    ix = FlatIndex(d, "l2", "bf16")
+    ix.add(x[:100])
+    ix.set_screen("int8")
+    ix.add(x[100:])
+    q = np.concatenate([np.repeat(base[7:8], 12, axis=0), -base[:8], np.zeros((4, d), np.float32)], axis=0)
+    D, I = _exact(ix, O.round_dtype(q, "bf16"), 40, "l2")
+    assert I[0, 0] == 7 and D[0, 0] == 0.0  # the earliest copy wins the tie
+    ix.close()
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("nq,k", [(1, 1), (1, 10), (3, 37), (8, 100)])
+def test_int8_gemv_screen_l2_exact(FlatIndex, dtype, nq, k):
+    N, d = 120_000, 200
+    x = _l2_rows(N, d, 5, False)
+    ix = FlatIndex(d, "l2", dtype)
+    ix.add(x)
+    ix.set_screen("int8")
+    q = O.synth_rows(O.SEED_QUERIES, 40 + nq, nq, d, True, "f32")
+    ix.set_timing(True)
+    _exact(ix, q, k, "l2")
+    ix.set_timing(False)
+    assert ix.timing_fetch()[1] in ("gemv_i8", "gemv")
+    assert ix.uncertified_count() == 0
+    ix.close()
+
+
+def test_int8_screen_l2_adversarial_seed_falls_back_exactly(FlatIndex):
+    d, k = 64, 10
+    cu = _num_cu()
+    tiles = 32 * cu + 3
+    N = tiles * 256
+    x = O.synth_rows(O.SEED_CORPUS, 0, N, d, True, "f32")
+    q = O.synth_rows(O.SEED_QUERIES, 0, 16, d, True, "f32")
+    rng = np.random.default_rng(11)
+    for j in range(cu):
+        for t in range(4):
+            x[(tiles * j // cu) * 256 + 5 + t] = q[(4 * j + t) % 16] + 0.01 * rng.standard_normal(d).astype(np.float32)
+    ix = FlatIndex(d, "l2", "bf16")
+    ix.add(x)
+    ix.set_screen("int8")
+    _exact(ix, O.round_dtype(q, "bf16"), k, "l2")
+    assert ix.uncertified_count() > 0
 
 
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])

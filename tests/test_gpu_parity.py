@@ -371,6 +371,39 @@ def test_device_shard_merge_matches_oracle(FlatIndex):
     np.testing.assert_array_equal(D.cpu().numpy(), Se.astype(np.float32))
 
 
+@pytest.mark.parametrize("metric", ["ip", "l2"])
+@pytest.mark.parametrize("G,k", [(1, 100), (3, 17), (8, 100), (8, 512), (16, 300), (5, 1000)])
+def test_device_shard_merge_ties_and_padding(metric, G, k):
+    # synthetic sorted lists with many equal scores (ties -> lower id), ragged padding; G * k <=
+    # 4096 takes the rank merge, larger ones the wave-per-query merge: both equal the oracle's merge
+    import torch
+    from photo_search_engine_amd.index import merge_shards_device
+    rng = np.random.default_rng(G * 1000 + k)
+    nq = 37
+    Sg = np.empty((G, nq, k), dtype=np.float64)
+    Ig = np.empty((G, nq, k), dtype=np.int64)
+    worst = -1.7976931348623157e308 if metric == "ip" else 1.7976931348623157e308
+    for g in range(G):
+        for qi in range(nq):
+            nv = int(rng.integers(0, k + 1)) if rng.random() < 0.3 else k
+            sc = rng.integers(0, 40, size=nv).astype(np.float64) / 8.0  # few distinct values
+            ids = rng.choice(1 << 40, size=nv, replace=False) + g  # globally distinct ids
+            order = np.lexsort((ids, -sc if metric == "ip" else sc))
+            Sg[g, qi, :nv], Ig[g, qi, :nv] = sc[order], ids[order]
+            Sg[g, qi, nv:], Ig[g, qi, nv:] = worst, -1
+    St, It = torch.from_numpy(Sg).cuda(), torch.from_numpy(Ig).cuda()
+    S = torch.empty((nq, k), dtype=torch.float64, device="cuda")
+    I = torch.empty((nq, k), dtype=torch.int64, device="cuda")
+    D = torch.empty((nq, k), dtype=torch.float32, device="cuda")
+    merge_shards_device(0 if metric == "ip" else 1, St.data_ptr(), It.data_ptr(), G, nq, k, S.data_ptr(),
+                        I.data_ptr(), D.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    Sm, Im = O.merge_topk(Sg, Ig, k, metric)
+    np.testing.assert_array_equal(I.cpu().numpy(), Im)
+    np.testing.assert_array_equal(S.cpu().numpy()[Im >= 0], Sm[Im >= 0])
+    assert (S.cpu().numpy()[Im < 0] == worst).all()
+
+
 def test_sharded_index_single_process_matches_oracle():
     import torch
     from photo_search_engine_amd.distributed import ShardedFlatIndex
