@@ -109,21 +109,26 @@ int vs_search_device_exact(vs_index* index, const float* q_dev, int64_t nq, int3
  * Results after the final all-gather + merge are identical to vs_search_device_exact's.  Every rank
  * must take the same path: vs_two_phase_ok depends only on the index configuration (int8 screen,
  * bf16/f16 rows) and on (nq, k) -- one int8 MFMA block, 8 < nq <= 256, k <= 1024.  world = the
- * number of shards (sets phase A's depth).  vs_search_pending_free drops a pending search whose
- * phase B will not run. */
+ * number of shards (sets phase A's depth).  stride: the element stride of the (S, I) outputs (2 =
+ * interleaved (score bits, id) pairs, ready for the all-gather; D_dev stays nq x k).
+ * vs_search_pending_free drops a pending search whose phase B will not run. */
 typedef struct vs_pending vs_pending;
 int vs_two_phase_ok(vs_index* index, int64_t nq, int32_t k);
 int vs_search_device_phase_a(vs_index* index, const float* q_dev, int64_t nq, int32_t k, int32_t world,
-                             int64_t id_offset, double* S_a, int64_t* I_a, void* stream, vs_pending** out);
+                             int64_t id_offset, double* S_a, int64_t* I_a, int32_t stride, void* stream,
+                             vs_pending** out);
 int vs_search_device_phase_b(vs_pending* pending, const double* floor_S, float* D_dev, int64_t* I_dev,
-                             double* S64_dev, void* stream);
+                             double* S64_dev, int32_t stride, void* stream);
 void vs_search_pending_free(vs_pending* pending);
 
 /* ---- merge of per-shard results (all-gather + K3 merge).
- * S_in/I_in: G x nq x k (device), each list sorted best-first; output nq x k best-first under
- * (score desc | asc for L2, id asc).  D_out is S_out rounded to fp32 (may be NULL). */
-int vs_merge_shards_device(int metric, const double* S_in, const int64_t* I_in, int G, int64_t nq,
-                           int32_t k, double* S_out, int64_t* I_out, float* D_out, void* stream);
+ * S_in/I_in: G x nq x k (device), each list sorted best-first, element (g, q, j) at index
+ * ((g * nq + q) * k + j) * in_stride (1 = separate arrays; 2 = one interleaved array of (score bits,
+ * id) pairs, S_in = its base, I_in = base + 8 bytes: what one all-gather of packed pairs yields);
+ * output nq x k best-first under (score desc | asc for L2, id asc).  D_out is S_out rounded to
+ * fp32 (may be NULL). */
+int vs_merge_shards_device(int metric, const double* S_in, const int64_t* I_in, int32_t in_stride, int G,
+                           int64_t nq, int32_t k, double* S_out, int64_t* I_out, float* D_out, void* stream);
 
 /* ---- reconstruct (index.reconstruct, utils/vector_store.py:207) */
 int vs_reconstruct(vs_index* index, int64_t id, float* out);

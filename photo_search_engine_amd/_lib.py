@@ -62,11 +62,11 @@ _SIGS = {
     "vs_search_device_exact": (ctypes.c_int, [_vp, _vp, _c_i64, ctypes.c_int32, _vp, _vp, _vp, _c_i64, _vp]),
     "vs_two_phase_ok": (ctypes.c_int, [_vp, _c_i64, ctypes.c_int32]),
     "vs_search_device_phase_a": (ctypes.c_int, [_vp, _vp, _c_i64, ctypes.c_int32, ctypes.c_int32, _c_i64, _vp, _vp,
-                                                _vp, ctypes.POINTER(ctypes.c_void_p)]),
-    "vs_search_device_phase_b": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
+                                                ctypes.c_int32, _vp, ctypes.POINTER(ctypes.c_void_p)]),
+    "vs_search_device_phase_b": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, ctypes.c_int32, _vp]),
     "vs_search_pending_free": (None, [_vp]),
-    "vs_merge_shards_device": (ctypes.c_int, [ctypes.c_int, _vp, _vp, ctypes.c_int, _c_i64, ctypes.c_int32, _vp,
-                                              _vp, _vp, _vp]),
+    "vs_merge_shards_device": (ctypes.c_int, [ctypes.c_int, _vp, _vp, ctypes.c_int32, ctypes.c_int, _c_i64,
+                                              ctypes.c_int32, _vp, _vp, _vp, _vp]),
     "vs_add_from_file": (ctypes.c_int, [_vp, ctypes.c_char_p, _c_i64, _c_i64]),
     "vs_write_rows_to_file": (ctypes.c_int, [_vp, ctypes.c_char_p, _c_i64, _c_i64, _c_i64]),
     "vs_reconstruct": (ctypes.c_int, [_vp, _c_i64, _vp]),

@@ -369,7 +369,7 @@ double i8_union_target(int k, double sampled, double n) {
 // returns its arguments in *keep for vs_search_device_phase_b
 void search_block_i8(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float* D, int64_t* I, double* S64,
                      int* cert, int64_t id_offset, hipStream_t st, int phase = 0, int KA1 = 0,
-                     RefineArgs* keep = nullptr) {
+                     RefineArgs* keep = nullptr, int ostride = 1) {
     const int64_t tiles = (ix->ntotal + TR - 1) / TR;
     ScreenArgs a{};
     a.corpus = ix->data8;
@@ -462,6 +462,7 @@ void search_block_i8(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float
     r.drop = a.drop;
     r.thr0 = a.thr0;
     r.fails = c->fails.as<int>();
+    r.ostride = ostride;
     if (phase == 1) {
         const int ka = KA1;
         c->pa.ensure((size_t)nqb * ka * 12 + (size_t)nqb * 16);
@@ -486,7 +487,7 @@ void search_block_i8(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float
 // counts in d_unres
 void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, float* D, int64_t* I, double* S64,
                   int* cert, int64_t id_offset, hipStream_t st, int seed_rank, bool redo = false,
-                  bool allow_i8 = true) {
+                  bool allow_i8 = true, int ostride = 1) {
     if (seed_rank > 0 && allow_i8 && use_i8(ix, nqb, k)) {
         search_block_i8(ix, c, q, nqb, k, D, I, S64, cert, id_offset, st);
         health_note(ix, c, st, 1, nqb);
@@ -684,6 +685,7 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
     r.fails = redo ? nullptr : c->fails.as<int>();
     r.redo = redo ? 1 : 0;
     r.gate = gate;
+    r.ostride = ostride;
     r.optimistic = optimistic ? 1 : 0;
     r.nsplit = redo ? 1 : refine_split(nqb, Kp, ix->dtype, ix->num_cu);
     if (r.nsplit > 1) {
@@ -810,7 +812,7 @@ struct vs_pending {
     hipStream_t st = nullptr;
     const float* q = nullptr;
     int64_t nq = 0;
-    int k = 0, ka = 0;
+    int k = 0, ka = 0, stride = 1;
     int64_t id_offset = 0;
     bool two = false;
     RefineArgs r{};
@@ -821,9 +823,10 @@ bool vs::two_phase_ok(const vs_index* ix, int64_t nq, int k) {
 }
 
 vs_pending* vs::search_phase_a(vs_index* ix, const float* q_dev, int64_t nq, int k, int world, int64_t id_offset,
-                               double* S_a, int64_t* I_a, hipStream_t st) {
+                               double* S_a, int64_t* I_a, int stride, hipStream_t st) {
     check_index(ix);
     if (k <= 0 || nq <= 0 || world <= 0) throw VsError(VS_ERR_ARG, "nq, k and world must be > 0");
+    if (stride < 1) throw VsError(VS_ERR_ARG, "stride must be >= 1");
     if (ix->ntotal == 0) throw VsError(VS_ERR_ARG, "index is empty");
     std::unique_ptr<vs_pending> p(new vs_pending());
     p->ix = ix;
@@ -845,20 +848,21 @@ vs_pending* vs::search_phase_a(vs_index* ix, const float* q_dev, int64_t nq, int
         const int share = (k + world - 1) / world;
         p->ka = (int)std::min<int64_t>(round_up(2 * k + 32, 32), round_up(2 * share + 32, 32));
         search_block_i8(ix, c, q_dev, (int)nq, k, nullptr, I_a, S_a, c->cert.as<int>(), id_offset, st, 1, p->ka,
-                        &p->r);
+                        &p->r, stride);
     } else {
         c->outS.ensure((size_t)nq * k * sizeof(double));
         c->outI.ensure((size_t)nq * k * sizeof(int64_t));
         c->outD.ensure((size_t)nq * k * sizeof(float));
         search_all(ix, c, q_dev, nq, k, screen_depth(k), c->outD.as<float>(), c->outI.as<int64_t>(),
                    c->outS.as<double>(), c->cert.as<int>(), id_offset, st, kOptimisticSeedRank, true);
-        HIP_CHECK(hipMemcpyAsync(S_a, c->outS.p, (size_t)nq * k * sizeof(double), hipMemcpyDeviceToDevice, st));
-        HIP_CHECK(hipMemcpyAsync(I_a, c->outI.p, (size_t)nq * k * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
+        HIP_CHECK(hipMemcpy2DAsync(S_a, (size_t)stride * 8, c->outS.p, 8, 8, (size_t)nq * k, hipMemcpyDeviceToDevice, st));
+        HIP_CHECK(hipMemcpy2DAsync(I_a, (size_t)stride * 8, c->outI.p, 8, 8, (size_t)nq * k, hipMemcpyDeviceToDevice, st));
     }
     return p.release();
 }
 
-void vs::search_phase_b(vs_pending* p, const double* floor_S, float* D, int64_t* I, double* S64, hipStream_t st) {
+void vs::search_phase_b(vs_pending* p, const double* floor_S, float* D, int64_t* I, double* S64, int stride,
+                        hipStream_t st) {
     std::unique_ptr<vs_pending> own(p);
     vs_index* ix = p->ix;
     DeviceGuard dg(ix->device);
@@ -873,9 +877,11 @@ void vs::search_phase_b(vs_pending* p, const double* floor_S, float* D, int64_t*
     }
     const int64_t nq = p->nq;
     const int k = p->k;
+    if (stride < 1) throw VsError(VS_ERR_ARG, "stride must be >= 1");
     if (!p->two) {
-        HIP_CHECK(hipMemcpyAsync(I, c->outI.p, (size_t)nq * k * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
-        if (S64) HIP_CHECK(hipMemcpyAsync(S64, c->outS.p, (size_t)nq * k * sizeof(double), hipMemcpyDeviceToDevice, st));
+        HIP_CHECK(hipMemcpy2DAsync(I, (size_t)stride * 8, c->outI.p, 8, 8, (size_t)nq * k, hipMemcpyDeviceToDevice, st));
+        if (S64)
+            HIP_CHECK(hipMemcpy2DAsync(S64, (size_t)stride * 8, c->outS.p, 8, 8, (size_t)nq * k, hipMemcpyDeviceToDevice, st));
         if (D) HIP_CHECK(hipMemcpyAsync(D, c->outD.p, (size_t)nq * k * sizeof(float), hipMemcpyDeviceToDevice, st));
         return;
     }
@@ -886,11 +892,12 @@ void vs::search_phase_b(vs_pending* p, const double* floor_S, float* D, int64_t*
     r.D = D;
     r.I = I;
     r.S64 = S64;
+    r.ostride = stride;
     HIP_CHECK(launch_refine_wide(r, (int)nq, p->ka, st));
     health_note(ix, c, st, 1, (int)nq);
     // the block's gated fallback round (native screen, local certificate), as search_all's
     search_block(ix, c, p->q, (int)nq, k, std::max(screen_depth(k), fallback_depth(ix)), D, I, S64,
-                 c->cert.as<int>(), p->id_offset, st, 0, true);
+                 c->cert.as<int>(), p->id_offset, st, 0, true, true, stride);
 }
 
 void vs::search_pending_free(vs_pending* p) { delete p; }
@@ -1187,24 +1194,25 @@ int vs_two_phase_ok(vs_index* ix, int64_t nq, int32_t k) {
 }
 
 int vs_search_device_phase_a(vs_index* ix, const float* q_dev, int64_t nq, int32_t k, int32_t world,
-                             int64_t id_offset, double* S_a, int64_t* I_a, void* stream, vs_pending** out) {
+                             int64_t id_offset, double* S_a, int64_t* I_a, int32_t stride, void* stream,
+                             vs_pending** out) {
     return guarded([&] {
         if (!out || !q_dev || !S_a || !I_a) throw VsError(VS_ERR_ARG, "null argument");
         *out = nullptr;
         if (screen_depth(k) < k) throw VsError(VS_ERR_ARG, "k too large (max " + std::to_string(KP_MAX * 4 / 5) + ")");
-        *out = search_phase_a(ix, q_dev, nq, k, world, id_offset, S_a, I_a, (hipStream_t)stream);
+        *out = search_phase_a(ix, q_dev, nq, k, world, id_offset, S_a, I_a, stride, (hipStream_t)stream);
     });
 }
 
 int vs_search_device_phase_b(vs_pending* p, const double* floor_S, float* D_dev, int64_t* I_dev, double* S64_dev,
-                             void* stream) {
+                             int32_t stride, void* stream) {
     return guarded([&] {
         if (!p) throw VsError(VS_ERR_ARG, "null pending search");
         if (!floor_S || !I_dev) {
             search_pending_free(p);
             throw VsError(VS_ERR_ARG, "null device buffer");
         }
-        search_phase_b(p, floor_S, D_dev, I_dev, S64_dev, (hipStream_t)stream);
+        search_phase_b(p, floor_S, D_dev, I_dev, S64_dev, stride, (hipStream_t)stream);
     });
 }
 
@@ -1295,13 +1303,15 @@ int vs_search(vs_index* ix, const float* q, int64_t nq, int32_t k, float* D, int
     });
 }
 
-int vs_merge_shards_device(int metric, const double* S_in, const int64_t* I_in, int G, int64_t nq, int32_t k,
-                           double* S_out, int64_t* I_out, float* D_out, void* stream) {
+int vs_merge_shards_device(int metric, const double* S_in, const int64_t* I_in, int32_t in_stride, int G, int64_t nq,
+                           int32_t k, double* S_out, int64_t* I_out, float* D_out, void* stream) {
     return guarded([&] {
         if (G <= 0 || G > 64) throw VsError(VS_ERR_ARG, "G must be in [1, 64]");
         if (k <= 0 || nq < 0) throw VsError(VS_ERR_ARG, "bad k / nq");
+        if (in_stride < 1) throw VsError(VS_ERR_ARG, "in_stride must be >= 1");
         if (nq == 0) return;
-        HIP_CHECK(launch_merge_shards(metric, S_in, I_in, G, nq, k, S_out, I_out, D_out, (hipStream_t)stream));
+        HIP_CHECK(launch_merge_shards(metric, S_in, I_in, G, nq, k, S_out, I_out, D_out, (hipStream_t)stream,
+                                      in_stride));
     });
 }
 

@@ -299,6 +299,7 @@ struct RefineArgs {
     int pa_cap;
     const double* tfloor;
     int tfloor_k;
+    int ostride;           // I / S64 element stride (0/1 = separate arrays; 2 = interleaved (score bits, id))
 };
 // workgroups per query of k_refine for a Kp-deep refine of nq queries (1 = no split)
 int refine_split(int nq, int Kp, int dt, int num_cu);
@@ -388,8 +389,9 @@ unsigned* unresolved_counter(vs_index* ix);  // device word behind vs_unresolved
 // two-phase exact device search (vs_search_device_phase_a / _b)
 bool two_phase_ok(const vs_index* ix, int64_t nq, int k);
 vs_pending* search_phase_a(vs_index* ix, const float* q_dev, int64_t nq, int k, int world, int64_t id_offset,
-                           double* S_a, int64_t* I_a, hipStream_t st);
-void search_phase_b(vs_pending* p, const double* floor_S, float* D, int64_t* I, double* S64, hipStream_t st);
+                           double* S_a, int64_t* I_a, int stride, hipStream_t st);
+void search_phase_b(vs_pending* p, const double* floor_S, float* D, int64_t* I, double* S64, int stride,
+                    hipStream_t st);
 void search_pending_free(vs_pending* p);
 // seed pass: screen one tile per workgroup (tile_stride) and write per-query 16-row-group maxima
 hipError_t launch_seed_mfma(int dt, const ScreenArgs& a, const uint8_t* qt, int nqb, hipStream_t st);
@@ -397,7 +399,7 @@ hipError_t launch_seed_mfma(int dt, const ScreenArgs& a, const uint8_t* qt, int 
 hipError_t launch_seed_select(const float* seedmax, int M, int nq, int rank, u64* thr0, hipStream_t st);
 
 hipError_t launch_merge_shards(int metric, const double* S_in, const int64_t* I_in, int G, int64_t nq, int k,
-                               double* S_out, int64_t* I_out, float* D_out, hipStream_t st);
+                               double* S_out, int64_t* I_out, float* D_out, hipStream_t st, int istride = 1);
 
 // ---- HNSW graph search (vs_hnsw.hip) ---------------------------------------------
 // faiss HNSW::search over a graph in faiss's layout (neighbors of node i on level l:

@@ -2512,15 +2512,15 @@ __device__ __forceinline__ void refine(const RefineArgs& a, int KP2) {
         if (!cert && a.fails) atomicAdd(a.fails, 1);
     }
     for (int j = tid; j < a.k; j += RF_THREADS) {
-        const size_t o = (size_t)q * a.k + j;
+        const size_t o = (size_t)q * a.k + j, ost = a.ostride > 1 ? (size_t)a.ostride : 1;
         if (j < nv) {
             if (a.D) a.D[o] = (float)sc[j];
-            a.I[o] = (int64_t)ids[j] + a.id_offset;
-            if (a.S64) a.S64[o] = sc[j];
+            a.I[o * ost] = (int64_t)ids[j] + a.id_offset;
+            if (a.S64) a.S64[o * ost] = sc[j];
         } else {
             if (a.D) a.D[o] = a.metric == METRIC_IP ? -3.402823466e+38f : 3.402823466e+38f;
-            a.I[o] = -1;
-            if (a.S64) a.S64[o] = a.metric == METRIC_IP ? -1.7976931348623157e308 : 1.7976931348623157e308;
+            a.I[o * ost] = -1;
+            if (a.S64) a.S64[o * ost] = a.metric == METRIC_IP ? -1.7976931348623157e308 : 1.7976931348623157e308;
         }
     }
 }
@@ -2731,11 +2731,11 @@ __global__ void __launch_bounds__(RF_THREADS) k_refine_wide(RefineArgs a, int KA
             a.pa_tA[q] = tA;
         }
         for (int j = tid; j < a.k; j += RF_THREADS) {
-            const size_t o = (size_t)q * a.k + j;
+            const size_t o = (size_t)q * a.k + j, ost = a.ostride > 1 ? (size_t)a.ostride : 1;
             const double v = j < nA ? (L2 ? -sc[j] : sc[j]) : (L2 ? 1.7976931348623157e308 : -1.7976931348623157e308);
             if (a.D) a.D[o] = j < nA ? (float)v : (L2 ? 3.402823466e+38f : -3.402823466e+38f);
-            a.I[o] = j < nA ? (int64_t)ids[j] + a.id_offset : -1;
-            if (a.S64) a.S64[o] = v;
+            a.I[o * ost] = j < nA ? (int64_t)ids[j] + a.id_offset : -1;
+            if (a.S64) a.S64[o * ost] = v;
         }
         return;
     }
@@ -2844,16 +2844,16 @@ __global__ void __launch_bounds__(RF_THREADS) k_refine_wide(RefineArgs a, int KA
         if (!cert && a.fails) atomicAdd(a.fails, 1);
     }
     for (int j = tid; j < a.k; j += RF_THREADS) {
-        const size_t o = (size_t)q * a.k + j;
+        const size_t o = (size_t)q * a.k + j, ost = a.ostride > 1 ? (size_t)a.ostride : 1;
         if (j < nF) {
             const double v = L2 ? -sc[j] : sc[j];
             if (a.D) a.D[o] = (float)v;
-            a.I[o] = (int64_t)ids[j] + a.id_offset;
-            if (a.S64) a.S64[o] = v;
+            a.I[o * ost] = (int64_t)ids[j] + a.id_offset;
+            if (a.S64) a.S64[o * ost] = v;
         } else {
             if (a.D) a.D[o] = L2 ? 3.402823466e+38f : -3.402823466e+38f;
-            a.I[o] = -1;
-            if (a.S64) a.S64[o] = L2 ? 1.7976931348623157e308 : -1.7976931348623157e308;
+            a.I[o * ost] = -1;
+            if (a.S64) a.S64[o * ost] = L2 ? 1.7976931348623157e308 : -1.7976931348623157e308;
         }
     }
 }
@@ -2944,7 +2944,8 @@ __global__ void __launch_bounds__(256) k_seed_select(const float* __restrict__ s
 // the ~k dependent steps (each a global load) of k_merge_shards' wave-per-query merge are gone.
 constexpr int kMergeRankMax = 4096;  // G * k entries (16 B each) in LDS
 __global__ void __launch_bounds__(256) k_merge_shards_rank(int metric, const double* __restrict__ S_in,
-                                                           const int64_t* __restrict__ I_in, int G, int64_t nq, int k,
+                                                           const int64_t* __restrict__ I_in, int istride, int G,
+                                                           int64_t nq, int k,
                                                            double* __restrict__ S_out, int64_t* __restrict__ I_out,
                                                            float* __restrict__ D_out) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -2959,7 +2960,7 @@ __global__ void __launch_bounds__(256) k_merge_shards_rank(int metric, const dou
     __syncthreads();
     for (int i = tid; i < n; i += 256) {
         const int g = i / k, j = i - g * k;
-        const size_t o = ((size_t)g * nq + q) * k + j;
+        const size_t o = (((size_t)g * nq + q) * k + j) * istride;
         const int64_t id = I_in[o];
         si[i] = id;
         ss[i] = id >= 0 ? S_in[o] : 0.0;
@@ -3004,7 +3005,8 @@ __global__ void __launch_bounds__(256) k_merge_shards_rank(int metric, const dou
 }
 
 __global__ void __launch_bounds__(256) k_merge_shards(int metric, const double* __restrict__ S_in,
-                                                      const int64_t* __restrict__ I_in, int G, int64_t nq, int k,
+                                                      const int64_t* __restrict__ I_in, int istride, int G,
+                                                      int64_t nq, int k,
                                                       double* __restrict__ S_out, int64_t* __restrict__ I_out,
                                                       float* __restrict__ D_out) {
     const int lane = threadIdx.x & 63;
@@ -3018,7 +3020,7 @@ __global__ void __launch_bounds__(256) k_merge_shards(int metric, const double* 
         hs = worst;
         hi = -1;
         if (lane < G && pos < k) {
-            const size_t o = ((size_t)lane * nq + q) * k + pos;
+            const size_t o = (((size_t)lane * nq + q) * k + pos) * istride;
             const int64_t id = I_in[o];
             if (id >= 0) {
                 hs = S_in[o];
@@ -3473,15 +3475,15 @@ hipError_t launch_ivf_scan_dyn(int dt, const IvfScanArgs& a, int grid, hipStream
 }
 
 hipError_t launch_merge_shards(int metric, const double* S_in, const int64_t* I_in, int G, int64_t nq, int k,
-                               double* S_out, int64_t* I_out, float* D_out, hipStream_t st) {
-    if (G > 64) return hipErrorInvalidValue;
+                               double* S_out, int64_t* I_out, float* D_out, hipStream_t st, int istride) {
+    if (G > 64 || istride < 1) return hipErrorInvalidValue;
     if ((int64_t)G * k <= kMergeRankMax) {
         hipLaunchKernelGGL(k_merge_shards_rank, dim3((unsigned)nq), dim3(256), (size_t)G * k * 16, st, metric, S_in,
-                           I_in, G, nq, k, S_out, I_out, D_out);
+                           I_in, istride, G, nq, k, S_out, I_out, D_out);
         return hipGetLastError();
     }
-    hipLaunchKernelGGL(k_merge_shards, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, st, metric, S_in, I_in, G, nq, k,
-                       S_out, I_out, D_out);
+    hipLaunchKernelGGL(k_merge_shards, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, st, metric, S_in, I_in, istride,
+                       G, nq, k, S_out, I_out, D_out);
     return hipGetLastError();
 }
 

@@ -60,6 +60,25 @@ def _device_merge(metric: int, Sg: torch.Tensor, Ig: torch.Tensor, k: int):
     return S, I, D
 
 
+def _device_merge_packed(metric: int, g: torch.Tensor, k: int):
+    """The HIP merge reading an all-gather of interleaved (score bits, id) pairs [G][nq][k][2] in
+    place (in_stride 2): no unpacking copies."""
+    from .index import merge_shards_device
+    G, nq = g.shape[0], g.shape[1]
+    S = torch.empty((nq, k), dtype=torch.float64, device=g.device)
+    I = torch.empty((nq, k), dtype=torch.int64, device=g.device)
+    D = torch.empty((nq, k), dtype=torch.float32, device=g.device)
+    stream = torch.cuda.current_stream(g.device).cuda_stream
+    merge_shards_device(metric, g.data_ptr(), g.data_ptr() + 8, G, nq, k, S.data_ptr(), I.data_ptr(), D.data_ptr(),
+                        stream, in_stride=2)
+    return S, I, D
+
+
+def _pack(S: torch.Tensor, I: torch.Tensor) -> torch.Tensor:
+    """(S fp64, I int64) [nq][k] -> interleaved (score bits, id) pairs [nq][k][2] (int64)."""
+    return torch.stack([S.contiguous().view(torch.int64), I.contiguous()], dim=-1)
+
+
 def _device_local_search(index, q: torch.Tensor, k: int, row0: int):
     """Exact top-k of the local shard as (S fp64, global I int64, D fp32) device tensors."""
     nq = q.shape[0]
@@ -74,24 +93,24 @@ def _device_local_search(index, q: torch.Tensor, k: int, row0: int):
 
 
 def _device_phase_a(index, q: torch.Tensor, k: int, row0: int, world: int):
-    """Two-phase local search, phase A: (S_a fp64, I_a int64) device lists + the pending search."""
+    """Two-phase local search, phase A: the shard's best-so-far lists as interleaved (score bits, id)
+    pairs [nq][k][2] (written in that layout by the library, ready for the all-gather) + the
+    pending search."""
     nq = q.shape[0]
-    S = torch.empty((nq, k), dtype=torch.float64, device=q.device)
-    I = torch.empty((nq, k), dtype=torch.int64, device=q.device)
+    SI = torch.empty((nq, k, 2), dtype=torch.int64, device=q.device)
     stream = torch.cuda.current_stream(q.device).cuda_stream
-    pend = index.search_phase_a(q.data_ptr(), nq, k, world, S.data_ptr(), I.data_ptr(), row0, stream)
-    return S, I, pend
+    pend = index.search_phase_a(q.data_ptr(), nq, k, world, SI.data_ptr(), SI.data_ptr() + 8, row0, stream, stride=2)
+    return SI, pend
 
 
 def _device_phase_b(index, pend, floor_S: torch.Tensor, q: torch.Tensor, k: int):
-    """Phase B with the merged phase-A lists as the floor: the shard's exact top-k (S, I, D)."""
+    """Phase B with the merged phase-A lists as the floor: the shard's exact top-k as interleaved
+    (score bits, id) pairs [nq][k][2]."""
     nq = q.shape[0]
-    S = torch.empty((nq, k), dtype=torch.float64, device=q.device)
-    I = torch.empty((nq, k), dtype=torch.int64, device=q.device)
-    D = torch.empty((nq, k), dtype=torch.float32, device=q.device)
+    SI = torch.empty((nq, k, 2), dtype=torch.int64, device=q.device)
     stream = torch.cuda.current_stream(q.device).cuda_stream
-    index.search_phase_b(pend, floor_S.data_ptr(), D.data_ptr(), I.data_ptr(), S.data_ptr(), stream)
-    return S, I, D
+    index.search_phase_b(pend, floor_S.data_ptr(), None, SI.data_ptr() + 8, SI.data_ptr(), stream, stride=2)
+    return SI
 
 
 def _device_two_phase_ok(index, nq: int, k: int) -> bool:
@@ -199,8 +218,9 @@ class ShardedFlatIndex:
         # (every rank takes the same branch: the test depends only on the index configuration)
         shards = self.shards_hint or self.world
         if shards > 1 and self._two_phase_ok(self.index, nq, k):
-            S, I, D = self._two_phase_local(q, k, shards)
-        elif self.n_local > 0:
+            # ONE more all-gather of the same shape first (the phase-A lists -> the floor)
+            return self._exchange_packed(self._two_phase_local(q, k, shards), k)
+        if self.n_local > 0:
             S, I, D = self._local_search(self.index, q, k, self.row0)
         else:  # empty shard (n_total < world): contributes only padding
             S, I, D = self._padding(nq, k, q.device)
@@ -208,7 +228,7 @@ class ShardedFlatIndex:
             return D, I, S
         # ONE all-gather of interleaved (fp64 score bits, id) pairs: a second collective would add
         # its full latency to every step (the payload is only nq * k * 16 B per rank)
-        return self._exchange(S, I, k)
+        return self._exchange_packed(_pack(S, I), k)
 
     def _padding(self, nq: int, k: int, device):
         S = torch.full((nq, k), _worst(self.metric), dtype=torch.float64, device=device)
@@ -217,24 +237,27 @@ class ShardedFlatIndex:
                        dtype=torch.float32, device=device)
         return S, I, D
 
-    def _exchange(self, S: torch.Tensor, I: torch.Tensor, k: int):
-        """all-gather of the (S, I) lists + the device merge: (D, I, S), identical on every rank."""
-        SI = torch.stack([S.contiguous().view(torch.int64), I.contiguous()], dim=-1)
+    def _exchange_packed(self, SI: torch.Tensor, k: int):
+        """all-gather of the packed (score bits, id) lists + the device merge: (D, I, S), identical on
+        every rank."""
         g = self._gather(SI)
-        S, I, D = self._merge(self.metric, g[..., 0].contiguous().view(torch.float64), g[..., 1].contiguous(), k)
+        if self._merge is _device_merge:  # the HIP merge reads the gathered pairs in place
+            S, I, D = _device_merge_packed(self.metric, g, k)
+        else:
+            S, I, D = self._merge(self.metric, g[..., 0].contiguous().view(torch.float64), g[..., 1].contiguous(), k)
         return D, I, S
 
-    def _two_phase_local(self, q: torch.Tensor, k: int, shards: int):
-        """The shard's exact top-k by the two-phase search: phase A, the exchange of the phase-A
-        lists (their merge = the floor), phase B."""
+    def _two_phase_local(self, q: torch.Tensor, k: int, shards: int) -> torch.Tensor:
+        """The shard's exact top-k (packed pairs) by the two-phase search: phase A, the exchange of
+        the phase-A lists (their merge = the floor), phase B."""
         nq = q.shape[0]
         pend = None
         if self.n_local > 0:
-            Sa, Ia, pend = self._phase_a(self.index, q, k, self.row0, shards)
+            SIa, pend = self._phase_a(self.index, q, k, self.row0, shards)
         else:
-            Sa, Ia, _ = self._padding(nq, k, q.device)
+            SIa = _pack(*self._padding(nq, k, q.device)[:2])
         try:
-            _, _, floor_S = self._exchange(Sa, Ia, k)
+            _, _, floor_S = self._exchange_packed(SIa, k)
         except BaseException:
             if pend is not None:
                 free = getattr(self.index, "search_pending_free", None)
@@ -244,7 +267,7 @@ class ShardedFlatIndex:
         if self.floor_override is not None:
             floor_S = self.floor_override
         if pend is None:
-            return self._padding(nq, k, q.device)
+            return _pack(*self._padding(nq, k, q.device)[:2])
         return self._phase_b(self.index, pend, floor_S, q, k)
 
     def close(self) -> None:

@@ -146,19 +146,20 @@ class FlatIndex:
         return int(check(self._L.vs_two_phase_ok(self._h, int(nq), int(k)))) == 1
 
     def search_phase_a(self, q_ptr: int, nq: int, k: int, world: int, S_ptr: int, I_ptr: int, id_offset: int = 0,
-                       stream: Optional[int] = None) -> int:
-        """Phase A: this shard's best-so-far (S, I) lists for the exchange; returns the pending search
-        for :meth:`search_phase_b` (or :meth:`search_pending_free`)."""
+                       stream: Optional[int] = None, stride: int = 1) -> int:
+        """Phase A: this shard's best-so-far (S, I) lists for the exchange (``stride=2``: interleaved
+        (score bits, id) pairs); returns the pending search for :meth:`search_phase_b` (or
+        :meth:`search_pending_free`)."""
         out = ctypes.c_void_p(0)
         check(self._L.vs_search_device_phase_a(self._h, q_ptr, int(nq), int(k), int(world), int(id_offset), S_ptr,
-                                               I_ptr, stream or None, ctypes.byref(out)))
+                                               I_ptr, int(stride), stream or None, ctypes.byref(out)))
         return int(out.value)
 
     def search_phase_b(self, pending: int, floor_S_ptr: int, D_ptr: Optional[int], I_ptr: int,
-                       S64_ptr: Optional[int] = None, stream: Optional[int] = None) -> None:
+                       S64_ptr: Optional[int] = None, stream: Optional[int] = None, stride: int = 1) -> None:
         """Phase B with the merged phase-A lists as the floor; frees the pending search."""
         check(self._L.vs_search_device_phase_b(ctypes.c_void_p(pending), floor_S_ptr, D_ptr or None, I_ptr,
-                                               S64_ptr or None, stream or None))
+                                               S64_ptr or None, int(stride), stream or None))
 
     def search_pending_free(self, pending: int) -> None:
         self._L.vs_search_pending_free(ctypes.c_void_p(pending))
@@ -203,11 +204,12 @@ class FlatIndex:
 
 
 def merge_shards_device(metric_type: int, S_ptr: int, I_ptr: int, G: int, nq: int, k: int, S_out: int, I_out: int,
-                        D_out: Optional[int] = None, stream: Optional[int] = None) -> None:
-    """Merge G per-shard sorted (S64, id) lists [G][nq][k] on the device (after an all-gather)."""
+                        D_out: Optional[int] = None, stream: Optional[int] = None, in_stride: int = 1) -> None:
+    """Merge G per-shard sorted (S64, id) lists [G][nq][k] on the device (after an all-gather);
+    ``in_stride=2``: one interleaved array of (score bits, id) pairs (``I_ptr = S_ptr + 8``)."""
     L = _lib.load()
-    check(L.vs_merge_shards_device(int(metric_type), S_ptr, I_ptr, int(G), int(nq), int(k), S_out, I_out,
-                                   D_out or None, stream or None))
+    check(L.vs_merge_shards_device(int(metric_type), S_ptr, I_ptr, int(in_stride), int(G), int(nq), int(k), S_out,
+                                   I_out, D_out or None, stream or None))
 
 
 def synthesize_device(device: int, seed: int, global_row0: int, n: int, d: int, out_ptr: int, normalize: bool = True,

@@ -12,7 +12,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from oracle import oracle as O
-from photo_search_engine_amd.distributed import ShardedFlatIndex, shard_range
+from photo_search_engine_amd.distributed import ShardedFlatIndex, _pack, shard_range
 from tests.oracle_index import OracleFlatIndex
 
 
@@ -53,13 +53,14 @@ def _pad(S, I, k, metric):
 
 def _oracle_phase_a(index, q, k, row0, world):
     """CPU restatement of vs_search_device_phase_a's contract: the shard's best KA rows (exact),
-    their top-k for the exchange; KA as the library picks it."""
+    their top-k for the exchange (packed pairs, as the device phase writes them); KA as the library
+    picks it."""
     metric = "ip" if index.metric_type == 0 else "l2"
     ka = min(-(-(2 * k + 32) // 32) * 32, -(-(2 * -(-k // world) + 32) // 32) * 32)
     S, I = O.knn_exact(index._x, q.numpy(), ka, metric)
     I = np.where(I >= 0, I + row0, -1)
     Sa, Ia = _pad(S, I, k, metric)
-    return torch.from_numpy(Sa), torch.from_numpy(Ia), {"S": S, "I": I, "metric": metric, "row0": row0}
+    return _pack(torch.from_numpy(Sa), torch.from_numpy(Ia)), {"S": S, "I": I, "metric": metric, "row0": row0}
 
 
 def _oracle_phase_b(index, pend, floor_S, q, k):
@@ -82,9 +83,7 @@ def _oracle_phase_b(index, pend, floor_S, q, k):
     S = np.array([r + [worst] * (m - len(r)) for r in outS], dtype=np.float64).reshape(len(outS), m)
     I = np.array([r + [-1] * (m - len(r)) for r in outI], dtype=np.int64).reshape(len(outI), m)
     S, I = _pad(S, I, k, metric)
-    D = S.astype(np.float32)
-    D[I < 0] = -3.4028235e38 if metric == "ip" else 3.4028235e38
-    return torch.from_numpy(S), torch.from_numpy(I), torch.from_numpy(D)
+    return _pack(torch.from_numpy(S), torch.from_numpy(I))
 
 
 def _worker(rank, world, port, N, d, nq, k, metric, use_broadcast, outdir, from_file=None, two_phase=False):
