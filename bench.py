@@ -227,7 +227,7 @@ def main():
         res_native = {k_: v.clone() for k_, v in result.items()}
         kn = float(np.mean(km_n)) if km_n else float("nan")
         bytes_n = n_local * d * es + nq * d * es + nq * k * 12 + (n_local * 4 if args.metric == "l2" else 0)
-        alt = {"screen": "native", "kernel": f"k_screen_{kind_n}", "value": round(nq * args.steps / el_n, 2),
+        alt = {"screen": "native", "kernel": _kernel_name(kind_n, dtype, d), "value": round(nq * args.steps / el_n, 2),
                "ms_per_step": round(el_n * 1e3 / args.steps, 4), "kernel_ms": round(kn, 4),
                "hbm_frac": round(bytes_n / (kn * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                "uncertified_first_pass": unc_n}
@@ -303,7 +303,7 @@ def main():
                            if G > 1 else "")},
             "roofline": {
                 # the int8 main pass runs the direct form when d is a multiple of 256 (vs_kernels.hip)
-                "kernel": "k_screen_i8d" if kind == "mfma_i8" and d % 256 == 0 else f"k_screen_{kind}",
+                "kernel": _kernel_name(kind, dtype, d),
                 "bound": "hbm",
                 "achieved": round(achieved_gbs, 1),
                 "peak": HBM_PEAK_GBS,
@@ -335,6 +335,17 @@ def main():
     sh.close()
     if G > 1 or args.shard_of > 1:
         dist.destroy_process_group()
+
+
+def _kernel_name(kind: str, dtype: str, d: int) -> str:
+    """The screen kernel the library ran (vs_kernels.hip): the main passes take the direct forms
+    when the K-steps per padded row are a multiple of 4 (int8: 64-element K-steps; bf16 / f16: 32)."""
+    dpad = max(-(-d // 64) * 64, 64)
+    if kind == "mfma_i8" and dpad % 256 == 0 and dpad >= 512:
+        return "k_screen_i8d"
+    if kind == "mfma" and dtype in ("bf16", "f16") and dpad % 128 == 0 and dpad >= 256:
+        return "k_screen_d16"
+    return f"k_screen_{kind}"
 
 
 def _shard_floor(args, N, d, dtype, nq, k, q, local, dev, torch):

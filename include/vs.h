@@ -84,14 +84,13 @@ int vs_search(vs_index* index, const float* q, int64_t nq, int32_t k, float* D, 
 int vs_search_device(vs_index* index, const float* q_dev, int64_t nq, int32_t k, float* D_dev,
                      int64_t* I_dev, double* S64_dev, int64_t id_offset, void* stream);
 
-/* Same outputs, but exact for every query.  bf16 / f16 indexes: each query block's first pass is
- * followed on the stream by a fallback round at the deepest screen (KP_MAX, proven seed) whose
- * kernels do nothing unless a certificate of that block failed, and which rewrites only the failed
- * queries -- no host sync: the call returns with the work queued.  A query even that round cannot
- * certify (more near-tied rows than KP_MAX: where vs_search returns VS_ERR_UNCERTIFIED) is counted
- * in vs_unresolved_count.  fp32 indexes: the certificate flags are read back (one host sync) and
- * uncertified queries re-searched with deeper screens, as vs_search does.  The product's multi-GPU
- * layers (photo_search_engine_amd/distributed.py, vs_multi_search) use this one. */
+/* Same outputs, but exact for every query (every dtype): each query block's first pass is
+ * followed on the stream by a fallback round at the deepest screen (KP_MAX, proven seed; the MFMA
+ * screen of the stored dtype, fp32 included) whose kernels do nothing unless a certificate of that
+ * block failed, and which rewrites only the failed queries -- no host sync: the call returns with
+ * the work queued.  A query even that round cannot certify (more near-tied rows than KP_MAX: where
+ * vs_search returns VS_ERR_UNCERTIFIED) is counted in vs_unresolved_count.  The product's
+ * multi-GPU layers (photo_search_engine_amd/distributed.py, vs_multi_search) use this one. */
 int vs_search_device_exact(vs_index* index, const float* q_dev, int64_t nq, int32_t k, float* D_dev,
                            int64_t* I_dev, double* S64_dev, int64_t id_offset, void* stream);
 

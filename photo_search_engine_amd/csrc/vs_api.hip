@@ -278,6 +278,7 @@ bool use_i8(const vs_index* ix, int nqb, int k) {
     return ix->screen == VS_SCREEN_I8 && nqb > GEMV_NQ_MAX && k <= I8_MAX_K;
 }
 
+constexpr int kF32MfmaMinQ = 64;     // fp32 native batches: MFMA screen from this many queries on
 constexpr int kI8RouteBatches = 64;  // searches routed to the native screen after a failing int8 batch
 constexpr int kSeedScaleMax = 6;     // native optimistic seed: at most 64x the default depth
 constexpr int kSeedRelax = 64;       // clean native batches before the depth is halved again
@@ -494,7 +495,8 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
         return;
     }
     const int64_t tiles = (ix->ntotal + TR - 1) / TR;
-    const bool use_mfma = ix->dtype != DT_F32 && (nqb > GEMV_NQ_MAX || redo);
+    // (search_all makes blocks of > GEMV_NQ_MAX queries only where the MFMA screen serves them)
+    const bool use_mfma = nqb > GEMV_NQ_MAX || redo;
     const int* gate = redo ? c->fails.as<int>() : nullptr;
     if (!redo) c->fails.ensure(sizeof(int));
     // int8 screen, few queries: the GEMV streams the int8 copy (1 B per element) with the fp32
@@ -525,7 +527,7 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
         QB = MFMA_QB;
         a.cap = MFMA_CAP;
         a.G = (int)std::min<int64_t>(tiles, ix->num_cu);
-        c->qtile.ensure((size_t)MFMA_QB * ix->dpad * 2);
+        c->qtile.ensure((size_t)MFMA_QB * ix->dpad * ix->es);
         c->gcnt.ensure(sizeof(int) * MFMA_QB);
         c->drop.ensure(sizeof(u64) * MFMA_QB);
         HIP_CHECK(launch_pack_qtile(ix->dtype, q, nqb, ix->d, ix->dpad, c->qtile.as<uint8_t>(), c->qinfo.as<float>(),
@@ -602,7 +604,9 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
         sa.tile_stride = (int)(tiles / sa.G);
         // seed tile = the first tile of each main-pass workgroup; its raw accumulators are kept so
         // the main pass starts one tile later
-        if (seed_reuse() && sa.G == a.G) {
+        // (bf16 / f16 main passes in the direct form screen their whole range themselves)
+        const bool direct = (ix->dtype == DT_BF16 || ix->dtype == DT_F16) && d16_direct_ok(ix->dpad);
+        if (seed_reuse() && sa.G == a.G && !direct) {
             c->seedacc.ensure((size_t)a.G * 128 * MF_WG_THREADS * sizeof(float));
             sa.seed_acc = c->seedacc.as<float>();
         }
@@ -728,7 +732,10 @@ void search_all(vs_index* ix, Ctx* c, const float* q, int64_t nq, int k, int Kp,
     while (done < nq) {
         const int64_t rem = nq - done;
         int nqb;
-        if (mfma_ok && rem > GEMV_NQ_MAX) nqb = (int)std::min<int64_t>(rem, MFMA_QB);
+        // fp32 rows on the native screen: the fp32 MFMA (compute-bound, all 256 columns) pays from
+        // ~kF32MfmaMinQ queries on; fewer take the GEMV, 8 queries per corpus pass
+        if ((mfma_ok && rem > GEMV_NQ_MAX) || (!i8 && ix->dtype == DT_F32 && rem >= kF32MfmaMinQ))
+            nqb = (int)std::min<int64_t>(rem, MFMA_QB);
         else nqb = (int)std::min<int64_t>(rem, GEMV_NQ_MAX);
         search_block(ix, c, q + done * ix->d, nqb, k, Kp, D ? D + done * k : nullptr, I + done * k,
                      S64 ? S64 + done * k : nullptr, cert ? cert + done : nullptr, id_offset, st, seed_rank, false, i8);
@@ -746,12 +753,11 @@ void check_index(const vs_index* ix) {
 }  // namespace
 
 // exact device search (vs_search_device_exact; the IVF coarse quantizer): like vs_search_device,
-// but certificate failures are re-searched.  bf16 / f16 indexes: on the device, by each query
-// block's gated fallback round at the deepest screen (KP_MAX, where vs_search's escalation ends).
-// async: no host round trip at all, the call returns with the work queued and a query even the
-// fallback cannot certify counts in vs_unresolved_count; otherwise the certificates are read back
-// and such a query raises VS_ERR_UNCERTIFIED, as in vs_search.  fp32 indexes (GEMV re-search):
-// read back the certificates and re-search with deeper screens, as vs_search does.
+// but certificate failures are re-searched on the device, by each query block's gated fallback
+// round at the deepest screen (KP_MAX, where vs_search's escalation ends; fp32 rows: the fp32 MFMA
+// screen).  async: no host round trip at all, the call returns with the work queued and a query
+// even the fallback cannot certify counts in vs_unresolved_count; otherwise the certificates are
+// read back and such a query raises VS_ERR_UNCERTIFIED, as in vs_search.
 void vs::search_exact_device(vs_index* ix, const float* q_dev, int64_t nq, int k, int64_t* I_dev, double* S64_dev,
                              hipStream_t st, float* D_dev, int64_t id_offset, bool async, unsigned* unres) {
     check_index(ix);
@@ -764,7 +770,7 @@ void vs::search_exact_device(vs_index* ix, const float* q_dev, int64_t nq, int k
     c->outD.ensure((size_t)nq * k * sizeof(float));
     c->cert.ensure((size_t)nq * sizeof(int));
     const int Kp = screen_depth(k);
-    const bool on_device = ix->dtype != DT_F32;
+    const bool on_device = true;  // (every dtype has the MFMA fallback round)
     struct UnresScope {  // the caller's counter for this call only (the Ctx goes back to the pool)
         Ctx* c;
         ~UnresScope() { c->unres = nullptr; }
@@ -819,7 +825,7 @@ struct vs_pending {
 };
 
 bool vs::two_phase_ok(const vs_index* ix, int64_t nq, int k) {
-    return ix->screen == VS_SCREEN_I8 && ix->dtype != DT_F32 && nq > GEMV_NQ_MAX && nq <= MFMA_QB && k <= I8_MAX_K;
+    return ix->screen == VS_SCREEN_I8 && nq > GEMV_NQ_MAX && nq <= MFMA_QB && k <= I8_MAX_K;
 }
 
 vs_pending* vs::search_phase_a(vs_index* ix, const float* q_dev, int64_t nq, int k, int world, int64_t id_offset,

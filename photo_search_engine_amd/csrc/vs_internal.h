@@ -235,6 +235,8 @@ hipError_t launch_screen_mfma(int dt, const ScreenArgs& a, const uint8_t* qt, in
 // the int8 main pass runs the direct form (k_screen_i8d) for this int8 row stride (K-steps per tile
 // a multiple of 4); it takes no seed-tile accumulators (ScreenArgs::seed_acc must be null)
 bool i8_direct_ok(int dpad8);
+// the same for bf16 / f16 rows (k_screen_d16: K-steps of 32 elements per tile a multiple of 4)
+bool d16_direct_ok(int dpad);
 // the same screen over pages of a page pool (IVF lists; bf16 / f16, unseeded, a.Kp <= MFMA_KP_MAX):
 // a.G workgroups, each with its own descriptor (a.wg_desc): <= MFMA_MAP_TILES pages of one list
 // (a.tile_map), one split query tile of <= 128 queries (qt + index * MFMA_QB * dpad * 2, made by

@@ -461,10 +461,12 @@ __global__ void __launch_bounds__(256) k_pack_qtile(const float* __restrict__ q,
     if (drop && lane == 0) drop[r] = 0ull;  // ... and its workgroups' drop bounds
     double n2 = 0.0, e2 = 0.0;
     const int64_t qr = (qidx && r < nqb) ? (int64_t)qidx[r] : (int64_t)r;
+    constexpr int KE = DT == DT_F32 ? 16 : 32;  // elements per K-step (64 B per query row)
+    constexpr int ES = DT == DT_F32 ? 4 : 2;
 #pragma unroll 8
     for (int i = lane; i < dpad; i += 64) {
         float v = (r < nqb && i < d) ? q[qr * d + i] : 0.0f;
-        float st = round_store<DT>(v, qt + (int64_t)(i >> 5) * MFMA_QB * 64 + (int64_t)r * 64 + (i & 31) * 2);
+        float st = round_store<DT>(v, qt + (int64_t)(i / KE) * MFMA_QB * 64 + (int64_t)r * 64 + (i % KE) * ES);
         n2 += (double)st * st;
         double df = (double)st - (double)v;
         e2 += df * df;
@@ -815,6 +817,16 @@ __device__ __forceinline__ floatx4 mfma16(const uint4 a, const uint4 b, floatx4 
     else if constexpr (DT == DT_BF16)
         return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
                                                        0, 0, 0);
+    else if constexpr (DT == DT_F32) {
+        // fp32 rows (the fallback round of fp32 indexes, and their large batches): a 16 B fragment
+        // holds 4 consecutive k of the K-step's 16, consumed by 4 16x16x4 MFMAs (MFMA k-slot g =
+        // lane >> 4 is physical k 4g + e in MFMA e, for A and B alike)
+        const floatx4 av = __builtin_bit_cast(floatx4, a), bv = __builtin_bit_cast(floatx4, b);
+        c = __builtin_amdgcn_mfma_f32_16x16x4f32(av[0], bv[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x4f32(av[1], bv[1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x4f32(av[2], bv[2], c, 0, 0, 0);
+        return __builtin_amdgcn_mfma_f32_16x16x4f32(av[3], bv[3], c, 0, 0, 0);
+    }
     else
         return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0,
                                                       0, 0);
@@ -983,13 +995,15 @@ __device__ __forceinline__ void screen_mfma(ScreenArgs a, const uint8_t* __restr
         flag[2] = 0;
         flag[3] = 0;
     }
-    const int nks = a.dpad / (I8 ? 64 : CH);  // K-steps per tile (16 KiB each)
-    const int64_t tbytes = (int64_t)TR * a.dpad * (I8 ? 1 : 2);
+    constexpr bool F32 = DT == DT_F32;
+    const int nks = a.dpad / (I8 ? 64 : F32 ? CH / 2 : CH);  // K-steps per tile (16 KiB each)
+    const int64_t tbytes = (int64_t)TR * a.dpad * (I8 ? 1 : F32 ? 4 : 2);
     constexpr int RS = I8 ? 6 : 7;  // log2 of the corpus row stride within a chunk (see mf_stage)
     // waves issuing the stage DMAs (8 each per K-step): the loader waves.  Spreading them over all
     // 8 waves (4 each) measured slower for both screens (int8 K1 4.39 -> 4.54 ms, bf16 7.60 -> 7.94)
     constexpr int NLW = 4;
-    // K-step ks of tile ti: int8 -> chunk ks (64 B per row); bf16 / f16 -> half (ks & 1) of chunk ks / 2
+    // K-step ks of tile ti: int8 -> chunk ks (64 B per row); bf16 / f16 / fp32 -> half (ks & 1) of
+    // chunk ks / 2 (128 B per row: 64 bf16 / 32 fp32 elements)
     auto kblock = [&](int ti, int ks) -> const uint8_t* {
         if constexpr (I8) return a.corpus + phys(ti) * tbytes + (int64_t)ks * 16384;
         else return a.corpus + phys(ti) * tbytes + (int64_t)(ks >> 1) * (TR * CHB) + (ks & 1) * 64;
@@ -1372,9 +1386,34 @@ __device__ __forceinline__ void i8d_wait_barrier(intx4& a0, intx4& a1) {
                  : "memory");
 }
 
-template <int METRIC>
-__global__ void __launch_bounds__(512, 2) k_screen_i8d(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
+// one K-step of the direct screen (the asm bodies of vs_i8_asm.h, chosen at compile time)
+template <int DT, bool FIRST>
+__device__ __forceinline__ void d_step(intx4 (&acc)[2][16], intx4 (&bt)[4], uint32_t slot_lds, intx4& A0, intx4& A1) {
+    if constexpr (DT == DT_I8) {
+        if constexpr (FIRST) I8D_STEP0(A0, A1);
+        else I8D_STEP(A0, A1);
+    } else if constexpr (DT == DT_BF16) {
+        if constexpr (FIRST) BFD_STEP0(A0, A1);
+        else BFD_STEP(A0, A1);
+    } else {
+        if constexpr (FIRST) HFD_STEP0(A0, A1);
+        else HFD_STEP(A0, A1);
+    }
+}
+// 16 B per lane into VGPRs with the default cache policy (bf16 / f16: a K-step reads one half of
+// each row's 128 B line, the next K-step the other half, from L2)
+__device__ __forceinline__ void gld16(intx4& v, const void* p) {
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+}
+
+// The direct form for int8 codes (k_screen_i8d) and for bf16 / f16 rows (k_screen_d16): the same
+// loop with the corpus dtype's MFMA.  16-bit rows: 32 elements per K-step, the K-step's 64 B of a
+// row being one half of its 128 B line; native keys (fp32 score; L2: 2 score - ||x||^2); a column
+// is tested by the max of its 8 keys.
+template <int DT, int METRIC>
+__device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
     constexpr bool L2 = METRIC == METRIC_L2;
+    constexpr bool I8 = DT == DT_I8;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint8_t* const sm = smem + I8D_RING;
     u64* thr_key = (u64*)sm;
@@ -1404,7 +1443,7 @@ __global__ void __launch_bounds__(512, 2) k_screen_i8d(ScreenArgs a, const uint8
         const float tf = !real ? INFINITY : (k0 == 0ull ? -INFINITY : key_score(k0));
         thr_f[tid] = tf;
         cnt[tid] = 0;
-        const float2 f = real ? a.qfac[tid] : make_float2(0.0f, 0.0f);
+        const float2 f = (I8 && real) ? a.qfac[tid] : make_float2(0.0f, 0.0f);
         qrec[tid] = make_float4(f.x, f.y, tf, 0.0f);
     }
     if (tid == 0) {
@@ -1414,20 +1453,24 @@ __global__ void __launch_bounds__(512, 2) k_screen_i8d(ScreenArgs a, const uint8
         flag[3] = 0;
     }
     __syncthreads();
-    const int nks = a.dpad / 64;
-    const int64_t tbytes = (int64_t)TR * a.dpad;
+    const int nks = a.dpad / (I8 ? 64 : CH);
+    const int64_t tbytes = (int64_t)TR * a.dpad * (I8 ? 1 : 2);
     u64* cand = a.cand + (size_t)blk * MFMA_QB * a.cap;
     const int trigger = a.cap - TR;
     const uint32_t ring = lds_addr(smem);
     const uint32_t rowx_lds = lds_addr((const uint8_t*)rowx);
     // this wave's side-data DMA (wave-uniform, scalar): source rows and LDS destination
     const int wid_s = __builtin_amdgcn_readfirstlane(wid);
-    const bool sq_wave = L2 && wid_s >= 4;
+    // (int8: waves 0-3 the (scale | beta) words, waves 4-7 ||x||^2 (L2) or the same words again;
+    // 16-bit rows: ||x||^2 into rowx (L2 only))
+    const bool sq_wave = L2 && (!I8 || wid_s >= 4);
     const uint32_t* const side_src = (sq_wave ? (const uint32_t*)a.sqn : a.rsb) + (wid_s & 3) * 64;
-    const uint32_t side_dst = (sq_wave ? lds_addr((const uint8_t*)rowq) : rowx_lds) + (uint32_t)((wid_s & 3) * 256);
+    const uint32_t side_dst = (sq_wave && I8 ? lds_addr((const uint8_t*)rowq) : rowx_lds) + (uint32_t)((wid_s & 3) * 256);
     const int r16 = lane & 15;
     const uint32_t lane_off = (uint32_t)(r16 * 64 + (((lane >> 4) ^ mf_swz(r16)) << 4));
-    const int a_off = wid * 2048 + r16 * 64 + (lane >> 4) * 16;  // lane's 16 B of the wave's first fragment
+    // lane's 16 B of the wave's first fragment (its second: 16 rows further)
+    const int a_off = I8 ? wid * 2048 + r16 * 64 + (lane >> 4) * 16 : (wid * 32 + r16) * CHB + (lane >> 4) * 16;
+    constexpr int A2 = I8 ? 1024 : 16 * CHB;
 
     intx4 A[I8D_U][2];  // corpus fragments of the K-steps in flight (set = K-step & 3)
     intx4 acc[2][16];   // acc[m][n][r]: row wid*32 + 16m + 4(lane >> 4) + r, query 16n + (lane & 15)
@@ -1441,7 +1484,7 @@ __global__ void __launch_bounds__(512, 2) k_screen_i8d(ScreenArgs a, const uint8
     do {                                                                                                 \
         /* 4 waves cover the tile's 1 KiB of (scale | beta); waves 4-7 load its ||x||^2 (L2) or      \
            rewrite the same bytes (inner product): the same op count for every wave */                 \
-        if (iks == nks - 1 && iti < t1)                                                                  \
+        if ((I8 || L2) && iks == nks - 1 && iti < t1)                                                    \
             glds4(side_src + (int64_t)iti * TR + lane,                                                   \
                   __builtin_amdgcn_readfirstlane(side_dst + (uint32_t)((iti & 1) * 1024)));              \
         const uint32_t qbase = __builtin_amdgcn_readfirstlane(ring + (uint32_t)((SET) * 16384 + wid * 1024)); \
@@ -1450,9 +1493,15 @@ __global__ void __launch_bounds__(512, 2) k_screen_i8d(ScreenArgs a, const uint8
             const int row = g >> 2, pos = g & 3;                                                         \
             glds16(qt + (int64_t)iks * 16384 + (row << 6) + ((pos ^ mf_swz(row)) << 4), qbase + it * 8192); \
         }                                                                                                \
-        const uint8_t* ab = a.corpus + (int64_t)(iti < t1 ? iti : t1 - 1) * tbytes + (int64_t)iks * 16384 + a_off; \
-        gld16_nt(A[SET][0], ab);                                                                         \
-        gld16_nt(A[SET][1], ab + 1024);                                                                  \
+        const uint8_t* ab = a.corpus + (int64_t)(iti < t1 ? iti : t1 - 1) * tbytes +                    \
+                            (I8 ? (int64_t)iks * 16384 : (int64_t)(iks >> 1) * (TR * CHB) + (iks & 1) * 64) + a_off; \
+        if (I8 || (iks & 1)) {  /* the line's last read: non-temporal */                                 \
+            gld16_nt(A[SET][0], ab);                                                                     \
+            gld16_nt(A[SET][1], ab + A2);                                                                \
+        } else {                                                                                         \
+            gld16(A[SET][0], ab);                                                                        \
+            gld16(A[SET][1], ab + A2);                                                                   \
+        }                                                                                                \
         if (++iks == nks) { iks = 0; ++iti; }                                                            \
     } while (0)
 
@@ -1470,7 +1519,7 @@ __global__ void __launch_bounds__(512, 2) k_screen_i8d(ScreenArgs a, const uint8
         i8d_wait_barrier(A[U_][0], A[U_][1]);                                        \
         I8D_ISSUE(((U_) + I8D_P) & 3);                                               \
         const uint32_t slot_lds = ring + (uint32_t)((U_) * 16384) + lane_off;        \
-        STEP_(A[U_][0], A[U_][1]);                                                   \
+        d_step<DT, STEP_>(acc, bt, slot_lds, A[U_][0], A[U_][1]);                    \
     } while (0)
     for (int ti = t0; ti < t1; ++ti) {
         // K-steps 0..3: the first writes the accumulators; the deferred compaction check of the
@@ -1525,16 +1574,16 @@ __global__ void __launch_bounds__(512, 2) k_screen_i8d(ScreenArgs a, const uint8
         }
         {
             const uint32_t slot_lds = ring + lane_off;
-            I8D_STEP0(A[0][0], A[0][1]);
+            d_step<DT, true>(acc, bt, slot_lds, A[0][0], A[0][1]);
         }
-        I8D_BODY(1, I8D_STEP);
-        I8D_BODY(2, I8D_STEP);
-        I8D_BODY(3, I8D_STEP);
+        I8D_BODY(1, false);
+        I8D_BODY(2, false);
+        I8D_BODY(3, false);
         for (int ks0 = I8D_U; ks0 < nks; ks0 += I8D_U) {
-            I8D_BODY(0, I8D_STEP);
-            I8D_BODY(1, I8D_STEP);
-            I8D_BODY(2, I8D_STEP);
-            I8D_BODY(3, I8D_STEP);
+            I8D_BODY(0, false);
+            I8D_BODY(1, false);
+            I8D_BODY(2, false);
+            I8D_BODY(3, false);
         }
         // the epilogue reads the last MFMAs' results (the hazard recognizer does not see the asm)
         asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
@@ -1551,10 +1600,12 @@ __global__ void __launch_bounds__(512, 2) k_screen_i8d(ScreenArgs a, const uint8
         // the shard's last tile: rows >= n_valid (garbage side data) never qualify -> no bound test,
         // every pair is staged, and the per-row path makes those rows NaN
         const bool edge = rowbase + TR > a.n_valid;
-        const float* rq = rowq + (ti & 1) * TR;  // (L2)
+        // (L2) the tile's ||x||^2: int8 -> rowq, 16-bit rows -> rowx
+        const float* rq = I8 ? rowq + (ti & 1) * TR : (const float*)rx;
         float smax = 0.0f, smin = 0.0f, bmax = 0.0f, sqmin = 0.0f;
         {
             const int rw0 = wid * 32 + (olane >> 4) * 4;
+            if constexpr (I8) {
             const uint4 w0 = *(const uint4*)(rx + rw0), w1 = *(const uint4*)(rx + rw0 + 16);
             const uint32_t w8[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
             smax = smin = __uint_as_float(w8[0] << 16);
@@ -1564,6 +1615,7 @@ __global__ void __launch_bounds__(512, 2) k_screen_i8d(ScreenArgs a, const uint8
                 smax = fmaxf(smax, __uint_as_float(w8[j] << 16));
                 smin = fminf(smin, __uint_as_float(w8[j] << 16));
                 bmax = fmaxf(bmax, __uint_as_float(w8[j] & 0xFFFF0000u));
+            }
             }
             if constexpr (L2) {
                 const float4 n0 = *(const float4*)(rq + rw0), n1 = *(const float4*)(rq + rw0 + 16);
@@ -1579,7 +1631,8 @@ __global__ void __launch_bounds__(512, 2) k_screen_i8d(ScreenArgs a, const uint8
                 const int q = 16 * n + (sl & 15);
                 const int r0 = wid * 32 + (sl >> 4) * 4;  // + 16 m + r
                 const intx4 c0 = rec[2 * lane], c1 = rec[2 * lane + 1];
-                const uint4 w0 = *(const uint4*)(rx + r0), w1 = *(const uint4*)(rx + r0 + 16);
+                const uint4 w0 = I8 ? *(const uint4*)(rx + r0) : make_uint4(0, 0, 0, 0);
+                const uint4 w1 = I8 ? *(const uint4*)(rx + r0 + 16) : make_uint4(0, 0, 0, 0);
                 const int cc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
                 const uint32_t w8[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
                 const float4 f = qrec[q];  // key = t_q * (s_x acc + beta_x ||q|| / t_q)
@@ -1588,8 +1641,9 @@ __global__ void __launch_bounds__(512, 2) k_screen_i8d(ScreenArgs a, const uint8
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const int row = r0 + (j >> 2) * 16 + (j & 3);
-                    float x = __builtin_fmaf(__uint_as_float(w8[j] & 0xFFFF0000u), f.y,
-                                             (float)cc[j] * __uint_as_float(w8[j] << 16)) * f.x;
+                    float x = I8 ? __builtin_fmaf(__uint_as_float(w8[j] & 0xFFFF0000u), f.y,
+                                                  (float)cc[j] * __uint_as_float(w8[j] << 16)) * f.x
+                                 : __int_as_float(cc[j]);
                     if constexpr (L2) x = __builtin_fmaf(2.0f, x, -rq[row]);  // 2 <x, q> - ||x||^2
                     v[j] = rowbase + row >= a.n_valid ? __builtin_nanf("") : x;
                     mh |= (v[j] >= f.z ? 1u : 0u) << j;  // (ties resolved by key below)
@@ -1626,10 +1680,18 @@ __global__ void __launch_bounds__(512, 2) k_screen_i8d(ScreenArgs a, const uint8
             // (acc >= 0) or smallest (acc < 0) scale, plus the largest error norm; each step is
             // monotone, so a key that would pass implies a bound that passes
             const float4 f = qrec[16 * n + qlane];
-            const int mi = max(max(max(acc[0][n][0], acc[0][n][1]), max(acc[0][n][2], acc[0][n][3])),
-                               max(max(acc[1][n][0], acc[1][n][1]), max(acc[1][n][2], acc[1][n][3])));
-            const float fm = (float)mi;
-            float b = __builtin_fmaf(bmax, f.y, fmaxf(smax * fm, smin * fm)) * f.x;
+            float b;
+            if constexpr (I8) {
+                const int mi = max(max(max(acc[0][n][0], acc[0][n][1]), max(acc[0][n][2], acc[0][n][3])),
+                                   max(max(acc[1][n][0], acc[1][n][1]), max(acc[1][n][2], acc[1][n][3])));
+                const float fm = (float)mi;
+                b = __builtin_fmaf(bmax, f.y, fmaxf(smax * fm, smin * fm)) * f.x;
+            } else {  // fp32 scores: the column's max
+                b = fmaxf(fmaxf(fmaxf(__int_as_float(acc[0][n][0]), __int_as_float(acc[0][n][1])),
+                                fmaxf(__int_as_float(acc[0][n][2]), __int_as_float(acc[0][n][3]))),
+                          fmaxf(fmaxf(__int_as_float(acc[1][n][0]), __int_as_float(acc[1][n][1])),
+                                fmaxf(__int_as_float(acc[1][n][2]), __int_as_float(acc[1][n][3]))));
+            }
             if constexpr (L2) b = __builtin_fmaf(2.0f, b, -sqmin);  // (monotone: >= every row's key)
             gomask |= (b >= f.z ? 1u : 0u) << n;
         }
@@ -1681,6 +1743,17 @@ __global__ void __launch_bounds__(512, 2) k_screen_i8d(ScreenArgs a, const uint8
     }
     mf_flush_wave<false>(a, cand, cnt, nqb, wid, lane);
 }
+
+template <int METRIC>
+__global__ void __launch_bounds__(512, 2) k_screen_i8d(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
+    screen_direct<DT_I8, METRIC>(a, qt, nqb);
+}
+template <int DT, int METRIC>
+__global__ void __launch_bounds__(512, 2) k_screen_d16(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
+    screen_direct<DT, METRIC>(a, qt, nqb);
+}
+// d16: K-steps of 32 elements per tile a multiple of 4 (and >= 8)
+bool d16_direct_ok(int dpad) { return dpad % (CH * I8D_U) == 0 && dpad >= 2 * CH * I8D_U; }
 
 // 16 B streaming load with the non-temporal hint (corpus and list bytes are read once per pass)
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
@@ -3139,7 +3212,10 @@ hipError_t launch_gather_rows(int dt, const uint8_t* data, const int64_t* ids, i
 
 hipError_t launch_pack_qtile(int dt, const float* q, int nqb, int d, int dpad, uint8_t* qt, float* qinfo, int* gcnt,
                              u64* drop, hipStream_t st, int* fails, const int* gate, const int* qidx) {
-    if (dt == DT_BF16)
+    if (dt == DT_F32)
+        hipLaunchKernelGGL(k_pack_qtile<DT_F32>, dim3(MFMA_QB / 4), dim3(256), 0, st, q, nqb, d, dpad, qt, qinfo,
+                           gcnt, drop, fails, gate, qidx);
+    else if (dt == DT_BF16)
         hipLaunchKernelGGL(k_pack_qtile<DT_BF16>, dim3(MFMA_QB / 4), dim3(256), 0, st, q, nqb, d, dpad, qt, qinfo,
                            gcnt, drop, fails, gate, qidx);
     else
@@ -3232,12 +3308,32 @@ static hipError_t launch_mfma_dt(int dt, const ScreenArgs& a, const uint8_t* qt,
         }
         if (a.metric == METRIC_IP) launch_mfma_one<DT_I8, METRIC_IP, SEED>(a, qt, nqb, st);
         else launch_mfma_one<DT_I8, METRIC_L2, SEED>(a, qt, nqb, st);
+    } else if ((dt == DT_BF16 || dt == DT_F16) && !SEED && !a.gate && d16_direct_ok(a.dpad)) {
+        // the main pass of bf16 / f16 rows: direct form (no seed-tile reuse); fallback rounds keep
+        // the tiled form
+        if (a.seed_acc || a.tile_stride != 0 || (a.metric == METRIC_L2 && !a.sqn)) return hipErrorInvalidValue;
+        const void* fn = dt == DT_BF16 ? (a.metric == METRIC_IP ? (const void*)k_screen_d16<DT_BF16, METRIC_IP>
+                                                                : (const void*)k_screen_d16<DT_BF16, METRIC_L2>)
+                                       : (a.metric == METRIC_IP ? (const void*)k_screen_d16<DT_F16, METRIC_IP>
+                                                                : (const void*)k_screen_d16<DT_F16, METRIC_L2>);
+        set_lds_attr(fn, I8D_LDS);
+        if (dt == DT_BF16 && a.metric == METRIC_IP)
+            hipLaunchKernelGGL((k_screen_d16<DT_BF16, METRIC_IP>), dim3(a.G), dim3(MF_THREADS), I8D_LDS, st, a, qt, nqb);
+        else if (dt == DT_BF16)
+            hipLaunchKernelGGL((k_screen_d16<DT_BF16, METRIC_L2>), dim3(a.G), dim3(MF_THREADS), I8D_LDS, st, a, qt, nqb);
+        else if (a.metric == METRIC_IP)
+            hipLaunchKernelGGL((k_screen_d16<DT_F16, METRIC_IP>), dim3(a.G), dim3(MF_THREADS), I8D_LDS, st, a, qt, nqb);
+        else
+            hipLaunchKernelGGL((k_screen_d16<DT_F16, METRIC_L2>), dim3(a.G), dim3(MF_THREADS), I8D_LDS, st, a, qt, nqb);
     } else if (dt == DT_BF16) {
         if (a.metric == METRIC_IP) launch_mfma_one<DT_BF16, METRIC_IP, SEED>(a, qt, nqb, st);
         else launch_mfma_one<DT_BF16, METRIC_L2, SEED>(a, qt, nqb, st);
     } else if (dt == DT_F16) {
         if (a.metric == METRIC_IP) launch_mfma_one<DT_F16, METRIC_IP, SEED>(a, qt, nqb, st);
         else launch_mfma_one<DT_F16, METRIC_L2, SEED>(a, qt, nqb, st);
+    } else if (dt == DT_F32) {
+        if (a.metric == METRIC_IP) launch_mfma_one<DT_F32, METRIC_IP, SEED>(a, qt, nqb, st);
+        else launch_mfma_one<DT_F32, METRIC_L2, SEED>(a, qt, nqb, st);
     } else {
         return hipErrorInvalidValue;
     }
@@ -3332,12 +3428,10 @@ hipError_t launch_merge(const u64* in, int nseg, int qstride, int nq, int Kp, u6
 template <int DT, int METRIC, bool QLDS>
 static void launch_refine_one(const RefineArgs& a, int nq, int KP2, size_t lds, hipStream_t st) {
     set_lds_attr((const void*)k_refine<DT, METRIC, QLDS>, 152 * 1024);
-    if constexpr (DT != DT_F32) set_lds_attr((const void*)k_refine_redo<DT, METRIC, QLDS>, 152 * 1024);
-    if constexpr (DT != DT_F32) {
-        if (a.redo) {
-            hipLaunchKernelGGL((k_refine_redo<DT, METRIC, QLDS>), dim3(nq), dim3(RF_THREADS), lds, st, a, KP2);
-            return;
-        }
+    set_lds_attr((const void*)k_refine_redo<DT, METRIC, QLDS>, 152 * 1024);
+    if (a.redo) {
+        hipLaunchKernelGGL((k_refine_redo<DT, METRIC, QLDS>), dim3(nq), dim3(RF_THREADS), lds, st, a, KP2);
+        return;
     }
     const int ns = a.nsplit > 1 ? a.nsplit : 1;
     hipLaunchKernelGGL((k_refine<DT, METRIC, QLDS>), dim3(nq, ns), dim3(RF_THREADS), lds, st, a, KP2);
@@ -3366,7 +3460,7 @@ static void launch_refine_dt(const RefineArgs& a, int nq, int KP2, size_t lds, b
 }
 
 hipError_t launch_refine(const RefineArgs& a, int nq, hipStream_t st) {
-    if (a.redo && (a.dt == DT_F32 || !a.gate || !a.cert)) return hipErrorInvalidValue;  // fallback: bf16 / f16
+    if (a.redo && (!a.gate || !a.cert)) return hipErrorInvalidValue;
     if (a.nsplit > 1 && (a.redo || !a.gsc || !a.gids || !a.gdone)) return hipErrorInvalidValue;
     int KP2 = 1;
     while (KP2 < a.Kp) KP2 <<= 1;

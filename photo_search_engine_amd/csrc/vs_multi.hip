@@ -121,7 +121,7 @@ struct MCtx {
     std::vector<hipEvent_t> ready;            // per device: its lists landed on device 0
     unsigned* unres_h = nullptr;              // pinned, per device: this call's unresolved queries
     DevBuf gS, gI, oS, oI, oD;                // device 0: gathered [G][nq][k] lists, merged outputs
-    Pool* pool = nullptr;                     // one worker per device (fp32 shards wait on the host)
+    Pool* pool = nullptr;                     // one worker per device
 };
 
 struct vs_multi {

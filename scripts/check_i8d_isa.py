@@ -4,7 +4,8 @@ read of a fragment register that could run before the kernel's own s_waitcnt (DE
 
     python scripts/check_i8d_isa.py [vs_kernels.s]   (default: compiles vs_kernels.hip to asm)
 
-Both instantiations are checked (inner product and L2).
+Both instantiations are checked (inner product and L2), and the bf16 / f16 direct form
+k_screen_d16 the same way.
 
 Checks, for the kernel's code: no scratch (spill) traffic; every register written by a corpus load
 (`global_load_dwordx4 ... nt`) is read only by v_mfma instructions; one s_barrier per K-step body.
@@ -49,10 +50,16 @@ def main() -> int:
     for metric, sym in (("ip", "_ZN2vs12k_screen_i8dILi0EEEvNS_10ScreenArgsEPKhi:"),
                         ("l2", "_ZN2vs12k_screen_i8dILi1EEEvNS_10ScreenArgsEPKhi:")):
         rc |= check(asm, metric, sym)
+    # the bf16 / f16 direct form (k_screen_d16): its corpus loads are global_load_dwordx4 with and
+    # without the nt hint (the first half of each 128 B line keeps the default policy)
+    for dt, dcode in (("bf16", 1), ("f16", 2)):
+        for metric, mcode in (("ip", 0), ("l2", 1)):
+            rc |= check(asm, f"{dt}/{metric}", f"_ZN2vs12k_screen_d16ILi{dcode}ELi{mcode}EEEvNS_10ScreenArgsEPKhi:",
+                        name="k_screen_d16", any_policy=True)
     return rc
 
 
-def check(asm: str, metric: str, sym: str) -> int:
+def check(asm: str, metric: str, sym: str, name: str = "k_screen_i8d", any_policy: bool = False) -> int:
     start = asm.index(sym)
     end = asm.index(".Lfunc_end", start)
     raw = asm[start:end].split("\n")
@@ -76,7 +83,7 @@ def check(asm: str, metric: str, sym: str) -> int:
     loaded = set()
     for i, l in enumerate(code):
         op, dst, _ = parsed[i]
-        if not (op == "global_load_dwordx4" and l.split(";")[0].rstrip().endswith("nt")):
+        if not (op == "global_load_dwordx4" and (any_policy or l.split(";")[0].rstrip().endswith("nt"))):
             continue
         loaded |= dst
         for j in range(i + 1, len(code)):
@@ -90,7 +97,7 @@ def check(asm: str, metric: str, sym: str) -> int:
                 break
     nmfma = sum(1 for l in code if l.strip().startswith("v_mfma"))
     nbar = sum(1 for l in code if l.strip().startswith("s_barrier"))
-    print(f"k_screen_i8d<{metric}>: {len(code)} instructions, {nmfma} MFMA, {nbar} s_barrier, "
+    print(f"{name}<{metric}>: {len(code)} instructions, {nmfma} MFMA, {nbar} s_barrier, "
           f"{len(loaded)} corpus-fragment VGPRs")
     for b in bad[:20]:
         print("FAIL:", b)

@@ -66,14 +66,33 @@ def test_gemv_path_exact(FlatIndex, metric, dtype, nq, k):
 
 
 @pytest.mark.parametrize("metric", ["ip", "l2"])
-@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+@pytest.mark.parametrize("dtype", ["bf16", "f16", "f32"])
 @pytest.mark.parametrize("nq,k,N,d", [(40, 10, 9000, 128), (256, 100, 20000, 192), (300, 7, 3001, 72),
                                      (64, 400, 150000, 96)])  # Kp 512: the largest MFMA screening depth
 def test_mfma_path_exact(FlatIndex, metric, dtype, nq, k, N, d):
+    # (fp32 rows: the fp32 MFMA screen from 64 queries on, four 16x16x4 MFMAs per fragment)
     ix = FlatIndex(d, metric, dtype)
     ix.add_synthetic(O.SEED_CORPUS, 0, N, True)
     q = O.synth_rows(O.SEED_QUERIES, 0, nq, d, True, dtype)  # queries in the corpus dtype (cfg3)
     _check_exact(ix, q, k, metric)
+
+
+@pytest.mark.parametrize("metric", ["ip", "l2"])
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+@pytest.mark.parametrize("nq,k,N,d", [(256, 100, None, 512), (64, 1000, 150_000, 256), (300, 10, 50_000, 384),
+                                     (20, 50, 3000, 1536)])
+def test_direct_16bit_screen_exact(FlatIndex, metric, dtype, nq, k, N, d):
+    """bf16 / f16 rows with 32-element K-steps per tile a multiple of 4: the main pass is the
+    direct form k_screen_d16 (corpus fragments HBM -> VGPRs, both halves of each 128 B line in
+    consecutive K-steps).  Seeded (>= 4 tiles per CU) and unseeded corpora, partial last tiles, k =
+    1000 (compaction in the K loop), two query blocks, fp32 queries."""
+    if N is None:
+        N = 256 * 4 * _num_cu() + 777
+    ix = FlatIndex(d, metric, dtype)
+    ix.add_synthetic(O.SEED_CORPUS + 3, 0, N, True)
+    q = O.synth_rows(O.SEED_QUERIES + 3, 0, nq, d, True, "f32")
+    _check_exact(ix, q, k, metric)
+    ix.close()
 
 
 def test_mfma_fp32_queries_over_bf16_corpus(FlatIndex):
@@ -82,6 +101,22 @@ def test_mfma_fp32_queries_over_bf16_corpus(FlatIndex):
     ix.add_synthetic(O.SEED_CORPUS, 0, 30000, True)
     q = O.synth_rows(O.SEED_QUERIES, 0, 64, 256, True, "f32")
     _check_exact(ix, q, 50, "ip")
+
+
+@pytest.mark.parametrize("metric", ["ip", "l2"])
+@pytest.mark.parametrize("nq,kind", [(63, "gemv"), (64, "mfma"), (256, "mfma")])
+def test_f32_batches_choose_mfma_from_64_queries(FlatIndex, metric, nq, kind):
+    # fp32 native batches: GEMV passes of 8 queries below 64, the fp32 MFMA screen from 64 on (d
+    # not a multiple of the 16-element K-step's chunk: padding), seeded (>= 4 tiles per CU)
+    d, N = 200, 256 * 4 * _num_cu() + 999
+    ix = FlatIndex(d, metric, "f32")
+    ix.add_synthetic(O.SEED_CORPUS, 0, N, True)
+    q = O.synth_rows(O.SEED_QUERIES, 0, nq, d, True, "f32")
+    ix.set_timing(True)
+    _check_exact(ix, q, 25, metric)
+    ix.set_timing(False)
+    assert ix.timing_fetch()[1] == kind
+    ix.close()
 
 
 def test_f32_batch_over_gemv_blocks(FlatIndex):
@@ -232,8 +267,8 @@ def test_optimistic_seed_failure_falls_back_exactly(FlatIndex):
     assert ix.uncertified_count() > 0  # the optimistic pass was rejected (and then redone exactly)
 
 
-@pytest.mark.parametrize("nq", [16, 300])
-def test_device_exact_search_re_searches_uncertified_queries(FlatIndex, nq):
+@pytest.mark.parametrize("nq,dtype", [(16, "bf16"), (300, "bf16"), (64, "f32"), (300, "f32")])
+def test_device_exact_search_re_searches_uncertified_queries(FlatIndex, nq, dtype):
     # the adversarial corpus above through the device API used by the multi-GPU layers: the
     # optimistic pass is rejected on the device and the failed queries are re-searched by the
     # fallback round queued behind it (no host round trip).  nq = 300: two query blocks, only the
@@ -248,9 +283,11 @@ def test_device_exact_search_re_searches_uncertified_queries(FlatIndex, nq):
     rng = np.random.default_rng(11)
     for j in range(cu):  # the sampled tile of workgroup j: the first of its range
         x[(tiles * j // cu) * 256 + 5] = q[j % 16] + 0.01 * rng.standard_normal(d).astype(np.float32)
-    ix = FlatIndex(d, "ip", "bf16")
+    # (fp32 rows: batches of >= 64 queries take the seeded fp32 MFMA screen, and the fallback round
+    # is the fp32 MFMA screen too, also queued without a host sync)
+    ix = FlatIndex(d, "ip", dtype)
     ix.add(x)
-    qb = O.round_dtype(q, "bf16")
+    qb = O.round_dtype(q, dtype)
     qd = torch.from_numpy(qb).cuda()
     S = torch.empty((nq, k), dtype=torch.float64, device="cuda")
     I = torch.empty((nq, k), dtype=torch.int64, device="cuda")
@@ -264,8 +301,9 @@ def test_device_exact_search_re_searches_uncertified_queries(FlatIndex, nq):
     assert ix.unresolved_count() == 0
 
 
+@pytest.mark.parametrize("dtype", ["bf16", "f32"])
 @pytest.mark.parametrize("nq,copies", [(1, 5000), (20, 12000)])
-def test_ties_beyond_max_depth_are_reported(FlatIndex, nq, copies):
+def test_ties_beyond_max_depth_are_reported(FlatIndex, nq, copies, dtype):
     # `copies` identical rows tie with the query's best score: more than any screen depth (KP_MAX =
     # 4096 rows for single queries; the batch refine's 8192 scored rows) can certify that no
     # unlisted copy wins.  vs_search raises VS_ERR_UNCERTIFIED; the device API (no host sync)
@@ -274,11 +312,11 @@ def test_ties_beyond_max_depth_are_reported(FlatIndex, nq, copies):
     from photo_search_engine_amd._lib import VsError
     from photo_search_engine_amd.index import MultiDeviceFlatIndex
     d, k = 64, 10
-    x = O.synth_rows(O.SEED_CORPUS, 0, 25_000, d, True, "bf16")
+    x = O.synth_rows(O.SEED_CORPUS, 0, 25_000, d, True, dtype)
     v = x[123].copy()
     x[np.random.default_rng(3).choice(25_000, copies, replace=False)] = v
     q = np.repeat(v[None], nq, axis=0)
-    ix = FlatIndex(d, "ip", "bf16")
+    ix = FlatIndex(d, "ip", dtype)
     ix.add(x)
     with pytest.raises(VsError) as e:
         ix.search(q, k)
@@ -287,7 +325,7 @@ def test_ties_beyond_max_depth_are_reported(FlatIndex, nq, copies):
     I = torch.empty((nq, k), dtype=torch.int64, device="cuda")
     ix.search_device_exact(qd.data_ptr(), nq, k, None, I.data_ptr(), None, 0, 0)
     assert ix.unresolved_count() == nq
-    m = MultiDeviceFlatIndex(d, "ip", "bf16", devices=[0, 0])
+    m = MultiDeviceFlatIndex(d, "ip", dtype, devices=[0, 0])
     m.add(x)
     with pytest.raises(VsError) as e:
         m.search(q, k)
