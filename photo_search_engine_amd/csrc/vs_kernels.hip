@@ -1410,10 +1410,14 @@ __device__ __forceinline__ void gld16(intx4& v, const void* p) {
 // loop with the corpus dtype's MFMA.  16-bit rows: 32 elements per K-step, the K-step's 64 B of a
 // row being one half of its 128 B line; native keys (fp32 score; L2: 2 score - ||x||^2); a column
 // is tested by the max of its 8 keys.
-template <int DT, int METRIC>
+// MAP: the IVF list scan over pages of a page pool (bf16 / f16), as screen_mfma's MAP form: the
+// workgroup's descriptor (list segment, query tile, qmap slice), its page table in LDS (one lookup
+// per tile), keys carrying storage slots, split (hi, lo) query columns summed in the epilogue.
+template <int DT, int METRIC, bool MAP = false>
 __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
     constexpr bool L2 = METRIC == METRIC_L2;
     constexpr bool I8 = DT == DT_I8;
+    static_assert(!(MAP && I8), "the mapped scan serves bf16 / f16 lists");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint8_t* const sm = smem + I8D_RING;
     u64* thr_key = (u64*)sm;
@@ -1434,8 +1438,25 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int blk = blockIdx.x;
-    const int t0 = (int)((int64_t)a.tiles * blk / a.G);
-    const int t1 = (int)((int64_t)a.tiles * (blk + 1) / a.G);
+    int t0 = (int)((int64_t)a.tiles * blk / a.G);
+    int t1 = (int)((int64_t)a.tiles * (blk + 1) / a.G);
+    int* tmap = (int*)(smem + I8D_LDS);  // MAP: page of logical tile t0 + i (published below)
+    if constexpr (MAP) {
+        const int* dsc = a.wg_desc + (size_t)blk * MAP_DESC;
+        const int tm_off = dsc[0], nt = dsc[1];
+        t0 = dsc[2];
+        t1 = t0 + nt;
+        a.n_valid = dsc[3];
+        qt += (size_t)dsc[4] * MFMA_QB * a.dpad * 2;
+        a.qmap += dsc[5];
+        nqb = dsc[6];
+        for (int i = tid; i < nt; i += MF_THREADS) tmap[i] = a.tile_map[tm_off + i];
+    }
+    const int tbase = t0;
+    auto phys = [&](int t) -> int64_t {  // storage tile of logical tile t
+        if constexpr (MAP) return (int64_t)tmap[t - tbase];
+        else return (int64_t)t;
+    };
     if (tid < 256) {
         const bool real = tid < nqb;
         const u64 k0 = real ? (a.thr0 ? a.thr0[tid] : 0ull) : ~0ull;
@@ -1455,7 +1476,7 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
     __syncthreads();
     const int nks = a.dpad / (I8 ? 64 : CH);
     const int64_t tbytes = (int64_t)TR * a.dpad * (I8 ? 1 : 2);
-    u64* cand = a.cand + (size_t)blk * MFMA_QB * a.cap;
+    u64* cand = a.cand + (size_t)blk * (MAP ? MFMA_QB / 2 : MFMA_QB) * a.cap;
     const int trigger = a.cap - TR;
     const uint32_t ring = lds_addr(smem);
     const uint32_t rowx_lds = lds_addr((const uint8_t*)rowx);
@@ -1480,12 +1501,13 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
     // data first when it is the tile's last K-step, then the query block, then the corpus
     // fragments (dummy steps past the range reload the last tile: same op count every step)
     int iti = t0, iks = 0;
+    int64_t pg = t1 > t0 ? phys(t0) : 0;  // storage tile of iti (MAP: looked up once per tile)
 #define I8D_ISSUE(SET)                                                                                   \
     do {                                                                                                 \
         /* 4 waves cover the tile's 1 KiB of (scale | beta); waves 4-7 load its ||x||^2 (L2) or      \
            rewrite the same bytes (inner product): the same op count for every wave */                 \
         if ((I8 || L2) && iks == nks - 1 && iti < t1)                                                    \
-            glds4(side_src + (int64_t)iti * TR + lane,                                                   \
+            glds4(side_src + pg * TR + lane,                                                             \
                   __builtin_amdgcn_readfirstlane(side_dst + (uint32_t)((iti & 1) * 1024)));              \
         const uint32_t qbase = __builtin_amdgcn_readfirstlane(ring + (uint32_t)((SET) * 16384 + wid * 1024)); \
         _Pragma("unroll") for (int it = 0; it < 2; ++it) {                                               \
@@ -1493,7 +1515,7 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
             const int row = g >> 2, pos = g & 3;                                                         \
             glds16(qt + (int64_t)iks * 16384 + (row << 6) + ((pos ^ mf_swz(row)) << 4), qbase + it * 8192); \
         }                                                                                                \
-        const uint8_t* ab = a.corpus + (int64_t)(iti < t1 ? iti : t1 - 1) * tbytes +                    \
+        const uint8_t* ab = a.corpus + pg * tbytes +                                                     \
                             (I8 ? (int64_t)iks * 16384 : (int64_t)(iks >> 1) * (TR * CHB) + (iks & 1) * 64) + a_off; \
         if (I8 || (iks & 1)) {  /* the line's last read: non-temporal */                                 \
             gld16_nt(A[SET][0], ab);                                                                     \
@@ -1502,7 +1524,11 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
             gld16(A[SET][0], ab);                                                                        \
             gld16(A[SET][1], ab + A2);                                                                   \
         }                                                                                                \
-        if (++iks == nks) { iks = 0; ++iti; }                                                            \
+        if (++iks == nks) {                                                                              \
+            iks = 0;                                                                                     \
+            ++iti;                                                                                       \
+            if (iti < t1) pg = phys(iti); /* (past the range: the last tile again, dummy steps) */       \
+        }                                                                                                \
     } while (0)
 
     if (t1 > t0) {
@@ -1594,7 +1620,8 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
         // time: per-column key code would run for the whole wave).
         int olane;  // asm-opaque lane id: lane-derived indices are not hoisted out of the K loop
         asm volatile("v_mov_b32 %0, %1" : "=v"(olane) : "v"(lane));
-        const int64_t rowbase = (int64_t)ti * TR;
+        const int64_t rowbase = (int64_t)ti * TR;  // logical (the n_valid mask)
+        const int64_t idbase = MAP ? phys(ti) * TR : rowbase;  // key ids (MAP: storage slots)
         const int qlane = olane & 15;  // + 16 n
         const uint32_t* rx = rowx + (ti & 1) * TR;
         // the shard's last tile: rows >= n_valid (garbage side data) never qualify -> no bound test,
@@ -1657,7 +1684,7 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
                     while (mh) {  // compact insert loop: the LDS pool, a direct store when it is full
                         const int j = __builtin_ctz(mh);
                         mh &= mh - 1u;
-                        const u64 key = mk_key(sv[j], (uint32_t)(rowbase + r0 + (j >> 2) * 16 + (j & 3)));
+                        const u64 key = mk_key(sv[j], (uint32_t)(idbase + r0 + (j >> 2) * 16 + (j & 3)));
                         if (key <= tk) continue;  // score == threshold and not ahead of it by id
                         const int ps = atomicAdd(&flag[1], 1);
                         if (ps < MF_POOL) {
@@ -1672,10 +1699,22 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
             }
             __builtin_amdgcn_wave_barrier();
         };
-        // the bound test of all 16 columns first (straight-line VALU, one bit per column)
+        // MAP: query p = columns 2p (hi) + 2p + 1 (lo): their fp32 sums, in place of the hi column
+        // (p = 0..7: the 128 queries of the split tile; columns 8..15 then hold nothing used)
+        constexpr int NCOL = MAP ? 8 : 16;
+        if constexpr (MAP) {
+#pragma unroll
+            for (int p = 0; p < 8; ++p)
+#pragma unroll
+                for (int m = 0; m < 2; ++m)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        acc[m][p][r] = __float_as_int(__int_as_float(acc[m][2 * p][r]) + __int_as_float(acc[m][2 * p + 1][r]));
+        }
+        // the bound test of all columns first (straight-line VALU, one bit per column)
         uint32_t gomask = 0;
 #pragma unroll
-        for (int n = 0; n < 16; ++n) {
+        for (int n = 0; n < NCOL; ++n) {
             // bound of the column's 8 keys: max acc (exact int) -> fp32, times the rows' largest
             // (acc >= 0) or smallest (acc < 0) scale, plus the largest error norm; each step is
             // monotone, so a key that would pass implies a bound that passes
@@ -1695,10 +1734,10 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
             if constexpr (L2) b = __builtin_fmaf(2.0f, b, -sqmin);  // (monotone: >= every row's key)
             gomask |= (b >= f.z ? 1u : 0u) << n;
         }
-        if (edge) gomask = 0xFFFFu;
+        if (edge) gomask = (1u << NCOL) - 1u;
         int nrec = 0;  // wave-uniform
 #pragma unroll
-        for (int n = 0; n < 16; ++n) {
+        for (int n = 0; n < NCOL; ++n) {
             const bool go = (gomask >> n) & 1u;
             const u64 bal = __ballot(go);
             if (bal == 0ull) continue;
@@ -1741,7 +1780,7 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
             if (lane == 0) cnt[q] = a.Kp;  // (read back by this wave's flush: LDS order within a wave)
         }
     }
-    mf_flush_wave<false>(a, cand, cnt, nqb, wid, lane);
+    mf_flush_wave<MAP>(a, cand, cnt, nqb, wid, lane);
 }
 
 template <int METRIC>
@@ -1752,6 +1791,12 @@ template <int DT, int METRIC>
 __global__ void __launch_bounds__(512, 2) k_screen_d16(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
     screen_direct<DT, METRIC>(a, qt, nqb);
 }
+template <int DT, int METRIC>
+__global__ void __launch_bounds__(512, 2) k_screen_d16_mapped(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
+    screen_direct<DT, METRIC, true>(a, qt, nqb);
+}
+constexpr int I8D_LDS_MAP = I8D_LDS + MFMA_MAP_TILES * 4;  // + the workgroup's page table
+static_assert(I8D_LDS_MAP <= 160 * 1024, "LDS budget (direct mapped screen)");
 // d16: K-steps of 32 elements per tile a multiple of 4 (and >= 8)
 bool d16_direct_ok(int dpad) { return dpad % (CH * I8D_U) == 0 && dpad >= 2 * CH * I8D_U; }
 
@@ -3345,6 +3390,11 @@ hipError_t launch_screen_mfma(int dt, const ScreenArgs& a, const uint8_t* qt, in
 
 template <int DT, int METRIC>
 static void launch_mapped_one(const ScreenArgs& a, const uint8_t* qt, hipStream_t st) {
+    if (d16_direct_ok(a.dpad)) {  // the direct form (corpus fragments HBM -> VGPRs)
+        set_lds_attr((const void*)k_screen_d16_mapped<DT, METRIC>, I8D_LDS_MAP);
+        hipLaunchKernelGGL((k_screen_d16_mapped<DT, METRIC>), dim3(a.G), dim3(MF_THREADS), I8D_LDS_MAP, st, a, qt, 0);
+        return;
+    }
     set_lds_attr((const void*)k_screen_mfma_mapped<DT, METRIC>, MF_LDS_MAP);
     hipLaunchKernelGGL((k_screen_mfma_mapped<DT, METRIC>), dim3(a.G), dim3(MF_THREADS), MF_LDS_MAP, st, a, qt, 0);
 }
