@@ -1387,9 +1387,16 @@ __device__ __forceinline__ void i8d_wait_barrier(intx4& a0, intx4& a1) {
 }
 
 // one K-step of the direct screen (the asm bodies of vs_i8_asm.h, chosen at compile time)
-template <int DT, bool FIRST>
+template <int DT, bool FIRST, int NG = 16>
 __device__ __forceinline__ void d_step(intx4 (&acc)[2][16], intx4 (&bt)[4], uint32_t slot_lds, intx4& A0, intx4& A1) {
-    if constexpr (DT == DT_I8) {
+    if constexpr (NG == 4 && DT == DT_BF16) {  // narrow query tiles (4 column groups)
+        if constexpr (FIRST) BFD_STEP0_N4(A0, A1);
+        else BFD_STEP_N4(A0, A1);
+    } else if constexpr (NG == 4) {
+        static_assert(DT == DT_F16, "narrow tiles: bf16 / f16");
+        if constexpr (FIRST) HFD_STEP0_N4(A0, A1);
+        else HFD_STEP_N4(A0, A1);
+    } else if constexpr (DT == DT_I8) {
         if constexpr (FIRST) I8D_STEP0(A0, A1);
         else I8D_STEP(A0, A1);
     } else if constexpr (DT == DT_BF16) {
@@ -1413,11 +1420,15 @@ __device__ __forceinline__ void gld16(intx4& v, const void* p) {
 // MAP: the IVF list scan over pages of a page pool (bf16 / f16), as screen_mfma's MAP form: the
 // workgroup's descriptor (list segment, query tile, qmap slice), its page table in LDS (one lookup
 // per tile), keys carrying storage slots, split (hi, lo) query columns summed in the epilogue.
-template <int DT, int METRIC, bool MAP = false>
+// NG: query column groups of 16 (16 = the 256-column tile; 4 = a narrow tile of 64 columns for
+// mapped scans of lists probed by <= 32 queries: a quarter of the MFMAs, and the query DMAs read
+// only the tile's first 64 rows, so the L2 holds a quarter of each tile)
+template <int DT, int METRIC, bool MAP = false, int NG = 16>
 __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
     constexpr bool L2 = METRIC == METRIC_L2;
     constexpr bool I8 = DT == DT_I8;
     static_assert(!(MAP && I8), "the mapped scan serves bf16 / f16 lists");
+    static_assert(NG == 16 || (NG == 4 && MAP), "narrow query tiles: mapped scans only");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint8_t* const sm = smem + I8D_RING;
     u64* thr_key = (u64*)sm;
@@ -1513,7 +1524,8 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
         _Pragma("unroll") for (int it = 0; it < 2; ++it) {                                               \
             const int g = it * 512 + wid * 64 + lane;                                                    \
             const int row = g >> 2, pos = g & 3;                                                         \
-            glds16(qt + (int64_t)iks * 16384 + (row << 6) + ((pos ^ mf_swz(row)) << 4), qbase + it * 8192); \
+            const int qrow = row & (NG * 16 - 1); /* (narrow tiles: rows >= 64 replaced by copies) */    \
+            glds16(qt + (int64_t)iks * 16384 + (qrow << 6) + ((pos ^ mf_swz(qrow)) << 4), qbase + it * 8192); \
         }                                                                                                \
         const uint8_t* ab = a.corpus + pg * tbytes +                                                     \
                             (I8 ? (int64_t)iks * 16384 : (int64_t)(iks >> 1) * (TR * CHB) + (iks & 1) * 64) + a_off; \
@@ -1545,7 +1557,7 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
         i8d_wait_barrier(A[U_][0], A[U_][1]);                                        \
         I8D_ISSUE(((U_) + I8D_P) & 3);                                               \
         const uint32_t slot_lds = ring + (uint32_t)((U_) * 16384) + lane_off;        \
-        d_step<DT, STEP_>(acc, bt, slot_lds, A[U_][0], A[U_][1]);                    \
+        d_step<DT, STEP_, NG>(acc, bt, slot_lds, A[U_][0], A[U_][1]);                \
     } while (0)
     for (int ti = t0; ti < t1; ++ti) {
         // K-steps 0..3: the first writes the accumulators; the deferred compaction check of the
@@ -1600,7 +1612,7 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
         }
         {
             const uint32_t slot_lds = ring + lane_off;
-            d_step<DT, true>(acc, bt, slot_lds, A[0][0], A[0][1]);
+            d_step<DT, true, NG>(acc, bt, slot_lds, A[0][0], A[0][1]);
         }
         I8D_BODY(1, false);
         I8D_BODY(2, false);
@@ -1701,10 +1713,10 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
         };
         // MAP: query p = columns 2p (hi) + 2p + 1 (lo): their fp32 sums, in place of the hi column
         // (p = 0..7: the 128 queries of the split tile; columns 8..15 then hold nothing used)
-        constexpr int NCOL = MAP ? 8 : 16;
+        constexpr int NCOL = MAP ? NG / 2 : NG;
         if constexpr (MAP) {
 #pragma unroll
-            for (int p = 0; p < 8; ++p)
+            for (int p = 0; p < NG / 2; ++p)
 #pragma unroll
                 for (int m = 0; m < 2; ++m)
 #pragma unroll
@@ -1791,9 +1803,14 @@ template <int DT, int METRIC>
 __global__ void __launch_bounds__(512, 2) k_screen_d16(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
     screen_direct<DT, METRIC>(a, qt, nqb);
 }
+// One launch for every list scan: a workgroup whose query tile holds <= 32 queries runs the narrow
+// form (64 columns = 32 queries x (hi, lo): a quarter of the MFMAs, a quarter of the tile's L2
+// footprint), the others the full 256-column form (two separately allocated code paths; the
+// choice is per workgroup, outside either K loop).
 template <int DT, int METRIC>
 __global__ void __launch_bounds__(512, 2) k_screen_d16_mapped(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
-    screen_direct<DT, METRIC, true>(a, qt, nqb);
+    if (a.wg_desc[(size_t)blockIdx.x * MAP_DESC + 6] <= 32) screen_direct<DT, METRIC, true, 4>(a, qt, nqb);
+    else screen_direct<DT, METRIC, true, 16>(a, qt, nqb);
 }
 constexpr int I8D_LDS_MAP = I8D_LDS + MFMA_MAP_TILES * 4;  // + the workgroup's page table
 static_assert(I8D_LDS_MAP <= 160 * 1024, "LDS budget (direct mapped screen)");
@@ -3390,7 +3407,7 @@ hipError_t launch_screen_mfma(int dt, const ScreenArgs& a, const uint8_t* qt, in
 
 template <int DT, int METRIC>
 static void launch_mapped_one(const ScreenArgs& a, const uint8_t* qt, hipStream_t st) {
-    if (d16_direct_ok(a.dpad)) {  // the direct form (corpus fragments HBM -> VGPRs)
+    if (d16_direct_ok(a.dpad)) {  // the direct form (corpus fragments HBM -> VGPRs; narrow tiles inside)
         set_lds_attr((const void*)k_screen_d16_mapped<DT, METRIC>, I8D_LDS_MAP);
         hipLaunchKernelGGL((k_screen_d16_mapped<DT, METRIC>), dim3(a.G), dim3(MF_THREADS), I8D_LDS_MAP, st, a, qt, 0);
         return;

@@ -56,6 +56,10 @@ def main() -> int:
         for metric, mcode in (("ip", 0), ("l2", 1)):
             rc |= check(asm, f"{dt}/{metric}", f"_ZN2vs12k_screen_d16ILi{dcode}ELi{mcode}EEEvNS_10ScreenArgsEPKhi:",
                         name="k_screen_d16", any_policy=True)
+            # the IVF list scan form (page table; wide and narrow query tiles in one kernel)
+            rc |= check(asm, f"{dt}/{metric}", f"_ZN2vs19k_screen_d16_mappedILi{dcode}ELi{mcode}EEEvNS_10ScreenArgsEPKhi:",
+                        name="k_screen_d16_mapped", any_policy=True)
+
     return rc
 
 
@@ -81,9 +85,17 @@ def check(asm: str, metric: str, sym: str, name: str = "k_screen_i8d", any_polic
         return op, regs(ops[0]), set().union(*[regs(o) for o in ops[1:]]) if len(ops) > 1 else set()
     parsed = [split(l) for l in code]
     loaded = set()
+    # (corpus loads come after the first barrier; a mapped scan's descriptor load before it is an
+    # ordinary compiler-waited load)
+    first_bar = next((i for i, l in enumerate(code) if l.strip().startswith("s_barrier")), 0)
     for i, l in enumerate(code):
         op, dst, _ = parsed[i]
-        if not (op == "global_load_dwordx4" and (any_policy or l.split(";")[0].rstrip().endswith("nt"))):
+        if i < first_bar:
+            continue
+        ins = l.split(";")[0].rstrip()
+        # (the corpus loads are the inline-asm ones: 64-bit VGPR address, "off"; the compiler's own
+        # loads of descriptors use the SGPR-base form and are waited for by the compiler)
+        if not (op == "global_load_dwordx4" and ", off" in ins and (any_policy or ins.endswith("nt"))):
             continue
         loaded |= dst
         for j in range(i + 1, len(code)):
