@@ -802,6 +802,34 @@ void vs::search_exact_device(vs_index* ix, const float* q_dev, int64_t nq, int k
     }
 }
 
+// S concurrent exact device searches over consecutive parts (whole query blocks) of one batch, each
+// on its own stream with its own leased workspace (leases held together, so no two parts share a
+// workspace and serialise on it); a part's unresolved queries count in unres[part].  The IVF
+// coarse assignment: one 256-row block of a small quantizer fills only nlist / 256 workgroups.
+void vs::search_exact_device_parts(vs_index* ix, const float* q_dev, int64_t nq, int k, int64_t* I_dev,
+                                   hipStream_t* streams, int S, unsigned* unres) {
+    check_index(ix);
+    if (nq <= 0) return;
+    std::shared_lock<std::shared_mutex> lk(ix->rw);
+    DeviceGuard dg(ix->device);
+    if (k <= 0) throw VsError(VS_ERR_ARG, "k must be > 0");
+    std::vector<std::unique_ptr<CtxLease>> leases;
+    for (int i = 0; i < S; ++i) leases.emplace_back(new CtxLease(ix, streams[i], false));
+    const int Kp = screen_depth(k);
+    const int64_t blocks = (nq + MFMA_QB - 1) / MFMA_QB;
+    for (int i = 0; i < S; ++i) {
+        const int64_t q0 = std::min(nq, blocks * i / S * MFMA_QB), q1 = std::min(nq, blocks * (i + 1) / S * MFMA_QB);
+        if (q1 <= q0) continue;
+        Ctx* c = leases[i]->c;
+        c->outD.ensure((size_t)(q1 - q0) * k * sizeof(float));
+        c->cert.ensure((size_t)(q1 - q0) * sizeof(int));
+        c->unres = unres + i;
+        search_all(ix, c, q_dev + q0 * ix->d, q1 - q0, k, Kp, c->outD.as<float>(), I_dev + q0 * k, nullptr,
+                   c->cert.as<int>(), 0, streams[i], kOptimisticSeedRank, true);
+        c->unres = nullptr;
+    }
+}
+
 unsigned* vs::unresolved_counter(vs_index* ix) { return ix->d_unres; }
 
 // ---- two-phase exact device search (the sharded step with a global T' exchange) ----

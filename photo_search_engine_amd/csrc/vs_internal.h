@@ -388,6 +388,10 @@ void search_exact_device(vs_index* ix, const float* q_dev, int64_t nq, int k, in
 // the shards that took their rows); the running maxima stay (they only widen certificate margins)
 void truncate_rows(vs_index* ix, int64_t n);
 unsigned* unresolved_counter(vs_index* ix);  // device word behind vs_unresolved_count
+// S concurrent exact device searches over parts of one batch (own streams and workspaces;
+// unres[i] counts part i's unresolved queries)
+void search_exact_device_parts(vs_index* ix, const float* q_dev, int64_t nq, int k, int64_t* I_dev,
+                               hipStream_t* streams, int S, unsigned* unres);
 // two-phase exact device search (vs_search_device_phase_a / _b)
 bool two_phase_ok(const vs_index* ix, int64_t nq, int k);
 vs_pending* search_phase_a(vs_index* ix, const float* q_dev, int64_t nq, int k, int world, int64_t id_offset,
