@@ -117,8 +117,10 @@ struct vs_index {
     // Screen health (first passes of MFMA batches): the certificate-failure count of a batch is read
     // back without a host wait (pinned word + event, observed by a later search).  A failed query
     // costs its block a full fallback round, so the index adapts to its corpus:
-    //  * an int8 batch with failures routes the next kI8RouteBatches searches to the native screen
-    //    (score distributions denser than the int8 error window, e.g. tight clusters);
+    //  * an int8 batch with failures doubles the int8 union (the rows listed above the seed), up
+    //    to 2^kI8ScaleMax; one failing at that depth routes the next kI8RouteBatches searches to
+    //    the native screen (score distributions denser than the int8 error window, e.g. tight
+    //    clusters); kSeedRelax clean int8 batches halve the depth again;
     //  * a native batch in which more than 1/64 of the queries failed doubles the optimistic seed's
     //    depth (rows listed ahead of the refine), up to 2^kSeedScaleMax; kSeedRelax clean batches
     //    halve it again.
@@ -129,6 +131,7 @@ struct vs_index {
     int h_nq = 0;               // queries of that batch
     int i8_route = 0;           // searches still routed to the native screen
     int seed_log2 = 0, seed_clean = 0;
+    int i8_log2 = 0, i8_clean = 0;  // int8 union depth: 2^i8_log2 times the target (dense corpora)
 };
 
 vs::FlatView vs::flat_view(vs_index* ix) {
@@ -282,13 +285,24 @@ constexpr int kF32MfmaMinQ = 64;     // fp32 native batches: MFMA screen from th
 constexpr int kI8RouteBatches = 64;  // searches routed to the native screen after a failing int8 batch
 constexpr int kSeedScaleMax = 6;     // native optimistic seed: at most 64x the default depth
 constexpr int kSeedRelax = 64;       // clean native batches before the depth is halved again
+constexpr int kI8ScaleMax = 4;       // int8 union: at most 16x its target before routing to native
 
 // observe a completed failure-count readback (caller holds h_mu)
 void health_poll(vs_index* ix) {
     if (ix->h_pending && hipEventQuery(ix->h_ev) == hipSuccess) {
         const unsigned f = *ix->h_fails;
         if (ix->h_pending == 1) {
-            if (f > 0) ix->i8_route = kI8RouteBatches;
+            // an int8 batch with failures: a deeper union first (dense score distributions put
+            // more rows inside the int8 error window), the native screen when even the deepest
+            // union failed; clean batches relax the depth again
+            if (f > 0) {
+                if (ix->i8_log2 < kI8ScaleMax) ++ix->i8_log2;
+                else ix->i8_route = kI8RouteBatches;
+                ix->i8_clean = 0;
+            } else if (ix->i8_log2 > 0 && ++ix->i8_clean >= kSeedRelax) {
+                --ix->i8_log2;
+                ix->i8_clean = 0;
+            }
         } else if (f > (unsigned)(ix->h_nq / 64)) {  // (a stray hard query does not deepen every batch)
             ix->seed_log2 = std::min(ix->seed_log2 + 1, kSeedScaleMax);
             ix->seed_clean = 0;
@@ -418,7 +432,11 @@ void search_block_i8(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float
         sa.seedmax = c->seedmax.as<float>();
         HIP_CHECK(launch_seed_mfma(DT_I8, sa, c->qtile.as<uint8_t>(), nqb, st));
         c->thr0.ensure(sizeof(u64) * MFMA_QB);
-        const double target = i8_union_target(k, (double)sa.G * TR, (double)ix->ntotal);
+        double target = i8_union_target(k, (double)sa.G * TR, (double)ix->ntotal);
+        {
+            std::lock_guard<std::mutex> g(ix->h_mu);
+            target *= (double)(1 << ix->i8_log2);
+        }
         const double r = std::ceil(target * (double)sa.G * TR / (double)ix->ntotal);
         const int rank = (int)std::min<double>(std::max<double>(r, (double)kOptimisticMinRank), (double)M);
         HIP_CHECK(launch_seed_select(sa.seedmax, M, nqb, rank, c->thr0.as<u64>(), st));
