@@ -1449,8 +1449,12 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int blk = blockIdx.x;
-    int t0 = (int)((int64_t)a.tiles * blk / a.G);
-    int t1 = (int)((int64_t)a.tiles * (blk + 1) / a.G);
+    // The loop runs over j in [t0, t1).  Flat shards: workgroup blk takes tiles blk, blk + G, ...
+    // (interleaved, so a corpus inserted cluster by cluster spreads every cluster over all the
+    // workgroups instead of packing a query's whole top-k and its window into one workgroup's
+    // 512-key lists); MAP: j is the list's logical tile, its page from the page table.
+    int t0 = 0;
+    int t1 = a.tiles > blk ? (a.tiles - blk + a.G - 1) / a.G : 0;
     int* tmap = (int*)(smem + I8D_LDS);  // MAP: page of logical tile t0 + i (published below)
     if constexpr (MAP) {
         const int* dsc = a.wg_desc + (size_t)blk * MAP_DESC;
@@ -1464,9 +1468,13 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
         for (int i = tid; i < nt; i += MF_THREADS) tmap[i] = a.tile_map[tm_off + i];
     }
     const int tbase = t0;
-    auto phys = [&](int t) -> int64_t {  // storage tile of logical tile t
+    auto phys = [&](int t) -> int64_t {  // storage tile of loop index t
         if constexpr (MAP) return (int64_t)tmap[t - tbase];
-        else return (int64_t)t;
+        else return (int64_t)blk + (int64_t)t * a.G;
+    };
+    auto ltile = [&](int t) -> int64_t {  // logical tile of loop index t (its rows: the n_valid mask)
+        if constexpr (MAP) return (int64_t)t;
+        else return (int64_t)blk + (int64_t)t * a.G;
     };
     if (tid < 256) {
         const bool real = tid < nqb;
@@ -1632,7 +1640,7 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
         // time: per-column key code would run for the whole wave).
         int olane;  // asm-opaque lane id: lane-derived indices are not hoisted out of the K loop
         asm volatile("v_mov_b32 %0, %1" : "=v"(olane) : "v"(lane));
-        const int64_t rowbase = (int64_t)ti * TR;  // logical (the n_valid mask)
+        const int64_t rowbase = ltile(ti) * TR;  // logical (the n_valid mask)
         const int64_t idbase = MAP ? phys(ti) * TR : rowbase;  // key ids (MAP: storage slots)
         const int qlane = olane & 15;  // + 16 n
         const uint32_t* rx = rowx + (ti & 1) * TR;

@@ -1,3 +1,4 @@
+"""fp32 rows: batch timing of the native (fp32 MFMA) and int8 screens at 1M x 1536 (profiles/r03_f32_mfma_timing.txt)."""
 import time, torch, numpy as np
 import os, sys; sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 from oracle import oracle as O
