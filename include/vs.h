@@ -278,6 +278,17 @@ int vs_hnsw_search(vs_hnsw* graph, const float* q, int64_t nq, int32_t k, int32_
                    int64_t* I);
 int64_t vs_hnsw_ntotal(const vs_hnsw* graph);
 
+/* HNSW graph build: faiss HNSW::shrink_neighbor_list (the neighbour-selection heuristic
+ * IndexHNSWFlat.add applies to a new node's candidates and to a full list receiving a reverse link,
+ * utils/vector_store.py:164) for m nodes at once on the GPU.  nodes[i] = row id of node i;
+ * cand[i * C ..] = its distinct candidate row ids, -1 padded at the end; with fewer than W
+ * candidates all are kept (faiss returns early below max_size), else candidates are taken in
+ * ascending (distance, id) order and one is kept unless an already kept neighbour is strictly closer
+ * to it than the node is, up to W.  Distances are the flat path's canonical fp64 scores (IP: -score).
+ * out[i * W ..] = kept ids best first, -1 padded.  C <= 2048, W <= 1024; ids are validated. */
+int vs_hnsw_prune(vs_index* index, int64_t m, const int64_t* nodes, const int32_t* cand, int32_t C, int32_t W,
+                  int32_t* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -328,3 +328,95 @@ def has_exact_ties(x_stored, q, metric="ip") -> bool:
     """True if some query is at exactly equal distance from two distinct rows."""
     Dm = _distances(x_stored, np.atleast_2d(np.asarray(q, dtype=np.float32)), metric)
     return any(len(np.unique(r)) != len(r) for r in Dm)
+
+
+# ---------------------------------------------------------------------------------------------
+# graph build: faiss's neighbour-selection heuristic
+# ---------------------------------------------------------------------------------------------
+def shrink_neighbor_list(dist, node: int, cand, W: int):
+    """faiss ``HNSW::shrink_neighbor_list`` (faiss/impl/HNSW.cpp; reached from ``add_links_starting_
+    from`` and ``add_link`` through the static overload that returns early when fewer than
+    ``max_size`` candidates are offered): candidates in ascending (distance to ``node``, id) order,
+    one kept unless an already kept neighbour is strictly closer to it than ``node`` is, stopping
+    at ``W`` kept.  ``dist[a, b]`` = distance with ``a`` as the query and ``b`` as the row (the
+    flat path's canonical fp64 value; IP: -score).  faiss orders equal distances by its heap; the
+    (distance, id) order here is what the HIP kernel (k_hnsw_prune) implements."""
+    cand = [int(c) for c in cand if c >= 0]
+    if len(cand) < W:
+        return sorted(cand, key=lambda c: (dist[node, c], c))
+    order = sorted(cand, key=lambda c: (dist[node, c], c))
+    kept = []
+    for c in order:
+        dq = dist[node, c]
+        if all(not (dist[c, r] < dq) for r in kept):
+            kept.append(c)
+            if len(kept) >= W:
+                break
+    return kept
+
+
+HP_C_MAX = 2048  # largest candidate list of one node (include/vs.h vs_hnsw_prune)
+
+
+def select_level(dist, members, cand_lists, W: int, cmax: int = HP_C_MAX):
+    """One level of the batch build (photo_search_engine_amd/hnsw.py ``select_level``): every member's
+    forward list = shrink(its candidates, W) (faiss, on inserting a node: shrink its efConstruction
+    candidates to the level's width); then every member j receives the reverse links i -> j and
+    keeps its forward list followed by the new sources in ascending id, unpruned while that fits W
+    (faiss ``add_link`` appends while a list has room), else shrunk to W over the union (faiss
+    ``add_link`` on a full list); a union longer than ``cmax`` is cut there first."""
+    members = [int(v) for v in members]
+    F = {v: shrink_neighbor_list(dist, v, cand_lists[i], W) for i, v in enumerate(members)}
+    R = {v: [] for v in members}
+    for i in members:
+        for j in F[i]:
+            R[j].append(i)
+    out = {}
+    for j in members:
+        fs = set(F[j])
+        U = (F[j] + [i for i in R[j] if i not in fs])[:cmax]
+        out[j] = U if len(U) <= W else shrink_neighbor_list(dist, j, U, W)
+    return out
+
+
+def heuristic_graph(x_stored, M: int, ef_construction: int, metric="ip", levels=None, seed: int = 12345) -> dict:
+    """The graph ``VectorStore._build_graph`` writes, restated: node levels as it draws them
+    (numpy's generator, ``seed``; or ``levels``, 1-based), and on every level each
+    member's candidates are its exact max(efConstruction, width) nearest members (itself excluded,
+    ties -> lower id), then :func:`select_level`.  Entry point: the first node of the top level."""
+    x = np.asarray(x_stored, dtype=np.float32)
+    n = x.shape[0]
+    probas, cum = _default_probas(M)
+    if levels is None:
+        f = np.random.default_rng(seed).random(n)
+        lev = np.full(n, len(probas) - 1, dtype=np.int64)
+        open_ = np.ones(n, dtype=bool)
+        for level, p in enumerate(probas):
+            hit = open_ & (f < p)
+            lev[hit] = level
+            open_ &= ~hit
+            f[open_] -= p
+    else:
+        lev = np.asarray(levels, dtype=np.int64) - 1
+    dist = _distances(x, x, metric)
+    offsets = np.zeros(n + 1, dtype=np.uint64)
+    offsets[1:] = np.cumsum(cum[lev + 1].astype(np.uint64))
+    nb = np.full(int(offsets[-1]), -1, dtype=np.int32)
+    top = int(lev.max()) if n else -1
+    for level in range(top + 1):
+        members = np.nonzero(lev >= level)[0]
+        width = int(cum[level + 1] - cum[level])
+        C = min(max(ef_construction, width), members.shape[0] - 1, HP_C_MAX)
+        cands = []
+        for i in members:
+            others = members[members != i]
+            order = np.lexsort((others, dist[i, others]))[:C]
+            cands.append(others[order])
+        sel = select_level(dist, members, cands, width)
+        for i in members:
+            base = int(offsets[i]) + int(cum[level])
+            row = sel[int(i)]
+            nb[base:base + len(row)] = row
+    return {"assign_probas": probas, "cum_nneighbor_per_level": cum, "levels": (lev + 1).astype(np.int32),
+            "offsets": offsets, "neighbors": nb, "entry_point": int(np.nonzero(lev == top)[0][0]) if n else -1,
+            "max_level": top, "efConstruction": int(ef_construction), "efSearch": 16, "upper_beam": 1}

@@ -129,6 +129,7 @@ _SIGS = {
     "vs_hnsw_destroy": (None, [_vp]),
     "vs_hnsw_search": (ctypes.c_int, [_vp, _vp, _c_i64, ctypes.c_int32, ctypes.c_int32, _vp, _vp]),
     "vs_hnsw_ntotal": (_c_i64, [_vp]),
+    "vs_hnsw_prune": (ctypes.c_int, [_vp, _c_i64, _vp, _vp, ctypes.c_int32, ctypes.c_int32, _vp]),
 }
 
 

@@ -5,6 +5,8 @@
 // flat vs_index on that index's device; vs_hnsw_search runs k_hnsw_search (vs_kernels.hip: faiss
 // HNSW::search with the flat path's exact canonical distances, one workgroup per query) in chunks
 // of queries, each with its own zeroed visited bitmap.  Results equal oracle/hnsw_oracle.py.
+// vs_hnsw_prune runs k_hnsw_prune (faiss HNSW::shrink_neighbor_list, the graph build's neighbour
+// selection) for a batch of nodes.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -190,6 +192,69 @@ int vs_hnsw_search(vs_hnsw* h, const float* q, int64_t nq, int32_t k, int32_t ef
             HIP_CHECK(hipMemcpyAsync(I + q0 * k, h->outI.p, (size_t)(m * k * 8), hipMemcpyDeviceToHost, h->st));
             HIP_CHECK(hipStreamSynchronize(h->st));
         }
+    });
+}
+
+int vs_hnsw_prune(vs_index* index, int64_t m, const int64_t* nodes, const int32_t* cand, int32_t C, int32_t W,
+                  int32_t* out) {
+    return guarded([&] {
+        if (!index || m < 0 || C < 1 || W < 1 || (m > 0 && (!nodes || !cand || !out)))
+            throw VsError(VS_ERR_ARG, "vs_hnsw_prune: bad arguments");
+        if (C > HP_C_MAX || W > HN_NB_MAX)
+            throw VsError(VS_ERR_ARG, "vs_hnsw_prune: C <= " + std::to_string(HP_C_MAX) + " and W <= " +
+                                          std::to_string(HN_NB_MAX));
+        if (m == 0) return;
+        std::shared_lock<std::shared_mutex> rl(flat_lock(index));
+        const FlatView fv = flat_view(index);
+        if (hnsw_prune_lds_bytes(fv.d, C, W) > 160 * 1024 - 512)
+            throw VsError(VS_ERR_ARG, "vs_hnsw_prune: d / C too large for one workgroup's LDS");
+        // every id is checked here: the kernel gathers rows by them
+        for (int64_t i = 0; i < m; ++i) {
+            if (nodes[i] < 0 || nodes[i] >= fv.ntotal) throw VsError(VS_ERR_ARG, "vs_hnsw_prune: node id out of range");
+            const int32_t* c = cand + i * C;
+            bool pad = false;
+            for (int j = 0; j < C; ++j) {
+                if (c[j] < 0) pad = true;
+                else if (pad || c[j] >= fv.ntotal)
+                    throw VsError(VS_ERR_ARG, "vs_hnsw_prune: candidate ids in range, -1 padding only at the end");
+            }
+        }
+        DeviceGuard g(fv.device);
+        hipStream_t st = nullptr;
+        HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        DevBuf dn, dc, dout;
+        try {
+            const int64_t chunk = std::min<int64_t>(m, std::max<int64_t>(1, (int64_t)(256u << 20) / ((int64_t)C * 4)));
+            dn.ensure((size_t)chunk * 8);
+            dc.ensure((size_t)chunk * C * 4);
+            dout.ensure((size_t)chunk * W * 4);
+            HnswPruneArgs a{};
+            a.corpus = fv.data;
+            a.d = fv.d;
+            a.dpad = fv.dpad;
+            a.dt = fv.dtype;
+            a.metric = fv.metric;
+            a.nodes = dn.as<int64_t>();
+            a.cand = dc.as<int>();
+            a.C = C;
+            a.W = W;
+            a.out = dout.as<int>();
+            for (int64_t i0 = 0; i0 < m; i0 += chunk) {
+                const int64_t mm = std::min(chunk, m - i0);
+                HIP_CHECK(hipMemcpyAsync(dn.p, nodes + i0, (size_t)mm * 8, hipMemcpyHostToDevice, st));
+                HIP_CHECK(hipMemcpyAsync(dc.p, cand + i0 * C, (size_t)mm * C * 4, hipMemcpyHostToDevice, st));
+                HIP_CHECK(launch_hnsw_prune(a, (int)mm, st));
+                HIP_CHECK(hipMemcpyAsync(out + i0 * W, dout.p, (size_t)mm * W * 4, hipMemcpyDeviceToHost, st));
+                HIP_CHECK(hipStreamSynchronize(st));
+            }
+        } catch (...) {
+            (void)hipStreamSynchronize(st);
+            for (DevBuf* b : {&dn, &dc, &dout}) b->release();
+            (void)hipStreamDestroy(st);
+            throw;
+        }
+        for (DevBuf* b : {&dn, &dc, &dout}) b->release();
+        HIP_CHECK(hipStreamDestroy(st));
     });
 }
 

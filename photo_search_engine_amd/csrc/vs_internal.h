@@ -434,4 +434,17 @@ struct HnswArgs {
 size_t hnsw_lds_bytes(int d, int k, int ef, int nbmax);  // dynamic LDS of one search workgroup
 hipError_t launch_hnsw_search(const HnswArgs& a, int nq, hipStream_t st);
 
+// faiss HNSW::shrink_neighbor_list per node (graph build): one workgroup per node
+constexpr int HP_C_MAX = 2048;  // largest candidate list of one node
+struct HnswPruneArgs {
+    const uint8_t* corpus;  // flat index rows (tiled layout)
+    int d, dpad, dt, metric;
+    const int64_t* nodes;   // [m] row ids
+    const int* cand;        // [m][C] distinct candidate row ids, -1 padded at the end
+    int C, W;               // candidates per node, neighbours kept
+    int* out;               // [m][W] kept ids best first, -1 padded
+};
+size_t hnsw_prune_lds_bytes(int d, int C, int W);
+hipError_t launch_hnsw_prune(const HnswPruneArgs& a, int m, hipStream_t st);
+
 }  // namespace vs

@@ -4001,4 +4001,160 @@ hipError_t launch_hnsw_search(const HnswArgs& a, int nq, hipStream_t st) {
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------------------------------------------
+// K8: HNSW neighbour selection (graph build; host side vs_hnsw.hip vs_hnsw_prune) -- faiss
+// HNSW::shrink_neighbor_list restated (oracle/hnsw_oracle.py shrink_neighbor_list): a node's
+// candidates in ascending (distance, id) order; a candidate is kept unless some already kept
+// neighbour is strictly closer to it than the node is; stop at W kept.  Fewer than W candidates are
+// kept whole (faiss returns early below max_size).  One 256-thread workgroup per node; distances
+// are exact_score_rows' canonical fp64 scores (IP: -score) with the node's, then each tested
+// candidate's, stored row staged in LDS as the query, so decisions equal the oracle's bit for bit.
+// ------------------------------------------------------------------------------------------------
+__host__ __device__ inline size_t hp_layout(int d, int C, int W, uint8_t* base, double** qs, double** cd, int** ci,
+                                            double** sd, int** si, int** kept) {
+    const size_t sz[6] = {(size_t)((d + 7) >> 3) * 64, (size_t)C * 8, (size_t)C * 4, (size_t)C * 8, (size_t)C * 4,
+                          (size_t)W * 4};
+    uint8_t* p[6];
+    size_t off = 0;
+    for (int i = 0; i < 6; ++i) {
+        p[i] = base + off;
+        off += (sz[i] + 15) & ~(size_t)15;
+    }
+    if (base) {
+        *qs = (double*)p[0];
+        *cd = (double*)p[1];
+        *ci = (int*)p[2];
+        *sd = (double*)p[3];
+        *si = (int*)p[4];
+        *kept = (int*)p[5];
+    }
+    return off;
+}
+size_t hnsw_prune_lds_bytes(int d, int C, int W) {
+    return hp_layout(d, C, W, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
+}
+
+template <int DT, int METRIC>
+__global__ void __launch_bounds__(HN_THREADS) k_hnsw_prune(HnswPruneArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr int NW = HN_THREADS / 64;
+    constexpr int RR = refine_rows<DT>();
+    constexpr int ES = DT == DT_F32 ? 4 : 2;
+    constexpr int CE = CHB / ES;
+    constexpr bool IP = METRIC == METRIC_IP;
+    __shared__ int s_m, s_bad[2];
+    double *qs, *cd, *sd;
+    int *ci, *si, *kept;
+    hp_layout(a.d, a.C, a.W, smem, &qs, &cd, &ci, &sd, &si, &kept);
+    const int node = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int ng = (a.d + 7) >> 3;
+    const int* cand = a.cand + (int64_t)node * a.C;
+    int* out = a.out + (int64_t)node * a.W;
+    // a stored row as the LDS query, in exact_score_rows' [e * ng + g] order
+    auto stage_row = [&](int64_t r) {
+        const uint8_t* rb = a.corpus + (r / TR) * (int64_t)TR * a.dpad * ES + (r % TR) * CHB;
+        for (int i = tid; i < a.d; i += HN_THREADS)
+            qs[(i & 7) * ng + (i >> 3)] = (double)load_elem<DT>(rb + (int64_t)(i / CE) * TR * CHB + (i % CE) * ES);
+        __syncthreads();
+    };
+    if (tid == 0) s_m = a.C;
+    __syncthreads();
+    for (int j = tid; j < a.C; j += HN_THREADS) {
+        const int v = cand[j];
+        ci[j] = v;
+        if (v < 0) atomicMin(&s_m, j);
+    }
+    stage_row(a.nodes[node]);  // (its barrier also publishes ci and s_m)
+    const int m = s_m;
+    // distances node -> candidates
+    for (int j0 = wid * RR; j0 < m; j0 += NW * RR) {
+        int64_t rr[RR];
+#pragma unroll
+        for (int i = 0; i < RR; ++i) rr[i] = j0 + i < m ? (int64_t)ci[j0 + i] : -1;
+        double s[RR];
+        exact_score_rows<DT, METRIC, true, RR>(a.corpus, rr, qs, nullptr, a.d, a.dpad, lane, s);
+        if (lane == 0)
+#pragma unroll
+            for (int i = 0; i < RR; ++i)
+                if (j0 + i < m) cd[j0 + i] = IP ? -s[i] : s[i];
+    }
+    __syncthreads();
+    for (int j = tid; j < m; j += HN_THREADS) {  // rank sort by (distance, id)
+        const double dj = cd[j];
+        const int ij = ci[j];
+        int r = 0;
+        for (int i = 0; i < m; ++i) r += hn_less(cd[i], ci[i], dj, ij) ? 1 : 0;
+        sd[r] = dj;
+        si[r] = ij;
+    }
+    __syncthreads();
+    if (m < a.W) {
+        for (int j = tid; j < a.W; j += HN_THREADS) out[j] = j < m ? si[j] : -1;
+        return;
+    }
+    int nk = 0;  // uniform
+    for (int i = 0; i < m && nk < a.W; ++i) {
+        const int c = si[i];
+        const double dq = sd[i];
+        bool good = true;
+        if (nk > 0) {
+            stage_row(c);
+            if (tid == 0) s_bad[0] = s_bad[1] = 0;
+            __syncthreads();
+            // kept neighbours in passes of NW * RR, stopping after the first pass that finds one
+            // closer (the nearest kept ones come first, so most rejections end in pass one).  Pass
+            // p raises flag p & 1: a fast wave's write in pass p + 1 cannot reach a slow wave still
+            // reading pass p's flag, and that flag was 0 in pass p - 1 or the loop had ended
+            int bad = 0;
+            for (int p0 = 0, par = 0; p0 < nk; p0 += NW * RR, par ^= 1) {
+                const int j0 = p0 + wid * RR;
+                if (j0 < nk) {
+                    int64_t rr[RR];
+#pragma unroll
+                    for (int t = 0; t < RR; ++t) rr[t] = j0 + t < nk ? (int64_t)kept[j0 + t] : -1;
+                    double s[RR];
+                    exact_score_rows<DT, METRIC, true, RR>(a.corpus, rr, qs, nullptr, a.d, a.dpad, lane, s);
+                    bool closer = false;
+#pragma unroll
+                    for (int t = 0; t < RR; ++t) closer |= j0 + t < nk && (IP ? -s[t] : s[t]) < dq;
+                    if (lane == 0 && closer) s_bad[par] = 1;
+                }
+                __syncthreads();
+                bad = s_bad[par];  // (uniform: read after the barrier)
+                if (bad) break;
+            }
+            good = bad == 0;
+            __syncthreads();  // every thread has read its flag and qs before the next stage
+        }
+        if (good) {
+            if (tid == 0) kept[nk] = c;
+            ++nk;
+            __syncthreads();
+        }
+    }
+    for (int j = tid; j < a.W; j += HN_THREADS) out[j] = j < nk ? kept[j] : -1;
+}
+
+template <int DT>
+static void launch_prune_dt(const HnswPruneArgs& a, int m, size_t lds, hipStream_t st) {
+    if (a.metric == METRIC_IP) {
+        set_lds_attr((const void*)k_hnsw_prune<DT, METRIC_IP>, (int)HN_LDS_CAP);
+        hipLaunchKernelGGL((k_hnsw_prune<DT, METRIC_IP>), dim3(m), dim3(HN_THREADS), lds, st, a);
+    } else {
+        set_lds_attr((const void*)k_hnsw_prune<DT, METRIC_L2>, (int)HN_LDS_CAP);
+        hipLaunchKernelGGL((k_hnsw_prune<DT, METRIC_L2>), dim3(m), dim3(HN_THREADS), lds, st, a);
+    }
+}
+hipError_t launch_hnsw_prune(const HnswPruneArgs& a, int m, hipStream_t st) {
+    if (m <= 0) return hipSuccess;
+    if (a.C < 1 || a.C > HP_C_MAX || a.W < 1 || a.W > HN_NB_MAX) return hipErrorInvalidValue;
+    const size_t lds = hnsw_prune_lds_bytes(a.d, a.C, a.W);
+    if (lds > HN_LDS_CAP) return hipErrorInvalidValue;
+    if (a.dt == DT_F32) launch_prune_dt<DT_F32>(a, m, lds, st);
+    else if (a.dt == DT_BF16) launch_prune_dt<DT_BF16>(a, m, lds, st);
+    else if (a.dt == DT_F16) launch_prune_dt<DT_F16>(a, m, lds, st);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
 }  // namespace vs

@@ -7,6 +7,12 @@ by :func:`faiss_format.single_level_graph` -- lives on the index's GPU next to i
 ``search`` runs faiss's ``HNSW::search`` there (include/vs.h "HNSW graph search"): one workgroup per
 query, the flat path's exact canonical scores as distances, so the same inputs give the same ids
 and scores as ``oracle/hnsw_oracle.py``.
+
+Graph build: :func:`select_level` applies faiss's neighbour-selection heuristic
+(``HNSW::shrink_neighbor_list``, which ``IndexHNSWFlat.add`` runs at /root/reference/utils/
+vector_store.py:164) to one level's candidate lists on the GPU (``vs_hnsw_prune``), then adds the
+reverse links the way faiss's ``add_link`` does: appended while a list has room, the list re-shrunk
+over the union once it would overflow.  ``VectorStore._build_graph`` feeds it exact candidates.
 """
 from __future__ import annotations
 
@@ -75,3 +81,59 @@ class HNSWGraph:
             self.close()
         except Exception:
             pass
+
+
+HP_C_MAX = 2048  # largest candidate list of one node (include/vs.h vs_hnsw_prune)
+
+
+def prune_neighbors(index, nodes, cand, W: int) -> np.ndarray:
+    """faiss ``HNSW::shrink_neighbor_list`` for every node, by the index (``FlatIndex.hnsw_prune``:
+    ``vs_hnsw_prune`` on the GPU): ``cand`` (m x C, distinct row ids, -1 padded at the end) ->
+    (m x W) kept ids best first, -1 padded."""
+    return index.hnsw_prune(nodes, cand, int(W))
+
+
+def select_level(index, members, cand, W: int, cmax: int = HP_C_MAX) -> np.ndarray:
+    """One level of the batch build (oracle/hnsw_oracle.py ``select_level``): ``members`` ascending
+    row ids, ``cand`` (m x C) their candidate row ids best first (-1 padded).  Forward lists =
+    shrink(candidates, W); each member then keeps its forward list followed by the members that
+    linked to it (ascending id, those already listed skipped) -- unpruned while that fits W, shrunk
+    to W over the union otherwise (a union longer than ``cmax`` is cut there first).  Returns
+    (m x W) neighbour ids, -1 padded."""
+    members = np.ascontiguousarray(members, dtype=np.int64)
+    m = members.shape[0]
+    W = int(W)
+    F = prune_neighbors(index, members, cand, W)
+    if m == 0:
+        return F
+    # (owner row, neighbour, group, key): forward entries keep their order, reverse ones ascend by source
+    fr, fc = np.nonzero(F >= 0)
+    fwd_owner, fwd_nb = fr, F[fr, fc].astype(np.int64)
+    rev_owner = np.searchsorted(members, fwd_nb)
+    rev_nb = members[fr]
+    n_glob = int(members[-1]) + 1
+    dup = np.isin(rev_owner * n_glob + rev_nb, fwd_owner * n_glob + fwd_nb)
+    rev_owner, rev_nb = rev_owner[~dup], rev_nb[~dup]
+    owner = np.concatenate([fwd_owner, rev_owner])
+    nb = np.concatenate([fwd_nb, rev_nb])
+    group = np.concatenate([np.zeros(fwd_owner.shape[0], np.int64), np.ones(rev_owner.shape[0], np.int64)])
+    key = np.concatenate([fc.astype(np.int64), rev_nb])
+    o = np.lexsort((key, group, owner))
+    owner, nb = owner[o], nb[o]
+    counts = np.bincount(owner, minlength=m)
+    starts = np.concatenate([[0], np.cumsum(counts)[:-1]])
+    pos = np.arange(owner.shape[0]) - starts[owner]
+    keep = pos < cmax
+    owner, nb, pos = owner[keep], nb[keep], pos[keep]
+    counts = np.minimum(counts, cmax)
+    U = np.full((m, int(counts.max())), -1, dtype=np.int32)
+    U[owner, pos] = nb
+    out = np.full((m, W), -1, dtype=np.int32)
+    small = counts <= W
+    out[small] = U[small, :W] if U.shape[1] >= W else np.pad(U[small], ((0, 0), (0, W - U.shape[1])),
+                                                             constant_values=-1)
+    big = np.nonzero(~small)[0]
+    if big.size:
+        Ub = U[big, :int(counts[big].max())]
+        out[big] = prune_neighbors(index, members[big], Ub, W)
+    return out

@@ -84,6 +84,19 @@ class FlatIndex:
             check(self._L.vs_reconstruct_n(self._h, int(i0), int(n), _ptr(out)))
         return out
 
+    def hnsw_prune(self, nodes, cand, W: int) -> np.ndarray:
+        """faiss's HNSW neighbour selection per node on the GPU (include/vs.h ``vs_hnsw_prune``):
+        ``cand`` (m x C distinct row ids, -1 padded at the end) -> (m x W) kept ids, -1 padded."""
+        nodes = np.ascontiguousarray(nodes, dtype=np.int64)
+        cand = np.ascontiguousarray(cand, dtype=np.int32)
+        if cand.ndim != 2 or cand.shape[0] != nodes.shape[0]:
+            raise ValueError("cand must be (len(nodes), C)")
+        m, C = cand.shape
+        out = np.full((m, int(W)), -1, dtype=np.int32)
+        if m:
+            check(self._L.vs_hnsw_prune(self._h, m, _ptr(nodes), _ptr(cand), int(C), int(W), _ptr(out)))
+        return out
+
     def reset(self) -> None:
         check(self._L.vs_reset(self._h))
 
@@ -290,6 +303,19 @@ class MultiDeviceFlatIndex:
 
     def reconstruct(self, i: int) -> np.ndarray:
         return self.reconstruct_n(int(i), 1)[0]
+
+    def hnsw_prune(self, nodes, cand, W: int) -> np.ndarray:
+        """:meth:`FlatIndex.hnsw_prune` on a one-device copy of the rows on ``devices[0]`` (the
+        kernel gathers rows by id from one device's HBM; graph builds are capped at
+        VECTOR_HNSW_GRAPH_MAX_ROWS rows)."""
+        tmp = FlatIndex(self.d, "ip" if self.metric_type == METRIC_IP else "l2", self.dtype, self.devices[0])
+        try:
+            n = self.ntotal
+            for r0 in range(0, n, 65536):
+                tmp.add(self.reconstruct_n(r0, min(65536, n - r0)))
+            return tmp.hnsw_prune(nodes, cand, W)
+        finally:
+            tmp.close()
 
     def reset(self) -> None:
         check(self._L.vs_multi_reset(self._h))

@@ -38,6 +38,7 @@ from typing import Any, Dict, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import faiss_format
+from . import hnsw as hnsw_mod
 from .hnsw import HNSWGraph
 from .index import FlatIndex, MultiDeviceFlatIndex
 
@@ -435,11 +436,14 @@ class VectorStore:
     def _build_graph(self, n: int) -> Dict[str, Any]:
         """A faiss-layout HNSW graph over the n stored rows: node levels drawn as faiss's
         ``HNSW::random_level`` does (``set_default_probas(M, 1/ln M)``; numpy's generator, seed
-        12345, not faiss's), and on every level each node's neighbours are its exact nearest nodes
-        of that level (2M on level 0, M above; the flat search, ties -> lower id), best first; the
-        entry point is the first node of the top level.  The sparse upper levels give the greedy
-        descent links between clusters that a one-level k-NN graph lacks (on clustered rows whose
-        clusters hold more than 2M rows a one-level graph never leaves the entry's cluster)."""
+        12345, not faiss's); on every level each node's candidates are its exact
+        max(efConstruction, width) nearest nodes of that level (the flat search, ties -> lower id)
+        and its neighbours (2M on level 0, M above) are chosen from them by faiss's heuristic,
+        reverse links included (:func:`hnsw.select_level`, on the GPU); the entry point is the
+        first node of the top level.  faiss inserts nodes one at a time and takes candidates from
+        an efConstruction beam over the graph built so far; here every node sees its exact
+        candidates at once, so the graph is the same construction without the insertion order
+        (oracle/hnsw_oracle.py ``heuristic_graph`` restates it)."""
         M = self.hnsw_m
         probas, cum = faiss_format.hnsw_default_probas(M)
         f = np.random.default_rng(12345).random(n)
@@ -458,10 +462,12 @@ class VectorStore:
         for level in range(top + 1):
             members = np.nonzero(lev >= level)[0]
             width = int(cum[level + 1] - cum[level])
-            knn = self._knn_graph(width, None if level == 0 else members)
+            C = min(max(int(self.hnsw_ef_construction), width), hnsw_mod.HP_C_MAX)
+            cand = self._knn_graph(C, None if level == 0 else members)
+            sel = hnsw_mod.select_level(self.index, members, cand, width)
             base = offsets[members].astype(np.int64) + int(cum[level])
             for j in range(members.shape[0]):
-                row = knn[j][knn[j] >= 0]
+                row = sel[j][sel[j] >= 0]
                 nb[base[j]:base[j] + len(row)] = row
         return {"assign_probas": probas, "cum_nneighbor_per_level": cum, "levels": levels, "offsets": offsets,
                 "neighbors": nb, "entry_point": int(np.nonzero(lev == top)[0][0]) if n else -1, "max_level": top,
@@ -489,11 +495,13 @@ class VectorStore:
             for r0 in range(0, m, 4096):
                 rows = index.reconstruct_n(r0, min(4096, m - r0))
                 _, I = index.search(rows, kk)
-                for j in range(I.shape[0]):
-                    nbr = [int(x) for x in I[j] if x >= 0 and x != r0 + j][:width]
-                    if ids is not None:
-                        nbr = [int(ids[x]) for x in nbr]
-                    out[r0 + j, :len(nbr)] = nbr
+                own = np.arange(r0, r0 + I.shape[0])[:, None]
+                ok = (I >= 0) & (I != own)
+                pos = np.cumsum(ok, axis=1) - 1  # order kept, itself dropped
+                ok &= pos < width
+                r, c = np.nonzero(ok)
+                nbr = I[r, c] if ids is None else ids[I[r, c]]
+                out[r0 + r, pos[r, c]] = nbr
         finally:
             if ids is not None and hasattr(index, "close"):
                 index.close()

@@ -2,8 +2,8 @@
 """HNSW graph search vs exact flat search on one MI355X, at the reference's
 HNSW settings (.env.example:82-83: M=48, efConstruction=320, efSearch=192; EMBEDDING_DIMENSION
 4096, TOP_K 10).  The graph is the one VectorStore.save() writes (VectorStore._build_graph: faiss's
-level draw, every level's exact k-NN among its nodes, built on the GPU by the flat search).  Prints
-one JSON line.
+level draw; every level's exact efConstruction candidates by the GPU flat search, then faiss's
+neighbour-selection heuristic with reverse links by k_hnsw_prune).  Prints one JSON line.
 
   python scripts/hnsw_bench.py [--rows 100000] [--d 4096] [--dtype bf16] [--nq 256] [--reps 5]
 """
@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--m", type=int, default=48)
     ap.add_argument("--ef", type=int, default=192)
+    ap.add_argument("--efc", type=int, default=320)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--data", default="mixture", choices=["mixture", "iso"],
                     help="mixture: unit rows around 1000 random centres (cosine ~0.8 to their centre), "
@@ -48,7 +49,7 @@ def main():
     os.environ["VECTOR_DTYPE"] = args.dtype
     os.environ["VECTOR_HNSW_SEARCH"] = "graph"
     store = VectorStore(dimension=d, index_path="/tmp/hnsw_bench.index", metadata_path="/tmp/hnsw_bench.json",
-                        metric="cosine", index_type="hnsw", hnsw_m=M, hnsw_ef_construction=320, hnsw_ef_search=args.ef)
+                        metric="cosine", index_type="hnsw", hnsw_m=M, hnsw_ef_construction=args.efc, hnsw_ef_search=args.ef)
     rng = np.random.default_rng(SEED_QUERIES)
     centres = rng.standard_normal((1000, d)).astype(np.float32)
     centres /= np.linalg.norm(centres, axis=1, keepdims=True)
@@ -92,7 +93,8 @@ def main():
     tg_ms, te_ms = 1e3 * float(np.median(tg)), 1e3 * float(np.median(te))
     out = {
         "workload": f"hnsw graph search N={N} d={d} {args.dtype} M={M} efSearch={args.ef} k={k} batch={args.nq}",
-        "graph": f"VectorStore._build_graph: {int(g['max_level']) + 1} levels, exact k-NN per level",
+        "graph": f"VectorStore._build_graph: {int(g['max_level']) + 1} levels, faiss heuristic over "
+                 f"exact efConstruction={args.efc} candidates, reverse links",
         "graph_build_s": round(build_s, 3),
         "hnsw_batch_ms": round(tg_ms, 3),
         "hnsw_qps": round(args.nq / (tg_ms / 1e3), 1),

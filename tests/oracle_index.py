@@ -35,6 +35,15 @@ class OracleFlatIndex:
         D[I < 0] = -3.4028235e38 if self.metric_type == 0 else 3.4028235e38
         return D, I
 
+    def hnsw_prune(self, nodes, cand, W: int) -> np.ndarray:
+        from oracle import hnsw_oracle as H
+        dist = H._distances(self._x, self._x, "ip" if self.metric_type == 0 else "l2")
+        out = np.full((len(nodes), int(W)), -1, dtype=np.int32)
+        for i, v in enumerate(nodes):
+            kept = H.shrink_neighbor_list(dist, int(v), cand[i], int(W))
+            out[i, :len(kept)] = kept
+        return out
+
     def reconstruct(self, i: int) -> np.ndarray:
         return self._x[int(i)].copy()
 
