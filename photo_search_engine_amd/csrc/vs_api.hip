@@ -616,16 +616,14 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
     a.thr0 = nullptr;
     bool optimistic = false;
     // (not in a fallback round: its launches cost their dispatch on every call, and it rarely runs)
-    // bf16 / f16 main passes in the direct form screen their whole range themselves, so they take a
-    // seed from one tile per workgroup upward (small shards: unseeded, every workgroup's first
-    // tiles list all their rows -- 100k x 4096 rows: screen 531 us, refine 0.9 ms at k = 10)
-    const bool direct = (ix->dtype == DT_BF16 || ix->dtype == DT_F16) && d16_direct_ok(ix->dpad);
-    if (use_mfma && !redo && (tiles >= 4 * (int64_t)a.G || (direct && tiles >= (int64_t)a.G && seed_rank > 0))) {
+    if (use_mfma && !redo && tiles >= 4 * (int64_t)a.G) {
         ScreenArgs sa = a;
         sa.G = std::min(sa.G, 512);  // k_seed_select holds up to 8192 maxima per query
         sa.tile_stride = (int)(tiles / sa.G);
         // seed tile = the first tile of each main-pass workgroup; its raw accumulators are kept so
         // the main pass starts one tile later
+        // (bf16 / f16 main passes in the direct form screen their whole range themselves)
+        const bool direct = (ix->dtype == DT_BF16 || ix->dtype == DT_F16) && d16_direct_ok(ix->dpad);
         if (seed_reuse() && sa.G == a.G && !direct) {
             c->seedacc.ensure((size_t)a.G * 128 * MF_WG_THREADS * sizeof(float));
             sa.seed_acc = c->seedacc.as<float>();

@@ -334,11 +334,13 @@ def test_ties_beyond_max_depth_are_reported(FlatIndex, nq, copies, dtype):
     ix.close()
 
 
-def test_batch_refine_certifies_ties_within_its_depth(FlatIndex):
+@pytest.mark.parametrize("d", [64, 512])
+def test_batch_refine_certifies_ties_within_its_depth(FlatIndex, d):
     """5000 exact ties (beyond KP_MAX = 4096) in a 20-query batch: the adaptive refine lists and
     scores every copy (<= 8192 rows), so the batch certifies with the exact answer -- the lowest-id
-    copies, faiss' tie order -- where a fixed-depth screen could only report the query."""
-    d, k, nq = 64, 10, 20
+    copies, faiss' tie order -- where a fixed-depth screen could only report the query.  d = 512:
+    the direct 16-bit screen, seeded from one tile per workgroup at this size."""
+    k, nq = 10, 20
     x = O.synth_rows(O.SEED_CORPUS, 0, 25_000, d, True, "bf16")
     v = x[123].copy()
     dup = np.random.default_rng(3).choice(25_000, 5000, replace=False)
