@@ -538,12 +538,12 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
     // batches (adaptive refine below) keep MFMA_KP_MAX: a workgroup that holds many of a query's
     // best rows (a cluster inserted contiguously) then drops only rows far below the k-th best.
     const bool wide = use_mfma && !redo && ix->metric == METRIC_IP && k <= I8_MAX_K && refine_split(nqb, Kp, ix->dtype, ix->num_cu) <= 1;
-    // (unseeded small shards -- under 4 tiles per workgroup -- keep max(128, 4 Kp) per workgroup:
+    // (unseeded small shards -- under 4 tiles per workgroup -- keep max(128, 2 Kp) per workgroup:
     // MFMA_KP_MAX lists of every row there made the refine's selection the cost, 0.9 ms at 100k x
     // 4096 bf16, batch 256, k = 10; a workgroup holding more of a query's best rows fails its
     // certificate and the fallback round lists every row)
     const bool small_shard = tiles < 4 * (int64_t)ix->num_cu;
-    a.Kp = use_mfma ? (wide ? (small_shard ? std::min(MFMA_KP_MAX, std::max(128, 4 * Kp)) : MFMA_KP_MAX)
+    a.Kp = use_mfma ? (wide ? (small_shard ? std::min(MFMA_KP_MAX, std::max(128, 2 * Kp)) : MFMA_KP_MAX)
                             : std::min(Kp, MFMA_KP_MAX))
                     : Kp;
     int QB;
