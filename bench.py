@@ -2,9 +2,11 @@
 """bench.py -- the BASELINE.json metric on MI355X: exact flat-IP k-NN queries/sec (+ recall@10 vs
 the faiss-semantics CPU restatement), N=10M d=1536 bf16, batch=256, top-100 (BASELINE cfg3).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg3|cfg2|cfg4]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg3|cfg1|cfg2|cfg4|cfg5]
 
-One process per GPU (torchrun for N > 1).  The corpus is row-sharded: rank r holds rows
+One process per GPU: under torchrun (WORLD_SIZE set, which must equal --gpus), or -- when
+--gpus N > 1 is given without a launcher -- this process spawns N fresh child processes with
+RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set and never touches a GPU itself.  The corpus is row-sharded: rank r holds rows
 [r*N/G, (r+1)*N/G) generated in place in HBM (counter-hash generator, bit-identical to
 oracle/vs_oracle.c); every rank holds the same synthetic query batch.  One step = the hot path on
 one batch: per-shard exact search (pack -> MFMA screen with fused top-k -> merge -> exact
@@ -31,6 +33,8 @@ WORKLOADS = {
     "cfg2": (1_000_000, 1536, "f32", 1, 10, "N=1M d=1536 fp32, batch=1, top-10 (GEMV path)"),
     "cfg4": (100_000_000, 768, "f16", 256, 10, "N=100M d=768 fp16, batch=256, top-10 (row-sharded)"),
 }
+# BASELINE cfg1: the reference's plumbing config, one query per VectorStore.search call
+CFG1 = (10_000, 1536, "f32", 1, 10, "N=10k d=1536 fp32, one query per VectorStore.search call, top-10 (plumbing)")
 IVF_WORKLOADS = {
     # name: (N, d, dtype, nq, k, nlist, nprobe, description)
     "cfg5": (50_000_000, 1536, "bf16", 256, 10, 4096, 32,
@@ -55,7 +59,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="cfg3", choices=sorted(WORKLOADS) + sorted(IVF_WORKLOADS))
+    ap.add_argument("--workload", default="cfg3", choices=sorted(WORKLOADS) + sorted(IVF_WORKLOADS) + ["cfg1"])
     ap.add_argument("--rows", type=int, default=0, help="override corpus rows (testing)")
     ap.add_argument("--shard-of", type=int, default=0,
                     help="measure ONE rank of a G-shard step on this GPU: its N/G-row shard, the two-phase "
@@ -75,7 +79,7 @@ def parse():
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal only: every rank on cuda:0 (with --dist-backend gloo on a 1-GPU box)")
     ap.add_argument("--zero-corpus", action="store_true",
-                    help="diagnostic only: all-zero corpus rows (DVFS/power test with VS_MF_ABLATE=9; results meaningless)")
+                    help="diagnostic only: all-zero corpus rows (the DVFS/power test of DESIGN §5; results meaningless)")
     ap.add_argument("--no-recall", action="store_true", help="cfg5: skip the exact ground truth (profiling runs)")
     ap.add_argument("--skew", type=float, default=0.0,
                     help="cfg5: Zipf exponent of the cluster sizes (0 = equal-sized clusters; 1.1 = a heavy head)")
@@ -94,9 +98,57 @@ def parse():
     return ap.parse_args()
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return int(so.getsockname()[1])
+
+
+def spawn_ranks(n: int) -> int:
+    """``--gpus N`` without a launcher: run N fresh children of this script, one per GPU (rank r on
+    cuda:r), with the torch.distributed environment set; rank 0 prints the JSON line.  The parent
+    never initialises a GPU (no torch import) and never re-execs itself; if a rank fails, the
+    others are stopped (they would wait in a collective) and the parent exits non-zero."""
+    import subprocess
+    env = dict(os.environ)
+    env.update({"WORLD_SIZE": str(n), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(_free_port()),
+                "LOCAL_WORLD_SIZE": str(n)})
+    procs = []
+    for r in range(n):
+        e = dict(env, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=e))
+    rc = 0
+    live = list(procs)
+    while live:
+        time.sleep(0.2)
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                _progress(f"rank {procs.index(p)} exited with {code}: stopping the other ranks")
+                for o in live:
+                    o.terminate()
+    return rc
+
+
 def main():
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
+    if env_world is not None and int(env_world) != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} does not match WORLD_SIZE={env_world} from the launcher")
+    if args.workload == "cfg1":
+        if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+            sys.exit("cfg1 is a single-GPU workload")
+        return run_cfg1(args)
     if args.workload in IVF_WORKLOADS:
+        if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+            sys.exit("cfg5 is a single-GPU workload")
         return run_ivf(args)
     import torch
     import torch.distributed as dist
@@ -184,6 +236,7 @@ def main():
         sh.floor_override = _shard_floor(args, N, d, dtype, nq, k, q, local, dev, torch)
     t_build = time.time() - t_build
     result = {}
+    per_rank = {}
 
     def step():
         result["D"], result["I"], result["S"] = sh.search(q, k)
@@ -201,7 +254,9 @@ def main():
             # the synchronous calls of a server; the timed steps are enqueued back to back)
             torch.cuda.synchronize()
         ix.timing_fetch()  # drop warmup events
+        sh.exchange_times_fetch()
         ix.set_timing(True)
+        sh.exchange_timing = True
         if G > 1:
             dist.barrier()
         torch.cuda.synchronize()
@@ -213,11 +268,18 @@ def main():
             dist.barrier()
         el = time.perf_counter() - t0
         ix.set_timing(False)
+        sh.exchange_timing = False
         km, kd = ix.timing_fetch()
+        xm = sh.exchange_times_fetch()
+        per_rank[scr] = [float(np.mean(km)) if km else float("nan"), sum(xm) / args.steps, len(xm) / args.steps,
+                         el * 1e3 / args.steps, float(n_local)]
         if G > 1:
             t = torch.tensor([el], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = float(t.item())
+            per_rank[scr] = _gather_rows(per_rank[scr], G, dev, args.dist_backend, torch, dist)
+        else:
+            per_rank[scr] = [per_rank[scr]]
         return el, km, kd, ix.uncertified_count() - u0, t_sw
 
     es = 2 if dtype in ("bf16", "f16") else 4
@@ -321,6 +383,12 @@ def main():
             "unresolved": unresolved,
             "build_s": round(t_build, 2),
         }
+        if G > 1 or args.shard_of > 1:
+            # per rank: its dominant kernel's mean ms (HIP events in the library), the all-gathers'
+            # ms per step (HIP events around each collective on the calling stream) and its wall ms
+            out["per_rank"] = [{"rank": r, "n_local": int(v[4]), "k1_ms": round(v[0], 4), "exchange_ms": round(v[1], 4),
+                                "exchanges_per_step": round(v[2], 2), "wall_ms_per_step": round(v[3], 4)}
+                               for r, v in enumerate(per_rank[screen])]
         if kind in ("mfma_i8", "gemv_i8"):
             out["int8_copy"] = {"hbm_bytes": ix.screen_copy_bytes(), "build_s": round(t_switch, 2),
                                 "note": "int8 codes + bf16 (scale, error norm) per row on top of the stored rows "
@@ -335,6 +403,14 @@ def main():
     sh.close()
     if G > 1 or args.shard_of > 1:
         dist.destroy_process_group()
+
+
+def _gather_rows(row, G, dev, backend, torch, dist):
+    """Every rank's list of floats -> rank-ordered list of lists (one small all-gather)."""
+    t = torch.tensor(row, dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+    out = [torch.empty_like(t) for _ in range(G)]
+    dist.all_gather(out, t)
+    return [o.cpu().tolist() for o in out]
 
 
 def _kernel_name(kind: str, dtype: str, d: int) -> str:
@@ -538,6 +614,97 @@ def _mixture_rows(seed, r0, m, d, centroids, sigma, dev, stream, cdf=None):
     return x / torch.linalg.vector_norm(x, dim=1, keepdim=True)
 
 
+def run_cfg1(args):
+    """BASELINE cfg1 end to end through the drop-in: ``VectorStore(dimension=1536)`` over 10k raw
+    rows (bulk ``add``; the store normalises them as the reference does), one step = ONE
+    ``store.search(query_list, 10)`` call -- host normalisation, the C-ABI call (H2D query, GEMV
+    screen + exact refine, D2H) and the result dicts -- over a cycle of 256 distinct queries.
+    value = calls per second; the dominant kernel's time comes from the library's HIP events.
+    Beside it: the faiss IndexFlatIP sequential scan (nq < 20) restated on one host thread, the
+    per-call latency faiss-cpu gives the reference at this config, and the ids of every timed call
+    checked against the oracle."""
+    import tempfile
+
+    import torch
+
+    from photo_search_engine_amd.vector_store import VectorStore
+    N, d, dtype, nq, k, desc = CFG1
+    if args.rows:
+        N = args.rows
+    torch.cuda.set_device(0)
+    from photo_search_engine_amd.index import synthesize_device
+    tmp = tempfile.mkdtemp(prefix="bench-cfg1-")
+    t_build = time.time()
+
+    def raw_rows(seed, n):  # raw (un-normalised) embeddings, generated on the device, to the host
+        t = torch.empty((n, d), dtype=torch.float32, device="cuda")
+        synthesize_device(0, seed, 0, n, d, t.data_ptr(), False, "f32", torch.cuda.current_stream().cuda_stream)
+        return t.cpu().numpy()
+
+    x = raw_rows(SEED_CORPUS, N)
+    qs = raw_rows(SEED_QUERIES, 256)
+    store = VectorStore(dimension=d, index_path=os.path.join(tmp, "photo_search.index"),
+                        metadata_path=os.path.join(tmp, "metadata.json"))
+    store.add(x, [{"photo_path": f"/photos/{i:05d}.jpg", "row": i} for i in range(N)])
+    t_build = time.time() - t_build
+    qlists = [qs[i].tolist() for i in range(qs.shape[0])]  # the embedding service hands over lists
+    ix = store.index
+    for i in range(args.warmup):
+        store.search(qlists[i % 256], k)
+    ix.timing_fetch()
+    ix.set_timing(True)
+    got = []
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        got.append(store.search(qlists[i % 256], k))
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    ix.set_timing(False)
+    kms, kinds = ix.timing_fetch()
+    kavg = float(np.mean(kms)) if kms else float("nan")
+    alg_bytes = N * d * 4 + d * 4 + k * 12
+    lat_ms = el * 1e3 / args.steps
+    out = {"metric": "VectorStore.search calls/sec (N=10k d=1536 fp32, batch=1, top-10, end to end)" +
+                     ("" if not args.rows else f" (rows override: N={N}, not the BASELINE config)"),
+           "value": round(args.steps / el, 2), "unit": "queries/s", "n_gpus": 1, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(lat_ms, 4), "higher_is_better": True, "scaling": "strong",
+           "vs_baseline": None, "dtype": dtype, "screen": "native",
+           "data": "synthetic raw counter-hash N(0,1) embeddings (seeds 20260417/20260418), normalised by the store",
+           "config": {"workload": "cfg1", "desc": desc, "N": N, "d": d, "batch": 1, "k": k, "metric": "cosine",
+                      "api": "VectorStore.search (host lists in, result dicts out)", "parallelism": "1 GPU"},
+           "roofline": {"kernel": _kernel_name(kinds if kinds != "none" else "gemv", dtype, d), "bound": "hbm",
+                        "achieved": round(alg_bytes / (kavg * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(alg_bytes / (kavg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                        "kernel_ms": round(kavg, 4), "alg_bytes_per_launch": alg_bytes,
+                        "note": "61 MB per call is a few microseconds of HBM: the call is launch/latency-bound"},
+           "build_s": round(t_build, 2)}
+    if not args.no_cpu_baseline:
+        from oracle import oracle as O
+        xn = np.stack([np.asarray(O.np_normalize_like_reference(r), dtype=np.float32) for r in x])
+        qn = np.stack([np.asarray(O.np_normalize_like_reference(r), dtype=np.float32) for r in qs])
+        reps = 200
+        O.knn_faiss_fp32(xn, qn[:1], k, "ip", 1)  # warm
+        t0 = time.perf_counter()
+        for i in range(reps):
+            O.knn_faiss_fp32(xn, qn[i % 256:i % 256 + 1], k, "ip", 1)
+        t1 = (time.perf_counter() - t0) / reps
+        S, I = O.knn_exact(xn, qn, k, "ip")
+        ok = sum(int([r["metadata"]["row"] for r in res] == I[i % 256].tolist() and
+                     [r["distance"] for r in res] == S[i % 256].astype(np.float32).tolist())
+                 for i, res in enumerate(got))
+        out["cpu_baseline"] = {"value": round(1.0 / t1, 2), "unit": "queries/s", "cores": 1, "kind": "port",
+                               "cpu_model": _cpu_model(), "latency_nq1_ms": round(t1 * 1e3, 4),
+                               "sample": f"faiss IndexFlatIP fp32 restatement (oracle/vs_oracle.c), sequential scan "
+                                         f"(nq < 20) on one thread, {reps} single-query calls over the {N} normalised "
+                                         f"rows; index search only (no wrapper overhead)"}
+        out["parity"] = {"calls_checked": len(got), "calls_identical_to_oracle": ok}
+    print(json.dumps(out), flush=True)
+    ix.close()
+    import shutil
+    shutil.rmtree(tmp, ignore_errors=True)
+
+
 def run_ivf(args):
     """BASELINE cfg5: IVF-Flat (photo_search_engine_amd.ivf) on one GPU.  One step = one batch:
     exact coarse probe -> list scans (k_ivf_scan) -> exact refine.  Centroids are 4096 synthetic
@@ -552,8 +719,6 @@ def run_ivf(args):
     from photo_search_engine_amd.index import FlatIndex, synthesize_device
     from photo_search_engine_amd.ivf import IVFFlatIndex
 
-    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
-        raise SystemExit("cfg5 is a single-GPU workload")
     N, d, dtype, nq, k, nlist, nprobe, desc = IVF_WORKLOADS[args.workload]
     if args.rows:
         N = args.rows

@@ -12,7 +12,7 @@ import sys
 import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("VS_LIB_PATH") or os.path.join(HERE, "libvs.so")  # override: A/B builds
+LIB_PATH = os.path.join(HERE, "libvs.so")  # the in-tree build (python -m photo_search_engine_amd.build)
 HEADER_PATH = os.path.join(HERE, "..", "include", "vs.h")
 
 METRIC_IP = 0

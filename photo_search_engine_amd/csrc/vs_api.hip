@@ -775,6 +775,17 @@ void check_index(const vs_index* ix) {
     if (!ix) throw VsError(VS_ERR_ARG, "null index");
 }
 
+// Points a leased Ctx's unresolved-query counter at the caller's device word for one call, and
+// clears it on every exit (exceptions included), before the Ctx returns to the pool: a later
+// lease must never count into a buffer it does not own.
+struct UnresScope {
+    Ctx* c;
+    UnresScope(Ctx* c_, unsigned* unres) : c(c_) { c->unres = unres; }
+    ~UnresScope() { c->unres = nullptr; }
+    UnresScope(const UnresScope&) = delete;
+    UnresScope& operator=(const UnresScope&) = delete;
+};
+
 }  // namespace
 
 // exact device search (vs_search_device_exact; the IVF coarse quantizer): like vs_search_device,
@@ -795,36 +806,17 @@ void vs::search_exact_device(vs_index* ix, const float* q_dev, int64_t nq, int k
     c->outD.ensure((size_t)nq * k * sizeof(float));
     c->cert.ensure((size_t)nq * sizeof(int));
     const int Kp = screen_depth(k);
-    const bool on_device = true;  // (every dtype has the MFMA fallback round)
-    struct UnresScope {  // the caller's counter for this call only (the Ctx goes back to the pool)
-        Ctx* c;
-        ~UnresScope() { c->unres = nullptr; }
-    } us{c};
-    c->unres = unres;
+    UnresScope us(c, unres);  // the caller's counter for this call only (the Ctx goes back to the pool)
+    // every dtype has the on-device MFMA fallback round, queued behind each block's first pass
     search_all(ix, c, q_dev, nq, k, Kp, D_dev ? D_dev : c->outD.as<float>(), I_dev, S64_dev, c->cert.as<int>(),
-               id_offset, st, kOptimisticSeedRank, on_device);
-    if (on_device && async) return;
+               id_offset, st, kOptimisticSeedRank, true);
+    if (async) return;
     c->hout.ensure((size_t)nq * sizeof(int));
     int* cert_h = (int*)c->hout.p;
     HIP_CHECK(hipMemcpyAsync(cert_h, c->cert.p, (size_t)nq * sizeof(int), hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));
-    if (on_device) {
-        for (int64_t qi = 0; qi < nq; ++qi)
-            if (!cert_h[qi]) throw VsError(VS_ERR_UNCERTIFIED, "exactness certificate failed at maximum screening depth");
-        return;
-    }
-    for (int64_t qi = 0; qi < nq; ++qi) {
-        int Kr = Kp;
-        while (!cert_h[qi]) {
-            if (Kr >= KP_MAX || Kr >= ix->ntotal)
-                throw VsError(VS_ERR_UNCERTIFIED, "exactness certificate failed at maximum screening depth");
-            Kr = (int)std::min<int64_t>(std::min<int64_t>((int64_t)Kr * 4, KP_MAX), round_up(ix->ntotal, 16));
-            search_all(ix, c, q_dev + qi * ix->d, 1, k, Kr, D_dev ? D_dev + qi * k : c->outD.as<float>(), I_dev + qi * k,
-                       S64_dev ? S64_dev + qi * k : nullptr, c->cert.as<int>(), id_offset, st, /*safe seed*/ 0);
-            HIP_CHECK(hipMemcpyAsync(&cert_h[qi], c->cert.p, sizeof(int), hipMemcpyDeviceToHost, st));
-            HIP_CHECK(hipStreamSynchronize(st));
-        }
-    }
+    for (int64_t qi = 0; qi < nq; ++qi)
+        if (!cert_h[qi]) throw VsError(VS_ERR_UNCERTIFIED, "exactness certificate failed at maximum screening depth");
 }
 
 // S concurrent exact device searches over consecutive parts (whole query blocks) of one batch, each
@@ -848,10 +840,9 @@ void vs::search_exact_device_parts(vs_index* ix, const float* q_dev, int64_t nq,
         Ctx* c = leases[i]->c;
         c->outD.ensure((size_t)(q1 - q0) * k * sizeof(float));
         c->cert.ensure((size_t)(q1 - q0) * sizeof(int));
-        c->unres = unres + i;
+        UnresScope us(c, unres + i);  // reset even if search_all throws
         search_all(ix, c, q_dev + q0 * ix->d, q1 - q0, k, Kp, c->outD.as<float>(), I_dev + q0 * k, nullptr,
                    c->cert.as<int>(), 0, streams[i], kOptimisticSeedRank, true);
-        c->unres = nullptr;
     }
 }
 

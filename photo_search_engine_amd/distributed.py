@@ -105,11 +105,18 @@ def _device_phase_a(index, q: torch.Tensor, k: int, row0: int, world: int):
 
 def _device_phase_b(index, pend, floor_S: torch.Tensor, q: torch.Tensor, k: int):
     """Phase B with the merged phase-A lists as the floor: the shard's exact top-k as interleaved
-    (score bits, id) pairs [nq][k][2]."""
-    nq = q.shape[0]
-    SI = torch.empty((nq, k, 2), dtype=torch.int64, device=q.device)
-    stream = torch.cuda.current_stream(q.device).cuda_stream
-    index.search_phase_b(pend, floor_S.data_ptr(), None, SI.data_ptr() + 8, SI.data_ptr(), stream, stride=2)
+    (score bits, id) pairs [nq][k][2].  Consumes ``pend`` whatever happens (a pending search holds
+    the index's read lock and a workspace lease until it is freed)."""
+    try:  # nothing may fail between here and the C call without freeing the pending search
+        nq = q.shape[0]
+        SI = torch.empty((nq, k, 2), dtype=torch.int64, device=q.device)
+        stream = torch.cuda.current_stream(q.device).cuda_stream
+        floor_ptr = floor_S.data_ptr()
+    except BaseException:
+        index.search_pending_free(pend)
+        raise
+    # (the library frees the pending search itself, on success and on every error)
+    index.search_phase_b(pend, floor_ptr, None, SI.data_ptr() + 8, SI.data_ptr(), stream, stride=2)
     return SI
 
 
@@ -156,6 +163,9 @@ class ShardedFlatIndex:
         # ... and the floor the other shards would have contributed (the G shards' merged phase-A
         # lists, computed beforehand), used in place of its one-rank exchange's merge
         self.floor_override: Optional[torch.Tensor] = None
+        # measurement only: HIP events around every all-gather on the calling stream
+        self.exchange_timing = False
+        self._xevents: list = []
 
     # -- build ---------------------------------------------------------------------------------
     def add_shard(self, x_local, row0: int, n_total: int) -> None:
@@ -196,10 +206,23 @@ class ShardedFlatIndex:
     # -- search --------------------------------------------------------------------------------
     def _gather(self, t: torch.Tensor) -> torch.Tensor:
         out = torch.empty((self.world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        ev = None
+        if self.exchange_timing and t.is_cuda:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
         if dist.get_backend(self.group) == "nccl":
             dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
         else:
             dist.all_gather(list(out.unbind(0)), t.contiguous(), group=self.group)
+        if ev is not None:
+            ev[1].record()
+            self._xevents.append(ev)
+        return out
+
+    def exchange_times_fetch(self) -> list:
+        """ms of every all-gather timed since the last fetch (synchronising; exchange_timing)."""
+        out = [a.elapsed_time(b) for a, b in self._xevents]
+        self._xevents = []
         return out
 
     def search(self, q: torch.Tensor, k: int, src: Optional[int] = None):
@@ -258,17 +281,17 @@ class ShardedFlatIndex:
             SIa = _pack(*self._padding(nq, k, q.device)[:2])
         try:
             _, _, floor_S = self._exchange_packed(SIa, k)
+            if self.floor_override is not None:
+                floor_S = self.floor_override
         except BaseException:
             if pend is not None:
                 free = getattr(self.index, "search_pending_free", None)
                 if free:
                     free(pend)
             raise
-        if self.floor_override is not None:
-            floor_S = self.floor_override
         if pend is None:
             return _pack(*self._padding(nq, k, q.device)[:2])
-        return self._phase_b(self.index, pend, floor_S, q, k)
+        return self._phase_b(self.index, pend, floor_S, q, k)  # consumes pend on every path
 
     def close(self) -> None:
         close = getattr(self.index, "close", None)

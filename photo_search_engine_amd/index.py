@@ -269,6 +269,7 @@ class MultiDeviceFlatIndex:
         self.metric_type = code
         self.dtype = dtype
         self.devices = devs
+        self._prune_copy = None  # (ntotal, FlatIndex on devices[0]) for hnsw_prune
 
     @property
     def ntotal(self) -> int:
@@ -281,6 +282,7 @@ class MultiDeviceFlatIndex:
         x = np.ascontiguousarray(x, dtype=np.float32)
         if x.ndim != 2 or x.shape[1] != self.d:
             raise ValueError(f"add expects an (n, {self.d}) array, got {x.shape}")
+        self._drop_prune_copy()
         check(self._L.vs_multi_add(self._h, _ptr(x), x.shape[0]))
 
     def search(self, q, k: int) -> Tuple[np.ndarray, np.ndarray]:
@@ -306,18 +308,31 @@ class MultiDeviceFlatIndex:
 
     def hnsw_prune(self, nodes, cand, W: int) -> np.ndarray:
         """:meth:`FlatIndex.hnsw_prune` on a one-device copy of the rows on ``devices[0]`` (the
-        kernel gathers rows by id from one device's HBM; graph builds are capped at
-        VECTOR_HNSW_GRAPH_MAX_ROWS rows)."""
-        tmp = FlatIndex(self.d, "ip" if self.metric_type == METRIC_IP else "l2", self.dtype, self.devices[0])
-        try:
-            n = self.ntotal
-            for r0 in range(0, n, 65536):
-                tmp.add(self.reconstruct_n(r0, min(65536, n - r0)))
-            return tmp.hnsw_prune(nodes, cand, W)
-        finally:
-            tmp.close()
+        kernel gathers rows by id from one device's HBM).  The copy is made once and kept until the
+        rows change (a graph build calls this twice per level)."""
+        if len(nodes) == 0:
+            return np.full((0, int(W)), -1, dtype=np.int32)
+        n = self.ntotal
+        if self._prune_copy is None or self._prune_copy[0] != n:
+            self._drop_prune_copy()
+            tmp = FlatIndex(self.d, "ip" if self.metric_type == METRIC_IP else "l2", self.dtype, self.devices[0])
+            try:
+                tmp.reserve(n)
+                for r0 in range(0, n, 65536):
+                    tmp.add(self.reconstruct_n(r0, min(65536, n - r0)))
+            except BaseException:
+                tmp.close()
+                raise
+            self._prune_copy = (n, tmp)
+        return self._prune_copy[1].hnsw_prune(nodes, cand, W)
+
+    def _drop_prune_copy(self) -> None:
+        pc, self._prune_copy = getattr(self, "_prune_copy", None), None
+        if pc is not None:
+            pc[1].close()
 
     def reset(self) -> None:
+        self._drop_prune_copy()
         check(self._L.vs_multi_reset(self._h))
 
     def set_screen(self, screen: str) -> None:
@@ -326,12 +341,14 @@ class MultiDeviceFlatIndex:
         check(self._L.vs_multi_set_screen(self._h, FlatIndex.SCREENS[screen]))
 
     def add_from_file(self, path: str, byte_offset: int, n: int) -> None:
+        self._drop_prune_copy()
         check(self._L.vs_multi_add_from_file(self._h, os.fsencode(path), int(byte_offset), int(n)))
 
     def write_rows(self, path: str, byte_offset: int, i0: int, n: int) -> None:
         check(self._L.vs_multi_write_rows_to_file(self._h, os.fsencode(path), int(byte_offset), int(i0), int(n)))
 
     def close(self) -> None:
+        self._drop_prune_copy()
         if self._h is not None and self._h.value:
             self._L.vs_multi_destroy(self._h)
         self._h = None

@@ -14,9 +14,10 @@ What changes underneath:
     runs faiss's HNSW search instead, on the GPU (:class:`~photo_search_engine_amd.hnsw.HNSWGraph`)
     with ``efSearch = hnsw_ef_search`` as the reference sets it (utils/vector_store.py:77,135), over
     the graph of the loaded IHNf file or the one ``save()`` writes.  ``save()`` writes an IHNf file
-    (a multi-level graph -- faiss's level draw, each level's exact k-NN among its nodes, built by
-    the GPU flat search -- + the flat storage) that the reference's faiss can load back, up to
-    ``VECTOR_HNSW_GRAPH_MAX_ROWS`` rows (flat IxFI/IxF2 above).  ``load()`` reads both.
+    that the reference's faiss can load back: faiss's level draw, each node's neighbours chosen by
+    faiss's selection heuristic (``HNSW::shrink_neighbor_list``, on the GPU) from exact candidates,
+    reverse links as faiss's ``add_link`` adds them, + the flat storage (``_build_graph``).
+    ``load()`` reads flat and HNSW files.
   * ``_embeddings`` caches only rows added in this process (a dict), not one Python list per row.
   * Bulk additions: :meth:`add` (n x d array) and :meth:`search_batch` (faiss (D, I) layout).
 
@@ -79,7 +80,11 @@ _GRAPH_REBUILD_GROWTH = 1.25
 def _merge_topk(D1: np.ndarray, I1: np.ndarray, D2: np.ndarray, I2: np.ndarray, k: int,
                 higher_is_better: bool) -> Tuple[np.ndarray, np.ndarray]:
     """Per query, the best k of two (D, I) result lists (faiss layout, -1 padded): by score (IP:
-    larger first; L2: smaller first), ties to the lower id, padding last."""
+    larger first; L2: smaller first), ties to the lower id, padding last.  The merge sees the fp32
+    distances only, so two rows whose canonical fp64 scores differ but round to the same fp32 value
+    are ordered by id here, where an exact search orders them by the fp64 score.  Only graph mode
+    merges (its graph results with the exactly searched rows added behind the graph), and graph
+    search is approximate to begin with."""
     D = np.concatenate([D1, D2], axis=1)
     I = np.concatenate([I1, I2], axis=1)
     key = -D if higher_is_better else D.copy()

@@ -1,6 +1,6 @@
 #!/bin/bash
 # usage: bash scripts/gpu_run.sh <step>...   (on the GPU box, through gpurun)
-#   smoke tests shapes bench bench_i8 bench_cfg2 bench_cfg4 bench_cfg5 bench_cfg5_skew prof prof_i8 rowsweep
+#   smoke tests t_new shapes bench_cfg1 bench_spawn2 bench bench_i8 bench_cfg2 bench_cfg4 bench_cfg5 bench_cfg5_skew prof prof_i8 rowsweep
 # Every GPU step runs under its own time limit; the first failing step ends the script.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -13,6 +13,9 @@ for s in "$@"; do
     tests) timeout -k 10 1200 $PYT tests -m gpu --durations=15 > gpurun_out/pytest_gpu.log 2>&1 ;;
     shapes) timeout -k 10 600 $PYT tests/test_gpu_baseline_shapes.py -m gpu --durations=0 > gpurun_out/shapes.log 2>&1 ;;
     quick) timeout -k 10 900 $PYT tests -m gpu -k "${K:-not baseline_shapes}" > gpurun_out/pytest_quick.log 2>&1 ;;
+    t_new) timeout -k 10 900 $PYT ${TESTS_NEW:-tests/test_gpu_cfg1.py} -m gpu > gpurun_out/pytest_new.log 2>&1 ;;
+    bench_cfg1) timeout -k 10 300 python bench.py --workload cfg1 --steps 1000 --warmup 50 > gpurun_out/bench_cfg1.log 2>&1 ;;
+    bench_spawn2) timeout -k 10 600 python bench.py --gpus 2 --same-device --dist-backend gloo --steps 10 --no-cpu-baseline ${BENCH_ARGS} > gpurun_out/bench_spawn2.log 2>&1 ;;
     bench) timeout -k 10 600 python bench.py > gpurun_out/bench.log 2>&1 ;;
     bench_i8) timeout -k 10 600 python bench.py --screen int8 > gpurun_out/bench_i8.log 2>&1 ;;
     bench_bf16) timeout -k 10 600 python bench.py --screen bf16 > gpurun_out/bench_bf16.log 2>&1 ;;

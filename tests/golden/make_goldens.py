@@ -11,6 +11,8 @@
    format.  What the fixture pins is the reference WRAPPER's behaviour around the arithmetic:
    normalisation bits, k clamping, -1 filtering, result layout, error types and messages,
    sidecar JSON and the index file bytes.
+3. cfg1_wrapper_golden.npz -- BASELINE cfg1 (N=10k, d=1536, one query per call, top-10) through the
+   reference wrapper imported the same way (``make_cfg1_golden``).
 2. oracle_golden.npz -- exact top-k (ids + fp64 scores + fp64 rank gaps) of the canonical oracle on
    cfg1-shaped synthetic data (N=10k, d=1536), cross-checked against the numpy twin and the faiss
    fp32 restatement at generation time.  Pins the oracle against regressions; the corpus itself
@@ -54,23 +56,35 @@ class _Flat:
     def __init__(self, d, metric_type):
         self.d = int(d)
         self.metric_type = metric_type
-        self._x = np.zeros((0, self.d), dtype=np.float32)
+        self._parts = []
+        self._cat = np.zeros((0, self.d), dtype=np.float32)
         self.is_trained = True
 
     @property
+    def _x(self):
+        if self._parts:  # appends are amortised: one concatenation per search / reconstruct
+            self._cat = np.concatenate([self._cat] + self._parts, axis=0)
+            self._parts = []
+        return self._cat
+
+    @property
     def ntotal(self):
-        return int(self._x.shape[0])
+        return int(self._cat.shape[0]) + sum(int(p.shape[0]) for p in self._parts)
 
     def add(self, x):
         x = np.ascontiguousarray(x, dtype=np.float32)
         assert x.ndim == 2 and x.shape[1] == self.d
-        self._x = np.concatenate([self._x, x], axis=0)
+        self._parts.append(x.copy())
 
     def search(self, q, k):
         q = np.ascontiguousarray(q, dtype=np.float32)
         if k <= 0:
             raise RuntimeError("Error in search: k > 0 failed")
-        S, I = _O.np_knn_exact(self._x, q, int(k), "ip" if self.metric_type == 0 else "l2")
+        x = self._x
+        # the C oracle and its numpy twin are the same canonical expression tree (tests/test_oracle.py);
+        # the twin is kept for the small scenarios, the C form for cfg1-sized corpora
+        knn = _O.knn_exact if x.shape[0] * q.shape[0] > 200000 else _O.np_knn_exact
+        S, I = knn(x, q, int(k), "ip" if self.metric_type == 0 else "l2")
         D = S.astype(np.float32)
         D[I < 0] = -3.4028235e38 if self.metric_type == 0 else 3.4028235e38
         return D, I
@@ -364,6 +378,80 @@ def make_oracle_golden():
     print("wrote oracle_golden.npz; faiss32 id agreement", float(np.mean(If == I)))
 
 
+CFG1_N, CFG1_D, CFG1_NQ, CFG1_NQ_L2 = 10000, 1536, 32, 8
+CFG1_TOPKS = (10, 1, 50)
+
+
+def cfg1_corpus():
+    """The cfg1 workload's raw embeddings: un-normalised counter-hash Gaussian rows and queries
+    (the wrapper normalises them, as it does the embedding service's vectors)."""
+    x = O.synth_rows(O.SEED_CORPUS, 0, CFG1_N, CFG1_D, False, "f32")
+    q = O.synth_rows(O.SEED_QUERIES, 0, CFG1_NQ, CFG1_D, False, "f32")
+    return x, q
+
+
+def make_cfg1_golden():
+    """BASELINE cfg1 through the REFERENCE wrapper: ``VectorStore(dimension=1536)`` fed the 10k raw
+    rows one ``add_item`` at a time (/root/reference/utils/vector_store.py:143-169), then
+    ``search(query, top_k)`` one query per call (:172-198) for top_k 10 (the config), 1 and 50;
+    an ``metric="l2"`` store over the same rows (no normalisation) for the L2 slice; the
+    normalised embeddings of three rows (:200-212) and the sha256 of the saved index file
+    (:217-237).  The stand-in faiss searches with the oracle's canonical exact search, so what is
+    pinned is the wrapper around it at the product's plumbing scale; the corpus is regenerated from
+    the counter hash, only results are stored."""
+    import hashlib
+    tmp = tempfile.mkdtemp(prefix="vsfaiss-")
+    try:
+        mod = import_reference_vector_store(tmp)
+        x, q = cfg1_corpus()
+        out = {"N": CFG1_N, "d": CFG1_D}
+        for metric, nq in (("cosine", CFG1_NQ), ("l2", CFG1_NQ_L2)):
+            work = tempfile.mkdtemp(prefix="vscfg1-")
+            store = mod.VectorStore(dimension=CFG1_D, index_path=os.path.join(work, "index.bin"),
+                                    metadata_path=os.path.join(work, "metadata.json"), metric=metric)
+            for i in range(CFG1_N):
+                store.add_item(x[i].tolist(), {"photo_path": f"/photos/{i:05d}.jpg", "row": i})
+            for top_k in CFG1_TOPKS:
+                ids = np.full((nq, top_k), -1, dtype=np.int32)
+                dist = np.zeros((nq, top_k), dtype=np.float32)
+                for a in range(nq):
+                    res = store.search(q[a].tolist(), top_k)
+                    assert len(res) == top_k
+                    ids[a] = [r["metadata"]["row"] for r in res]
+                    dist[a] = [r["distance"] for r in res]
+                out[f"{metric}_top{top_k}_I"] = ids
+                out[f"{metric}_top{top_k}_D"] = dist
+            probe = [0, 4321, CFG1_N - 1]
+            out[f"{metric}_probe_rows"] = np.array(probe, dtype=np.int32)
+            out[f"{metric}_probe_emb"] = np.array(
+                [store.get_embedding_by_photo_path(f"/photos/{i:05d}.jpg") for i in probe], dtype=np.float32)
+            store.save()
+            with open(os.path.join(work, "index.bin"), "rb") as f:
+                out[f"{metric}_index_sha256"] = np.array(hashlib.sha256(f.read()).hexdigest())
+            shutil.rmtree(work, ignore_errors=True)
+        # cross-check at generation time: the same top-10 from the oracle on numpy-normalised rows
+        xn = np.array([O.np_normalize_like_reference(r) for r in x], dtype=np.float32)
+        qn = np.array([O.np_normalize_like_reference(r) for r in q], dtype=np.float32)
+        S, I = O.knn_exact(xn, qn, 10, "ip")
+        assert np.array_equal(I, out["cosine_top10_I"]) and np.array_equal(S.astype(np.float32), out["cosine_top10_D"])
+        # VECTOR_DTYPE=bf16 (not a reference option): the oracle on the bf16-rounded normalised rows
+        Sb, Ib = O.knn_exact(O.round_dtype(xn, "bf16"), qn, 10, "ip")
+        out["cosine_bf16_top10_I"] = Ib.astype(np.int32)
+        out["cosine_bf16_top10_D"] = Sb.astype(np.float32)
+        path = os.path.join(HERE, "cfg1_wrapper_golden.npz")
+        np.savez_compressed(path, **out)
+        print("wrote", path, os.path.getsize(path), "bytes")
+    finally:
+        sys.path.remove(tmp)
+        sys.modules.pop("faiss", None)
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
 if __name__ == "__main__":
-    make_wrapper_golden()
-    make_oracle_golden()
+    which = sys.argv[1:] or ["wrapper", "oracle", "cfg1"]
+    if "wrapper" in which:
+        make_wrapper_golden()
+    if "oracle" in which:
+        make_oracle_golden()
+    if "cfg1" in which:
+        make_cfg1_golden()
