@@ -54,7 +54,7 @@ struct Ctx {
     // returned with kernels still queued is never overwritten by the next caller's pack
     hipEvent_t idle = nullptr;
     bool pending = false;
-    DevBuf qdev, qtile, qinfo, qpad, cand, part, merge_a, merge_b, outD, outI, outS, cert, thr0, seedmax, gcnt;
+    DevBuf qdev, qtile, qinfo, qpad, cand, part, merge_a, merge_b, outD, outI, outS, cert, thr0, seedmax, gcnt, seedsync;
     DevBuf qfac, qeps, drop;  // int8 screen: per-query code scale and norm, refine margin, drop bounds
     DevBuf fails;             // the current query block's certificate-failure count (fallback gate)
     DevBuf rsc, rdone;        // split refine: per-query scores + ids of the kept rows, done counters
@@ -69,7 +69,7 @@ struct Ctx {
     unsigned* unres = nullptr;  // this call's unresolved-query counter (device), instead of the index's
     ~Ctx() {
         for (DevBuf* b : {&qdev, &qtile, &qinfo, &qpad, &cand, &part, &merge_a, &merge_b, &outD, &outI, &outS, &cert, &thr0,
-                          &seedmax, &gcnt, &rows[0], &rows[1], &tilectr, &seedacc, &outAll, &qfac, &qeps, &drop, &fails, &rsc, &rdone,
+                          &seedsync, &seedmax, &gcnt, &rows[0], &rows[1], &tilectr, &seedacc, &outAll, &qfac, &qeps, &drop, &fails, &rsc, &rdone,
                           &pa})
             b->release();
         pin.release();
@@ -404,10 +404,16 @@ void search_block_i8(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float
     c->drop.ensure(sizeof(u64) * MFMA_QB);
     c->gcnt.ensure(sizeof(int) * MFMA_QB);
     c->fails.ensure(sizeof(int));
+    // threshold seeding: inside the direct main pass (its workgroups sample, select and adopt the
+    // seed themselves, k_screen_i8d_seeded), else a seed pass + select before it
+    const bool seeded = tiles >= 4 * (int64_t)a.G;
+    const bool seed_in_kernel =
+        seeded && ix->metric == METRIC_IP && i8_direct_ok(ix->dpad8) && a.G * 16 <= kI8dSeedMaxima;
+    if (seed_in_kernel) c->seedsync.ensure(4 * sizeof(int));
     HIP_CHECK(launch_pack_qtile_i8(q, nqb, ix->d, ix->dpad8, c->qtile.as<uint8_t>(), c->qfac.as<float2>(),
                                    c->qeps.as<float>(), ix->d_maxsq + 2, c->gcnt.as<int>(), c->drop.as<u64>(), st,
                                    c->fails.as<int>(), ix->metric == METRIC_L2 ? ix->d_maxsq : nullptr,
-                                   gamma_of(ix->d)));
+                                   gamma_of(ix->d), seed_in_kernel ? c->seedsync.as<int>() : nullptr));
     a.qfac = c->qfac.as<float2>();
     a.drop = c->drop.as<u64>();
     a.lcap = a.G * a.Kp;
@@ -417,7 +423,24 @@ void search_block_i8(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float
     a.glist = c->part.as<u64>();
     a.gcnt = c->gcnt.as<int>();
     a.thr0 = nullptr;
-    if (tiles >= 4 * (int64_t)a.G) {  // optimistic threshold seed from one tile per workgroup
+    auto seed_rank_of = [&](double sampled, int M) {
+        double target = i8_union_target(k, sampled, (double)ix->ntotal);
+        {
+            std::lock_guard<std::mutex> g(ix->h_mu);
+            target *= (double)(1 << ix->i8_log2);
+        }
+        const double r = std::ceil(target * sampled / (double)ix->ntotal);
+        return (int)std::min<double>(std::max<double>(r, (double)kOptimisticMinRank), (double)M);
+    };
+    if (seed_in_kernel) {  // one sample tile per workgroup, as the seed pass below
+        const int M = a.G * 16;
+        c->seedmax.ensure(sizeof(float) * MFMA_QB * M);
+        c->thr0.ensure(sizeof(u64) * MFMA_QB);
+        a.seedmax = c->seedmax.as<float>();
+        a.seed_sync = c->seedsync.as<int>();
+        a.thr_out = c->thr0.as<u64>();
+        a.seed_rank = seed_rank_of((double)a.G * TR, M);
+    } else if (seeded) {  // optimistic threshold seed from one tile per workgroup
         ScreenArgs sa = a;
         sa.G = std::min(sa.G, 512);
         sa.tile_stride = (int)(tiles / sa.G);
@@ -432,13 +455,7 @@ void search_block_i8(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float
         sa.seedmax = c->seedmax.as<float>();
         HIP_CHECK(launch_seed_mfma(DT_I8, sa, c->qtile.as<uint8_t>(), nqb, st));
         c->thr0.ensure(sizeof(u64) * MFMA_QB);
-        double target = i8_union_target(k, (double)sa.G * TR, (double)ix->ntotal);
-        {
-            std::lock_guard<std::mutex> g(ix->h_mu);
-            target *= (double)(1 << ix->i8_log2);
-        }
-        const double r = std::ceil(target * (double)sa.G * TR / (double)ix->ntotal);
-        const int rank = (int)std::min<double>(std::max<double>(r, (double)kOptimisticMinRank), (double)M);
+        const int rank = seed_rank_of((double)sa.G * TR, M);
         HIP_CHECK(launch_seed_select(sa.seedmax, M, nqb, rank, c->thr0.as<u64>(), st));
         a.thr0 = c->thr0.as<u64>();
         a.seed_acc = sa.seed_acc;
@@ -479,7 +496,7 @@ void search_block_i8(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float
     r.uncert = ix->d_uncert;
     r.qeps = c->qeps.as<float>();
     r.drop = a.drop;
-    r.thr0 = a.thr0;
+    r.thr0 = a.thr_out ? a.thr_out : a.thr0;  // (in-kernel seeding: complete when the screen ends)
     r.fails = c->fails.as<int>();
     r.ostride = ostride;
     if (phase == 1) {
@@ -912,7 +929,7 @@ vs_pending* vs::search_phase_a(vs_index* ix, const float* q_dev, int64_t nq, int
 }
 
 void vs::search_phase_b(vs_pending* p, const double* floor_S, float* D, int64_t* I, double* S64, int stride,
-                        hipStream_t st) {
+                        hipStream_t st, unsigned* unres) {
     std::unique_ptr<vs_pending> own(p);
     vs_index* ix = p->ix;
     DeviceGuard dg(ix->device);
@@ -946,6 +963,7 @@ void vs::search_phase_b(vs_pending* p, const double* floor_S, float* D, int64_t*
     HIP_CHECK(launch_refine_wide(r, (int)nq, p->ka, st));
     health_note(ix, c, st, 1, (int)nq);
     // the block's gated fallback round (native screen, local certificate), as search_all's
+    UnresScope us(c, unres);
     search_block(ix, c, p->q, (int)nq, k, std::max(screen_depth(k), fallback_depth(ix)), D, I, S64,
                  c->cert.as<int>(), p->id_offset, st, 0, true, true, stride);
 }

@@ -202,8 +202,17 @@ struct ScreenArgs {
     const int* wg_desc;      // mapped screen: per workgroup MAP_DESC ints {tile_map offset of its
                              // first tile, tiles, logical index of the first tile in its list
                              // segment, rows of that segment, query tile index, qmap offset, queries}
+    // In-kernel threshold seeding (the int8 direct main pass, k_screen_i8d_seeded): each workgroup
+    // screens a sample tile first, publishes its 16-row-group maxima to seedmax and counts itself
+    // in; the rank-th largest maximum per query is selected by the workgroups themselves and
+    // adopted by all of them while they screen (no wait on another workgroup anywhere).
+    int* seed_sync;          // [0] workgroups arrived, [1] selections published, [2] selections claimed
+                             // (zeroed by the query pack); null = no in-kernel seeding
+    u64* thr_out;            // [QB] the selected thresholds (the refine's thr0)
+    int seed_rank;           // rank of the selected maximum among the G * 16 of a query
 };
 constexpr int MAP_DESC = 8;
+constexpr int kI8dSeedMaxima = 4096;  // G * 16 group maxima per query the in-kernel seed select holds
 constexpr int MFMA_MAP_TILES = 256;  // mapped screen: logical tiles per workgroup (its LDS page table)
 int gemv_blocks_per_cu(int dt, int nqpad);  // resident k_screen_gemv blocks per CU (occupancy API)
 
@@ -314,7 +323,7 @@ hipError_t launch_quant_rows(int dt, const uint8_t* data, int dpad, int64_t r0, 
                              int dpad8, uint32_t* rsb, unsigned* maxes, hipStream_t st);
 hipError_t launch_pack_qtile_i8(const float* q, int nqb, int d, int dpad8, uint8_t* qt, float2* qfac, float* qeps,
                                 const unsigned* maxes, int* gcnt, u64* drop, hipStream_t st, int* fails = nullptr,
-                                const unsigned* l2max = nullptr, float gamma = 0.0f);
+                                const unsigned* l2max = nullptr, float gamma = 0.0f, int* seed_sync = nullptr);
 
 // ---- IVF-Flat (vs_ivf.hip) ---------------------------------------------------------------------
 // Inverted lists are chains of pages: a page is one row tile (TR rows, the flat layout above) of
@@ -396,8 +405,9 @@ void search_exact_device_parts(vs_index* ix, const float* q_dev, int64_t nq, int
 bool two_phase_ok(const vs_index* ix, int64_t nq, int k);
 vs_pending* search_phase_a(vs_index* ix, const float* q_dev, int64_t nq, int k, int world, int64_t id_offset,
                            double* S_a, int64_t* I_a, int stride, hipStream_t st);
+// (unres: this call's counter of queries the fallback round cannot certify; null = the index's)
 void search_phase_b(vs_pending* p, const double* floor_S, float* D, int64_t* I, double* S64, int stride,
-                    hipStream_t st);
+                    hipStream_t st, unsigned* unres = nullptr);
 void search_pending_free(vs_pending* p);
 // seed pass: screen one tile per workgroup (tile_stride) and write per-query 16-row-group maxima
 hipError_t launch_seed_mfma(int dt, const ScreenArgs& a, const uint8_t* qt, int nqb, hipStream_t st);

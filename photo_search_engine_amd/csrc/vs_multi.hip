@@ -9,7 +9,10 @@
 //   * a search runs every shard's exact search (vs_search_device_exact) concurrently, one host
 //     worker and one stream per device; each shard maps its local ids to global ids on its device
 //     and copies its (fp64 score, id) lists to device 0 over xGMI (peer copies); device 0 merges
-//     the G sorted lists (k_merge_shards: score, then lower global id) and returns D / I.
+//     the G sorted lists (k_merge_shards: score, then lower global id) and returns D / I;
+//   * with the int8 screen on bf16 / f16 shards (vs_two_phase_ok) the search is the two-phase
+//     step of the torch-distributed path: phase A on every device, the lists merged on device 0
+//     into a floor that goes back to every device, phase B, then the same final merge.
 // The merged order is total, so the result equals one index over all rows, bit for bit.
 // Concurrency (the reference serves from Flask's threaded server, /root/reference/main.py:353):
 // searches hold the handle's lock shared and lease a per-call context (streams, buffers, events,
@@ -118,9 +121,12 @@ void throw_rc(int rc) {
 struct MCtx {
     std::vector<hipStream_t> st;
     std::vector<DevBuf> qdev, S, I, unres_d;  // per device: queries, per-shard lists, unresolved count
+    std::vector<DevBuf> floor;                // per device: the two-phase floor (device 0's merged phase-A lists)
     std::vector<hipEvent_t> ready;            // per device: its lists landed on device 0
     unsigned* unres_h = nullptr;              // pinned, per device: this call's unresolved queries
     DevBuf gS, gI, oS, oI, oD;                // device 0: gathered [G][nq][k] lists, merged outputs
+    DevBuf fS, fI, fD;                        // device 0: the merged phase-A lists (two-phase step)
+    hipEvent_t floor_ready = nullptr;         // device 0: the floor is merged
     Pool* pool = nullptr;                     // one worker per device
 };
 
@@ -174,13 +180,14 @@ void destroy_ctx(vs_multi* m, MCtx* c) {
     for (int g = 0; g < (int)c->st.size(); ++g) {
         DeviceGuard dg(m->dev[g]);
         if (c->st[g]) (void)hipStreamSynchronize(c->st[g]);
-        for (DevBuf* b : {&c->qdev[g], &c->S[g], &c->I[g], &c->unres_d[g]}) b->release();
+        for (DevBuf* b : {&c->qdev[g], &c->S[g], &c->I[g], &c->unres_d[g], &c->floor[g]}) b->release();
         if (c->ready[g]) (void)hipEventDestroy(c->ready[g]);
         if (c->st[g]) (void)hipStreamDestroy(c->st[g]);
     }
     if (!m->dev.empty()) {
         DeviceGuard dg(m->dev[0]);
-        for (DevBuf* b : {&c->gS, &c->gI, &c->oS, &c->oI, &c->oD}) b->release();
+        for (DevBuf* b : {&c->gS, &c->gI, &c->oS, &c->oI, &c->oD, &c->fS, &c->fI, &c->fD}) b->release();
+        if (c->floor_ready) (void)hipEventDestroy(c->floor_ready);
     }
     if (c->unres_h) (void)hipHostFree(c->unres_h);
     delete c;
@@ -195,12 +202,17 @@ MCtx* make_ctx(vs_multi* m) {
     c->S.resize(G);
     c->I.resize(G);
     c->unres_d.resize(G);
+    c->floor.resize(G);
     try {
         for (int g = 0; g < G; ++g) {
             DeviceGuard dg(m->dev[g]);
             HIP_CHECK(hipStreamCreateWithFlags(&c->st[g], hipStreamNonBlocking));
             HIP_CHECK(hipEventCreateWithFlags(&c->ready[g], hipEventDisableTiming));
             c->unres_d[g].ensure(sizeof(unsigned));
+        }
+        {
+            DeviceGuard dg(m->dev[0]);
+            HIP_CHECK(hipEventCreateWithFlags(&c->floor_ready, hipEventDisableTiming));
         }
         HIP_CHECK(hipHostMalloc((void**)&c->unres_h, sizeof(unsigned) * G, hipHostMallocDefault));
         std::memset(c->unres_h, 0, sizeof(unsigned) * G);
@@ -234,6 +246,84 @@ struct CtxLease {
         m->ctx_idle.push_back(c);
     }
 };
+
+// Two-phase step over the devices (every shard non-empty and two_phase_ok): phase A on every
+// device -> its lists (global ids) to device 0 -> merged there into the floor -> the floor to every
+// device -> phase B (each shard's exact top-k, certified against the floor; its fallback round
+// counts into this call's counter) -> the lists to device 0's gather buffers.  The caller merges
+// them (the same final merge as the one-phase step).  A pending phase A is freed on every error.
+void multi_search_two_phase(vs_multi* m, MCtx* c, const float* q, int64_t nq, int kk) {
+    const int G = m->G;
+    const size_t lb = (size_t)nq * kk;
+    {
+        DeviceGuard dg(m->dev[0]);
+        c->fS.ensure(lb * sizeof(double));
+        c->fI.ensure(lb * sizeof(int64_t));
+        c->fD.ensure(lb * sizeof(float));
+    }
+    std::vector<vs_pending*> pend(G, nullptr);
+    auto free_all = [&] {
+        for (int g = 0; g < G; ++g) {
+            if (pend[g]) {
+                DeviceGuard dg(m->dev[g]);
+                search_pending_free(pend[g]);
+                pend[g] = nullptr;
+            }
+        }
+    };
+    try {
+        c->pool->run([&](int g) {  // phase A
+            DeviceGuard dg(m->dev[g]);
+            hipStream_t s = c->st[g];
+            c->qdev[g].ensure((size_t)nq * m->d * sizeof(float));
+            c->S[g].ensure(lb * sizeof(double));
+            c->I[g].ensure(lb * sizeof(int64_t));
+            c->floor[g].ensure(lb * sizeof(double));
+            c->unres_h[g] = 0;
+            HIP_CHECK(hipMemcpyAsync(c->qdev[g].p, q, (size_t)nq * m->d * sizeof(float), hipMemcpyHostToDevice, s));
+            int64_t* Ig = c->I[g].as<int64_t>();
+            pend[g] = search_phase_a(m->ix[g], c->qdev[g].as<float>(), nq, kk, G, 0, c->S[g].as<double>(), Ig, 1, s);
+            hipLaunchKernelGGL(k_local_to_global, dim3((unsigned)((lb + 255) / 256)), dim3(256), 0, s, Ig, (int64_t)lb, G, g);
+            HIP_CHECK(hipGetLastError());
+            HIP_CHECK(hipMemcpyPeerAsync(c->gS.as<double>() + lb * g, m->dev[0], c->S[g].p, m->dev[g], lb * sizeof(double), s));
+            HIP_CHECK(hipMemcpyPeerAsync(c->gI.as<int64_t>() + lb * g, m->dev[0], Ig, m->dev[g], lb * sizeof(int64_t), s));
+            HIP_CHECK(hipEventRecord(c->ready[g], s));
+        });
+        {  // the floor: the merged phase-A lists (a lower bound of every query's global k-th best)
+            DeviceGuard dg(m->dev[0]);
+            hipStream_t s0 = c->st[0];
+            for (int g = 1; g < G; ++g) HIP_CHECK(hipStreamWaitEvent(s0, c->ready[g], 0));
+            HIP_CHECK(launch_merge_shards(m->metric, c->gS.as<double>(), c->gI.as<int64_t>(), G, nq, kk, c->fS.as<double>(),
+                                          c->fI.as<int64_t>(), c->fD.as<float>(), s0));
+            HIP_CHECK(hipEventRecord(c->floor_ready, s0));
+        }
+        c->pool->run([&](int g) {  // phase B
+            DeviceGuard dg(m->dev[g]);
+            hipStream_t s = c->st[g];
+            const double* fl = c->fS.as<double>();
+            if (g != 0) {  // device 0's floor over xGMI
+                HIP_CHECK(hipStreamWaitEvent(s, c->floor_ready, 0));
+                HIP_CHECK(hipMemcpyPeerAsync(c->floor[g].p, m->dev[g], c->fS.p, m->dev[0], lb * sizeof(double), s));
+                fl = c->floor[g].as<double>();
+            }
+            unsigned* ud = c->unres_d[g].as<unsigned>();
+            HIP_CHECK(hipMemsetAsync(ud, 0, sizeof(unsigned), s));
+            int64_t* Ig = c->I[g].as<int64_t>();
+            vs_pending* p = pend[g];
+            pend[g] = nullptr;  // (phase B frees it, on success and on every error)
+            search_phase_b(p, fl, nullptr, Ig, c->S[g].as<double>(), 1, s, ud);
+            HIP_CHECK(hipMemcpyAsync(&c->unres_h[g], ud, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+            hipLaunchKernelGGL(k_local_to_global, dim3((unsigned)((lb + 255) / 256)), dim3(256), 0, s, Ig, (int64_t)lb, G, g);
+            HIP_CHECK(hipGetLastError());
+            HIP_CHECK(hipMemcpyPeerAsync(c->gS.as<double>() + lb * g, m->dev[0], c->S[g].p, m->dev[g], lb * sizeof(double), s));
+            HIP_CHECK(hipMemcpyPeerAsync(c->gI.as<int64_t>() + lb * g, m->dev[0], Ig, m->dev[g], lb * sizeof(int64_t), s));
+            HIP_CHECK(hipEventRecord(c->ready[g], s));
+        });
+    } catch (...) {
+        free_all();
+        throw;
+    }
+}
 
 }  // namespace
 
@@ -391,6 +481,14 @@ int vs_multi_search(vs_multi* m, const float* q, int64_t nq, int32_t k, float* D
             c->oI.ensure(lb * sizeof(int64_t));
             c->oD.ensure(lb * sizeof(float));
         }
+        // the two-phase step (as the torch-distributed path's, photo_search_engine_amd/distributed.py):
+        // every shard's phase A, the merged phase-A lists as a floor shared by all shards, then
+        // each shard's phase B scores only its share of the global refine window
+        bool two = G > 1;
+        for (int g = 0; g < G && two; ++g) two = vs_ntotal(m->ix[g]) > 0 && two_phase_ok(m->ix[g], nq, kk);
+        if (two) {
+            multi_search_two_phase(m, c, q, nq, kk);
+        } else {
         c->pool->run([&](int g) {
             DeviceGuard dg(m->dev[g]);
             hipStream_t s = c->st[g];
@@ -425,6 +523,7 @@ int vs_multi_search(vs_multi* m, const float* q, int64_t nq, int32_t k, float* D
             HIP_CHECK(hipMemcpyPeerAsync(c->gI.as<int64_t>() + lb * g, m->dev[0], Ig, m->dev[g], lb * sizeof(int64_t), s));
             HIP_CHECK(hipEventRecord(c->ready[g], s));
         });
+        }
         DeviceGuard dg(m->dev[0]);
         hipStream_t s0 = c->st[0];
         for (int g = 1; g < G; ++g) HIP_CHECK(hipStreamWaitEvent(s0, c->ready[g], 0));

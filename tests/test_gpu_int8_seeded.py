@@ -1,0 +1,181 @@
+"""The int8 direct main pass with its threshold seeded inside the kernel (k_screen_i8d_seeded,
+inner product, d a multiple of 256, >= 4 tiles per workgroup): each workgroup screens a sample
+tile first, publishes its 16-row-group maxima, and the workgroups select and adopt each query's
+seed themselves while they screen.  Results must be bit-exact against ``oracle.knn_exact`` on the
+stored values whatever the seed does: a provisional or a published threshold that lies only fails
+the certificate (the device fallback round re-searches), it never changes an answer.
+
+Cases: every storage dtype, k 1 / 10 / 100 / 1000, one and two query blocks, a partial last
+tile, near-copies of the queries planted in exactly the sample tiles (the selected seed sits
+among them: certificate failures, exact re-search), a sample tile holding a query's whole top-k
+(the provisional threshold lies), exact duplicates across the corpus (ties -> lower id), the
+device API with an id offset, and the two-phase sharded step's phase A / B.
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def FlatIndex():
+    from photo_search_engine_amd.index import FlatIndex as FI
+    return FI
+
+
+def _num_cu():
+    import torch
+    return torch.cuda.get_device_properties(0).multi_processor_count
+
+
+def _exact(ix, q, k):
+    x = ix.reconstruct_n(0, ix.ntotal)
+    D, I = ix.search(q, k)
+    S, Ie = O.knn_exact(x, q, k, "ip")
+    np.testing.assert_array_equal(I, Ie)
+    np.testing.assert_array_equal(D, S.astype(np.float32))
+    return D, I
+
+
+def _sample_tiles(tiles, G):
+    """Each workgroup's seed tile (loop index 0 of k_screen_i8d_seeded): position
+    p = b * T_b // G of its interleaved set b, b + G, ..."""
+    out = []
+    for b in range(G):
+        tb = (tiles - b + G - 1) // G
+        out.append(b + (b * tb // G) * G)
+    return out
+
+
+@pytest.mark.parametrize("dtype,d,nq,k,tpc", [
+    ("bf16", 512, 256, 10, 4.5),
+    ("f16", 512, 64, 100, 5.25),
+    ("f32", 768, 100, 1, 4.0),
+    ("bf16", 1536, 256, 100, 4.8),
+    ("bf16", 512, 300, 25, 6.1),   # two query blocks (256 + 44)
+    ("bf16", 512, 32, 1000, 4.2),  # deep screens: compaction inside the K loop
+])
+def test_seeded_direct_exact(FlatIndex, dtype, d, nq, k, tpc):
+    G = _num_cu()
+    N = int(256 * G * tpc) + 77  # a partial last tile
+    ix = FlatIndex(d, "ip", dtype)
+    ix.add_synthetic(O.SEED_CORPUS + 9, 0, N, True)
+    ix.set_screen("int8")
+    q = O.synth_rows(O.SEED_QUERIES + 9, 0, nq, d, True, "f32")
+    _exact(ix, q, k)
+    assert ix.uncertified_count() == 0
+    assert ix.unresolved_count() == 0
+    ix.close()
+
+
+def test_seeded_native_and_int8_identical_at_cfg3_width(FlatIndex):
+    G = _num_cu()
+    N, d, nq, k = 256 * G * 5 + 1, 1536, 128, 100
+    ix = FlatIndex(d, "ip", "bf16")
+    ix.add_synthetic(O.SEED_CORPUS, 0, N, True)
+    q = O.synth_rows(O.SEED_QUERIES, 0, nq, d, True, "f32")
+    Dn, In = ix.search(q, k)
+    ix.set_screen("int8")
+    for _ in range(3):  # repeated launches: the counters and thresholds are per launch
+        D8, I8 = ix.search(q, k)
+        np.testing.assert_array_equal(I8, In)
+        np.testing.assert_array_equal(D8, Dn)
+    assert ix.uncertified_count() == 0
+    ix.close()
+
+
+def test_seeded_planted_sample_tiles_fall_back_exactly(FlatIndex):
+    # near-copies of 16 queries in exactly the sample tiles (4 rows per tile, ~64 per query, in one
+    # 16-row group each): the rank-r seed lands among them, too few rows are listed, the
+    # certificate rejects and the fallback round re-searches -- the answer stays exact
+    G = _num_cu()
+    d, k, nq = 512, 10, 16
+    tiles = 6 * G + 5
+    N = tiles * 256
+    x = O.synth_rows(O.SEED_CORPUS, 0, N, d, True, "f32")
+    q = O.synth_rows(O.SEED_QUERIES, 0, nq, d, True, "f32")
+    rng = np.random.default_rng(17)
+    for j, t in enumerate(_sample_tiles(tiles, G)):
+        for r in range(4):
+            x[t * 256 + 3 + r] = q[(4 * j + r) % nq] + 0.01 * rng.standard_normal(d).astype(np.float32)
+    ix = FlatIndex(d, "ip", "bf16")
+    ix.add(x)
+    ix.set_screen("int8")
+    qb = O.round_dtype(q, "bf16")
+    _exact(ix, np.concatenate([qb, qb]), k)  # 32 queries: the MFMA path
+    assert ix.uncertified_count() > 0
+    assert ix.unresolved_count() == 0
+    ix.close()
+
+
+def test_seeded_sample_tile_holding_the_top_k(FlatIndex):
+    # one sample tile holds 200 near-copies of query 0 spread over all 16 of its groups: its
+    # provisional threshold (4th group maximum) drops most of them in that tile's own epilogue --
+    # the drop bound must make the certificate fail rather than return a wrong answer
+    G = _num_cu()
+    d, k, nq = 512, 100, 24
+    tiles = 5 * G + 1
+    N = tiles * 256
+    x = O.synth_rows(O.SEED_CORPUS + 1, 0, N, d, True, "f32")
+    q = O.synth_rows(O.SEED_QUERIES + 1, 0, nq, d, True, "f32")
+    t = _sample_tiles(tiles, G)[G // 3]
+    rng = np.random.default_rng(5)
+    x[t * 256:t * 256 + 200] = q[0] + 0.05 * rng.standard_normal((200, d)).astype(np.float32)
+    ix = FlatIndex(d, "ip", "f16")
+    ix.add(x)
+    ix.set_screen("int8")
+    _exact(ix, q, k)
+    assert ix.unresolved_count() == 0
+    ix.close()
+
+
+def test_seeded_exact_duplicates_tie_to_lower_id(FlatIndex):
+    G = _num_cu()
+    d, k, nq = 512, 20, 40
+    N = 256 * G * 4 + 300
+    x = O.synth_rows(O.SEED_CORPUS + 2, 0, N, d, True, "f32")
+    q = O.synth_rows(O.SEED_QUERIES + 2, 0, nq, d, True, "f32")
+    # each query's best-matching row copied 12 times across the corpus (exact score ties)
+    S, I = O.knn_exact(O.round_dtype(x, "bf16"), O.round_dtype(q, "bf16"), 1, "ip")
+    rng = np.random.default_rng(3)
+    for qi in range(nq):
+        for pos in rng.choice(N, 12, replace=False):
+            x[pos] = x[I[qi, 0]]
+    ix = FlatIndex(d, "ip", "bf16")
+    ix.add(x)
+    ix.set_screen("int8")
+    _exact(ix, O.round_dtype(q, "bf16"), k)
+    ix.close()
+
+
+def test_seeded_device_api_with_offset_and_phases(FlatIndex):
+    import torch
+    G = _num_cu()
+    d, nq, k = 512, 64, 30
+    N = 256 * G * 4 + 999
+    ix = FlatIndex(d, "ip", "bf16")
+    ix.add_synthetic(O.SEED_CORPUS + 3, 0, N, True)
+    ix.set_screen("int8")
+    x = ix.reconstruct_n(0, N)
+    q = O.synth_rows(O.SEED_QUERIES + 3, 0, nq, d, True, "f32")
+    Se, Ie = O.knn_exact(x, q, k, "ip")
+    qd = torch.from_numpy(q).cuda()
+    S = torch.empty((nq, k), dtype=torch.float64, device="cuda")
+    I = torch.empty((nq, k), dtype=torch.int64, device="cuda")
+    D = torch.empty((nq, k), dtype=torch.float32, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    ix.search_device_exact(qd.data_ptr(), nq, k, D.data_ptr(), I.data_ptr(), S.data_ptr(), 1000, stream)
+    np.testing.assert_array_equal(I.cpu().numpy(), Ie + 1000)
+    np.testing.assert_array_equal(S.cpu().numpy(), Se)
+    # the two-phase step on this one index (its own phase-A lists as the floor) equals the search
+    assert ix.two_phase_ok(nq, k)
+    Sa = torch.empty((nq, k), dtype=torch.float64, device="cuda")
+    Ia = torch.empty((nq, k), dtype=torch.int64, device="cuda")
+    p = ix.search_phase_a(qd.data_ptr(), nq, k, 1, Sa.data_ptr(), Ia.data_ptr(), 0, stream)
+    ix.search_phase_b(p, Sa.data_ptr(), D.data_ptr(), I.data_ptr(), S.data_ptr(), stream)
+    np.testing.assert_array_equal(I.cpu().numpy(), Ie)
+    np.testing.assert_array_equal(S.cpu().numpy(), Se)
+    assert ix.unresolved_count() == 0
+    ix.close()

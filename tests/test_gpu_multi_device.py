@@ -154,3 +154,40 @@ def test_failed_add_rolls_back_every_shard(Multi, tmp_path):
     q = O.synth_rows(O.SEED_QUERIES + 62, 0, 12, d, True, "f32")
     _exact(ix, x, q, 10, "ip")
     ix.close()
+
+
+@pytest.mark.parametrize("metric,dtype,nq,k,N,d", [
+    ("ip", "bf16", 64, 25, 400_000, 512),    # three shards of ~133k rows: the direct int8 screen
+    ("ip", "f16", 256, 100, 300_000, 256),
+    ("l2", "bf16", 40, 10, 250_000, 512),
+    ("ip", "bf16", 9, 1, 200_000, 768),      # the smallest two-phase batch
+])
+def test_int8_two_phase_step_matches_one_index(Multi, metric, dtype, nq, k, N, d):
+    # int8 screen on bf16 / f16 shards: vs_multi_search takes the two-phase step (phase A on every
+    # device, the merged phase-A lists as every shard's floor, phase B, the final merge) -- the
+    # answer must equal one index over all rows, bit for bit
+    x = O.synth_rows(O.SEED_CORPUS + 7, 0, N, d, True, dtype)
+    ix = Multi(d, metric, dtype, devices=[0, 0, 0])
+    ix.add(x)
+    ix.set_screen("int8")
+    q = O.synth_rows(O.SEED_QUERIES + 7, 0, nq, d, True, "f32")
+    for _ in range(2):  # (leased contexts reused)
+        _exact(ix, x, q, k, metric)
+    ix.close()
+
+
+def test_int8_two_phase_concurrent_searches(Multi):
+    from concurrent.futures import ThreadPoolExecutor
+    N, d, k = 300_000, 512, 20
+    x = O.synth_rows(O.SEED_CORPUS + 8, 0, N, d, True, "bf16")
+    ix = Multi(d, "ip", "bf16", devices=[0, 0, 0])
+    ix.add(x)
+    ix.set_screen("int8")
+    qs = [O.synth_rows(O.SEED_QUERIES + 8, 100 * t, 16 + 8 * t, d, True, "f32") for t in range(6)]
+    want = [O.knn_exact(x, q, k, "ip") for q in qs]
+    with ThreadPoolExecutor(6) as ex:
+        got = list(ex.map(lambda t: ix.search(qs[t], k), range(6)))
+    for (D, I), (S, Ie) in zip(got, want):
+        np.testing.assert_array_equal(I, Ie)
+        np.testing.assert_array_equal(D, S.astype(np.float32))
+    ix.close()
