@@ -420,3 +420,96 @@ def heuristic_graph(x_stored, M: int, ef_construction: int, metric="ip", levels=
     return {"assign_probas": probas, "cum_nneighbor_per_level": cum, "levels": (lev + 1).astype(np.int32),
             "offsets": offsets, "neighbors": nb, "entry_point": int(np.nonzero(lev == top)[0][0]) if n else -1,
             "max_level": top, "efConstruction": int(ef_construction), "efSearch": 16, "upper_beam": 1}
+
+
+# ---------------------------------------------------------------------------------------------
+# incremental build: faiss's insertion (IndexHNSWFlat.add of new rows), batched
+# ---------------------------------------------------------------------------------------------
+def draw_levels(n: int, probas, seed: int = 12345) -> np.ndarray:
+    """0-based node levels as ``VectorStore._build_graph`` draws them (numpy's generator, seeded;
+    faiss's ``random_level`` rule over ``assign_probas``).  The stream is prefix-consistent: the
+    first n of a longer draw are these, so a graph extended row by row keeps every old level."""
+    f = np.random.default_rng(seed).random(n)
+    lev = np.full(n, len(probas) - 1, dtype=np.int64)
+    open_ = np.ones(n, dtype=bool)
+    for level, p in enumerate(probas):
+        hit = open_ & (f < p)
+        lev[hit] = level
+        open_ &= ~hit
+        f[open_] -= p
+    return lev
+
+
+def insert_batch(x_stored, graph: dict, n_old: int, ef_construction: int, metric="ip", seed: int = 12345,
+                 cmax: int = HP_C_MAX) -> dict:
+    """The graph ``hnsw.insert_rows`` makes of ``graph`` (nodes [0, n_old)) and the new rows
+    [n_old, n) of ``x_stored``, restated.  faiss inserts one node at a time: on each of its levels
+    it takes efConstruction candidates from a beam over the graph so far, keeps a shrunk list
+    (``shrink_neighbor_list``) and links back (``add_link``).  The batch form: for a new node u and
+    each level l <= level(u), its candidates are
+      * level 0: the best C = max(efConstruction, width) of a beam search over the OLD graph
+        (``_search_one``, ef = efConstruction, k = C), and
+      * level >= 1: the exact best C old level-l members (the upper levels are small),
+    together with the exact best C new nodes of level >= l (itself excluded); the union goes through
+    the heuristic, forward lists first; then every node v named by a new forward list receives the
+    new sources: a new v keeps its forward list followed by them (ascending, unlisted ones), an old
+    v its old list followed by them -- unpruned while that fits the width, else shrunk over the
+    union (cut at ``cmax`` first).  A new node above the old top level becomes the entry point
+    (the first such of the highest level)."""
+    x = np.asarray(x_stored, dtype=np.float32)
+    n = x.shape[0]
+    probas = np.asarray(graph["assign_probas"])
+    cum = np.asarray(graph["cum_nneighbor_per_level"])
+    old_lev = np.asarray(graph["levels"], dtype=np.int64)[:n_old] - 1
+    lev = np.concatenate([old_lev, draw_levels(n, probas, seed)[n_old:]])  # new node i: entry i of the draw
+    dist = _distances(x, x, metric)
+    offsets = np.zeros(n + 1, dtype=np.uint64)
+    offsets[1:] = np.cumsum(cum[lev + 1].astype(np.uint64))
+    nb = np.full(int(offsets[-1]), -1, dtype=np.int32)
+    old_off = np.asarray(graph["offsets"], dtype=np.uint64)
+    nb[:int(old_off[n_old])] = np.asarray(graph["neighbors"], dtype=np.int32)[:int(old_off[n_old])]
+    old = {"levels": old_lev + 1, "offsets": old_off[:n_old + 1], "neighbors": graph["neighbors"],
+           "cum_nneighbor_per_level": cum, "entry_point": graph["entry_point"], "max_level": graph["max_level"]}
+    new = np.arange(n_old, n)
+    top_new = int(lev[new].max()) if new.size else -1
+    for level in range(max(top_new, -1), -1, -1):
+        width = int(cum[level + 1] - cum[level])
+        C = min(max(int(ef_construction), width), cmax)
+        nmem = new[lev[new] >= level]
+        omem = np.nonzero(old_lev >= level)[0]
+        cands = {}
+        for u in nmem:
+            u = int(u)
+            if level == 0 and n_old > 0:
+                # the beam over the old graph: its rows only (distance row restricted to [0, n_old))
+                res = _search_one(old, dist[u, :n_old], C, int(ef_construction))
+                oc = [v for _, v in res]
+            else:
+                oc = [int(v) for v in omem[np.lexsort((omem, dist[u, omem]))[:C]]] if omem.size else []
+            others = nmem[nmem != u]
+            bc = [int(v) for v in others[np.lexsort((others, dist[u, others]))[:C]]] if others.size else []
+            cands[u] = sorted(set(oc) | set(bc))
+        F = {int(u): shrink_neighbor_list(dist, int(u), cands[int(u)], width) for u in nmem}
+        R = {}
+        for u in sorted(F):
+            for v in F[u]:
+                R.setdefault(v, []).append(u)
+        for v in sorted(set(F) | set(R)):
+            base = int(offsets[v]) + int(cum[level])
+            if v >= n_old:
+                head = F[v]
+            else:
+                head = [int(t) for t in nb[base:base + width] if t >= 0]
+            hs = set(head)
+            U = (head + [u for u in sorted(R.get(v, [])) if u not in hs])[:cmax]
+            row = U if len(U) <= width else shrink_neighbor_list(dist, v, U, width)
+            nb[base:base + width] = -1
+            nb[base:base + len(row)] = row
+    entry, top = int(graph["entry_point"]), int(graph["max_level"])
+    if top_new > top or entry < 0:
+        top = top_new
+        entry = int(new[lev[new] == top_new][0])
+    out = dict(graph)
+    out.update({"levels": (lev + 1).astype(np.int32), "offsets": offsets, "neighbors": nb, "entry_point": entry,
+                "max_level": top, "efConstruction": int(ef_construction)})
+    return out

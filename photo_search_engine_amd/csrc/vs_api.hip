@@ -366,6 +366,22 @@ int i8_gemv_depth(const vs_index* ix, int k) {
 constexpr double kI8Window = 15.0;
 constexpr double kI8UnionMaxPerK = 64.0;
 constexpr double kI8UnionMin = 1024.0;
+// The in-kernel seed's provisional threshold on a sample tile: the j-th largest of its 16
+// group maxima, j the smallest rank that the published seed (the rank whose share of all maxima is
+// p) exceeds except with probability < 1e-4 per (tile, query): P(Binomial(16, p) >= j) < 1e-4.
+int i8d_provisional_rank(double p) {
+    p = std::min(1.0, std::max(0.0, p));
+    for (int j = 1; j <= 16; ++j) {
+        double tail = 0.0;  // P(X >= j), X ~ Binomial(16, p)
+        for (int i = j; i <= 16; ++i) {
+            double c = 1.0;
+            for (int t = 0; t < i; ++t) c = c * (16 - t) / (t + 1);
+            tail += c * std::pow(p, i) * std::pow(1.0 - p, 16 - i);
+        }
+        if (tail < 1e-4) return j;
+    }
+    return 16;
+}
 double i8_union_target(int k, double sampled, double n) {
     const double need = kI8Window * k;
     double u = std::max(need, kI8UnionMin);
@@ -440,6 +456,7 @@ void search_block_i8(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float
         a.seed_sync = c->seedsync.as<int>();
         a.thr_out = c->thr0.as<u64>();
         a.seed_rank = seed_rank_of((double)a.G * TR, M);
+        a.seed_prov_rank = i8d_provisional_rank((double)a.seed_rank / M);
     } else if (seeded) {  // optimistic threshold seed from one tile per workgroup
         ScreenArgs sa = a;
         sa.G = std::min(sa.G, 512);

@@ -210,6 +210,7 @@ struct ScreenArgs {
                              // (zeroed by the query pack); null = no in-kernel seeding
     u64* thr_out;            // [QB] the selected thresholds (the refine's thr0)
     int seed_rank;           // rank of the selected maximum among the G * 16 of a query
+    int seed_prov_rank;      // the sample tile's own provisional threshold: this rank of its 16 maxima
 };
 constexpr int MAP_DESC = 8;
 constexpr int kI8dSeedMaxima = 4096;  // G * 16 group maxima per query the in-kernel seed select holds

@@ -1418,15 +1418,17 @@ __device__ __forceinline__ void gld16(intx4& v, const void* p) {
 // The separate seed pass + k_seed_select (two launches, ~50 us per cfg3 batch) become part of the
 // main pass: each workgroup's FIRST tile is its sample (spread over the shard), whose 16-row-group
 // key maxima it publishes (seedmax) before counting itself in (seed_sync[0]); that tile's own
-// epilogue uses a provisional threshold (the 4th largest of its 16 group maxima, folded into drop
-// so the refine's certificate covers it).  Once every workgroup has arrived, each query's
+// epilogue uses a provisional threshold (a rank of its 16 group maxima that the published seed
+// exceeds with near certainty; where it does not, it goes into drop, the refine certificate's
+// bound).  Once every workgroup has arrived, each query's
 // rank-th largest maximum is selected by whichever workgroup claims it at a tile boundary
 // (seed_sync[2]) and published (thr_out, seed_sync[1]); a workgroup adopts the thresholds at the
 // first tile boundary after all are published.  No workgroup ever waits for another: polls are
 // loads issued one tile ahead, and whatever is left unclaimed when a workgroup finishes its tiles
 // it selects itself (the last to arrive selects all that remain), so thr_out is complete when the
-// kernel ends.  Rows rejected before a workgroup adopts are below its provisional / compaction
-// threshold (drop), after it below thr_out: the refine certifies against max(thr_out, drop).
+// kernel ends.  Rows rejected before a workgroup adopts are below the threshold then in force, which
+// is either below thr_out or folded into drop at adoption (at the end, if it never adopts); after
+// it below max(thr_out, drop): the refine certifies against max(thr_out, drop).
 constexpr int I8D_SEED_VPT = 8;  // 512 threads x 8 = the G * 16 <= 4096 maxima of one query
 // the seeding's pointers are kept in LDS (written once at kernel start) and read in the cold blocks
 // that use them: no SGPRs held across the K loop for them
@@ -1525,19 +1527,32 @@ __device__ __forceinline__ void i8d_seed_select(const ScreenArgs& a, int c, unsi
 }
 
 // adopt the published thresholds (every query's): raise the workgroup's own where they are lower
+// Rows rejected before this point are below the threshold in force (thr_key: the provisional one
+// or a compaction bound); where that is above the published threshold it goes into drop (the
+// certificate's bound), else the published one -- which the refine reads as thr0 -- covers them.
 __device__ __forceinline__ void i8d_seed_adopt(const int* sst, int nqb, u64* thr_key, float* thr_f, float4* qrec) {
     __threadfence();  // acquire: each threshold was released before its count
     const int tid = vtid_here();
+    const SeedPtrs* sp = (const SeedPtrs*)(sst + 8);
     if (tid < nqb) {
-        const u64 v = __hip_atomic_load(lds_ptr(&((const SeedPtrs*)(sst + 8))->thr_out) + tid, __ATOMIC_RELAXED,
-                                        __HIP_MEMORY_SCOPE_AGENT);
-        if (v > thr_key[tid]) {
+        const u64 v = __hip_atomic_load(lds_ptr(&sp->thr_out) + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const u64 cur = thr_key[tid];
+        if (v > cur) {
             const float f = key_score(v);
             thr_key[tid] = v;
             thr_f[tid] = f;
             qrec[tid].z = f;
+        } else if (cur > v) {
+            atomicMax(lds_ptr(&sp->drop) + tid, cur);
         }
     }
+    __syncthreads();
+}
+// a workgroup that never adopted: every threshold it used is at most its last, into drop
+__device__ __forceinline__ void i8d_seed_unadopted(const int* sst, int nqb, const u64* thr_key) {
+    const int tid = vtid_here();
+    const SeedPtrs* sp = (const SeedPtrs*)(sst + 8);
+    if (tid < nqb && thr_key[tid] != 0ull) atomicMax(lds_ptr(&sp->drop) + tid, thr_key[tid]);
     __syncthreads();
 }
 
@@ -1945,26 +1960,30 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
                     }
                 }
                 __syncthreads();
-                if (stid < nqb) {  // provisional threshold: the 4th largest group maximum of the sample
-                    float t4[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+                if (stid < nqb) {
+                    // provisional threshold: the seed_prov_rank-th largest of the sample's 16 group
+                    // maxima (a rank the published seed exceeds with near certainty; i8d_seed_adopt
+                    // accounts for it where it does not)
+                    const int pr = a.seed_prov_rank;
+                    float tp = -INFINITY;
 #pragma unroll
                     for (int g = 0; g < 16; ++g) {
-                        float x = gm[stid * 16 + g];
+                        const float x = gm[stid * 16 + g];
+                        int above = 0;  // maxima ahead of x: larger, or equal at a lower group
 #pragma unroll
-                        for (int i = 0; i < 4; ++i) {
-                            const float hi = fmaxf(t4[i], x);
-                            x = fminf(t4[i], x);
-                            t4[i] = hi;
+                        for (int h = 0; h < 16; ++h) {
+                            const float y = gm[stid * 16 + h];
+                            above += (y > x || (y == x && h < g)) ? 1 : 0;
                         }
+                        if (above == pr - 1) tp = x;
                     }
-                    if (t4[3] > -INFINITY) {
-                        const u64 k4 = (u64)ord_f32(t4[3]) << 32;
-                        if (k4 > thr_key[stid]) {
-                            thr_key[stid] = k4;
-                            thr_f[stid] = t4[3];
-                            qrec[stid].z = t4[3];
+                    if (tp > -INFINITY) {
+                        const u64 kp = (u64)ord_f32(tp) << 32;
+                        if (kp > thr_key[stid]) {
+                            thr_key[stid] = kp;
+                            thr_f[stid] = tp;
+                            qrec[stid].z = tp;
                         }
-                        atomicMax(lds_ptr(&sp->drop) + stid, k4);  // rows below it go unlisted: the certificate's bound
                     }
                 }
                 __threadfence();  // release this workgroup's maxima before counting it in
@@ -2036,6 +2055,7 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
 #undef I8D_BODY
     if constexpr (SEEDK) {
         mf_barrier_drain();  // (the dummy steps' loads and the last poll)
+        if (!seed_adopted) i8d_seed_unadopted(sst, nqb, thr_key);
         i8d_seed_help(a, nqb, shist, sst);
     }
     // ---- flush: pool -> buffers, then the best <= Kp per query -> the query's survivor list ----
@@ -3634,6 +3654,7 @@ static hipError_t launch_mfma_dt(int dt, const ScreenArgs& a, const uint8_t* qt,
             if (a.seed_acc || a.tile_stride != 0) return hipErrorInvalidValue;
             if (a.seed_sync) {  // threshold seeded in the kernel (inner product; L2 keeps the seed pass)
                 if (a.metric != METRIC_IP || !a.seedmax || !a.thr_out || !a.drop || a.thr0 || a.seed_rank < 1 ||
+                    a.seed_prov_rank < 1 || a.seed_prov_rank > 16 ||
                     a.G * 16 > kI8dSeedMaxima || (int64_t)a.tiles < 4 * (int64_t)a.G)
                     return hipErrorInvalidValue;
                 set_lds_attr((const void*)k_screen_i8d_seeded, I8D_LDS + I8D_SEED_LDS);

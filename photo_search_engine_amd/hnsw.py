@@ -137,3 +137,164 @@ def select_level(index, members, cand, W: int, cmax: int = HP_C_MAX) -> np.ndarr
         Ub = U[big, :int(counts[big].max())]
         out[big] = prune_neighbors(index, members[big], Ub, W)
     return out
+
+
+# ---------------------------------------------------------------------------------------------
+# incremental build (faiss IndexHNSWFlat.add of new rows, batched)
+# ---------------------------------------------------------------------------------------------
+def draw_levels(n: int, probas, seed: int = 12345) -> np.ndarray:
+    """0-based node levels: faiss's ``random_level`` rule over ``assign_probas`` with numpy's
+    generator (seeded; not faiss's).  Prefix-consistent: a longer draw starts with these, so a
+    graph extended by insertions keeps every old node's level."""
+    f = np.random.default_rng(seed).random(n)
+    lev = np.full(n, len(probas) - 1, dtype=np.int64)
+    open_ = np.ones(n, dtype=bool)
+    for level, p in enumerate(probas):
+        hit = open_ & (f < p)
+        lev[hit] = level
+        open_ &= ~hit
+        f[open_] -= p
+    return lev
+
+
+def beam_search(index, graph: dict, q: np.ndarray, k: int, ef: int) -> np.ndarray:
+    """Ids (nq x k, -1 padded) of faiss's HNSW search over ``graph`` (the GPU kernel, or the
+    index's own ``hnsw_search`` where it has one)."""
+    f = getattr(index, "hnsw_search", None)
+    if f is not None:
+        return f(graph, q, k, ef)
+    g = HNSWGraph(index, graph, ef)
+    try:
+        return g.search(q, k, ef)[1]
+    finally:
+        g.close()
+
+
+def _exact_candidates(make_index, index, members: np.ndarray, queries: np.ndarray, C: int,
+                      exclude_self: bool) -> list:
+    """Per query node (global id in ``queries``): its exact best C of ``members`` (ascending global
+    ids), by a temporary flat index over their stored values (ties -> lower id), itself excluded."""
+    out = [[] for _ in range(queries.shape[0])]
+    m = int(members.shape[0])
+    if m == 0 or queries.shape[0] == 0:
+        return out
+    tmp = make_index()
+    try:
+        for r0 in range(0, m, 65536):
+            tmp.add(np.ascontiguousarray(_rows(index, members[r0:r0 + 65536])))
+        kk = min(m, C + (1 if exclude_self else 0))
+        for r0 in range(0, queries.shape[0], 4096):
+            qs = queries[r0:r0 + 4096]
+            _, I = tmp.search(np.ascontiguousarray(_rows(index, qs)), kk)
+            for a in range(qs.shape[0]):
+                row = [int(members[i]) for i in I[a] if i >= 0]
+                if exclude_self:
+                    row = [v for v in row if v != int(qs[a])]
+                out[r0 + a] = row[:C]
+    finally:
+        close = getattr(tmp, "close", None)
+        if close:
+            close()
+    return out
+
+
+def _rows(index, ids: np.ndarray) -> np.ndarray:
+    """Stored values of rows ``ids`` (ascending or not), by contiguous runs."""
+    ids = np.asarray(ids, dtype=np.int64)
+    out = np.empty((ids.shape[0], index.d), dtype=np.float32)
+    if ids.size == 0:
+        return out
+    order = np.argsort(ids, kind="stable")
+    s = ids[order]
+    cuts = np.nonzero(np.diff(s) != 1)[0] + 1
+    for seg in np.split(np.arange(s.shape[0]), cuts):
+        lo, hi = int(s[seg[0]]), int(s[seg[-1]]) + 1
+        out[order[seg]] = index.reconstruct_n(lo, hi - lo)
+    return out
+
+
+def insert_rows(index, graph: dict, n_old: int, n: int, ef_construction: int, make_index, seed: int = 12345,
+                batch: int = 4096, cmax: int = HP_C_MAX) -> dict:
+    """Extend ``graph`` (nodes [0, n_old) of ``index``'s rows) to nodes [0, n) the way faiss's
+    ``IndexHNSWFlat.add`` inserts rows (/root/reference/utils/vector_store.py:164), in batches of
+    ``batch`` rows: for a new node on each of its levels, the candidates are the best C =
+    max(efConstruction, width) old nodes -- on level 0 from faiss's search over the old graph
+    (beam efConstruction), above it exactly (the upper levels are small) -- together with the
+    exact best C new nodes of that level; the heuristic keeps its forward list
+    (``vs_hnsw_prune``); every node it names gets the new sources appended (faiss ``add_link``),
+    the list re-shrunk over the union when it would overflow.  A new node above the old top level
+    becomes the entry point.  Equal to ``oracle/hnsw_oracle.py insert_batch`` batch by batch."""
+    while n_old < n:
+        n1 = min(n, n_old + int(batch))
+        graph = _insert_batch(index, graph, n_old, n1, int(ef_construction), make_index, seed, cmax)
+        n_old = n1
+    return graph
+
+
+def _insert_batch(index, graph: dict, n_old: int, n: int, ef_construction: int, make_index, seed: int,
+                  cmax: int) -> dict:
+    probas = np.asarray(graph["assign_probas"])
+    cum = np.asarray(graph["cum_nneighbor_per_level"]).astype(np.int64)
+    # old nodes keep the graph's levels (a faiss-built graph's included); new node i gets entry i of
+    # this build's draw
+    old_lev = np.asarray(graph["levels"], dtype=np.int64)[:n_old] - 1
+    lev = np.concatenate([old_lev, draw_levels(n, probas, seed)[n_old:]])
+    offsets = np.zeros(n + 1, dtype=np.uint64)
+    offsets[1:] = np.cumsum(cum[lev + 1].astype(np.uint64))
+    old_off = np.asarray(graph["offsets"], dtype=np.uint64)
+    nb = np.full(int(offsets[-1]), -1, dtype=np.int32)
+    nb[:int(old_off[n_old])] = np.asarray(graph["neighbors"], dtype=np.int32)[:int(old_off[n_old])]
+    old = dict(graph, levels=(old_lev + 1).astype(np.int32), offsets=old_off[:n_old + 1],
+               neighbors=np.ascontiguousarray(np.asarray(graph["neighbors"], dtype=np.int32)[:int(old_off[n_old])]))
+    new = np.arange(n_old, n, dtype=np.int64)
+    top_new = int(lev[new].max()) if new.size else -1
+    for level in range(top_new, -1, -1):
+        width = int(cum[level + 1] - cum[level])
+        C = min(max(ef_construction, width), cmax)
+        nmem = new[lev[new] >= level]
+        omem = np.nonzero(old_lev >= level)[0]
+        if level == 0 and n_old > 0:
+            I = beam_search(index, old, np.ascontiguousarray(_rows(index, nmem)), C, ef_construction)
+            oc = [[int(v) for v in row if v >= 0] for row in I]
+        else:
+            oc = _exact_candidates(make_index, index, omem, nmem, C, exclude_self=False)
+        bc = _exact_candidates(make_index, index, nmem, nmem, C, exclude_self=True)
+        union = [sorted(set(a) | set(b)) for a, b in zip(oc, bc)]
+        U = np.full((nmem.shape[0], max(1, max((len(u) for u in union), default=1))), -1, dtype=np.int32)
+        for i, u in enumerate(union):
+            U[i, :len(u)] = u
+        F = index.hnsw_prune(nmem, U, width) if nmem.size else np.zeros((0, width), dtype=np.int32)
+        # reverse links: every node named by a new forward list gets the new sources
+        src = {}
+        for i, u in enumerate(nmem.tolist()):
+            for v in F[i][F[i] >= 0].tolist():
+                src.setdefault(v, []).append(u)
+        fwd = {u: F[i][F[i] >= 0].tolist() for i, u in enumerate(nmem.tolist())}
+        targets = sorted(set(fwd) | set(src))
+        heads, lists = [], []
+        for v in targets:
+            base = int(offsets[v]) + int(cum[level])
+            head = fwd[v] if v >= n_old else [int(t) for t in nb[base:base + width] if t >= 0]
+            hs = set(head)
+            lists.append((head + [u for u in sorted(src.get(v, [])) if u not in hs])[:cmax])
+            heads.append(v)
+        big = [i for i, L in enumerate(lists) if len(L) > width]
+        if big:
+            Ub = np.full((len(big), max(len(lists[i]) for i in big)), -1, dtype=np.int32)
+            for r, i in enumerate(big):
+                Ub[r, :len(lists[i])] = lists[i]
+            shr = index.hnsw_prune(np.array([heads[i] for i in big], dtype=np.int64), Ub, width)
+            for r, i in enumerate(big):
+                lists[i] = shr[r][shr[r] >= 0].tolist()
+        for v, L in zip(heads, lists):
+            base = int(offsets[v]) + int(cum[level])
+            nb[base:base + width] = -1
+            nb[base:base + len(L)] = L
+    entry, top = int(graph["entry_point"]), int(graph["max_level"])
+    if new.size and (top_new > top or entry < 0):
+        top = top_new
+        entry = int(new[lev[new] == top_new][0])
+    out = dict(graph)
+    out.update({"levels": (lev + 1).astype(np.int32), "offsets": offsets, "neighbors": nb, "entry_point": entry,
+                "max_level": top, "efConstruction": int(ef_construction)})
+    return out

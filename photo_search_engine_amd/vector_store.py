@@ -67,8 +67,9 @@ _index_factory = _default_index_factory
 
 
 def _hnsw_graph_max_rows() -> int:
-    """Largest index saved as an HNSW (IHNf) file under ``index_type="hnsw"``; above it the
-    exact k-NN graph build is skipped and a flat file is written (this backend loads both)."""
+    """Rows of an ``index_type="hnsw"`` store whose graph is built at once from exact candidates
+    (:meth:`VectorStore._build_graph`); rows beyond it are inserted into that graph in batches,
+    faiss's way (:func:`hnsw.insert_rows`), so every save writes an IHNf file whatever the size."""
     return int(os.environ.get("VECTOR_HNSW_GRAPH_MAX_ROWS", "200000") or 200000)
 
 
@@ -312,10 +313,11 @@ class VectorStore:
         # written -- the bytes are identical to a full rewrite.  Payload bytes stream HBM -> file.
         n, d, mt = int(self.index.ntotal), int(self.index.d), int(self.index.metric_type)
         old = self._appendable_rows(d, mt)
-        if self.index_type == "hnsw" and n <= _hnsw_graph_max_rows():
-            # an IHNf file the reference's faiss can load (rollback); a graph loaded from file is
-            # kept, with efSearch as configured (the reference sets hnsw.efSearch after every load,
-            # utils/vector_store.py:135, and faiss writes it back)
+        if self.index_type == "hnsw":
+            # an IHNf file the reference's faiss can load (rollback), at every size; a graph loaded
+            # from file is kept (rows added since are inserted into it), with efSearch as configured
+            # (the reference sets hnsw.efSearch after every load, utils/vector_store.py:135, and faiss
+            # writes it back)
             graph = (dict(self._graph_arrays, efSearch=self.hnsw_ef_search) if self._graph_covers(n) else
                      self._build_graph(n))
             faiss_format.write_hnsw(self.index_path, graph, d, n, mt, lambda path, off: self.index.write_rows(path, off, 0, n))
@@ -439,26 +441,36 @@ class VectorStore:
         self._graph_tail = None
 
     def _build_graph(self, n: int) -> Dict[str, Any]:
-        """A faiss-layout HNSW graph over the n stored rows: node levels drawn as faiss's
-        ``HNSW::random_level`` does (``set_default_probas(M, 1/ln M)``; numpy's generator, seed
-        12345, not faiss's); on every level each node's candidates are its exact
-        max(efConstruction, width) nearest nodes of that level (the flat search, ties -> lower id)
-        and its neighbours (2M on level 0, M above) are chosen from them by faiss's heuristic,
-        reverse links included (:func:`hnsw.select_level`, on the GPU); the entry point is the
-        first node of the top level.  faiss inserts nodes one at a time and takes candidates from
-        an efConstruction beam over the graph built so far; here every node sees its exact
-        candidates at once, so the graph is the same construction without the insertion order
-        (oracle/hnsw_oracle.py ``heuristic_graph`` restates it)."""
+        """The faiss-layout HNSW graph over the n stored rows.  A graph already covering the first
+        m < n rows (the one last saved or loaded, a faiss-built file's included) is extended by
+        inserting rows [m, n) the way faiss's ``IndexHNSWFlat.add`` does, batched
+        (:func:`hnsw.insert_rows`: an efConstruction beam over the existing graph + the batch's
+        exact candidates, the selection heuristic, reverse links); otherwise the first
+        ``VECTOR_HNSW_GRAPH_MAX_ROWS`` rows are built at once from exact candidates
+        (:meth:`_build_graph_exact`) and the rest inserted.  Cost per save: the new rows only."""
+        g = self._graph_arrays
+        make = lambda: self._create_index(self.dimension)  # noqa: E731
+        if g is not None and 0 < int(np.asarray(g["levels"]).shape[0]) < n:
+            return hnsw_mod.insert_rows(self.index, g, int(np.asarray(g["levels"]).shape[0]), n,
+                                        int(self.hnsw_ef_construction), make)
+        n0 = min(n, max(1, _hnsw_graph_max_rows()))
+        g = self._build_graph_exact(n0)
+        if n0 < n:
+            g = hnsw_mod.insert_rows(self.index, g, n0, n, int(self.hnsw_ef_construction), make)
+        return g
+
+    def _build_graph_exact(self, n: int) -> Dict[str, Any]:
+        """A faiss-layout HNSW graph over the first n stored rows built at once: node levels drawn
+        as faiss's ``HNSW::random_level`` does (``set_default_probas(M, 1/ln M)``; numpy's
+        generator, seed 12345, not faiss's: :func:`hnsw.draw_levels`); on every level each node's
+        candidates are its exact max(efConstruction, width) nearest nodes of that level (the flat
+        search, ties -> lower id) and its neighbours (2M on level 0, M above) are chosen from them
+        by faiss's heuristic, reverse links included (:func:`hnsw.select_level`, on the GPU); the
+        entry point is the first node of the top level (oracle/hnsw_oracle.py ``heuristic_graph``
+        restates it)."""
         M = self.hnsw_m
         probas, cum = faiss_format.hnsw_default_probas(M)
-        f = np.random.default_rng(12345).random(n)
-        lev = np.full(n, len(probas) - 1, dtype=np.int64)
-        open_ = np.ones(n, dtype=bool)
-        for level, p in enumerate(probas):
-            hit = open_ & (f < p)
-            lev[hit] = level
-            open_ &= ~hit
-            f[open_] -= p
+        lev = hnsw_mod.draw_levels(n, probas)
         levels = (lev + 1).astype(np.int32)
         offsets = np.zeros(n + 1, dtype=np.uint64)
         offsets[1:] = np.cumsum(cum[levels].astype(np.uint64))
@@ -468,7 +480,7 @@ class VectorStore:
             members = np.nonzero(lev >= level)[0]
             width = int(cum[level + 1] - cum[level])
             C = min(max(int(self.hnsw_ef_construction), width), hnsw_mod.HP_C_MAX)
-            cand = self._knn_graph(C, None if level == 0 else members)
+            cand = self._knn_graph(C, None if level == 0 and n == int(self.index.ntotal) else members)
             sel = hnsw_mod.select_level(self.index, members, cand, width)
             base = offsets[members].astype(np.int64) + int(cum[level])
             for j in range(members.shape[0]):

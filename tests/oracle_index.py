@@ -66,3 +66,15 @@ class OracleFlatIndex:
 
 def oracle_factory(dimension: int, metric: str):
     return OracleFlatIndex(dimension, "ip" if metric == "cosine" else "l2")
+
+
+def _hnsw_search(self, graph, q, k, ef):
+    """ids of faiss's HNSW search over ``graph`` (the oracle's ordered-multiset statement, the
+    kernel's): the checker-backed form of ``hnsw.beam_search``."""
+    from oracle import hnsw_oracle as H
+    n = int(np.asarray(graph["levels"]).shape[0])
+    _, I = H.search(self._x[:n], graph, q, int(k), int(ef), "ip" if self.metric_type == 0 else "l2")
+    return I
+
+
+OracleFlatIndex.hnsw_search = _hnsw_search

@@ -82,3 +82,50 @@ def test_store_graph_equals_oracle_build(tmp_path, metric, monkeypatch):
     D, I = store.search_batch(q, 10)
     _, I_e = O.knn_exact(x, q, 10, om)
     assert O.recall_at(I, I_e, 10) >= 0.9
+
+
+@pytest.mark.parametrize("dtype,metric", [("bf16", "ip"), ("f32", "l2")])
+def test_insert_rows_matches_oracle(dtype, metric):
+    # faiss's insertion, batched (hnsw.insert_rows): the GPU graph search's efConstruction beam over
+    # the old graph, the batch's exact candidates (flat search), the prune kernel and the host's
+    # reverse links equal oracle/hnsw_oracle.py insert_batch batch by batch
+    n, d, n0 = 2600, 64, 800
+    ix = FlatIndex(d, metric, dtype, device=0)
+    ix.add_synthetic(O.SEED_CORPUS + 71, 0, n, True)
+    x = ix.reconstruct_n(0, n)
+    assert not H.has_exact_ties(x, x[:50], metric)
+    g0 = H.heuristic_graph(x[:n0], 8, 48, metric)
+    got = hnsw_mod.insert_rows(ix, g0, n0, n, 48, lambda: FlatIndex(d, metric, dtype, device=0), batch=700)
+    want = g0
+    for a in range(n0, n, 700):
+        want = H.insert_batch(x[:min(n, a + 700)], want, a, 48, metric)
+    for key in ("levels", "offsets", "neighbors"):
+        assert np.array_equal(np.asarray(got[key]), np.asarray(want[key])), key
+    assert (got["entry_point"], got["max_level"]) == (want["entry_point"], want["max_level"])
+    # the grown graph searches like the at-once one
+    q = O.synth_rows(O.SEED_QUERIES + 71, 0, 40, d, True, "f32")
+    _, I_e = O.knn_exact(x, q, 10, metric)
+    g = hnsw_mod.HNSWGraph(ix, got, 64)
+    _, I_g = g.search(q, 10, 64)
+    assert O.recall_at(I_g, I_e, 10) >= 0.9
+    g.close()
+    ix.close()
+
+
+def test_store_beyond_exact_build_size_saves_ihnf(tmp_path, monkeypatch):
+    from photo_search_engine_amd import faiss_format as F
+    monkeypatch.setenv("VECTOR_HNSW_GRAPH_MAX_ROWS", "1000")
+    n, d = 3000, 96
+    ix = FlatIndex(d, "ip", "f32", device=0)
+    ix.add_synthetic(O.SEED_CORPUS + 72, 0, n, False)
+    X = ix.reconstruct_n(0, n)
+    ix.close()
+    store = VectorStore(dimension=d, index_path=str(tmp_path / "i"), metadata_path=str(tmp_path / "m"),
+                        index_type="hnsw", hnsw_m=8, hnsw_ef_construction=40, hnsw_ef_search=32)
+    store.add(X, [{"photo_path": f"/{i}"} for i in range(n)])
+    store.save()
+    assert F.read_index(str(tmp_path / "i")).kind == "hnsw"
+    g = F.read_hnsw_graph(str(tmp_path / "i"))
+    xs = store.index.reconstruct_n(0, n)
+    want = H.insert_batch(xs, H.heuristic_graph(xs[:1000], 8, 40, "ip"), 1000, 40, "ip")
+    assert np.array_equal(g["neighbors"], want["neighbors"]) and np.array_equal(g["levels"], want["levels"])

@@ -71,3 +71,55 @@ def test_host_select_level_matches_oracle(metric, monkeypatch):
     got_c = hnsw_mod.select_level(None, members, cand, W, cmax=8)
     for j, v in enumerate(members):
         assert got_c[j][got_c[j] >= 0].tolist() == ref_c[int(v)]
+
+
+@pytest.mark.parametrize("metric", ["ip", "l2"])
+def test_oracle_insertion_from_empty_is_the_batch_build(metric):
+    # inserting every row into an empty graph (one batch: exact candidates among the batch) is the
+    # at-once build
+    rng = np.random.default_rng(8)
+    x = rng.standard_normal((150, 10)).astype(np.float32)
+    probas, cum = H._default_probas(4)
+    empty = {"assign_probas": probas, "cum_nneighbor_per_level": cum, "levels": np.zeros(0, np.int32),
+             "offsets": np.zeros(1, np.uint64), "neighbors": np.zeros(0, np.int32), "entry_point": -1,
+             "max_level": -1, "efConstruction": 20, "efSearch": 16, "upper_beam": 1}
+    a = H.insert_batch(x, empty, 0, 20, metric)
+    b = H.heuristic_graph(x, 4, 20, metric)
+    for key in ("levels", "offsets", "neighbors"):
+        assert np.array_equal(np.asarray(a[key]), np.asarray(b[key])), key
+    assert (a["entry_point"], a["max_level"]) == (b["entry_point"], b["max_level"])
+
+
+def test_oracle_insertion_keeps_recall():
+    # a graph grown by insertions (several batches) searches as well as one built at once
+    rng = np.random.default_rng(9)
+    d, n = 24, 1500
+    centers = rng.standard_normal((15, d)).astype(np.float32)
+    x = centers[rng.integers(0, 15, n)] + 0.35 * rng.standard_normal((n, d)).astype(np.float32)
+    x /= np.linalg.norm(x, axis=1, keepdims=True)
+    q = x[rng.choice(n, 40, replace=False)] + 0.05 * rng.standard_normal((40, d)).astype(np.float32)
+    _, I_e = O.knn_exact(x, q, 10, "ip")
+    g = H.heuristic_graph(x[:300], 4, 40, "ip")
+    for a, b in ((300, 700), (700, 1100), (1100, n)):
+        g = H.insert_batch(x[:b], g, a, 40, "ip")
+    _, I_g = H.search(x, g, q, 10, 24, "ip")
+    assert O.recall_at(I_g, I_e, 10) >= 0.9
+
+
+@pytest.mark.parametrize("metric", ["ip", "l2"])
+def test_host_insert_rows_matches_oracle(metric):
+    # photo_search_engine_amd/hnsw.py insert_rows over the checker-backed index (its prune and beam
+    # are the oracle's) equals the oracle's insert_batch, batch by batch
+    from oracle_index import OracleFlatIndex
+    rng = np.random.default_rng(10)
+    x = rng.standard_normal((400, 14)).astype(np.float32)
+    ix = OracleFlatIndex(14, metric)
+    ix.add(x)
+    g0 = H.heuristic_graph(x[:100], 6, 30, metric)
+    got = hnsw_mod.insert_rows(ix, g0, 100, 400, 30, lambda: OracleFlatIndex(14, metric), batch=120)
+    want = g0
+    for a in (100, 220, 340):
+        want = H.insert_batch(x[:min(400, a + 120)], want, a, 30, metric)
+    for key in ("levels", "offsets", "neighbors"):
+        assert np.array_equal(np.asarray(got[key]), np.asarray(want[key])), key
+    assert (got["entry_point"], got["max_level"]) == (want["entry_point"], want["max_level"])

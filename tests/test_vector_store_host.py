@@ -201,14 +201,42 @@ def test_reference_hnsw_fixture_rewrites_byte_identical(tmp_path):
     assert open(out, "rb").read() == open(src, "rb").read()
 
 
-def test_hnsw_store_above_graph_cap_saves_flat(VS, tmp_path, monkeypatch):
+def test_hnsw_store_beyond_exact_build_inserts_and_saves_ihnf(VS, tmp_path, monkeypatch):
+    # every size saves an IHNf file (rollback to the reference's faiss): the first
+    # VECTOR_HNSW_GRAPH_MAX_ROWS rows get the exact-candidate build, the rest are inserted the way
+    # faiss's IndexHNSWFlat.add does (batched), and each later save inserts only the new rows
+    from oracle import hnsw_oracle as H
     from photo_search_engine_amd import faiss_format as F
-    monkeypatch.setenv("VECTOR_HNSW_GRAPH_MAX_ROWS", "10")
+    monkeypatch.setenv("VECTOR_HNSW_GRAPH_MAX_ROWS", "50")
     rng = np.random.default_rng(3)
-    store = VS(dimension=8, index_path=str(tmp_path / "i"), metadata_path=str(tmp_path / "m"), index_type="hnsw")
-    store.add(rng.standard_normal((20, 8)).astype(np.float32), [{} for _ in range(20)])
+    X = rng.standard_normal((170, 12)).astype(np.float32)
+    kw = dict(index_path=str(tmp_path / "i"), metadata_path=str(tmp_path / "m"), index_type="hnsw", hnsw_m=4,
+              hnsw_ef_construction=24, hnsw_ef_search=16)
+    store = VS(dimension=12, **kw)
+    store.add(X[:130], [{"photo_path": f"/{i}"} for i in range(130)])
     store.save()
-    assert F.read_index(str(tmp_path / "i")).kind == "flat"
+    assert F.read_index(str(tmp_path / "i")).kind == "hnsw"
+    g = F.read_hnsw_graph(str(tmp_path / "i"))
+    xs = store.index.reconstruct_n(0, 130)
+    want = H.insert_batch(xs, H.heuristic_graph(xs[:50], 4, 24, "ip"), 50, 24, "ip")
+    for key in ("levels", "offsets", "neighbors"):
+        assert np.array_equal(np.asarray(g[key]), np.asarray(want[key])), key
+    assert (g["entry_point"], g["max_level"]) == (want["entry_point"], want["max_level"])
+    # the next batch of the indexer: only the new rows are inserted
+    store.add(X[130:], [{"photo_path": f"/{i}"} for i in range(130, 170)])
+    store.save()
+    g2 = F.read_hnsw_graph(str(tmp_path / "i"))
+    want2 = H.insert_batch(store.index.reconstruct_n(0, 170), want, 130, 24, "ip")
+    assert np.array_equal(g2["neighbors"], want2["neighbors"]) and np.array_equal(g2["levels"], want2["levels"])
+    # reload (graph mode keeps the file's graph) and grow again: the loaded graph is extended
+    monkeypatch.setenv("VECTOR_HNSW_SEARCH", "graph")
+    s2 = VS(dimension=12, **kw)
+    assert s2.load() and s2.get_total_items() == 170
+    s2.add(X[:5] * 2.0, [{"photo_path": f"/x{i}"} for i in range(5)])
+    s2.save()
+    g3 = F.read_hnsw_graph(str(tmp_path / "i"))
+    want3 = H.insert_batch(s2.index.reconstruct_n(0, 175), want2, 170, 24, "ip")
+    assert np.array_equal(g3["neighbors"], want3["neighbors"])
 
 
 @pytest.mark.parametrize("d", [8, 1536, 4096])
