@@ -54,7 +54,7 @@ struct Ctx {
     // returned with kernels still queued is never overwritten by the next caller's pack
     hipEvent_t idle = nullptr;
     bool pending = false;
-    DevBuf qdev, qtile, qinfo, qpad, cand, part, merge_a, merge_b, outD, outI, outS, cert, thr0, seedmax, gcnt, seedsync;
+    DevBuf qdev, qtile, qinfo, qpad, cand, part, merge_a, merge_b, outD, outI, outS, cert, thr0, seedmax, gcnt, seedsync, gT;
     DevBuf qfac, qeps, drop;  // int8 screen: per-query code scale and norm, refine margin, drop bounds
     DevBuf fails;             // the current query block's certificate-failure count (fallback gate)
     DevBuf rsc, rdone;        // split refine: per-query scores + ids of the kept rows, done counters
@@ -69,7 +69,7 @@ struct Ctx {
     unsigned* unres = nullptr;  // this call's unresolved-query counter (device), instead of the index's
     ~Ctx() {
         for (DevBuf* b : {&qdev, &qtile, &qinfo, &qpad, &cand, &part, &merge_a, &merge_b, &outD, &outI, &outS, &cert, &thr0,
-                          &seedsync, &seedmax, &gcnt, &rows[0], &rows[1], &tilectr, &seedacc, &outAll, &qfac, &qeps, &drop, &fails, &rsc, &rdone,
+                          &seedsync, &gT, &seedmax, &gcnt, &rows[0], &rows[1], &tilectr, &seedacc, &outAll, &qfac, &qeps, &drop, &fails, &rsc, &rdone,
                           &pa})
             b->release();
         pin.release();
@@ -102,6 +102,12 @@ struct vs_index {
     uint8_t* data8 = nullptr;
     uint32_t* rsb = nullptr;  // per row: bf16 scale | bf16 error norm (rounded up) << 16
     float i8_bmax = 0.0f;     // host copy of the largest row error norm (int8 GEMV depth)
+    // group residuals (inner product, direct int8 screen): bf16 means of I8_GROUP_ROWS-row groups
+    // [gcap][dpad8] the codes are taken against (zero for groups without a mean worth it);
+    // d_maxsq[5] = max ||mu_g|| (fp32 bits), d_maxsq[6] = groups that have a mean
+    uint16_t* gmean = nullptr;
+    int64_t gcap = 0;
+    bool i8_res = false;  // some group has a mean: the int8 screen adds <mu_g, q> to its keys
     hipStream_t own = nullptr;  // ingest stream
     DevBuf stage[2];            // add_rows_host: fp32 chunks on the device ...
     PinnedPair pin;             // ... and their pinned host sources
@@ -216,10 +222,17 @@ void ensure_capacity(vs_index* ix, int64_t rows_needed, bool exact = false) {
 void free_i8(vs_index* ix) {
     if (ix->data8) (void)hipFree(ix->data8);
     if (ix->rsb) (void)hipFree(ix->rsb);
+    if (ix->gmean) (void)hipFree(ix->gmean);
     ix->data8 = nullptr;
     ix->rsb = nullptr;
+    ix->gmean = nullptr;
     ix->cap8 = 0;
+    ix->gcap = 0;
+    ix->i8_res = false;
 }
+
+// group residuals apply to inner-product indexes whose int8 main pass is the direct form
+bool i8_groups_apply(const vs_index* ix) { return ix->metric == METRIC_IP && i8_direct_ok(ix->dpad8); }
 
 // grow the int8 screen copy to ix->cap_rows rows (device copy of the rows present; the old and new
 // arrays coexist only for the copy, as for the primary rows)
@@ -229,37 +242,60 @@ void ensure_capacity_i8(vs_index* ix) {
     const size_t tb8 = (size_t)TR * ix->dpad8;
     uint8_t* nd = nullptr;
     uint32_t* nr = nullptr;
+    uint16_t* ng = nullptr;
+    const int64_t gcap = i8_groups_apply(ix) ? (ncap + I8_GROUP_ROWS - 1) / I8_GROUP_ROWS : 0;
     hipError_t e = hipMalloc(&nd, (size_t)(ncap / TR) * tb8);
     if (e == hipSuccess) e = hipMalloc(&nr, (size_t)ncap * sizeof(uint32_t));
+    if (e == hipSuccess && gcap) e = hipMalloc(&ng, (size_t)gcap * ix->dpad8 * sizeof(uint16_t));
     if (e != hipSuccess) {
         if (nd) hipFree(nd);
+        if (nr) hipFree(nr);
         HIP_CHECK(e);
     }
     if (ix->data8 && ix->ntotal > 0) {
         const int64_t used_tiles = (ix->ntotal + TR - 1) / TR;
         HIP_CHECK(hipMemcpyAsync(nd, ix->data8, (size_t)used_tiles * tb8, hipMemcpyDeviceToDevice, ix->own));
         HIP_CHECK(hipMemcpyAsync(nr, ix->rsb, (size_t)ix->ntotal * sizeof(uint32_t), hipMemcpyDeviceToDevice, ix->own));
+        if (ng && ix->gmean) {
+            const int64_t used_groups = (ix->ntotal + I8_GROUP_ROWS - 1) / I8_GROUP_ROWS;
+            HIP_CHECK(hipMemcpyAsync(ng, ix->gmean, (size_t)used_groups * ix->dpad8 * sizeof(uint16_t),
+                                     hipMemcpyDeviceToDevice, ix->own));
+        }
     }
     HIP_CHECK(hipStreamSynchronize(ix->own));
+    const bool res = ix->i8_res;
     free_i8(ix);
     ix->data8 = nd;
     ix->rsb = nr;
+    ix->gmean = ng;
+    ix->gcap = gcap;
+    ix->i8_res = res;
     ix->cap8 = ncap;
 }
 
-// int8 screen copy of rows [r0, r0 + n) once they are packed (stream-ordered after the pack)
+// int8 screen copy of rows [r0, r0 + n) once they are packed (stream-ordered after the pack).  With
+// group residuals, the groups the rows fall in get their means (re)computed over every row they
+// hold now, and their rows are (re)quantised from the group's first row.
 void quantize_rows(vs_index* ix, int64_t r0, int64_t n, hipStream_t st) {
     if (ix->screen != VS_SCREEN_I8 || n <= 0) return;
+    if (ix->gmean) {
+        const int64_t g0 = r0 / I8_GROUP_ROWS, g1 = (r0 + n + I8_GROUP_ROWS - 1) / I8_GROUP_ROWS;
+        HIP_CHECK(launch_group_means(ix->dtype, ix->data, ix->dpad, ix->d, g0, g1 - g0, r0 + n, ix->dpad8, ix->gmean,
+                                     ix->d_maxsq + 5, st));
+        n += r0 - g0 * I8_GROUP_ROWS;
+        r0 = g0 * I8_GROUP_ROWS;
+    }
     HIP_CHECK(launch_quant_rows(ix->dtype, ix->data, ix->dpad, r0, n, ix->d, ix->data8, ix->dpad8, ix->rsb,
-                                ix->d_maxsq + 2, st));
+                                ix->d_maxsq + 2, st, ix->gmean));
 }
 
 void refresh_maxsq(vs_index* ix) {
-    unsigned bits[4] = {0, 0, 0, 0};
+    unsigned bits[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     HIP_CHECK(hipMemcpyAsync(bits, ix->d_maxsq, sizeof(bits), hipMemcpyDeviceToHost, ix->own));
     HIP_CHECK(hipStreamSynchronize(ix->own));
     std::memcpy(&ix->maxsq, &bits[0], 4);
     std::memcpy(&ix->i8_bmax, &bits[3], 4);  // int8 copy: the largest row error norm
+    ix->i8_res = ix->gmean != nullptr && bits[6] != 0;  // some group coded against its mean
 }
 
 // optimistic seed: a 16-row-group maximum of the strided tile sample, at the rank that leaves
@@ -278,7 +314,12 @@ constexpr bool gemv_dyn() { return true; }
 // The int8 pre-screen serves first passes of MFMA-sized batches (k <= I8_MAX_K) of an index with
 // VS_SCREEN_I8; a query its certificate rejects is re-searched by the caller on the native path.
 bool use_i8(const vs_index* ix, int nqb, int k) {
-    return ix->screen == VS_SCREEN_I8 && nqb > GEMV_NQ_MAX && k <= I8_MAX_K;
+    if (ix->screen != VS_SCREEN_I8 || nqb <= GEMV_NQ_MAX || k > I8_MAX_K) return false;
+    if (!ix->i8_res) return true;
+    // group-residual codes: only the seeded direct main pass adds <mu_g, q> (else: native)
+    const int64_t tiles = (ix->ntotal + TR - 1) / TR;
+    const int64_t G = std::max<int64_t>(1, std::min<int64_t>(tiles, ix->num_cu));
+    return tiles >= 4 * G && G * 16 <= kI8dSeedMaxima;
 }
 
 constexpr int kF32MfmaMinQ = 64;     // fp32 native batches: MFMA screen from this many queries on
@@ -425,6 +466,13 @@ void search_block_i8(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float
     const bool seeded = tiles >= 4 * (int64_t)a.G;
     const bool seed_in_kernel =
         seeded && ix->metric == METRIC_IP && i8_direct_ok(ix->dpad8) && a.G * 16 <= kI8dSeedMaxima;
+    if (ix->i8_res && !seed_in_kernel) throw VsError(VS_ERR_INTERNAL, "group-residual int8 codes need the seeded direct pass");
+    if (ix->i8_res) {  // <mu_g, q> of every group for this block's queries
+        const int64_t ng = (ix->ntotal + I8_GROUP_ROWS - 1) / I8_GROUP_ROWS;
+        c->gT.ensure((size_t)ng * MFMA_QB * sizeof(float));
+        HIP_CHECK(launch_group_dots(ix->gmean, ng, ix->dpad8, q, nqb, ix->d, c->gT.as<float>(), st));
+        a.gT = c->gT.as<float>();
+    }
     if (seed_in_kernel) c->seedsync.ensure(4 * sizeof(int));
     HIP_CHECK(launch_pack_qtile_i8(q, nqb, ix->d, ix->dpad8, c->qtile.as<uint8_t>(), c->qfac.as<float2>(),
                                    c->qeps.as<float>(), ix->d_maxsq + 2, c->gcnt.as<int>(), c->drop.as<u64>(), st,
@@ -553,7 +601,7 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
     if (!redo) c->fails.ensure(sizeof(int));
     // int8 screen, few queries: the GEMV streams the int8 copy (1 B per element) with the fp32
     // query; its keys carry the row error bound, so it screens deeper (first passes only)
-    bool gemv_i8 = !use_mfma && seed_rank > 0 && ix->screen == VS_SCREEN_I8 && ix->data8 != nullptr;
+    bool gemv_i8 = !use_mfma && seed_rank > 0 && ix->screen == VS_SCREEN_I8 && ix->data8 != nullptr && !ix->i8_res;
     if (gemv_i8) {
         const int kp8 = i8_gemv_depth(ix, k);
         gemv_i8 = kp8 <= kI8GemvMaxDepth;  // a single query's refine is one workgroup: deep lists cost
@@ -1153,8 +1201,10 @@ int vs_reset(vs_index* ix) {
         ix->ntotal = 0;
         ix->maxsq = 0.0f;
         ix->i8_bmax = 0.0f;
+        ix->i8_res = false;
         HIP_CHECK(hipMemsetAsync(ix->d_maxsq, 0, sizeof(unsigned), ix->own));
         HIP_CHECK(hipMemsetAsync(ix->d_maxsq + 2, 0, 2 * sizeof(unsigned), ix->own));
+        HIP_CHECK(hipMemsetAsync(ix->d_maxsq + 5, 0, 2 * sizeof(unsigned), ix->own));
         HIP_CHECK(hipStreamSynchronize(ix->own));
     });
 }
@@ -1437,6 +1487,7 @@ int vs_set_screen(vs_index* ix, int screen) {
         ix->dpad8 = (int)std::max<int64_t>(round_up(ix->d, 64), 128);  // >= 2 K-steps per tile (see dpad)
         try {
             HIP_CHECK(hipMemsetAsync(ix->d_maxsq + 2, 0, 2 * sizeof(unsigned), ix->own));
+            HIP_CHECK(hipMemsetAsync(ix->d_maxsq + 5, 0, 2 * sizeof(unsigned), ix->own));
             ensure_capacity_i8(ix);
             quantize_rows(ix, 0, ix->ntotal, ix->own);
             HIP_CHECK(hipStreamSynchronize(ix->own));
@@ -1491,7 +1542,8 @@ int64_t vs_screen_copy_bytes(vs_index* ix) {
     if (!ix) return -1;
     if (!ix->data8) return 0;
     const int64_t rows = ix->cap8;
-    return (rows / TR) * (int64_t)TR * ix->dpad8 + rows * (int64_t)sizeof(uint32_t);
+    return (rows / TR) * (int64_t)TR * ix->dpad8 + rows * (int64_t)sizeof(uint32_t) +
+           ix->gcap * ix->dpad8 * (int64_t)sizeof(uint16_t);
 }
 
 int64_t vs_unresolved_count(vs_index* ix) {

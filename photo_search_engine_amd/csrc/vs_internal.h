@@ -211,6 +211,8 @@ struct ScreenArgs {
     u64* thr_out;            // [QB] the selected thresholds (the refine's thr0)
     int seed_rank;           // rank of the selected maximum among the G * 16 of a query
     int seed_prov_rank;      // the sample tile's own provisional threshold: this rank of its 16 maxima
+    const float* gT;         // int8 group residuals: [group][QB] <mu_g, q> added to every key of the
+                             // group's rows (k_screen_i8d_seeded_res), or null
 };
 constexpr int MAP_DESC = 8;
 constexpr int kI8dSeedMaxima = 4096;  // G * 16 group maxima per query the in-kernel seed select holds
@@ -318,10 +320,18 @@ int refine_split(int nq, int Kp, int dt, int num_cu);
 hipError_t launch_refine(const RefineArgs& a, int nq, hipStream_t st);
 // exact refine behind the int8 screen: adaptive two-phase depth (KA keys first), IP only
 hipError_t launch_refine_wide(const RefineArgs& a, int nq, int KA, hipStream_t st);
+constexpr int I8_GROUP_ROWS = 4096;  // rows per group of the int8 copy's group residuals (16 tiles)
 constexpr int I8_MAX_K = 1024;  // largest k the int8 screen serves (k_refine_wide: 2 * KA <= RFW_CAP)
 // int8 screen copy of stored rows [r0, r0 + n) (maxes[0..1]: running max ||x_hat||, max beta)
 hipError_t launch_quant_rows(int dt, const uint8_t* data, int dpad, int64_t r0, int64_t n, int d, uint8_t* data8,
-                             int dpad8, uint32_t* rsb, unsigned* maxes, hipStream_t st);
+                             int dpad8, uint32_t* rsb, unsigned* maxes, hipStream_t st, const uint16_t* gmean = nullptr);
+// group means of the int8 copy (groups [g0, g0 + ng) of I8_GROUP_ROWS rows, rows < n_rows; bf16
+// [group][dpad8], zero where the mean is not worth coding against; maxes[0] = max ||mu|| (fp32
+// bits), maxes[1] += groups with a mean) and their dots with a query batch (T [group][MFMA_QB])
+hipError_t launch_group_means(int dt, const uint8_t* data, int dpad, int d, int64_t g0, int64_t ng, int64_t n_rows,
+                              int dpad8, uint16_t* gmean, unsigned* maxes, hipStream_t st);
+hipError_t launch_group_dots(const uint16_t* gmean, int64_t ngroups, int dpad8, const float* q, int nq, int d, float* T,
+                             hipStream_t st);
 hipError_t launch_pack_qtile_i8(const float* q, int nqb, int d, int dpad8, uint8_t* qt, float2* qfac, float* qeps,
                                 const unsigned* maxes, int* gcnt, u64* drop, hipStream_t st, int* fails = nullptr,
                                 const unsigned* l2max = nullptr, float gamma = 0.0f, int* seed_sync = nullptr);

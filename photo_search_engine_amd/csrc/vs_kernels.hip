@@ -560,43 +560,156 @@ __device__ __forceinline__ uint32_t bf16_bits_up(float f) {  // smallest bf16 >=
     return (u >> 16) + ((u & 0xFFFFu) ? 1u : 0u);
 }
 
+// Group residuals (inner-product int8 screens, DESIGN §5 "clustered corpora"): rows are coded as
+// x = mu_g + r with mu_g the bf16-rounded mean of their group of I8_GROUP_ROWS consecutive rows, when
+// that mean carries at least a quarter of the group's energy (a corpus inserted cluster by cluster);
+// else mu_g = 0.  The error norm then scales with ||r||, not ||x||; the screen adds <mu_g, q> (fp32,
+// k_group_dots) to every key of the group.  One block per group: the mean over the rows present,
+// its bf16 rounding, the energy test; maxes[0] (fp32 bits) = the largest ||mu_g|| (rounded up),
+// maxes[1] counts the groups with a mean.
+template <int DT>
+__global__ void __launch_bounds__(256) k_group_means(const uint8_t* __restrict__ data, int dpad, int d, int64_t g0,
+                                                      int64_t n_rows, int dpad8, uint16_t* __restrict__ gmean,
+                                                      unsigned* __restrict__ maxes) {
+    constexpr int ES = DT == DT_F32 ? 4 : 2;
+    __shared__ double red[2][4];
+    const int64_t g = g0 + blockIdx.x;
+    const int64_t lo = g * I8_GROUP_ROWS, hi = min(n_rows, lo + I8_GROUP_ROWS);
+    const int tid = threadIdx.x;
+    const double cnt = (double)(hi - lo);
+    double m2 = 0.0, x2 = 0.0;
+    uint16_t* dst = gmean + (size_t)g * dpad8;
+    for (int i = tid; i < dpad8; i += 256) {
+        double s = 0.0;
+        if (i < d)
+            for (int64_t r = lo; r < hi; ++r) {
+                const double v = (double)load_elem<DT>(data + tiled_off(r, i, dpad, ES));
+                s += v;
+                x2 += v * v;
+            }
+        const uint16_t b = (i < d && cnt > 0) ? f32_to_bf16_rne((float)(s / cnt)) : (uint16_t)0;
+        dst[i] = b;
+        const double mu = (double)bf16_bits_to_f32(b);
+        m2 += mu * mu;
+    }
+    m2 = wave_sum_f64(m2);
+    x2 = wave_sum_f64(x2);
+    if ((tid & 63) == 0) {
+        red[0][tid >> 6] = m2;
+        red[1][tid >> 6] = x2;
+    }
+    __syncthreads();
+    const double M2 = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    const double X2 = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+    // a mean worth coding against: >= 1/4 of the group's mean row energy
+    const bool use = cnt > 0 && M2 * cnt >= 0.25 * X2 && M2 > 0.0;
+    if (!use)
+        for (int i = tid; i < dpad8; i += 256) dst[i] = 0;
+    if (tid == 0 && use) {
+        atomicMax(&maxes[0], __float_as_uint(f32_up(sqrt(M2) * (1.0 + 1e-9))));
+        atomicAdd(&maxes[1], 1u);
+    }
+}
+
 template <int DT>
 __global__ void __launch_bounds__(256) k_quant_rows(const uint8_t* __restrict__ data, int dpad, int64_t r0, int64_t n,
                                                      int d, uint8_t* __restrict__ data8, int dpad8,
-                                                     uint32_t* __restrict__ rsb, unsigned* __restrict__ maxes) {
+                                                     uint32_t* __restrict__ rsb, unsigned* __restrict__ maxes,
+                                                     const uint16_t* __restrict__ gmean) {
     constexpr int ES = DT == DT_F32 ? 4 : 2;
     const int lane = threadIdx.x & 63;
     const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= n) return;
     const int64_t row = r0 + r;
+    // group residual: the codes quantise x - mu_g, computed exactly in fp64 (mu_g = 0: the row)
+    const uint16_t* mu = gmean ? gmean + (size_t)(row / I8_GROUP_ROWS) * dpad8 : nullptr;
+    auto resid = [&](int i) -> double {
+        const double x = (double)load_elem<DT>(data + tiled_off(row, i, dpad, ES));
+        return mu ? x - (double)bf16_bits_to_f32(mu[i]) : x;
+    };
     float mx = 0.0f;
-    for (int i = lane; i < d; i += 64) mx = fmaxf(mx, fabsf(load_elem<DT>(data + tiled_off(row, i, dpad, ES))));
+    for (int i = lane; i < d; i += 64) mx = fmaxf(mx, (float)fabs(resid(i)));
 #pragma unroll
     for (int s = 32; s > 0; s >>= 1) mx = fmaxf(mx, __shfl_xor(mx, s, 64));
     const uint32_t sbits = f32_to_bf16_rne(mx / 127.0f);
     const float sc = bf16_bits_to_f32(sbits);  // the scale as stored: codes and error use exactly it
     uint8_t* dst = data8 + (row / TR) * (int64_t)TR * dpad8 + (row % TR) * 64;
-    double e2 = 0.0, c2 = 0.0;
+    double e2 = 0.0, c2 = 0.0, r2 = 0.0;
     for (int i = lane; i < dpad8; i += 64) {
         int c = 0;
-        float x = 0.0f;
+        double x = 0.0;
         if (i < d) {
-            x = load_elem<DT>(data + tiled_off(row, i, dpad, ES));
-            if (sc > 0.0f) c = max(-127, min(127, (int)rintf(x / sc)));
+            x = resid(i);
+            if (sc > 0.0f) c = max(-127, min(127, (int)rint(x / (double)sc)));
         }
         dst[(int64_t)(i >> 6) * TR * 64 + (i & 63)] = (uint8_t)(int8_t)c;
-        // exact in fp64: c != 0 needs |x| >= s / 2, so x and s c span < 53 bits; c == 0 gives e = x
-        const double e = (double)x - (double)sc * (double)c;
+        // fp64: s c is exact; x - s c rounds at most once (relative 2^-53); with a group mean, x
+        // itself (the stored value minus mu) may have rounded once too (|err| <= 2^-53 |x|): both are
+        // covered by the norm's rounding-up below plus 2^-51 ||x||
+        const double e = x - (double)sc * (double)c;
         e2 += e * e;
         c2 += (double)(c * c);
+        r2 += x * x;
     }
     e2 = wave_sum_f64(e2);
     c2 = wave_sum_f64(c2);
+    r2 = wave_sum_f64(r2);
     if (lane == 0) {
-        const uint32_t bbits = bf16_bits_up(f32_up(sqrt(e2) * (1.0 + 1e-9)));
+        const uint32_t bbits = bf16_bits_up(f32_up(sqrt(e2) * (1.0 + 1e-9) + (mu ? sqrt(r2) * 4.440892098500626e-16 : 0.0)));
         rsb[row] = sbits | (bbits << 16);
         atomicMax(&maxes[0], __float_as_uint(f32_up(sqrt(c2) * (double)sc * (1.0 + 1e-9))));
         atomicMax(&maxes[1], bbits << 16);  // the fp32 bits of the bf16 bound
+    }
+}
+
+// T[g][q] = <mu_g, q> for the group means of the int8 copy (k_group_means) and a batch of fp32
+// queries, by bf16 MFMA with each query split exactly into hi = bf16(q) + lo = bf16(q - hi): the
+// products are exact in fp32, so |T - <mu_g, q>| <= (gamma_2d + 2^-16) ||mu_g|| ||q|| (|q - hi - lo|
+// <= 2^-17 |q| elementwise) -- k_pack_qtile_i8 adds that to every query's margin.  One block per 16
+// groups; wave w takes queries 64w .. 64w + 63 (four 16-column tiles), hi and lo into the same
+// accumulators.  Groups without a mean (mu_g = 0) give T = 0.
+__global__ void __launch_bounds__(256) k_group_dots(const uint16_t* __restrict__ gmean, int64_t ngroups, int dpad8,
+                                                     const float* __restrict__ q, int nq, int d, float* __restrict__ T) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t g0 = (int64_t)blockIdx.x * 16;
+    const int r16 = lane & 15, kc = (lane >> 4) * 8;
+    const int64_t ga = min(g0 + r16, ngroups - 1);
+    const uint16_t* arow = gmean + (size_t)ga * dpad8;
+    floatx4 acc[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[c] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+    for (int k0 = 0; k0 < dpad8; k0 += 32) {
+        const uint4 av = *(const uint4*)(arow + k0 + kc);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int qq = 64 * w + 16 * c + r16;
+            uint32_t hi[4], lo[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int k = k0 + kc + 2 * e;
+                const float v0 = (qq < nq && k < d) ? q[(int64_t)qq * d + k] : 0.0f;
+                const float v1 = (qq < nq && k + 1 < d) ? q[(int64_t)qq * d + k + 1] : 0.0f;
+                const uint32_t h0 = f32_to_bf16_rne(v0), h1 = f32_to_bf16_rne(v1);
+                const uint32_t l0 = f32_to_bf16_rne(v0 - bf16_bits_to_f32(h0)), l1 = f32_to_bf16_rne(v1 - bf16_bits_to_f32(h1));
+                hi[e] = h0 | (h1 << 16);
+                lo[e] = l0 | (l1 << 16);
+            }
+            acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, av),
+                                                             __builtin_bit_cast(bf16x8, make_uint4(hi[0], hi[1], hi[2], hi[3])),
+                                                             acc[c], 0, 0, 0);
+            acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, av),
+                                                             __builtin_bit_cast(bf16x8, make_uint4(lo[0], lo[1], lo[2], lo[3])),
+                                                             acc[c], 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int qq = 64 * w + 16 * c + r16;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int64_t g = g0 + 4 * (lane >> 4) + j;
+            if (g < ngroups) T[(size_t)g * MFMA_QB + qq] = qq < nq ? acc[c][j] : 0.0f;
+        }
     }
 }
 
@@ -667,9 +780,13 @@ __global__ void __launch_bounds__(256) k_pack_qtile_i8(const float* __restrict__
         const double eq = sqrt(e2) * (1.0 + 1e-9);
         const double qh = sqrt(c2) * (double)t * (1.0 + 1e-9);  // ||t_q c_q||
         const double X = (double)__uint_as_float(maxes[0]), B = (double)__uint_as_float(maxes[1]);
-        // the key's fp32 evaluation t * fma(beta, fl(qn / t), fl(s * fl(acc))): <= 6 roundings
-        // relative 2^-24 of |sigma| + beta qn (|sigma| <= X ||t_q c_q||); 8 of them budgeted
-        const double slop = 8.0 * 5.9604644775390625e-08 * (X * qh + B * (double)qn) + 1e-30;
+        // group residuals (inner product): the key adds T = fl<mu_g, q> (k_group_dots), within
+        // (gamma_2d + 2^-16) ||mu_g|| ||q|| of the true dot; Mu = max ||mu_g|| (0 without them)
+        const double Mu = (double)__uint_as_float(maxes[3]);
+        // the key's fp32 evaluation t * fma(beta, fl(qn / t), fl(s * fl(acc))) [+ T]: <= 7 roundings
+        // relative 2^-24 of |sigma| + beta qn [+ |T|] (|sigma| <= X ||t_q c_q||); 8 of them budgeted
+        const double slop = 8.0 * 5.9604644775390625e-08 * (X * qh + B * (double)qn + Mu * (double)qn) + 1e-30 +
+                            (2.02 * (double)gamma + 1.52587890625e-05) * Mu * (double)qn;
         // the screen computes key = t_q * (s_x acc + beta_x * (||q|| / t_q)); a zero query has t_q = 0
         // and every key 0
         qfac[r] = make_float2(t, t > 0.0f ? qn / t : 0.0f);
@@ -1453,6 +1570,8 @@ __device__ __forceinline__ int vtid_here() {
 constexpr int I8D_SEED_LDS = 32 + (int)sizeof(SeedPtrs);  // sst[8]: [0] decision, [2] claimed query, [3] digit,
                                   // [4] rank, [5..6] poll, [7] claims exhausted; then the SeedPtrs
 static_assert(MF_THREADS * I8D_SEED_VPT >= kI8dSeedMaxima, "in-kernel seed select capacity");
+constexpr int I8D_RES_LDS = 2 * MFMA_QB * 4;  // group residuals: <mu_g, q> of two tiles
+static_assert(I8_GROUP_ROWS % TR == 0, "a tile lies in one group");
 
 // the rank-th largest of query c's G * 16 maxima (k_seed_select's 8-bit radix select on this
 // workgroup's 512 threads) -> thr_out[c], then published
@@ -1584,12 +1703,13 @@ __device__ __forceinline__ void i8d_seed_help(const ScreenArgs& a, int nqb, unsi
 // NG: query column groups of 16 (16 = the 256-column tile; 4 = a narrow tile of 64 columns for
 // mapped scans of lists probed by <= 32 queries: a quarter of the MFMAs, and the query DMAs read
 // only the tile's first 64 rows, so the L2 holds a quarter of each tile)
-template <int DT, int METRIC, bool MAP = false, int NG = 16, bool SEEDK = false>
+template <int DT, int METRIC, bool MAP = false, int NG = 16, bool SEEDK = false, bool RES = false>
 __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
     constexpr bool L2 = METRIC == METRIC_L2;
     constexpr bool I8 = DT == DT_I8;
     static_assert(!(MAP && I8), "the mapped scan serves bf16 / f16 lists");
     static_assert(!SEEDK || (I8 && !MAP && !L2), "in-kernel seeding: the int8 flat inner-product main pass");
+    static_assert(!RES || SEEDK, "group residuals: the seeded int8 main pass");
     static_assert(NG == 16 || (NG == 4 && MAP), "narrow query tiles: mapped scans only");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint8_t* const sm = smem + I8D_RING;
@@ -1646,6 +1766,9 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
         else return (int64_t)blk + seq(t) * a.G;
     };
     int* const sst = (int*)(smem + I8D_LDS);  // SEEDK: the seeding state (I8D_SEED_LDS bytes)
+    // RES: <mu_g, q> of the tile's group (two tiles, by parity), LDS-DMA'd by waves 4-7 one tile ahead
+    // and copied into qrec[q].w at the tile's K-step 0
+    float* const tlds = (float*)(smem + I8D_LDS + I8D_SEED_LDS);
     unsigned* const shist = (unsigned*)(sm + 256 * 16 + 16 + MF_POOL * 12);  // SEEDK: select histogram (records' area)
     if (tid < 256) {
         const bool real = tid < nqb;
@@ -1680,8 +1803,11 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
     // (int8: waves 0-3 the (scale | beta) words, waves 4-7 ||x||^2 (L2) or the same words again;
     // 16-bit rows: ||x||^2 into rowx (L2 only))
     const bool sq_wave = L2 && (!I8 || wid_s >= 4);
-    const uint32_t* const side_src = (sq_wave ? (const uint32_t*)a.sqn : a.rsb) + (wid_s & 3) * 64;
-    const uint32_t side_dst = (sq_wave && I8 ? lds_addr((const uint8_t*)rowq) : rowx_lds) + (uint32_t)((wid_s & 3) * 256);
+    // (RES: waves 4-7 load the tile group's 1 KiB of <mu_g, q> instead of repeating the words)
+    const bool t_wave = RES && wid_s >= 4;
+    const uint32_t* const side_src = (t_wave ? (const uint32_t*)a.gT : sq_wave ? (const uint32_t*)a.sqn : a.rsb) + (wid_s & 3) * 64;
+    const uint32_t side_dst = (t_wave ? lds_addr((const uint8_t*)tlds) : sq_wave && I8 ? lds_addr((const uint8_t*)rowq) : rowx_lds) +
+                              (uint32_t)((wid_s & 3) * 256);
     const int r16 = lane & 15;
     const uint32_t lane_off = (uint32_t)(r16 * 64 + (((lane >> 4) ^ mf_swz(r16)) << 4));
     // lane's 16 B of the wave's first fragment (its second: 16 rows further)
@@ -1701,9 +1827,14 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
     do {                                                                                                 \
         /* 4 waves cover the tile's 1 KiB of (scale | beta); waves 4-7 load its ||x||^2 (L2) or      \
            rewrite the same bytes (inner product): the same op count for every wave */                 \
-        if ((I8 || L2) && iks == nks - 1 && iti < t1)                                                    \
-            glds4(side_src + pg * TR + lane,                                                             \
-                  __builtin_amdgcn_readfirstlane(side_dst + (uint32_t)((iti & 1) * 1024)));              \
+        if ((I8 || L2) && iks == nks - 1 && iti < t1) {                                                  \
+            if (!t_wave)                                                                                 \
+                glds4(side_src + pg * TR + lane,                                                         \
+                      __builtin_amdgcn_readfirstlane(side_dst + (uint32_t)((iti & 1) * 1024)));          \
+            else /* RES: the NEXT tile's <mu_g, q> (read at its K-step 0; past the end: this one's) */    \
+                glds4(side_src + ((iti + 1 < t1 ? phys(iti + 1) : pg) * TR / I8_GROUP_ROWS) * MFMA_QB + lane, \
+                      __builtin_amdgcn_readfirstlane(side_dst + (uint32_t)(((iti + 1) & 1) * 1024)));    \
+        }                                                                                                \
         const uint32_t qbase = __builtin_amdgcn_readfirstlane(ring + (uint32_t)((SET) * 16384 + wid * 1024)); \
         _Pragma("unroll") for (int it = 0; it < 2; ++it) {                                               \
             const int g = it * 512 + wid * 64 + lane;                                                    \
@@ -1728,6 +1859,10 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
     } while (0)
 
     if (t1 > t0) {
+        if constexpr (RES)  // the first tile's <mu_g, q> (later tiles': one tile ahead, in I8D_ISSUE)
+            if (t_wave)
+                glds4(side_src + (pg * TR / I8_GROUP_ROWS) * MFMA_QB + lane,
+                      __builtin_amdgcn_readfirstlane(side_dst + (uint32_t)((t0 & 1) * 1024)));
         I8D_ISSUE(0);
         I8D_ISSUE(1);
         I8D_ISSUE(2);
@@ -1813,6 +1948,11 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
                 __syncthreads();
             }
         }
+        if constexpr (RES) {  // this tile's <mu_g, q> into qrec .w (read by the epilogue, K-steps later)
+            int otid;
+            asm volatile("v_mov_b32 %0, %1" : "=v"(otid) : "v"(tid));
+            if (otid < MFMA_QB) qrec[otid].w = tlds[(ti & 1) * MFMA_QB + otid];
+        }
         {
             const uint32_t slot_lds = ring + lane_off;
             d_step<DT, true, NG>(acc, bt, slot_lds, A[0][0], A[0][1]);
@@ -1887,6 +2027,7 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
                                                   (float)cc[j] * __uint_as_float(w8[j] << 16)) * f.x
                                  : __int_as_float(cc[j]);
                     if constexpr (L2) x = __builtin_fmaf(2.0f, x, -rq[row]);  // 2 <x, q> - ||x||^2
+                    if constexpr (RES) x += f.w;  // + <mu_g, q>
                     v[j] = rowbase + row >= a.n_valid ? __builtin_nanf("") : x;
                     mh |= (v[j] >= f.z ? 1u : 0u) << j;  // (ties resolved by key below)
                 }
@@ -1946,6 +2087,7 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
                             float x = __builtin_fmaf(__uint_as_float(w & 0xFFFF0000u), f.y,
                                                      (float)acc[m][n][r] * __uint_as_float(w << 16)) * f.x;
                             if constexpr (L2) x = __builtin_fmaf(2.0f, x, -rq[row]);
+                            if constexpr (RES) x += f.w;  // + <mu_g, q>
                             if (rowbase + row < a.n_valid) mx = fmaxf(mx, x);
                         }
                         mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
@@ -2012,6 +2154,7 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
                                 fmaxf(__int_as_float(acc[1][n][2]), __int_as_float(acc[1][n][3]))));
             }
             if constexpr (L2) b = __builtin_fmaf(2.0f, b, -sqmin);  // (monotone: >= every row's key)
+            if constexpr (RES) b += f.w;  // + <mu_g, q> (the tile's group: every row's)
             gomask |= (b >= f.z ? 1u : 0u) << n;
         }
         if (edge) gomask = (1u << NCOL) - 1u;
@@ -2090,6 +2233,10 @@ __global__ void __launch_bounds__(512, 2) k_screen_i8d(ScreenArgs a, const uint8
 // inner product (the L2 form's extra epilogue state leaves no registers for it: it keeps the pass)
 __global__ void __launch_bounds__(512, 2) k_screen_i8d_seeded(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
     screen_direct<DT_I8, METRIC_IP, false, 16, true>(a, qt, nqb);
+}
+// ... over group-residual codes (a corpus stored cluster by cluster): every key + <mu_g, q>
+__global__ void __launch_bounds__(512, 2) k_screen_i8d_seeded_res(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
+    screen_direct<DT_I8, METRIC_IP, false, 16, true, true>(a, qt, nqb);
 }
 template <int DT, int METRIC>
 __global__ void __launch_bounds__(512, 2) k_screen_d16(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
@@ -3591,14 +3738,30 @@ hipError_t launch_pack_qtile_split(int dt, const float* q, const int* qidx, cons
     return hipGetLastError();
 }
 
+hipError_t launch_group_means(int dt, const uint8_t* data, int dpad, int d, int64_t g0, int64_t ng, int64_t n_rows,
+                              int dpad8, uint16_t* gmean, unsigned* maxes, hipStream_t st) {
+    if (ng <= 0) return hipSuccess;
+    VS_DISPATCH_DT(dt, k_group_means, dim3((unsigned)ng), dim3(256), 0, st, data, dpad, d, g0, n_rows, dpad8, gmean, maxes);
+    return hipGetLastError();
+}
+
+hipError_t launch_group_dots(const uint16_t* gmean, int64_t ngroups, int dpad8, const float* q, int nq, int d, float* T,
+                             hipStream_t st) {
+    if (ngroups <= 0) return hipSuccess;
+    if (nq > MFMA_QB || dpad8 % 64 != 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_group_dots, dim3((unsigned)((ngroups + 15) / 16)), dim3(256), 0, st, gmean, ngroups, dpad8, q, nq,
+                       d, T);
+    return hipGetLastError();
+}
+
 hipError_t launch_quant_rows(int dt, const uint8_t* data, int dpad, int64_t r0, int64_t n, int d, uint8_t* data8,
-                             int dpad8, uint32_t* rsb, unsigned* maxes, hipStream_t st) {
+                             int dpad8, uint32_t* rsb, unsigned* maxes, hipStream_t st, const uint16_t* gmean) {
     if (n <= 0) return hipSuccess;
     const int64_t CHUNK = 1 << 22;  // rows per launch (grid-size bound)
     for (int64_t c0 = 0; c0 < n; c0 += CHUNK) {
         const int64_t m = n - c0 < CHUNK ? n - c0 : CHUNK;
         VS_DISPATCH_DT(dt, k_quant_rows, dim3(blocks4(m)), dim3(256), 0, st, data, dpad, r0 + c0, m, d, data8, dpad8,
-                       rsb, maxes);
+                       rsb, maxes, gmean);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -3657,6 +3820,12 @@ static hipError_t launch_mfma_dt(int dt, const ScreenArgs& a, const uint8_t* qt,
                     a.seed_prov_rank < 1 || a.seed_prov_rank > 16 ||
                     a.G * 16 > kI8dSeedMaxima || (int64_t)a.tiles < 4 * (int64_t)a.G)
                     return hipErrorInvalidValue;
+                if (a.gT) {  // group residuals
+                    set_lds_attr((const void*)k_screen_i8d_seeded_res, I8D_LDS + I8D_SEED_LDS + I8D_RES_LDS);
+                    hipLaunchKernelGGL(k_screen_i8d_seeded_res, dim3(a.G), dim3(MF_THREADS),
+                                       I8D_LDS + I8D_SEED_LDS + I8D_RES_LDS, st, a, qt, nqb);
+                    return hipGetLastError();
+                }
                 set_lds_attr((const void*)k_screen_i8d_seeded, I8D_LDS + I8D_SEED_LDS);
                 hipLaunchKernelGGL(k_screen_i8d_seeded, dim3(a.G), dim3(MF_THREADS), I8D_LDS + I8D_SEED_LDS, st, a, qt, nqb);
                 return hipGetLastError();

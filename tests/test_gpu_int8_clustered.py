@@ -77,3 +77,33 @@ def test_int8_screen_reference_photo_vectors():
         if dtype == "f32":
             assert (I8[:, 0] == np.arange(77)).all()  # every (unit) photo vector finds itself first
         ix.close()
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+def test_int8_group_residuals_incremental_adds(dtype):
+    """Cluster-sorted rows with the int8 screen switched on first and rows added in chunks that end
+    mid-group: each add re-derives the means of the groups it touches and re-quantises their rows
+    against them (group residuals).  Batches through the seeded direct pass add
+    <mu_g, q> to every key; smaller batches and shards without that pass take the native screen.
+    Every answer bit-exact against the oracle; the sorted clusters certify (no collapse)."""
+    from photo_search_engine_amd.index import FlatIndex
+
+    N, d, C = 300_000, 512, 32
+    x = _mixture(N, d, C, 0.3, O.SEED_CORPUS + 81, True)
+    q = _mixture(96, d, C, 0.3, O.SEED_QUERIES + 81, False)
+    ix = FlatIndex(d, "ip", dtype)
+    ix.set_screen("int8")
+    for a in range(0, N, 70_001):
+        ix.add(x[a:a + 70_001])
+    xs = ix.reconstruct_n(0, N)
+    for nq, k in ((96, 50), (64, 10), (4, 10), (1, 100)):
+        S, Ie = O.knn_exact(xs, q[:nq], k, "ip")
+        for _ in range(3):
+            D, I = ix.search(q[:nq], k)
+            np.testing.assert_array_equal(I, Ie)
+            np.testing.assert_array_equal(D, S.astype(np.float32))
+    u0 = ix.uncertified_count()
+    for _ in range(4):
+        ix.search(q, 50)
+    assert ix.uncertified_count() - u0 <= 96 // 16  # group residuals keep the int8 screen certifying
+    ix.close()
