@@ -365,7 +365,7 @@ def main():
                            if G > 1 else "")},
             "roofline": {
                 # the int8 main pass runs the direct form when d is a multiple of 256 (vs_kernels.hip)
-                "kernel": _kernel_name(kind, dtype, d),
+                "kernel": _kernel_name(kind, dtype, d, n_local, args.metric),
                 "bound": "hbm",
                 "achieved": round(achieved_gbs, 1),
                 "peak": HBM_PEAK_GBS,
@@ -377,6 +377,7 @@ def main():
                 "mfma_tflops": round(alg_flops / (kavg * 1e-3) / 1e12, 1),
                 "mfma_frac": round(alg_flops / (kavg * 1e-3) / 1e12 / peak_flops, 4),
                 "mfma_peak_tflops": peak_flops,
+                **_power_ceiling(kind, args.workload, alg_bytes, n_local, N),
             },
             # first-pass certificate failures; every one was re-searched exactly (search_device_exact)
             "uncertified_first_pass": uncert,
@@ -405,6 +406,27 @@ def main():
         dist.destroy_process_group()
 
 
+def _power_ceiling(kind: str, workload: str, alg_bytes: int, n_local: int, N: int) -> dict:
+    """The int8 K1 loop's own bound on this board (profiles/r04_k1_power_pair.json, from
+    scripts/k1_micro.hip at the cfg3 shape): the same loop (loads + query-fragment reads + MFMAs, no
+    epilogue) on random int8 codes vs on an all-zero corpus -- equal cycles, but the board holds a
+    lower clock under the MFMAs on random operands.  ``power_ceiling_ms`` is that loop's time on
+    random codes scaled to this launch's rows: no schedule of the same MFMA work goes below it on
+    this board, so ``frac`` cannot exceed ``power_ceiling_frac``."""
+    if kind != "mfma_i8" or workload != "cfg3":  # (the micro ran at cfg3's d = 1536)
+        return {}
+    try:
+        with open(os.path.join(REPO, "profiles", "r04_k1_power_pair.json")) as f:
+            pp = json.load(f)
+    except (OSError, ValueError):
+        return {}
+    ms = float(pp["full_random_codes_ms"]) * n_local / float(pp["rows"])
+    return {"power_ceiling_ms": round(ms, 4),
+            "power_ceiling_frac": round(alg_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "power_ceiling_zero_operands_ms": round(float(pp["full_zero_ms"]) * n_local / float(pp["rows"]), 4),
+            "power_ceiling_source": "profiles/r04_k1_power_pair.json (scripts/k1_micro.hip)"}
+
+
 def _gather_rows(row, G, dev, backend, torch, dist):
     """Every rank's list of floats -> rank-ordered list of lists (one small all-gather)."""
     t = torch.tensor(row, dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
@@ -413,12 +435,14 @@ def _gather_rows(row, G, dev, backend, torch, dist):
     return [o.cpu().tolist() for o in out]
 
 
-def _kernel_name(kind: str, dtype: str, d: int) -> str:
+def _kernel_name(kind: str, dtype: str, d: int, n_local: int = 0, metric: str = "ip") -> str:
     """The screen kernel the library ran (vs_kernels.hip): the main passes take the direct forms
-    when the K-steps per padded row are a multiple of 4 (int8: 64-element K-steps; bf16 / f16: 32)."""
+    when the K-steps per padded row are a multiple of 4 (int8: 64-element K-steps; bf16 / f16: 32);
+    the int8 inner-product form seeds its threshold itself when every workgroup has >= 4 tiles."""
     dpad = max(-(-d // 64) * 64, 64)
     if kind == "mfma_i8" and dpad % 256 == 0 and dpad >= 512:
-        return "k_screen_i8d"
+        tiles = -(-n_local // 256)
+        return "k_screen_i8d_seeded" if metric == "ip" and tiles >= 4 * min(tiles, 256) else "k_screen_i8d"
     if kind == "mfma" and dtype in ("bf16", "f16") and dpad % 128 == 0 and dpad >= 256:
         return "k_screen_d16"
     return f"k_screen_{kind}"

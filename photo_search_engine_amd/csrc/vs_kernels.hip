@@ -560,6 +560,7 @@ __device__ __forceinline__ uint32_t bf16_bits_up(float f) {  // smallest bf16 >=
     return (u >> 16) + ((u & 0xFFFFu) ? 1u : 0u);
 }
 
+constexpr int GM_COLS = 1536;  // columns per pass of k_group_means (its LDS partial sums)
 // Group residuals (inner-product int8 screens, DESIGN §5 "clustered corpora"): rows are coded as
 // x = mu_g + r with mu_g the bf16-rounded mean of their group of I8_GROUP_ROWS consecutive rows, when
 // that mean carries at least a quarter of the group's energy (a corpus inserted cluster by cluster);
@@ -571,42 +572,61 @@ template <int DT>
 __global__ void __launch_bounds__(256) k_group_means(const uint8_t* __restrict__ data, int dpad, int d, int64_t g0,
                                                       int64_t n_rows, int dpad8, uint16_t* __restrict__ gmean,
                                                       unsigned* __restrict__ maxes) {
+    // wave w sums rows w, w + 4, ... of the group; lane l columns l, l + 64, ... (one 128 B line of
+    // the tiled layout per row and 64 columns at 16-bit): GM_COLS / 64 independent loads per row
     constexpr int ES = DT == DT_F32 ? 4 : 2;
-    __shared__ double red[2][4];
+    constexpr int NC = GM_COLS / 64;
+    __shared__ float part[4][GM_COLS];
+    __shared__ float e2[4];
+    __shared__ double m2w[4];
     const int64_t g = g0 + blockIdx.x;
     const int64_t lo = g * I8_GROUP_ROWS, hi = min(n_rows, lo + I8_GROUP_ROWS);
-    const int tid = threadIdx.x;
-    const double cnt = (double)(hi - lo);
-    double m2 = 0.0, x2 = 0.0;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     uint16_t* dst = gmean + (size_t)g * dpad8;
-    for (int i = tid; i < dpad8; i += 256) {
-        double s = 0.0;
-        if (i < d)
-            for (int64_t r = lo; r < hi; ++r) {
-                const double v = (double)load_elem<DT>(data + tiled_off(r, i, dpad, ES));
-                s += v;
+    const float cnt = (float)(hi - lo);
+    float x2 = 0.0f;
+    double m2 = 0.0;  // ||mu||^2 of the stored bf16 means, exactly enough for the margin (fp64)
+    for (int c0 = 0; c0 < dpad8; c0 += GM_COLS) {  // column blocks (d > GM_COLS)
+        float s[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) s[c] = 0.0f;
+        for (int64_t r = lo + w; r < hi; r += 4) {
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                const int i = c0 + 64 * c + lane;
+                const float v = i < d ? load_elem<DT>(data + tiled_off(r, i, dpad, ES)) : 0.0f;
+                s[c] += v;
                 x2 += v * v;
             }
-        const uint16_t b = (i < d && cnt > 0) ? f32_to_bf16_rne((float)(s / cnt)) : (uint16_t)0;
-        dst[i] = b;
-        const double mu = (double)bf16_bits_to_f32(b);
-        m2 += mu * mu;
+        }
+#pragma unroll
+        for (int c = 0; c < NC; ++c) part[w][64 * c + lane] = s[c];
+        __syncthreads();
+        for (int i = tid; i < GM_COLS && c0 + i < dpad8; i += 256) {
+            const float t = part[0][i] + part[1][i] + part[2][i] + part[3][i];
+            const uint16_t b = (c0 + i < d && cnt > 0.0f) ? f32_to_bf16_rne(t / cnt) : (uint16_t)0;
+            dst[c0 + i] = b;
+            const double mu = (double)bf16_bits_to_f32(b);
+            m2 += mu * mu;
+        }
+        __syncthreads();
     }
+    x2 = wave_sum_fp32_canon(x2);
     m2 = wave_sum_f64(m2);
-    x2 = wave_sum_f64(x2);
-    if ((tid & 63) == 0) {
-        red[0][tid >> 6] = m2;
-        red[1][tid >> 6] = x2;
+    if (lane == 0) {
+        e2[w] = x2;
+        m2w[w] = m2;
     }
     __syncthreads();
-    const double M2 = red[0][0] + red[0][1] + red[0][2] + red[0][3];
-    const double X2 = red[1][0] + red[1][1] + red[1][2] + red[1][3];
-    // a mean worth coding against: >= 1/4 of the group's mean row energy
-    const bool use = cnt > 0 && M2 * cnt >= 0.25 * X2 && M2 > 0.0;
+    const double M2 = m2w[0] + m2w[1] + m2w[2] + m2w[3];
+    const float X2 = e2[0] + e2[1] + e2[2] + e2[3];
+    // a mean worth coding against: >= 1/4 of the group's mean row energy (a heuristic choice:
+    // any mean, zero included, gives exact keys)
+    const bool use = cnt > 0.0f && M2 > 0.0 && (float)M2 * cnt >= 0.25f * X2;
     if (!use)
         for (int i = tid; i < dpad8; i += 256) dst[i] = 0;
     if (tid == 0 && use) {
-        atomicMax(&maxes[0], __float_as_uint(f32_up(sqrt(M2) * (1.0 + 1e-9))));
+        atomicMax(&maxes[0], __float_as_uint(f32_up(sqrt(M2) * (1.0 + 1e-9))));  // the margin's max ||mu||
         atomicAdd(&maxes[1], 1u);
     }
 }
