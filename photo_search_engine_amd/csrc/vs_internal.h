@@ -433,7 +433,8 @@ hipError_t launch_merge_shards(int metric, const double* S_in, const int64_t* I_
 // neighbors[offsets[i] + cum[l] .. offsets[i] + cum[l + 1]), -1 padded), rows of a flat index,
 // canonical fp64 distances.  One workgroup per query; the candidate and result heaps are sorted
 // LDS arrays under (distance, id).
-constexpr int HN_THREADS = 256;
+constexpr int HN_THREADS = 256;          // k_hnsw_prune: one workgroup per node
+constexpr int HN_SEARCH_THREADS = 512;   // k_hnsw_search: one workgroup per query (8 waves score a list)
 constexpr int HN_EF_MAX = 2048;  // largest max(efSearch, k)
 constexpr int HN_NB_MAX = 1024;  // largest neighbour list of one level
 struct HnswArgs {

@@ -4142,9 +4142,11 @@ hipError_t launch_merge_shards(int metric, const double* S_in, const int64_t* I_
 // K7: HNSW graph search (host side vs_hnsw.hip) -- faiss HNSW::search restated
 // (oracle/hnsw_oracle.py): greedy descent on the upper levels, then level 0 with a candidate set of
 // capacity ef (popped entries stay and count in the stop test) and a result set of k.  One
-// 256-thread workgroup per query.  Distances are exact_score_rows' canonical fp64 scores (IP:
+// 1024-thread workgroup per query (the steps are dependent: 16 waves score a neighbour list in one
+// or two rounds of 4 rows each, where 4 waves took up to 6 -- the step latency, not the bytes, sets
+// the time).  Distances are exact_score_rows' canonical fp64 scores (IP:
 // -score).  Both sets are sorted LDS arrays under (distance, id) and take a whole neighbour list
-// per step: the new rows are scored by all four waves, rank-sorted, and merged (an element's new
+// per step: the new rows are scored by all 16 waves, rank-sorted, and merged (an element's new
 // position = its index in its own list + its rank in the other, one binary search) -- the same
 // decisions as faiss's array heaps whenever no two rows tie in distance.
 // ------------------------------------------------------------------------------------------------
@@ -4224,9 +4226,9 @@ __device__ __forceinline__ int hn_count_below(const double* d, int n, double t) 
 }
 
 template <int DT, int METRIC, bool QLDS>
-__global__ void __launch_bounds__(HN_THREADS) k_hnsw_search(HnswArgs a) {
+__global__ void __launch_bounds__(HN_SEARCH_THREADS) k_hnsw_search(HnswArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    constexpr int NW = HN_THREADS / 64;
+    constexpr int NW = HN_SEARCH_THREADS / 64;
     constexpr bool IP = METRIC == METRIC_IP;
     __shared__ int s_m, s_imin, s_valid;
     __shared__ int s_new[NW], s_wj[NW];
@@ -4240,14 +4242,14 @@ __global__ void __launch_bounds__(HN_THREADS) k_hnsw_search(HnswArgs a) {
     float* Dq = a.D + (int64_t)q * a.k;
     int64_t* Iq = a.I + (int64_t)q * a.k;
     if (a.entry < 0 || a.n == 0) {
-        for (int j = tid; j < a.k; j += HN_THREADS) {
+        for (int j = tid; j < a.k; j += HN_SEARCH_THREADS) {
             Dq[j] = IP ? -__FLT_MAX__ : __FLT_MAX__;
             Iq[j] = -1;
         }
         return;
     }
     if constexpr (QLDS)
-        for (int i = tid; i < a.d; i += HN_THREADS) L.qs[(i & 7) * ng + (i >> 3)] = (double)qv[i];
+        for (int i = tid; i < a.d; i += HN_SEARCH_THREADS) L.qs[(i & 7) * ng + (i >> 3)] = (double)qv[i];
 
     // faiss distances of the rows bi[0 .. m) into bd (all waves, refine_rows rows per wave-step)
     auto score = [&](int m) {
@@ -4272,7 +4274,7 @@ __global__ void __launch_bounds__(HN_THREADS) k_hnsw_search(HnswArgs a) {
         __syncthreads();
         if (tid == 0) s_m = w;
         __syncthreads();
-        for (int t = tid; t < w; t += HN_THREADS) {
+        for (int t = tid; t < w; t += HN_SEARCH_THREADS) {
             const int u = src[t];
             L.bl[t] = u;
             if (u < 0) atomicMin(&s_m, t);
@@ -4290,13 +4292,13 @@ __global__ void __launch_bounds__(HN_THREADS) k_hnsw_search(HnswArgs a) {
     for (int l = a.max_level; l >= 1; --l) {
         for (int64_t guard = 0; guard <= a.n; ++guard) {  // the distance strictly decreases
             const int m = load_list(near, l);
-            for (int t = tid; t < m; t += HN_THREADS) L.bi[t] = L.bl[t];
+            for (int t = tid; t < m; t += HN_SEARCH_THREADS) L.bi[t] = L.bl[t];
             __syncthreads();
             score(m);
             // the first neighbour at the smallest distance (faiss: first strictly closer, in order)
             double bd = INFINITY;
             int bj = 0x7FFFFFFF;
-            for (int t = tid; t < m; t += HN_THREADS) {
+            for (int t = tid; t < m; t += HN_SEARCH_THREADS) {
                 const double v = L.bd[t];
                 if (v < bd) {
                     bd = v;
@@ -4349,7 +4351,7 @@ __global__ void __launch_bounds__(HN_THREADS) k_hnsw_search(HnswArgs a) {
             s_valid = 0;
         }
         __syncthreads();
-        for (int i = tid; i < nc; i += HN_THREADS)
+        for (int i = tid; i < nc; i += HN_SEARCH_THREADS)
             if (L.cv[cur][i]) {
                 atomicMin(&s_imin, i);
                 break;
@@ -4366,7 +4368,7 @@ __global__ void __launch_bounds__(HN_THREADS) k_hnsw_search(HnswArgs a) {
         const int m = load_list(v0, 0);
         // visited test-and-set; the new neighbours compacted in list order into bi
         int nn = 0;
-        for (int t0 = 0; t0 < m; t0 += HN_THREADS) {
+        for (int t0 = 0; t0 < m; t0 += HN_SEARCH_THREADS) {
             const int t = t0 + tid;
             bool isnew = false;
             int v = -1;
@@ -4390,7 +4392,7 @@ __global__ void __launch_bounds__(HN_THREADS) k_hnsw_search(HnswArgs a) {
         }
         if (nn == 0) continue;
         score(nn);
-        for (int j = tid; j < nn; j += HN_THREADS) {  // rank sort by (distance, id)
+        for (int j = tid; j < nn; j += HN_SEARCH_THREADS) {  // rank sort by (distance, id)
             const double dj = L.bd[j];
             const int ij = L.bi[j];
             int r = 0;
@@ -4400,14 +4402,14 @@ __global__ void __launch_bounds__(HN_THREADS) k_hnsw_search(HnswArgs a) {
         }
         __syncthreads();
         const int nxt = cur ^ 1;
-        for (int i = tid; i < nres; i += HN_THREADS) {  // results: the best k of the union
+        for (int i = tid; i < nres; i += HN_SEARCH_THREADS) {  // results: the best k of the union
             const int p = i + hn_rank(L.sd, L.si, nn, L.rd[cur][i], L.ri[cur][i]);
             if (p < a.k) {
                 L.rd[nxt][p] = L.rd[cur][i];
                 L.ri[nxt][p] = L.ri[cur][i];
             }
         }
-        for (int j = tid; j < nn; j += HN_THREADS) {
+        for (int j = tid; j < nn; j += HN_SEARCH_THREADS) {
             const int p = j + hn_rank(L.rd[cur], L.ri[cur], nres, L.sd[j], L.si[j]);
             if (p < a.k) {
                 L.rd[nxt][p] = L.sd[j];
@@ -4415,7 +4417,7 @@ __global__ void __launch_bounds__(HN_THREADS) k_hnsw_search(HnswArgs a) {
             }
         }
         int myvalid = 0;  // candidates: the best ef of the union, popped entries included
-        for (int i = tid; i < nc; i += HN_THREADS) {
+        for (int i = tid; i < nc; i += HN_SEARCH_THREADS) {
             const int p = i + hn_rank(L.sd, L.si, nn, L.cd[cur][i], L.ci[cur][i]);
             if (p < a.ef) {
                 L.cd[nxt][p] = L.cd[cur][i];
@@ -4424,7 +4426,7 @@ __global__ void __launch_bounds__(HN_THREADS) k_hnsw_search(HnswArgs a) {
                 myvalid += L.cv[cur][i];
             }
         }
-        for (int j = tid; j < nn; j += HN_THREADS) {
+        for (int j = tid; j < nn; j += HN_SEARCH_THREADS) {
             const int p = j + hn_rank(L.cd[cur], L.ci[cur], nc, L.sd[j], L.si[j]);
             if (p < a.ef) {
                 L.cd[nxt][p] = L.sd[j];
@@ -4443,7 +4445,7 @@ __global__ void __launch_bounds__(HN_THREADS) k_hnsw_search(HnswArgs a) {
         __syncthreads();  // s_valid read by every thread before the next step resets it
     }
     __syncthreads();
-    for (int j = tid; j < a.k; j += HN_THREADS) {
+    for (int j = tid; j < a.k; j += HN_SEARCH_THREADS) {
         if (j < nres) {
             const double dv = L.rd[cur][j];
             Dq[j] = (float)(IP ? -dv : dv);
@@ -4458,7 +4460,7 @@ __global__ void __launch_bounds__(HN_THREADS) k_hnsw_search(HnswArgs a) {
 template <int DT, int METRIC, bool QLDS>
 static void launch_hnsw_one(const HnswArgs& a, int nq, size_t lds, hipStream_t st) {
     set_lds_attr((const void*)k_hnsw_search<DT, METRIC, QLDS>, (int)HN_LDS_CAP);
-    hipLaunchKernelGGL((k_hnsw_search<DT, METRIC, QLDS>), dim3(nq), dim3(HN_THREADS), lds, st, a);
+    hipLaunchKernelGGL((k_hnsw_search<DT, METRIC, QLDS>), dim3(nq), dim3(HN_SEARCH_THREADS), lds, st, a);
 }
 template <int DT>
 static void launch_hnsw_dt(const HnswArgs& a, int nq, size_t lds, bool qlds, hipStream_t st) {

@@ -1,0 +1,40 @@
+#!/bin/bash
+# One GPU call of round-4 checks: the changed/new GPU suites (all of them run: a failing test does
+# not stop the call), then the benches.  A crash, abort, fault or time limit (rc 124/134/137/139 or
+# any rc > 128) ends the call there.
+#   STEPS="tests cfg3 shard8 mix03 micro multi" bash scripts/r04_gpu_batch.sh
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+PYT="python -u -m pytest -v --timeout 300 --timeout-method thread"
+TESTS=${TESTS:-"tests/test_gpu_int8_seeded.py tests/test_gpu_int8_clustered.py tests/test_gpu_multi_device.py tests/test_gpu_hnsw_build.py tests/test_gpu_hnsw.py tests/test_gpu_cfg1.py tests/test_gpu_int8_screen.py tests/test_gpu_distributed.py"}
+fatal() { [ "$1" -ge 124 ] && [ "$1" -ne 0 ]; }
+run() {  # name, seconds, command...
+  local name=$1 secs=$2; shift 2
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "step $name rc=$rc" >> gpurun_out/steps.log
+  if fatal $rc; then echo "fatal rc=$rc in $name: stopping" >> gpurun_out/steps.log; exit $rc; fi
+  return 0
+}
+for s in ${STEPS:-tests cfg3 shard8 mix03 micro multi}; do
+  case $s in
+    tests) run pytest_new 1500 $PYT $TESTS -m gpu ;;
+    full) run pytest_gpu 1500 $PYT tests -m gpu ;;
+    smoke) run smoke 300 python __graft_entry__.py --smoke ;;
+    cfg3) run bench_cfg3 600 python bench.py ;;
+    cfg1) run bench_cfg1 300 python bench.py --workload cfg1 --steps 1000 --warmup 50 ;;
+    shard8) run bench_shard8 300 python bench.py --shard-of 8 --steps 30 --no-cpu-baseline ;;
+    spawn2) run bench_spawn2 600 python bench.py --gpus 2 --same-device --dist-backend gloo --rows 2000000 --steps 10 --no-cpu-baseline ;;
+    mix03) run bench_mix03 600 python bench.py --data mixture-sorted --sigma 0.3 --no-cpu-baseline ;;
+    mix10) run bench_mix10 600 python bench.py --data mixture-sorted --sigma 1.0 --no-cpu-baseline ;;
+    micro) for m in 0 2 9; do for dt in 1 2; do
+             timeout -k 10 120 ./abtmp/k1_micro 10000000 1536 20 $dt $m >> gpurun_out/k1_micro.txt 2>&1
+             rc=$?; if [ $rc -ne 0 ]; then echo "step micro rc=$rc" >> gpurun_out/steps.log; exit $rc; fi
+           done; done; echo "step micro rc=0" >> gpurun_out/steps.log ;;
+    multi) run multi_step 600 python scripts/multi_step_timing.py ;;
+    hnsw) run hnsw_bench 900 python scripts/hnsw_bench.py ;;
+    *) echo "unknown step $s" >> gpurun_out/steps.log; exit 2 ;;
+  esac
+done
