@@ -620,9 +620,10 @@ __global__ void __launch_bounds__(256) k_group_means(const uint8_t* __restrict__
     __syncthreads();
     const double M2 = m2w[0] + m2w[1] + m2w[2] + m2w[3];
     const float X2 = e2[0] + e2[1] + e2[2] + e2[3];
-    // a mean worth coding against: >= 1/4 of the group's mean row energy (a heuristic choice:
-    // any mean, zero included, gives exact keys)
-    const bool use = cnt > 0.0f && M2 > 0.0 && (float)M2 * cnt >= 0.25f * X2;
+    // a mean worth coding against: >= 1/4 of the group's mean row energy, over at least a tile of
+    // rows (a few rows are their own mean, whatever the corpus) -- a heuristic choice: any mean,
+    // zero included, gives exact keys
+    const bool use = cnt >= (float)TR && M2 > 0.0 && (float)M2 * cnt >= 0.25f * X2;
     if (!use)
         for (int i = tid; i < dpad8; i += 256) dst[i] = 0;
     if (tid == 0 && use) {
