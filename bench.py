@@ -365,7 +365,8 @@ def main():
                            if G > 1 else "")},
             "roofline": {
                 # the int8 main pass runs the direct form when d is a multiple of 256 (vs_kernels.hip)
-                "kernel": _kernel_name(kind, dtype, d, n_local, args.metric),
+                "kernel": _kernel_name(kind, dtype, d, n_local, args.metric,
+                                       bool(ix.screen_state()["group_residuals"]) if kind == "mfma_i8" else False),
                 "bound": "hbm",
                 "achieved": round(achieved_gbs, 1),
                 "peak": HBM_PEAK_GBS,
@@ -382,6 +383,8 @@ def main():
             # first-pass certificate failures; every one was re-searched exactly (search_device_exact)
             "uncertified_first_pass": uncert,
             "unresolved": unresolved,
+            # group residuals, margins and the screen-health state after the timed steps (vs_screen_state)
+            "screen_state": ix.screen_state(),
             "build_s": round(t_build, 2),
         }
         if G > 1 or args.shard_of > 1:
@@ -408,8 +411,8 @@ def main():
 
 def _power_ceiling(kind: str, workload: str, alg_bytes: int, n_local: int, N: int) -> dict:
     """The int8 K1 loop's own bound on this board (profiles/r04_k1_power_pair.json, from
-    scripts/k1_micro.hip at the cfg3 shape): the same loop (loads + query-fragment reads + MFMAs, no
-    epilogue) on random int8 codes vs on an all-zero corpus -- equal cycles, but the board holds a
+    scripts/k1_micro.hip mode 9 at the cfg3 shape): the same loop (loads + query-fragment reads + MFMAs +
+    the product's bound epilogue) on int8 codes of Gaussian rows vs on an all-zero corpus -- equal cycles, but the board holds a
     lower clock under the MFMAs on random operands.  ``power_ceiling_ms`` is that loop's time on
     random codes scaled to this launch's rows: no schedule of the same MFMA work goes below it on
     this board, so ``frac`` cannot exceed ``power_ceiling_frac``."""
@@ -435,14 +438,17 @@ def _gather_rows(row, G, dev, backend, torch, dist):
     return [o.cpu().tolist() for o in out]
 
 
-def _kernel_name(kind: str, dtype: str, d: int, n_local: int = 0, metric: str = "ip") -> str:
+def _kernel_name(kind: str, dtype: str, d: int, n_local: int = 0, metric: str = "ip", residual: bool = False) -> str:
     """The screen kernel the library ran (vs_kernels.hip): the main passes take the direct forms
     when the K-steps per padded row are a multiple of 4 (int8: 64-element K-steps; bf16 / f16: 32);
-    the int8 inner-product form seeds its threshold itself when every workgroup has >= 4 tiles."""
+    int8 codes taken against group means (``residual``) run the inner-product form that adds
+    <mu_g, q> and seeds its threshold itself (every workgroup >= 4 tiles)."""
     dpad = max(-(-d // 64) * 64, 64)
     if kind == "mfma_i8" and dpad % 256 == 0 and dpad >= 512:
         tiles = -(-n_local // 256)
-        return "k_screen_i8d_seeded" if metric == "ip" and tiles >= 4 * min(tiles, 256) else "k_screen_i8d"
+        if residual and metric == "ip" and tiles >= 4 * min(tiles, 256):
+            return "k_screen_i8d_seeded_res"
+        return "k_screen_i8d"
     if kind == "mfma" and dtype in ("bf16", "f16") and dpad % 128 == 0 and dpad >= 256:
         return "k_screen_d16"
     return f"k_screen_{kind}"

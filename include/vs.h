@@ -178,6 +178,12 @@ int64_t vs_host_staging_bytes(vs_index* index);
 /* HBM bytes the screen copies hold beyond the stored rows (VS_SCREEN_I8: int8 codes, per-row scale |
  * error norm); 0 for native screens */
 int64_t vs_screen_copy_bytes(vs_index* index);
+/* the screen's state, up to `cap` doubles: [0] screen, [1] group residuals in use, [2] groups coded
+ * against a mean, [3] max ||mu_g||, [4] max ||x_hat|| of the int8 codes, [5] max row error norm,
+ * [6] int8 union log2 depth, [7] searches still routed to the native screen, [8] native seed log2
+ * depth (the screen-health feedback described at vs_search_device_exact); synchronises */
+#define VS_SCREEN_STATE_N 9
+int vs_screen_state(vs_index* index, double* out, int cap);
 
 /* ==== multi-device flat index (one process, several GPUs; SURVEY.md §8 b/e) =================
  * The reference holds ONE index in ONE process (main.py:59-68 -> utils/vector_store.py:72-81); this

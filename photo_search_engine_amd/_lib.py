@@ -86,6 +86,7 @@ _SIGS = {
     "vs_unresolved_count": (_c_i64, [_vp]),
     "vs_host_staging_bytes": (_c_i64, [_vp]),
     "vs_screen_copy_bytes": (_c_i64, [_vp]),
+    "vs_screen_state": (ctypes.c_int, [_vp, _vp, ctypes.c_int]),
     # multi-device flat index
     "vs_multi_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp,
                                        ctypes.POINTER(_vp)]),

@@ -138,6 +138,7 @@ struct vs_index {
     int i8_route = 0;           // searches still routed to the native screen
     int seed_log2 = 0, seed_clean = 0;
     int i8_log2 = 0, i8_clean = 0;  // int8 union depth: 2^i8_log2 times the target (dense corpora)
+    int i8_route_log2 = 0;          // consecutive routings (each twice as long as the last)
 };
 
 vs::FlatView vs::flat_view(vs_index* ix) {
@@ -294,7 +295,7 @@ void refresh_maxsq(vs_index* ix) {
     HIP_CHECK(hipMemcpyAsync(bits, ix->d_maxsq, sizeof(bits), hipMemcpyDeviceToHost, ix->own));
     HIP_CHECK(hipStreamSynchronize(ix->own));
     std::memcpy(&ix->maxsq, &bits[0], 4);
-    std::memcpy(&ix->i8_bmax, &bits[3], 4);  // int8 copy: the largest row error norm
+    std::memcpy(&ix->i8_bmax, &bits[7], 4);  // int8 copy: the largest ||x - s c|| (GEMV keys' error)
     ix->i8_res = ix->gmean != nullptr && bits[6] != 0;  // some group coded against its mean
 }
 
@@ -327,6 +328,7 @@ constexpr int kI8RouteBatches = 64;  // searches routed to the native screen aft
 constexpr int kSeedScaleMax = 6;     // native optimistic seed: at most 64x the default depth
 constexpr int kSeedRelax = 64;       // clean native batches before the depth is halved again
 constexpr int kI8ScaleMax = 4;       // int8 union: at most 16x its target before routing to native
+constexpr int kI8RouteLog2Max = 6;   // routing stretches: at most 64 x kI8RouteBatches searches
 
 // observe a completed failure-count readback (caller holds h_mu)
 void health_poll(vs_index* ix) {
@@ -336,13 +338,24 @@ void health_poll(vs_index* ix) {
             // an int8 batch with failures: a deeper union first (dense score distributions put
             // more rows inside the int8 error window), the native screen when even the deepest
             // union failed; clean batches relax the depth again
+            // (a batch where over a quarter of the queries failed deepens two steps at once; each
+            // routing that follows a failure at the deepest union lasts twice as long as the last,
+            // up to 2^kI8RouteLog2Max times kI8RouteBatches, so a corpus the int8 window cannot
+            // serve costs one failing batch per ever longer native stretch)
             if (f > 0) {
-                if (ix->i8_log2 < kI8ScaleMax) ++ix->i8_log2;
-                else ix->i8_route = kI8RouteBatches;
+                if (ix->i8_log2 < kI8ScaleMax) {
+                    ix->i8_log2 = std::min(kI8ScaleMax, ix->i8_log2 + (f > (unsigned)(ix->h_nq / 4) ? 2 : 1));
+                } else {
+                    ix->i8_route = kI8RouteBatches << ix->i8_route_log2;
+                    ix->i8_route_log2 = std::min(ix->i8_route_log2 + 1, kI8RouteLog2Max);
+                }
                 ix->i8_clean = 0;
-            } else if (ix->i8_log2 > 0 && ++ix->i8_clean >= kSeedRelax) {
-                --ix->i8_log2;
-                ix->i8_clean = 0;
+            } else {
+                ix->i8_route_log2 = 0;
+                if (ix->i8_log2 > 0 && ++ix->i8_clean >= kSeedRelax) {
+                    --ix->i8_log2;
+                    ix->i8_clean = 0;
+                }
             }
         } else if (f > (unsigned)(ix->h_nq / 64)) {  // (a stray hard query does not deepen every batch)
             ix->seed_log2 = std::min(ix->seed_log2 + 1, kSeedScaleMax);
@@ -464,8 +477,13 @@ void search_block_i8(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float
     // threshold seeding: inside the direct main pass (its workgroups sample, select and adopt the
     // seed themselves, k_screen_i8d_seeded), else a seed pass + select before it
     const bool seeded = tiles >= 4 * (int64_t)a.G;
-    const bool seed_in_kernel =
-        seeded && ix->metric == METRIC_IP && i8_direct_ok(ix->dpad8) && a.G * 16 <= kI8dSeedMaxima;
+    // (only for group-residual codes, which need that kernel's <mu_g, q> terms: measured on MI355X,
+    // the seed pass + select ahead of k_screen_i8d beat the in-kernel seeding by 0.19-0.23 ms per
+    // batch at cfg3 (K1 3.73 vs 3.96 ms) and 0.2 ms at the 8-shard's 1.25M rows (0.52 vs 0.72 ms):
+    // the tiles screened under the provisional thresholds cost more than the two launches,
+    // profiles/r04_seed_ab.txt)
+    const bool seed_in_kernel = ix->i8_res && seeded && ix->metric == METRIC_IP && i8_direct_ok(ix->dpad8) &&
+                                a.G * 16 <= kI8dSeedMaxima;
     if (ix->i8_res && !seed_in_kernel) throw VsError(VS_ERR_INTERNAL, "group-residual int8 codes need the seeded direct pass");
     if (ix->i8_res) {  // <mu_g, q> of every group for this block's queries
         const int64_t ng = (ix->ntotal + I8_GROUP_ROWS - 1) / I8_GROUP_ROWS;
@@ -1156,7 +1174,8 @@ int vs_create(int d, int metric, int dtype, int device, vs_index** out) {
         try {
             HIP_CHECK(hipStreamCreateWithFlags(&ix->own, hipStreamNonBlocking));
             // [0] max ||x||^2, [1] uncertified counter, [2..3] int8 screen maxima (fp32 bits),
-            // [4] unresolved counter (device fallback)
+            // [4] unresolved counter (device fallback), [5..6] group residuals (max ||mu_g||,
+            // groups with a mean), [7] max ||x - s c|| of the int8 codes
             HIP_CHECK(hipMalloc(&ix->d_maxsq, sizeof(unsigned) * 8));
             HIP_CHECK(hipMemset(ix->d_maxsq, 0, sizeof(unsigned) * 8));
             ix->d_uncert = ix->d_maxsq + 1;
@@ -1204,7 +1223,7 @@ int vs_reset(vs_index* ix) {
         ix->i8_res = false;
         HIP_CHECK(hipMemsetAsync(ix->d_maxsq, 0, sizeof(unsigned), ix->own));
         HIP_CHECK(hipMemsetAsync(ix->d_maxsq + 2, 0, 2 * sizeof(unsigned), ix->own));
-        HIP_CHECK(hipMemsetAsync(ix->d_maxsq + 5, 0, 2 * sizeof(unsigned), ix->own));
+        HIP_CHECK(hipMemsetAsync(ix->d_maxsq + 5, 0, 3 * sizeof(unsigned), ix->own));
         HIP_CHECK(hipStreamSynchronize(ix->own));
     });
 }
@@ -1487,7 +1506,7 @@ int vs_set_screen(vs_index* ix, int screen) {
         ix->dpad8 = (int)std::max<int64_t>(round_up(ix->d, 64), 128);  // >= 2 K-steps per tile (see dpad)
         try {
             HIP_CHECK(hipMemsetAsync(ix->d_maxsq + 2, 0, 2 * sizeof(unsigned), ix->own));
-            HIP_CHECK(hipMemsetAsync(ix->d_maxsq + 5, 0, 2 * sizeof(unsigned), ix->own));
+            HIP_CHECK(hipMemsetAsync(ix->d_maxsq + 5, 0, 3 * sizeof(unsigned), ix->own));
             ensure_capacity_i8(ix);
             quantize_rows(ix, 0, ix->ntotal, ix->own);
             HIP_CHECK(hipStreamSynchronize(ix->own));
@@ -1544,6 +1563,27 @@ int64_t vs_screen_copy_bytes(vs_index* ix) {
     const int64_t rows = ix->cap8;
     return (rows / TR) * (int64_t)TR * ix->dpad8 + rows * (int64_t)sizeof(uint32_t) +
            ix->gcap * ix->dpad8 * (int64_t)sizeof(uint16_t);
+}
+
+int vs_screen_state(vs_index* ix, double* out, int cap) {
+    return guarded([&] {
+        check_index(ix);
+        if (!out || cap < 0) throw VsError(VS_ERR_ARG, "null output");
+        DeviceGuard dg(ix->device);
+        HIP_CHECK(hipDeviceSynchronize());
+        unsigned bits[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        HIP_CHECK(hipMemcpy(bits, ix->d_maxsq, sizeof(bits), hipMemcpyDeviceToHost));
+        auto f = [&](int i) {
+            float v;
+            std::memcpy(&v, &bits[i], 4);
+            return (double)v;
+        };
+        std::lock_guard<std::mutex> g(ix->h_mu);
+        health_poll(ix);
+        const double v[VS_SCREEN_STATE_N] = {(double)ix->screen, ix->i8_res ? 1.0 : 0.0, (double)bits[6], f(5), f(2),
+                                             f(3), (double)ix->i8_log2, (double)ix->i8_route, (double)ix->seed_log2};
+        for (int i = 0; i < cap && i < VS_SCREEN_STATE_N; ++i) out[i] = v[i];
+    });
 }
 
 int64_t vs_unresolved_count(vs_index* ix) {

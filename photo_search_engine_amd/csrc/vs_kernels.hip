@@ -535,8 +535,9 @@ __global__ void __launch_bounds__(256) k_pack_qtile_split(const float* __restric
 
 // ------------------------------------------------------------------------------------------------
 // int8 screen copy (DESIGN §5 "int8 screen").  Per row, over its STORED values x: scale
-// s = bf16(max|x| / 127), codes c = rint(x / s) in [-127, 127], and the exact error norm
-// beta = ||x - s c||_2 (fp64, rounded up to bf16); (s, beta) packed in one u32 per row (the screen
+// s = bf16(max|x| / 127), codes c = rint(x / s) in [-127, 127], and the bound
+// beta = ||x - s c||_2 + eps_q ||s c|| (fp64, rounded up to bf16; eps_q: the query's share, see
+// i8_eps_q); (s, beta) packed in one u32 per row (the screen
 // epilogue reads 4 B per row).  Also the running maxima of ||s c|| and beta
 // (maxes[0], maxes[1], fp32 bits) that bound the query-side and rounding terms of the refine's
 // certificate.  The codes need not be the nearest: whatever rint gives, beta is measured.
@@ -632,6 +633,16 @@ __global__ void __launch_bounds__(256) k_group_means(const uint8_t* __restrict__
     }
 }
 
+// The query side's int8 error ||q - t_q c_q|| is bounded per row, not per corpus: each row's bound
+// word carries beta_x = ||x - s_x c_x|| + eps_q ||s_x c_x||, eps_q the typical relative int8 error of
+// a d-vector (rms t / sqrt(12) per element, t = max / 127 ~ sqrt(2 ln 2d) sigma / 127), +10%; a
+// query whose own error exceeds eps_q ||q|| pays the excess x max ||s_x c_x|| in its margin
+// (k_pack_qtile_i8).  So a row far from its group mean widens only its own key, not every query's
+// margin (cluster-boundary rows of group residuals: ||s_x c_x|| up to ~1.4 ||x||).
+__host__ __device__ inline double i8_eps_q(int d) {
+    return 1.1 * sqrt(2.0 * log(2.0 * (double)(d > 1 ? d : 1))) / (127.0 * 3.4641016151377544);
+}
+
 template <int DT>
 __global__ void __launch_bounds__(256) k_quant_rows(const uint8_t* __restrict__ data, int dpad, int64_t r0, int64_t n,
                                                      int d, uint8_t* __restrict__ data8, int dpad8,
@@ -676,10 +687,13 @@ __global__ void __launch_bounds__(256) k_quant_rows(const uint8_t* __restrict__ 
     c2 = wave_sum_f64(c2);
     r2 = wave_sum_f64(r2);
     if (lane == 0) {
-        const uint32_t bbits = bf16_bits_up(f32_up(sqrt(e2) * (1.0 + 1e-9) + (mu ? sqrt(r2) * 4.440892098500626e-16 : 0.0)));
+        const double xh = sqrt(c2) * (double)sc;  // ||s_x c_x|| (the query error's row factor)
+        const uint32_t bbits = bf16_bits_up(f32_up((sqrt(e2) + i8_eps_q(d) * xh) * (1.0 + 1e-9) +
+                                                   (mu ? sqrt(r2) * 4.440892098500626e-16 : 0.0)));
         rsb[row] = sbits | (bbits << 16);
         atomicMax(&maxes[0], __float_as_uint(f32_up(sqrt(c2) * (double)sc * (1.0 + 1e-9))));
         atomicMax(&maxes[1], bbits << 16);  // the fp32 bits of the bf16 bound
+        atomicMax(&maxes[5], __float_as_uint(f32_up(sqrt(e2) * (1.0 + 1e-9))));  // max ||x - s c|| (GEMV depth)
     }
 }
 
@@ -737,7 +751,8 @@ __global__ void __launch_bounds__(256) k_group_dots(const uint16_t* __restrict__
 // int8 query tile [nks8][256][64] (codes of q / t_q, t_q = max|q| / 127) for the int8 MFMA screen,
 // one wave per query.  qfac = (t_q, ||q|| rounded up / t_q); qeps = the query-side margin of the
 // screen key (key = s_x t_q <c_x, c_q> + beta_x ||q||, see k_screen_mfma):
-//   true <x, q> <= key + ||s_x c_x|| ||q - t_q c_q|| + rounding <= key_score + qeps.
+//   true <x, q> <= s_x t_q <c_x, c_q> + ||x - s_x c_x|| ||q|| + ||s_x c_x|| ||q - t_q c_q|| + rounding
+//               <= key + max ||s_x c_x|| max(0, ||q - t_q c_q|| - eps_q ||q||) + rounding <= key_score + qeps.
 // Also zeroes the survivor-list lengths and the workgroup drop bounds of the screen that follows.
 __global__ void __launch_bounds__(256) k_pack_qtile_i8(const float* __restrict__ q, int nqb, int d, int dpad8,
                                                         uint8_t* __restrict__ qt, float2* __restrict__ qfac,
@@ -811,7 +826,10 @@ __global__ void __launch_bounds__(256) k_pack_qtile_i8(const float* __restrict__
         // the screen computes key = t_q * (s_x acc + beta_x * (||q|| / t_q)); a zero query has t_q = 0
         // and every key 0
         qfac[r] = make_float2(t, t > 0.0f ? qn / t : 0.0f);
-        double e = X * eq + slop;
+        // the rows' bound words cover eps_q ||q|| of this query's error (k_quant_rows); the excess
+        // over it, times the largest ||s_x c_x||
+        const double excess = fmax(0.0, eq - i8_eps_q(d) * sqrt(n2) * (1.0 - 1e-9));
+        double e = X * excess + slop;
         if (l2max) {
             // L2 keys fl(2 fl(t v) - ||x||^2_fp32) bound 2 <x, q> - ||x||^2: twice the inner-product
             // margin, the fp32 norm's error (gamma_d ||x||^2, its canonical sum) and the key's last
@@ -2344,6 +2362,7 @@ __global__ void __launch_bounds__(256) k_screen_gemv(ScreenArgs a, const float* 
     const int nch = a.dpad / CHK;
     const int64_t tbytes = (int64_t)TR * a.dpad * ES;
     u64* cand = a.cand + (size_t)blk * NQ * a.cap;
+    const float epsq = I8 ? (float)(i8_eps_q(a.d) * (1.0 - 1e-6)) : 0.0f;  // (rounded below)
     const int trigger = a.cap - TR;
 
     // tiles: a static contiguous range, or (next_tile) one at a time from a work queue with a grid
@@ -2364,10 +2383,13 @@ __global__ void __launch_bounds__(256) k_screen_gemv(ScreenArgs a, const float* 
         const int64_t rowbase = (int64_t)ti * TR;
         for (int gb = 0; gb < RG / RB; ++gb) {
             float acc[RB][NQ];
+            float cc2[RB];  // int8: sum of the codes' squares (||s_x c_x|| = s_x sqrt(cc2))
 #pragma unroll
-            for (int r = 0; r < RB; ++r)
+            for (int r = 0; r < RB; ++r) {
+                cc2[r] = 0.0f;
 #pragma unroll
                 for (int qi = 0; qi < NQ; ++qi) acc[r][qi] = 0.0f;
+            }
 #pragma unroll 2
             for (int c = 0; c < nch; ++c) {
                 float qv[NQ][EPU];
@@ -2396,6 +2418,9 @@ __global__ void __launch_bounds__(256) k_screen_gemv(ScreenArgs a, const float* 
                     for (int qi = 0; qi < NQ; ++qi)
 #pragma unroll
                         for (int e = 0; e < EPU; ++e) acc[r][qi] = fmaf(xv[e], qv[qi][e], acc[r][qi]);
+                    if constexpr (I8)
+#pragma unroll
+                        for (int e = 0; e < EPU; ++e) cc2[r] = fmaf(xv[e], xv[e], cc2[r]);
                 }
             }
 #pragma unroll
@@ -2407,6 +2432,11 @@ __global__ void __launch_bounds__(256) k_screen_gemv(ScreenArgs a, const float* 
                     for (int s = 1; s < LPR; s <<= 1) v += __shfl_xor(v, s, 64);
                     acc[r][qi] = v;
                 }
+            if constexpr (I8)
+#pragma unroll
+                for (int r = 0; r < RB; ++r)
+#pragma unroll
+                    for (int s = 1; s < LPR; s <<= 1) cc2[r] += __shfl_xor(cc2[r], s, 64);
             if (unit == 0) {
 #pragma unroll
                 for (int r = 0; r < RB; ++r) {
@@ -2417,7 +2447,12 @@ __global__ void __launch_bounds__(256) k_screen_gemv(ScreenArgs a, const float* 
                     if constexpr (I8) {
                         const uint32_t w = a.rsb[gr];
                         sq = __uint_as_float(w << 16);            // scale s_x
-                        rbeta = __uint_as_float(w & 0xFFFF0000u);  // error norm beta_x
+                        // the bound word less the query-error share it carries for the int8 MFMA
+                        // screen (k_quant_rows): this screen's query is exact fp32.  ||s_x c_x|| from
+                        // below (cc2's fp32 sum: relative error <= d 2^-24), so the result still
+                        // bounds ||x - s_x c_x||
+                        const float xh = sq * sqrtf(cc2[r]) * (1.0f - 3.0f * (float)a.dpad * 5.9604645e-08f - 1e-6f);
+                        rbeta = fmaxf(0.0f, __uint_as_float(w & 0xFFFF0000u) - epsq * xh);
                     } else {
                         sq = a.metric == METRIC_L2 ? a.sqn[gr] : 0.0f;
                     }

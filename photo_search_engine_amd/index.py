@@ -190,6 +190,15 @@ class FlatIndex:
         """First-pass certificate failures so far (each one was re-searched)."""
         return int(check(self._L.vs_uncertified_count(self._h)))
 
+    def screen_state(self) -> dict:
+        """The screen's state (include/vs.h ``vs_screen_state``): group residuals, the int8 margins'
+        maxima and the screen-health feedback (int8 union depth, native routing, native seed depth)."""
+        buf = (ctypes.c_double * 9)()
+        check(self._L.vs_screen_state(self._h, buf, 9))
+        keys = ("screen", "group_residuals", "groups_with_mean", "max_mean_norm", "max_code_norm",
+                "max_row_error", "i8_union_log2", "i8_routed_searches", "native_seed_log2")
+        return {k: (float(buf[i]) if "max" in k else int(buf[i])) for i, k in enumerate(keys)}
+
     def unresolved_count(self) -> int:
         """Queries ``search_device_exact``'s device fallback could not certify either (must stay 0)."""
         return int(check(self._L.vs_unresolved_count(self._h)))

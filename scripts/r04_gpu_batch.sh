@@ -27,12 +27,15 @@ for s in ${STEPS:-tests cfg3 shard8 mix03 micro multi}; do
     cfg1) run bench_cfg1 300 python bench.py --workload cfg1 --steps 1000 --warmup 50 ;;
     shard8) run bench_shard8 300 python bench.py --shard-of 8 --steps 30 --no-cpu-baseline ;;
     spawn2) run bench_spawn2 600 python bench.py --gpus 2 --same-device --dist-backend gloo --rows 2000000 --steps 10 --no-cpu-baseline ;;
-    mix03) run bench_mix03 600 python bench.py --data mixture-sorted --sigma 0.3 --no-cpu-baseline ;;
-    mix10) run bench_mix10 600 python bench.py --data mixture-sorted --sigma 1.0 --no-cpu-baseline ;;
+    mix03) run bench_mix03 600 python bench.py --data mixture-sorted --sigma 0.3 --warmup 8 --no-cpu-baseline ;;
+    mix05) run bench_mix05 600 python bench.py --data mixture-sorted --sigma 0.5 --warmup 8 --no-cpu-baseline ;;
+    mix10) run bench_mix10 600 python bench.py --data mixture-sorted --sigma 1.0 --warmup 8 --no-cpu-baseline ;;
     micro) for m in 0 2 9; do for dt in 1 2; do
              timeout -k 10 120 ./abtmp/k1_micro 10000000 1536 20 $dt $m >> gpurun_out/k1_micro.txt 2>&1
              rc=$?; if [ $rc -ne 0 ]; then echo "step micro rc=$rc" >> gpurun_out/steps.log; exit $rc; fi
            done; done; echo "step micro rc=0" >> gpurun_out/steps.log ;;
+    cfg2) run bench_cfg2 300 python bench.py --workload cfg2 --no-cpu-baseline ;;
+    diagmix) run diag_mix03 600 python scripts/diag_mixture.py --sorted --sigma 0.3 ;;
     multi) run multi_step 600 python scripts/multi_step_timing.py ;;
     hnsw) run hnsw_bench 900 python scripts/hnsw_bench.py ;;
     *) echo "unknown step $s" >> gpurun_out/steps.log; exit 2 ;;

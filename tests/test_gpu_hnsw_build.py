@@ -84,12 +84,13 @@ def test_store_graph_equals_oracle_build(tmp_path, metric, monkeypatch):
     assert O.recall_at(I, I_e, 10) >= 0.9
 
 
-@pytest.mark.parametrize("dtype,metric", [("bf16", "ip"), ("f32", "l2")])
-def test_insert_rows_matches_oracle(dtype, metric):
+@pytest.mark.parametrize("dtype,metric,d", [("bf16", "ip", 128), ("f32", "l2", 64)])
+def test_insert_rows_matches_oracle(dtype, metric, d):
     # faiss's insertion, batched (hnsw.insert_rows): the GPU graph search's efConstruction beam over
     # the old graph, the batch's exact candidates (flat search), the prune kernel and the host's
-    # reverse links equal oracle/hnsw_oracle.py insert_batch batch by batch
-    n, d, n0 = 2600, 64, 800
+    # reverse links equal oracle/hnsw_oracle.py insert_batch batch by batch (bf16 at d=128: at d=64
+    # its inner products of 2600 rows hold exact ties)
+    n, n0 = 2600, 800
     ix = FlatIndex(d, metric, dtype, device=0)
     ix.add_synthetic(O.SEED_CORPUS + 71, 0, n, True)
     x = ix.reconstruct_n(0, n)
@@ -105,9 +106,9 @@ def test_insert_rows_matches_oracle(dtype, metric):
     # the grown graph searches like the at-once one
     q = O.synth_rows(O.SEED_QUERIES + 71, 0, 40, d, True, "f32")
     _, I_e = O.knn_exact(x, q, 10, metric)
-    g = hnsw_mod.HNSWGraph(ix, got, 64)
-    _, I_g = g.search(q, 10, 64)
-    assert O.recall_at(I_g, I_e, 10) >= 0.9
+    g = hnsw_mod.HNSWGraph(ix, got, 128)
+    _, I_g = g.search(q, 10, 128)
+    assert O.recall_at(I_g, I_e, 10) >= 0.9  # oracle's own search on this graph: 0.9225 / 0.9725
     g.close()
     ix.close()
 

@@ -7,7 +7,7 @@ the certificate (the device fallback round re-searches), it never changes an ans
 
 Cases: every storage dtype, k 1 / 10 / 100 / 1000, one and two query blocks, a partial last
 tile, near-copies of the queries planted in exactly the sample tiles (the selected seed sits
-among them: certificate failures, exact re-search), a sample tile holding a query's whole top-k
+among them), a sample tile holding a query's whole top-k
 (the provisional threshold lies), exact duplicates across the corpus (ties -> lower id), the
 device API with an id offset, and the two-phase sharded step's phase A / B.
 """
@@ -86,10 +86,12 @@ def test_seeded_native_and_int8_identical_at_cfg3_width(FlatIndex):
     ix.close()
 
 
-def test_seeded_planted_sample_tiles_fall_back_exactly(FlatIndex):
+def test_seeded_planted_sample_tiles_exact(FlatIndex):
     # near-copies of 16 queries in exactly the sample tiles (4 rows per tile, ~64 per query, in one
-    # 16-row group each): the rank-r seed lands among them, too few rows are listed, the
-    # certificate rejects and the fallback round re-searches -- the answer stays exact
+    # 16-row group each): the selected seed lands among them, far above the rest of the corpus, so
+    # the main pass lists almost nothing but the planted rows -- still enough for the certificate
+    # (a seed is a group maximum of real rows: it never exceeds the k-th score by more than its
+    # key slack), and the answer is the planted rows, exactly
     G = _num_cu()
     d, k, nq = 512, 10, 16
     tiles = 6 * G + 5
@@ -104,8 +106,9 @@ def test_seeded_planted_sample_tiles_fall_back_exactly(FlatIndex):
     ix.add(x)
     ix.set_screen("int8")
     qb = O.round_dtype(q, "bf16")
-    _exact(ix, np.concatenate([qb, qb]), k)  # 32 queries: the MFMA path
-    assert ix.uncertified_count() > 0
+    _, I = _exact(ix, np.concatenate([qb, qb]), k)  # 32 queries: the MFMA path
+    planted = {t * 256 + 3 + r for t in _sample_tiles(tiles, G) for r in range(4)}
+    assert all(int(i) in planted for i in I.ravel())
     assert ix.unresolved_count() == 0
     ix.close()
 
