@@ -442,13 +442,10 @@ def _kernel_name(kind: str, dtype: str, d: int, n_local: int = 0, metric: str = 
     """The screen kernel the library ran (vs_kernels.hip): the main passes take the direct forms
     when the K-steps per padded row are a multiple of 4 (int8: 64-element K-steps; bf16 / f16: 32);
     int8 codes taken against group means (``residual``) run the inner-product form that adds
-    <mu_g, q> and seeds its threshold itself (every workgroup >= 4 tiles)."""
+    <mu_g, q> to every key."""
     dpad = max(-(-d // 64) * 64, 64)
     if kind == "mfma_i8" and dpad % 256 == 0 and dpad >= 512:
-        tiles = -(-n_local // 256)
-        if residual and metric == "ip" and tiles >= 4 * min(tiles, 256):
-            return "k_screen_i8d_seeded_res"
-        return "k_screen_i8d"
+        return "k_screen_i8d_res" if residual and metric == "ip" else "k_screen_i8d"
     if kind == "mfma" and dtype in ("bf16", "f16") and dpad % 128 == 0 and dpad >= 256:
         return "k_screen_d16"
     return f"k_screen_{kind}"

@@ -127,9 +127,8 @@ struct vs_index {
     //    to 2^kI8ScaleMax; one failing at that depth routes the next kI8RouteBatches searches to
     //    the native screen (score distributions denser than the int8 error window, e.g. tight
     //    clusters); kSeedRelax clean int8 batches halve the depth again;
-    //  * a native batch in which more than 1/64 of the queries failed doubles the optimistic seed's
-    //    depth (rows listed ahead of the refine), up to 2^kSeedScaleMax; kSeedRelax clean batches
-    //    halve it again.
+    //  * a native batch with a failed query doubles the optimistic seed's depth (rows listed ahead
+    //    of the refine), up to 2^kSeedScaleMax; kSeedRelax clean batches halve it again.
     std::mutex h_mu;
     unsigned* h_fails = nullptr;  // pinned
     hipEvent_t h_ev = nullptr;
@@ -317,10 +316,10 @@ constexpr bool gemv_dyn() { return true; }
 bool use_i8(const vs_index* ix, int nqb, int k) {
     if (ix->screen != VS_SCREEN_I8 || nqb <= GEMV_NQ_MAX || k > I8_MAX_K) return false;
     if (!ix->i8_res) return true;
-    // group-residual codes: only the seeded direct main pass adds <mu_g, q> (else: native)
+    // group-residual codes: only the seed pass and the direct main pass add <mu_g, q> (else: native)
     const int64_t tiles = (ix->ntotal + TR - 1) / TR;
     const int64_t G = std::max<int64_t>(1, std::min<int64_t>(tiles, ix->num_cu));
-    return tiles >= 4 * G && G * 16 <= kI8dSeedMaxima;
+    return tiles >= 4 * G;
 }
 
 constexpr int kF32MfmaMinQ = 64;     // fp32 native batches: MFMA screen from this many queries on
@@ -357,7 +356,7 @@ void health_poll(vs_index* ix) {
                     ix->i8_clean = 0;
                 }
             }
-        } else if (f > (unsigned)(ix->h_nq / 64)) {  // (a stray hard query does not deepen every batch)
+        } else if (f > 0) {  // (one failed query costs its block a whole fallback screen: deepen)
             ix->seed_log2 = std::min(ix->seed_log2 + 1, kSeedScaleMax);
             ix->seed_clean = 0;
         } else if (ix->seed_log2 > 0 && ++ix->seed_clean >= kSeedRelax) {
@@ -482,9 +481,9 @@ void search_block_i8(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float
     // batch at cfg3 (K1 3.73 vs 3.96 ms) and 0.2 ms at the 8-shard's 1.25M rows (0.52 vs 0.72 ms):
     // the tiles screened under the provisional thresholds cost more than the two launches,
     // profiles/r04_seed_ab.txt)
-    const bool seed_in_kernel = ix->i8_res && seeded && ix->metric == METRIC_IP && i8_direct_ok(ix->dpad8) &&
-                                a.G * 16 <= kI8dSeedMaxima;
-    if (ix->i8_res && !seed_in_kernel) throw VsError(VS_ERR_INTERNAL, "group-residual int8 codes need the seeded direct pass");
+    const bool seed_in_kernel = false;
+    if (ix->i8_res && !(seeded && ix->metric == METRIC_IP && i8_direct_ok(ix->dpad8)))
+        throw VsError(VS_ERR_INTERNAL, "group-residual int8 codes need the seeded direct pass");
     if (ix->i8_res) {  // <mu_g, q> of every group for this block's queries
         const int64_t ng = (ix->ntotal + I8_GROUP_ROWS - 1) / I8_GROUP_ROWS;
         c->gT.ensure((size_t)ng * MFMA_QB * sizeof(float));
@@ -637,7 +636,11 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
     // against the workgroups' compaction bounds (drop) in the refine.  First passes of inner-product
     // batches (adaptive refine below) keep MFMA_KP_MAX: a workgroup that holds many of a query's
     // best rows (a cluster inserted contiguously) then drops only rows far below the k-th best.
-    const bool wide = use_mfma && !redo && ix->metric == METRIC_IP && k <= I8_MAX_K && refine_split(nqb, Kp, ix->dtype, ix->num_cu) <= 1;
+    // (the device fallback round too: its fixed-depth certificate needs two margins between the
+    // k-th and the KP_MAX-th best, which a tight cluster -- scores denser than the bf16 query
+    // rounding -- does not leave; the adaptive refine scores the rows inside one margin instead)
+    const bool wide = use_mfma && ix->metric == METRIC_IP && k <= I8_MAX_K &&
+                      (redo || refine_split(nqb, Kp, ix->dtype, ix->num_cu) <= 1);
     // (unseeded small shards -- under 4 tiles per workgroup -- keep max(128, 2 Kp) per workgroup:
     // MFMA_KP_MAX lists of every row there made the refine's selection the cost, 0.9 ms at 100k x
     // 4096 bf16, batch 256, k = 10; a workgroup holding more of a query's best rows fails its
@@ -834,8 +837,9 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
     // distributions (clustered corpora) certify without a re-search; the fixed-depth refine's
     // certificate needs a gap of 2 margins between the k-th and the Kp-th best
     if (wide) {
-        HIP_CHECK(launch_refine_wide(r, nqb, (int)round_up(std::max(Kp, k + 32), 32), st));
-        health_note(ix, c, st, 2, nqb);
+        const int ka = redo ? screen_depth(k) : Kp;  // (a fallback round's Kp is the listing depth)
+        HIP_CHECK(launch_refine_wide(r, nqb, (int)round_up(std::max(ka, k + 32), 32), st));
+        if (!redo) health_note(ix, c, st, 2, nqb);
         return;
     }
     HIP_CHECK(launch_refine(r, nqb, st));
@@ -915,8 +919,23 @@ void vs::search_exact_device(vs_index* ix, const float* q_dev, int64_t nq, int k
     int* cert_h = (int*)c->hout.p;
     HIP_CHECK(hipMemcpyAsync(cert_h, c->cert.p, (size_t)nq * sizeof(int), hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));
-    for (int64_t qi = 0; qi < nq; ++qi)
-        if (!cert_h[qi]) throw VsError(VS_ERR_UNCERTIFIED, "exactness certificate failed at maximum screening depth");
+    // a query even the fallback round left uncertified (scores denser than the bf16 query rounding
+    // in the MFMA keys, e.g. a tight cluster): re-screened alone on the GEMV screen, whose fp32
+    // query leaves only the accumulation error in its keys, 4x deeper each round (vs_search's
+    // escalation); its outputs are rewritten in place
+    for (int64_t qi = 0; qi < nq; ++qi) {
+        int Kr = Kp;
+        int* cq = c->cert.as<int>() + qi;
+        while (!cert_h[qi]) {
+            if (Kr >= KP_MAX || Kr >= ix->ntotal)
+                throw VsError(VS_ERR_UNCERTIFIED, "exactness certificate failed at maximum screening depth");
+            Kr = (int)std::min<int64_t>(std::min<int64_t>((int64_t)Kr * 4, KP_MAX), round_up(ix->ntotal, 16));
+            search_all(ix, c, q_dev + qi * ix->d, 1, k, Kr, (D_dev ? D_dev : c->outD.as<float>()) + qi * k,
+                       I_dev + qi * k, S64_dev ? S64_dev + qi * k : nullptr, cq, id_offset, st, /*safe seed*/ 0);
+            HIP_CHECK(hipMemcpyAsync(&cert_h[qi], cq, sizeof(int), hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipStreamSynchronize(st));
+        }
+    }
 }
 
 // S concurrent exact device searches over consecutive parts (whole query blocks) of one batch, each

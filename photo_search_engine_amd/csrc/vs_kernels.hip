@@ -1115,6 +1115,15 @@ __device__ __forceinline__ void screen_mfma(ScreenArgs a, const uint8_t* __restr
         t1 = t0 + 1 <= a.tiles ? t0 + 1 : a.tiles;
     }
     static_assert(!(MAP && SEED), "the mapped screen is unseeded");
+    // a fallback round (gated) interleaves its tiles as the direct main passes do (workgroup blk:
+    // tiles blk, blk + G, ...): a cluster stored contiguously then spreads over every workgroup's
+    // MFMA_KP_MAX-deep lists instead of filling two or three of them, whose compaction bounds would
+    // sit inside the query's top rows
+    const bool ilv = !MAP && !SEED && a.gate != nullptr;
+    if (ilv) {
+        t0 = 0;
+        t1 = a.tiles > blk ? (a.tiles - blk + a.G - 1) / a.G : 0;
+    }
     int* tmap = (int*)(smem + MF_LDS);  // MAP: page of logical tile tbase + i
     if constexpr (MAP) {  // this workgroup's list segment, query tile and page table
         const int* dsc = a.wg_desc + (size_t)blk * MAP_DESC;
@@ -1132,7 +1141,7 @@ __device__ __forceinline__ void screen_mfma(ScreenArgs a, const uint8_t* __restr
     // storage tile of logical tile t
     auto phys = [&](int t) -> int64_t {
         if constexpr (MAP) return (int64_t)tmap[t - tbase];
-        else return (int64_t)t;
+        else return ilv ? (int64_t)blk + (int64_t)t * a.G : (int64_t)t;
     };
     const bool reuse = !MAP && !SEED && a.seed_acc != nullptr && t1 > t0;
     const int tseed = t0;
@@ -1232,7 +1241,7 @@ __device__ __forceinline__ void screen_mfma(ScreenArgs a, const uint8_t* __restr
         }
         int olane;
         asm volatile("v_mov_b32 %0, %1" : "=v"(olane) : "v"(lane));
-        const int64_t rowbase = (int64_t)ti * TR;  // logical (the n_valid mask)
+        const int64_t rowbase = (MAP ? (int64_t)ti : phys(ti)) * TR;  // logical (the n_valid mask)
         const int64_t idbase = MAP ? phys(ti) * TR : rowbase;  // key ids: storage slots
         const int rid0 = wm * 64 + (olane >> 4) * 4;  // + mi*16 + r
         const int q0 = wn * 128 + (olane & 15);        // + ni*16
@@ -1332,6 +1341,10 @@ __device__ __forceinline__ void screen_mfma(ScreenArgs a, const uint8_t* __restr
             // one compare per query column; the insert path runs only where something passes,
             // and then costs one LDS atomic per lane plus predicated stores
             if constexpr (SEED) {  // group g = wm*4 + lane/16 of the tile: 16 distinct rows
+                // group residuals: + <mu_g, q> of the tile's group, as the main pass's keys
+                // (fl(fl(t max v) + T) = max fl(fl(t v) + T): the seed is a real row's key)
+                if constexpr (I8 && !I8L2)
+                    if (a.gT) mx += a.gT[(size_t)((int64_t)ti * TR / I8_GROUP_ROWS) * MFMA_QB + q];
                 a.seedmax[(size_t)q * (a.G * 16) + blk * 16 + wm * 4 + (olane >> 4)] = mx;
                 continue;
             }
@@ -1748,7 +1761,7 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
     constexpr bool I8 = DT == DT_I8;
     static_assert(!(MAP && I8), "the mapped scan serves bf16 / f16 lists");
     static_assert(!SEEDK || (I8 && !MAP && !L2), "in-kernel seeding: the int8 flat inner-product main pass");
-    static_assert(!RES || SEEDK, "group residuals: the seeded int8 main pass");
+    static_assert(!RES || (I8 && !MAP && !L2), "group residuals: the int8 flat inner-product main pass");
     static_assert(NG == 16 || (NG == 4 && MAP), "narrow query tiles: mapped scans only");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint8_t* const sm = smem + I8D_RING;
@@ -1807,7 +1820,7 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
     int* const sst = (int*)(smem + I8D_LDS);  // SEEDK: the seeding state (I8D_SEED_LDS bytes)
     // RES: <mu_g, q> of the tile's group (two tiles, by parity), LDS-DMA'd by waves 4-7 one tile ahead
     // and copied into qrec[q].w at the tile's K-step 0
-    float* const tlds = (float*)(smem + I8D_LDS + I8D_SEED_LDS);
+    float* const tlds = (float*)(smem + I8D_LDS + (SEEDK ? I8D_SEED_LDS : 0));
     unsigned* const shist = (unsigned*)(sm + 256 * 16 + 16 + MF_POOL * 12);  // SEEDK: select histogram (records' area)
     if (tid < 256) {
         const bool real = tid < nqb;
@@ -2267,6 +2280,11 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
 template <int METRIC>
 __global__ void __launch_bounds__(512, 2) k_screen_i8d(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
     screen_direct<DT_I8, METRIC>(a, qt, nqb);
+}
+// ... over group-residual codes (a corpus stored cluster by cluster): every key + <mu_g, q>
+// (inner product; the seed pass adds the same terms to its maxima)
+__global__ void __launch_bounds__(512, 2) k_screen_i8d_res(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
+    screen_direct<DT_I8, METRIC_IP, false, 16, false, true>(a, qt, nqb);
 }
 // the same main pass with its threshold seeded in the kernel (no seed pass / select launches);
 // inner product (the L2 form's extra epilogue state leaves no registers for it: it keeps the pass)
@@ -3269,6 +3287,8 @@ __global__ void __launch_bounds__(RF_THREADS) k_refine_wide(RefineArgs a, int KA
     __shared__ int nb_s;
     __shared__ double qq_s;
     const int q = blockIdx.x, tid = threadIdx.x;
+    // a device fallback round: only the block's uncertified queries, and only when there are any
+    if (a.redo && (*a.gate == 0 || a.cert[q] != 0)) return;
     const int ng = (a.d + 7) >> 3;
     const u64* src = a.cand + (size_t)q * a.lcap;
     const int n = min(a.cand_n[q], a.lcap);
@@ -3869,6 +3889,8 @@ static hipError_t launch_mfma_dt(int dt, const ScreenArgs& a, const uint8_t* qt,
     if (a.gate && (SEED || dt == DT_I8)) return hipErrorInvalidValue;  // fallback rounds: native main screen
     if (dt == DT_I8) {
         if (!a.rsb || !a.qfac || (a.metric == METRIC_L2 && !a.sqn)) return hipErrorInvalidValue;
+        // group-residual keys (+ <mu_g, q>): the seed pass and the direct inner-product main pass only
+        if (a.gT && (a.metric != METRIC_IP || !i8_direct_ok(a.dpad))) return hipErrorInvalidValue;
         if (!SEED && i8_direct_ok(a.dpad)) {  // the main pass: direct form (no seed-tile reuse)
             if (a.seed_acc || a.tile_stride != 0) return hipErrorInvalidValue;
             if (a.seed_sync) {  // threshold seeded in the kernel (inner product; L2 keeps the seed pass)
@@ -3884,6 +3906,12 @@ static hipError_t launch_mfma_dt(int dt, const ScreenArgs& a, const uint8_t* qt,
                 }
                 set_lds_attr((const void*)k_screen_i8d_seeded, I8D_LDS + I8D_SEED_LDS);
                 hipLaunchKernelGGL(k_screen_i8d_seeded, dim3(a.G), dim3(MF_THREADS), I8D_LDS + I8D_SEED_LDS, st, a, qt, nqb);
+                return hipGetLastError();
+            }
+            if (a.gT) {  // group residuals (inner product)
+                if (a.metric != METRIC_IP) return hipErrorInvalidValue;
+                set_lds_attr((const void*)k_screen_i8d_res, I8D_LDS + I8D_RES_LDS);
+                hipLaunchKernelGGL(k_screen_i8d_res, dim3(a.G), dim3(MF_THREADS), I8D_LDS + I8D_RES_LDS, st, a, qt, nqb);
                 return hipGetLastError();
             }
             const void* fn = a.metric == METRIC_IP ? (const void*)k_screen_i8d<METRIC_IP> : (const void*)k_screen_i8d<METRIC_L2>;
@@ -4081,7 +4109,7 @@ static void launch_refine_wide_one(const RefineArgs& a, int nq, int KA, size_t l
 hipError_t launch_refine_wide(const RefineArgs& a, int nq, int KA, hipStream_t st) {
     // L2: int8 keys only (their margin qeps covers the transformed key; native L2 uses k_refine)
     if ((a.metric != METRIC_IP && !(a.metric == METRIC_L2 && a.qeps)) || !(a.qeps || a.qinfo) || !a.cand_n ||
-        KA <= 0 || 2 * KA > RFW_CAP)
+        KA <= 0 || 2 * KA > RFW_CAP || (a.redo && (!a.gate || !a.cert || a.phase != 0)))
         return hipErrorInvalidValue;
     const size_t base = (size_t)RFW_CAP * 12;
     const size_t qbytes = (size_t)((a.d + 7) >> 3) * 64;

@@ -50,6 +50,8 @@ def main() -> int:
     for metric, sym in (("ip", "_ZN2vs12k_screen_i8dILi0EEEvNS_10ScreenArgsEPKhi:"),
                         ("l2", "_ZN2vs12k_screen_i8dILi1EEEvNS_10ScreenArgsEPKhi:")):
         rc |= check(asm, metric, sym)
+    # the main pass over group-residual codes (inner product; + <mu_g, q> per key)
+    rc |= check(asm, "ip", "_ZN2vs16k_screen_i8d_resENS_10ScreenArgsEPKhi:", name="k_screen_i8d_res")
     # the same main pass with its threshold seeded in the kernel (inner product)
     rc |= check(asm, "ip", "_ZN2vs19k_screen_i8d_seededENS_10ScreenArgsEPKhi:", name="k_screen_i8d_seeded")
     # ... over group-residual codes

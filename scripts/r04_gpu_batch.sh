@@ -35,6 +35,8 @@ for s in ${STEPS:-tests cfg3 shard8 mix03 micro multi}; do
              rc=$?; if [ $rc -ne 0 ]; then echo "step micro rc=$rc" >> gpurun_out/steps.log; exit $rc; fi
            done; done; echo "step micro rc=0" >> gpurun_out/steps.log ;;
     cfg2) run bench_cfg2 300 python bench.py --workload cfg2 --no-cpu-baseline ;;
+    profmix05) mkdir -p gpurun_out/prof_mix05 && run prof_mix05 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_mix05 -o run --output-format csv -- python bench.py --data mixture-sorted --sigma 0.5 --screen native --steps 5 --warmup 3 --no-cpu-baseline ;;
+    diagmix10m) run diag_mix03_10m 600 python scripts/diag_mixture.py --sorted --sigma 0.3 --rows 10000000 --batches 4 --check ;;
     diagmix) run diag_mix03 600 python scripts/diag_mixture.py --sorted --sigma 0.3 ;;
     multi) run multi_step 600 python scripts/multi_step_timing.py ;;
     hnsw) run hnsw_bench 900 python scripts/hnsw_bench.py ;;

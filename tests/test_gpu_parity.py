@@ -304,17 +304,22 @@ def test_device_exact_search_re_searches_uncertified_queries(FlatIndex, nq, dtyp
 @pytest.mark.parametrize("dtype", ["bf16", "f32"])
 @pytest.mark.parametrize("nq,copies", [(1, 5000), (20, 12000)])
 def test_ties_beyond_max_depth_are_reported(FlatIndex, nq, copies, dtype):
-    # `copies` identical rows tie with the query's best score: more than any screen depth (KP_MAX =
-    # 4096 rows for single queries; the batch refine's 8192 scored rows) can certify that no
-    # unlisted copy wins.  vs_search raises VS_ERR_UNCERTIFIED; the device API (no host sync)
-    # counts the query in unresolved_count; the multi-device handle raises.
+    # `copies` identical rows tie with the query's best score: more than vs_search's deepest screen
+    # (KP_MAX = 4096 rows) can certify that no unlisted copy wins: it raises VS_ERR_UNCERTIFIED.
+    # The device API's fallback round (no host sync) lists up to
+    # MFMA_KP_MAX rows per workgroup and scores every listed row within one margin of T' (up to the
+    # adaptive refine's 8192): 5000 copies it certifies -- the k lowest ids of the tie --, 12000 it
+    # counts in unresolved_count (the multi-device handle, whose shards run that path, likewise
+    # answers the first and raises on the second).
     import torch
     from photo_search_engine_amd._lib import VsError
     from photo_search_engine_amd.index import MultiDeviceFlatIndex
     d, k = 64, 10
     x = O.synth_rows(O.SEED_CORPUS, 0, 25_000, d, True, dtype)
     v = x[123].copy()
-    x[np.random.default_rng(3).choice(25_000, copies, replace=False)] = v
+    pos = np.random.default_rng(3).choice(25_000, copies, replace=False)
+    x[pos] = v
+    tie = np.unique(np.concatenate([pos, [123]]))
     q = np.repeat(v[None], nq, axis=0)
     ix = FlatIndex(d, "ip", dtype)
     ix.add(x)
@@ -324,12 +329,20 @@ def test_ties_beyond_max_depth_are_reported(FlatIndex, nq, copies, dtype):
     qd = torch.from_numpy(q).cuda()
     I = torch.empty((nq, k), dtype=torch.int64, device="cuda")
     ix.search_device_exact(qd.data_ptr(), nq, k, None, I.data_ptr(), None, 0, 0)
-    assert ix.unresolved_count() == nq
-    m = MultiDeviceFlatIndex(d, "ip", dtype, devices=[0, 0])
+    if copies <= 7000:
+        assert ix.unresolved_count() == 0
+        np.testing.assert_array_equal(I.cpu().numpy(), np.repeat(tie[None, :k], nq, axis=0))
+    else:
+        assert ix.unresolved_count() == nq
+    m = MultiDeviceFlatIndex(d, "ip", dtype, devices=[0, 0])  # (its shards run the device path)
     m.add(x)
-    with pytest.raises(VsError) as e:
-        m.search(q, k)
-    assert e.value.code == -4
+    if copies <= 7000:
+        _, Im = m.search(q, k)
+        np.testing.assert_array_equal(Im, np.repeat(tie[None, :k], nq, axis=0))
+    else:
+        with pytest.raises(VsError) as e:
+            m.search(q, k)
+        assert e.value.code == -4
     m.close()
     ix.close()
 
