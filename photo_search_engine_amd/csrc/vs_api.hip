@@ -54,7 +54,7 @@ struct Ctx {
     // returned with kernels still queued is never overwritten by the next caller's pack
     hipEvent_t idle = nullptr;
     bool pending = false;
-    DevBuf qdev, qtile, qinfo, qpad, cand, part, merge_a, merge_b, outD, outI, outS, cert, thr0, seedmax, gcnt, seedsync, gT;
+    DevBuf qdev, qtile, qinfo, qpad, cand, part, merge_a, merge_b, outD, outI, outS, cert, thr0, seedmax, gcnt, gT;
     DevBuf qfac, qeps, drop;  // int8 screen: per-query code scale and norm, refine margin, drop bounds
     DevBuf fails;             // the current query block's certificate-failure count (fallback gate)
     DevBuf rsc, rdone;        // split refine: per-query scores + ids of the kept rows, done counters
@@ -69,7 +69,7 @@ struct Ctx {
     unsigned* unres = nullptr;  // this call's unresolved-query counter (device), instead of the index's
     ~Ctx() {
         for (DevBuf* b : {&qdev, &qtile, &qinfo, &qpad, &cand, &part, &merge_a, &merge_b, &outD, &outI, &outS, &cert, &thr0,
-                          &seedsync, &gT, &seedmax, &gcnt, &rows[0], &rows[1], &tilectr, &seedacc, &outAll, &qfac, &qeps, &drop, &fails, &rsc, &rdone,
+                          &gT, &seedmax, &gcnt, &rows[0], &rows[1], &tilectr, &seedacc, &outAll, &qfac, &qeps, &drop, &fails, &rsc, &rdone,
                           &pa})
             b->release();
         pin.release();
@@ -419,22 +419,6 @@ int i8_gemv_depth(const vs_index* ix, int k) {
 constexpr double kI8Window = 15.0;
 constexpr double kI8UnionMaxPerK = 64.0;
 constexpr double kI8UnionMin = 1024.0;
-// The in-kernel seed's provisional threshold on a sample tile: the j-th largest of its 16
-// group maxima, j the smallest rank that the published seed (the rank whose share of all maxima is
-// p) exceeds except with probability < 1e-4 per (tile, query): P(Binomial(16, p) >= j) < 1e-4.
-int i8d_provisional_rank(double p) {
-    p = std::min(1.0, std::max(0.0, p));
-    for (int j = 1; j <= 16; ++j) {
-        double tail = 0.0;  // P(X >= j), X ~ Binomial(16, p)
-        for (int i = j; i <= 16; ++i) {
-            double c = 1.0;
-            for (int t = 0; t < i; ++t) c = c * (16 - t) / (t + 1);
-            tail += c * std::pow(p, i) * std::pow(1.0 - p, 16 - i);
-        }
-        if (tail < 1e-4) return j;
-    }
-    return 16;
-}
 double i8_union_target(int k, double sampled, double n) {
     const double need = kI8Window * k;
     double u = std::max(need, kI8UnionMin);
@@ -473,15 +457,13 @@ void search_block_i8(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float
     c->drop.ensure(sizeof(u64) * MFMA_QB);
     c->gcnt.ensure(sizeof(int) * MFMA_QB);
     c->fails.ensure(sizeof(int));
-    // threshold seeding: inside the direct main pass (its workgroups sample, select and adopt the
-    // seed themselves, k_screen_i8d_seeded), else a seed pass + select before it
+    // threshold seeding: a seed pass + select before the main pass (>= 4 tiles per workgroup).
+    // (Round 4 measured the alternative -- each workgroup of the direct main pass screening a sample
+    // tile first and the workgroups selecting and adopting the seed among themselves, no extra
+    // launches -- on MI355X: 0.19-0.23 ms slower per cfg3 batch (K1 3.96 vs 3.73 ms) and 0.2 ms at
+    // the 8-shard's 1.25M rows, the tiles screened under provisional thresholds costing more than
+    // the two launches, profiles/r04_seed_ab.txt; it was removed.)
     const bool seeded = tiles >= 4 * (int64_t)a.G;
-    // (only for group-residual codes, which need that kernel's <mu_g, q> terms: measured on MI355X,
-    // the seed pass + select ahead of k_screen_i8d beat the in-kernel seeding by 0.19-0.23 ms per
-    // batch at cfg3 (K1 3.73 vs 3.96 ms) and 0.2 ms at the 8-shard's 1.25M rows (0.52 vs 0.72 ms):
-    // the tiles screened under the provisional thresholds cost more than the two launches,
-    // profiles/r04_seed_ab.txt)
-    const bool seed_in_kernel = false;
     if (ix->i8_res && !(seeded && ix->metric == METRIC_IP && i8_direct_ok(ix->dpad8)))
         throw VsError(VS_ERR_INTERNAL, "group-residual int8 codes need the seeded direct pass");
     if (ix->i8_res) {  // <mu_g, q> of every group for this block's queries
@@ -490,11 +472,10 @@ void search_block_i8(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float
         HIP_CHECK(launch_group_dots(ix->gmean, ng, ix->dpad8, q, nqb, ix->d, c->gT.as<float>(), st));
         a.gT = c->gT.as<float>();
     }
-    if (seed_in_kernel) c->seedsync.ensure(4 * sizeof(int));
     HIP_CHECK(launch_pack_qtile_i8(q, nqb, ix->d, ix->dpad8, c->qtile.as<uint8_t>(), c->qfac.as<float2>(),
                                    c->qeps.as<float>(), ix->d_maxsq + 2, c->gcnt.as<int>(), c->drop.as<u64>(), st,
                                    c->fails.as<int>(), ix->metric == METRIC_L2 ? ix->d_maxsq : nullptr,
-                                   gamma_of(ix->d), seed_in_kernel ? c->seedsync.as<int>() : nullptr));
+                                   gamma_of(ix->d)));
     a.qfac = c->qfac.as<float2>();
     a.drop = c->drop.as<u64>();
     a.lcap = a.G * a.Kp;
@@ -513,16 +494,7 @@ void search_block_i8(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float
         const double r = std::ceil(target * sampled / (double)ix->ntotal);
         return (int)std::min<double>(std::max<double>(r, (double)kOptimisticMinRank), (double)M);
     };
-    if (seed_in_kernel) {  // one sample tile per workgroup, as the seed pass below
-        const int M = a.G * 16;
-        c->seedmax.ensure(sizeof(float) * MFMA_QB * M);
-        c->thr0.ensure(sizeof(u64) * MFMA_QB);
-        a.seedmax = c->seedmax.as<float>();
-        a.seed_sync = c->seedsync.as<int>();
-        a.thr_out = c->thr0.as<u64>();
-        a.seed_rank = seed_rank_of((double)a.G * TR, M);
-        a.seed_prov_rank = i8d_provisional_rank((double)a.seed_rank / M);
-    } else if (seeded) {  // optimistic threshold seed from one tile per workgroup
+    if (seeded) {  // optimistic threshold seed from one tile per workgroup
         ScreenArgs sa = a;
         sa.G = std::min(sa.G, 512);
         sa.tile_stride = (int)(tiles / sa.G);
@@ -578,7 +550,7 @@ void search_block_i8(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float
     r.uncert = ix->d_uncert;
     r.qeps = c->qeps.as<float>();
     r.drop = a.drop;
-    r.thr0 = a.thr_out ? a.thr_out : a.thr0;  // (in-kernel seeding: complete when the screen ends)
+    r.thr0 = a.thr0;
     r.fails = c->fails.as<int>();
     r.ostride = ostride;
     if (phase == 1) {

@@ -202,20 +202,10 @@ struct ScreenArgs {
     const int* wg_desc;      // mapped screen: per workgroup MAP_DESC ints {tile_map offset of its
                              // first tile, tiles, logical index of the first tile in its list
                              // segment, rows of that segment, query tile index, qmap offset, queries}
-    // In-kernel threshold seeding (the int8 direct main pass, k_screen_i8d_seeded): each workgroup
-    // screens a sample tile first, publishes its 16-row-group maxima to seedmax and counts itself
-    // in; the rank-th largest maximum per query is selected by the workgroups themselves and
-    // adopted by all of them while they screen (no wait on another workgroup anywhere).
-    int* seed_sync;          // [0] workgroups arrived, [1] selections published, [2] selections claimed
-                             // (zeroed by the query pack); null = no in-kernel seeding
-    u64* thr_out;            // [QB] the selected thresholds (the refine's thr0)
-    int seed_rank;           // rank of the selected maximum among the G * 16 of a query
-    int seed_prov_rank;      // the sample tile's own provisional threshold: this rank of its 16 maxima
     const float* gT;         // int8 group residuals: [group][QB] <mu_g, q> added to every key of the
-                             // group's rows (k_screen_i8d_seeded_res), or null
+                             // group's rows (the seed pass and k_screen_i8d_res), or null
 };
 constexpr int MAP_DESC = 8;
-constexpr int kI8dSeedMaxima = 4096;  // G * 16 group maxima per query the in-kernel seed select holds
 constexpr int MFMA_MAP_TILES = 256;  // mapped screen: logical tiles per workgroup (its LDS page table)
 int gemv_blocks_per_cu(int dt, int nqpad);  // resident k_screen_gemv blocks per CU (occupancy API)
 
@@ -334,7 +324,7 @@ hipError_t launch_group_dots(const uint16_t* gmean, int64_t ngroups, int dpad8, 
                              hipStream_t st);
 hipError_t launch_pack_qtile_i8(const float* q, int nqb, int d, int dpad8, uint8_t* qt, float2* qfac, float* qeps,
                                 const unsigned* maxes, int* gcnt, u64* drop, hipStream_t st, int* fails = nullptr,
-                                const unsigned* l2max = nullptr, float gamma = 0.0f, int* seed_sync = nullptr);
+                                const unsigned* l2max = nullptr, float gamma = 0.0f);
 
 // ---- IVF-Flat (vs_ivf.hip) ---------------------------------------------------------------------
 // Inverted lists are chains of pages: a page is one row tile (TR rows, the flat layout above) of

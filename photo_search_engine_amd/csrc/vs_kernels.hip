@@ -759,12 +759,11 @@ __global__ void __launch_bounds__(256) k_pack_qtile_i8(const float* __restrict__
                                                         float* __restrict__ qeps, const unsigned* __restrict__ maxes,
                                                         int* __restrict__ gcnt, u64* __restrict__ drop,
                                                         int* __restrict__ fails, const unsigned* __restrict__ l2max,
-                                                        float gamma, int* __restrict__ seed_sync) {
+                                                        float gamma) {
     const int lane = threadIdx.x & 63;
     const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= MFMA_QB) return;
     if (fails && r == 0 && lane == 0) *fails = 0;
-    if (seed_sync && r == 0 && lane < 4) seed_sync[lane] = 0;  // the screen's in-kernel seeding counters
     if (lane == 0) {
         gcnt[r] = 0;
         drop[r] = 0ull;
@@ -1583,167 +1582,7 @@ __device__ __forceinline__ void gld16(intx4& v, const void* p) {
     asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
 }
 
-// ---- in-kernel threshold seeding (k_screen_i8d_seeded) ----
-// The separate seed pass + k_seed_select (two launches, ~50 us per cfg3 batch) become part of the
-// main pass: each workgroup's FIRST tile is its sample (spread over the shard), whose 16-row-group
-// key maxima it publishes (seedmax) before counting itself in (seed_sync[0]); that tile's own
-// epilogue uses a provisional threshold (a rank of its 16 group maxima that the published seed
-// exceeds with near certainty; where it does not, it goes into drop, the refine certificate's
-// bound).  Once every workgroup has arrived, each query's
-// rank-th largest maximum is selected by whichever workgroup claims it at a tile boundary
-// (seed_sync[2]) and published (thr_out, seed_sync[1]); a workgroup adopts the thresholds at the
-// first tile boundary after all are published.  No workgroup ever waits for another: polls are
-// loads issued one tile ahead, and whatever is left unclaimed when a workgroup finishes its tiles
-// it selects itself (the last to arrive selects all that remain), so thr_out is complete when the
-// kernel ends.  Rows rejected before a workgroup adopts are below the threshold then in force, which
-// is either below thr_out or folded into drop at adoption (at the end, if it never adopts); after
-// it below max(thr_out, drop): the refine certifies against max(thr_out, drop).
-constexpr int I8D_SEED_VPT = 8;  // 512 threads x 8 = the G * 16 <= 4096 maxima of one query
-// the seeding's pointers are kept in LDS (written once at kernel start) and read in the cold blocks
-// that use them: no SGPRs held across the K loop for them
-struct SeedPtrs {
-    int* sync;
-    unsigned* maxima;
-    u64* thr_out;
-    u64* drop;
-};
-template <typename T>
-__device__ __forceinline__ T* lds_ptr(T* const* slot) {
-    const uint64_t v = *(const volatile uint64_t*)slot;
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-    return (T*)(((uint64_t)hi << 32) | lo);
-}
-// the thread id redefined at this point: lane-derived indices are not hoisted out of the K loop
-__device__ __forceinline__ int vtid_here() {
-    int t;
-    asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"((int)threadIdx.x));
-    return t;
-}
-constexpr int I8D_SEED_LDS = 32 + (int)sizeof(SeedPtrs);  // sst[8]: [0] decision, [2] claimed query, [3] digit,
-                                  // [4] rank, [5..6] poll, [7] claims exhausted; then the SeedPtrs
-static_assert(MF_THREADS * I8D_SEED_VPT >= kI8dSeedMaxima, "in-kernel seed select capacity");
 constexpr int I8D_RES_LDS = 2 * MFMA_QB * 4;  // group residuals: <mu_g, q> of two tiles
-static_assert(I8_GROUP_ROWS % TR == 0, "a tile lies in one group");
-
-// the rank-th largest of query c's G * 16 maxima (k_seed_select's 8-bit radix select on this
-// workgroup's 512 threads) -> thr_out[c], then published
-__device__ __forceinline__ void i8d_seed_select(const ScreenArgs& a, int c, unsigned* hist, int* sst) {
-    const int tid = vtid_here(), lane = tid & 63;
-    const int M = a.G * 16;
-    const SeedPtrs* sp = (const SeedPtrs*)(sst + 8);
-    __threadfence();  // acquire: every workgroup released its maxima before counting itself in
-    uint32_t v[I8D_SEED_VPT];
-    const unsigned* src = lds_ptr(&sp->maxima) + (size_t)c * M;
-#pragma unroll
-    for (int e = 0; e < I8D_SEED_VPT; ++e) {
-        const int j = tid + MF_THREADS * e;
-        v[e] = j < M ? ord_f32(__uint_as_float(__hip_atomic_load(src + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
-                     : 0u;  // 0 = padding (below every value)
-    }
-    uint32_t prefix = 0u, mask = 0u;
-    int r = a.seed_rank;
-    for (int shift = 24; shift >= 0; shift -= 8) {
-        if (tid < 256) hist[tid] = 0u;
-        __syncthreads();
-#pragma unroll
-        for (int e = 0; e < I8D_SEED_VPT; ++e)
-            if ((v[e] & mask) == prefix) atomicAdd(&hist[(v[e] >> shift) & 255u], 1u);
-        __syncthreads();
-        if (tid < 64) {  // lane l holds bins 255-4l .. 252-4l (descending)
-            unsigned cn[4], sum = 0;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                cn[i] = hist[255 - 4 * lane - i];
-                sum += cn[i];
-            }
-            unsigned incl = sum;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const unsigned t = __shfl_up(incl, o, 64);
-                if (lane >= o) incl += t;
-            }
-            const unsigned excl = incl - sum;
-            const bool here = excl < (unsigned)r && incl >= (unsigned)r;
-            if (here) {
-                unsigned cum = excl;
-                int i = 0;
-                while (cum + cn[i] < (unsigned)r) cum += cn[i++];
-                sst[3] = (int)(255u - 4u * lane - (unsigned)i);
-                sst[4] = r - (int)cum;
-            }
-            if (__ballot(here) == 0ull && lane == 0) {  // fewer than `rank` values in total
-                sst[3] = 0;
-                sst[4] = 0;
-            }
-        }
-        __syncthreads();
-        const int rk = __builtin_amdgcn_readfirstlane(sst[4]);
-        if (rk == 0) {  // not enough values: no threshold
-            prefix = 0u;
-            break;
-        }
-        prefix |= (uint32_t)__builtin_amdgcn_readfirstlane(sst[3]) << shift;
-        mask |= 255u << shift;
-        r = rk;
-        __syncthreads();
-    }
-    if (tid == 0) {
-        const float T = unord_f32(prefix);
-        const u64 th = (prefix == 0u || T == -INFINITY) ? 0ull : ((u64)prefix << 32);
-        __hip_atomic_store(lds_ptr(&sp->thr_out) + c, th, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __threadfence();  // release the threshold before counting it published
-        atomicAdd(lds_ptr(&sp->sync) + 1, 1);
-    }
-    __syncthreads();
-}
-
-// adopt the published thresholds (every query's): raise the workgroup's own where they are lower
-// Rows rejected before this point are below the threshold in force (thr_key: the provisional one
-// or a compaction bound); where that is above the published threshold it goes into drop (the
-// certificate's bound), else the published one -- which the refine reads as thr0 -- covers them.
-__device__ __forceinline__ void i8d_seed_adopt(const int* sst, int nqb, u64* thr_key, float* thr_f, float4* qrec) {
-    __threadfence();  // acquire: each threshold was released before its count
-    const int tid = vtid_here();
-    const SeedPtrs* sp = (const SeedPtrs*)(sst + 8);
-    if (tid < nqb) {
-        const u64 v = __hip_atomic_load(lds_ptr(&sp->thr_out) + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const u64 cur = thr_key[tid];
-        if (v > cur) {
-            const float f = key_score(v);
-            thr_key[tid] = v;
-            thr_f[tid] = f;
-            qrec[tid].z = f;
-        } else if (cur > v) {
-            atomicMax(lds_ptr(&sp->drop) + tid, cur);
-        }
-    }
-    __syncthreads();
-}
-// a workgroup that never adopted: every threshold it used is at most its last, into drop
-__device__ __forceinline__ void i8d_seed_unadopted(const int* sst, int nqb, const u64* thr_key) {
-    const int tid = vtid_here();
-    const SeedPtrs* sp = (const SeedPtrs*)(sst + 8);
-    if (tid < nqb && thr_key[tid] != 0ull) atomicMax(lds_ptr(&sp->drop) + tid, thr_key[tid]);
-    __syncthreads();
-}
-
-// claim-and-select loop of a workgroup whose tiles are done: every selection still unclaimed once
-// all workgroups have arrived (a workgroup that finishes before that leaves them to the last one)
-__device__ __forceinline__ void i8d_seed_help(const ScreenArgs& a, int nqb, unsigned* hist, int* sst) {
-    for (;;) {
-        __syncthreads();
-        if (vtid_here() == 0) {
-            int* const sy = lds_ptr(&((const SeedPtrs*)(sst + 8))->sync);
-            const int arr = __hip_atomic_load(sy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            sst[2] = arr >= a.G ? atomicAdd(sy + 2, 1) : nqb;
-        }
-        __syncthreads();
-        const int c = __builtin_amdgcn_readfirstlane(sst[2]);
-        if (c >= nqb) break;
-        i8d_seed_select(a, c, hist, sst);
-    }
-    __syncthreads();
-}
 
 // The direct form for int8 codes (k_screen_i8d) and for bf16 / f16 rows (k_screen_d16): the same
 // loop with the corpus dtype's MFMA.  16-bit rows: 32 elements per K-step, the K-step's 64 B of a
@@ -1755,12 +1594,11 @@ __device__ __forceinline__ void i8d_seed_help(const ScreenArgs& a, int nqb, unsi
 // NG: query column groups of 16 (16 = the 256-column tile; 4 = a narrow tile of 64 columns for
 // mapped scans of lists probed by <= 32 queries: a quarter of the MFMAs, and the query DMAs read
 // only the tile's first 64 rows, so the L2 holds a quarter of each tile)
-template <int DT, int METRIC, bool MAP = false, int NG = 16, bool SEEDK = false, bool RES = false>
+template <int DT, int METRIC, bool MAP = false, int NG = 16, bool RES = false>
 __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
     constexpr bool L2 = METRIC == METRIC_L2;
     constexpr bool I8 = DT == DT_I8;
     static_assert(!(MAP && I8), "the mapped scan serves bf16 / f16 lists");
-    static_assert(!SEEDK || (I8 && !MAP && !L2), "in-kernel seeding: the int8 flat inner-product main pass");
     static_assert(!RES || (I8 && !MAP && !L2), "group residuals: the int8 flat inner-product main pass");
     static_assert(NG == 16 || (NG == 4 && MAP), "narrow query tiles: mapped scans only");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -1802,26 +1640,17 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
         for (int i = tid; i < nt; i += MF_THREADS) tmap[i] = a.tile_map[tm_off + i];
     }
     const int tbase = t0;
-    // SEEDK: loop index 0 is the workgroup's seed sample, position p_seed of its interleaved set
-    // (spread over the shard: ~blk / G of the way through it); the other tiles follow in order
-    const int p_seed = SEEDK ? (int)(((int64_t)blk * (int64_t)t1) / a.G) : 0;
-    auto seq = [&](int t) -> int64_t {
-        if constexpr (SEEDK) return t == 0 ? p_seed : (t <= p_seed ? t - 1 : t);
-        else return t;
-    };
     auto phys = [&](int t) -> int64_t {  // storage tile of loop index t
         if constexpr (MAP) return (int64_t)tmap[t - tbase];
-        else return (int64_t)blk + seq(t) * a.G;
+        else return (int64_t)blk + (int64_t)t * a.G;
     };
     auto ltile = [&](int t) -> int64_t {  // logical tile of loop index t (its rows: the n_valid mask)
         if constexpr (MAP) return (int64_t)t;
-        else return (int64_t)blk + seq(t) * a.G;
+        else return (int64_t)blk + (int64_t)t * a.G;
     };
-    int* const sst = (int*)(smem + I8D_LDS);  // SEEDK: the seeding state (I8D_SEED_LDS bytes)
     // RES: <mu_g, q> of the tile's group (two tiles, by parity), LDS-DMA'd by waves 4-7 one tile ahead
     // and copied into qrec[q].w at the tile's K-step 0
-    float* const tlds = (float*)(smem + I8D_LDS + (SEEDK ? I8D_SEED_LDS : 0));
-    unsigned* const shist = (unsigned*)(sm + 256 * 16 + 16 + MF_POOL * 12);  // SEEDK: select histogram (records' area)
+    float* const tlds = (float*)(smem + I8D_LDS);
     if (tid < 256) {
         const bool real = tid < nqb;
         const u64 k0 = real ? (a.thr0 ? a.thr0[tid] : 0ull) : ~0ull;
@@ -1837,11 +1666,6 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
         flag[1] = 0;
         flag[2] = 0;
         flag[3] = 0;
-        if constexpr (SEEDK) {
-            sst[0] = 0;
-            sst[7] = 0;
-            *(SeedPtrs*)(sst + 8) = SeedPtrs{a.seed_sync, (unsigned*)a.seedmax, a.thr_out, a.drop};
-        }
     }
     __syncthreads();
     const int nks = a.dpad / (I8 ? 64 : CH);
@@ -1920,8 +1744,6 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
         I8D_ISSUE(2);
     }
     bool check_pending = false;
-    // SEEDK state (wave-uniform): thresholds adopted (the rest lives in LDS, sst)
-    bool seed_adopted = false;
     // one K-step: wait for its fragments + query block, barrier, issue the step 3 ahead, then the
     // MFMA block STEP_ (a static choice per call site: a runtime choice between asm variants makes
     // the register allocator shuffle the 128 accumulators)
@@ -1981,23 +1803,6 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
                     }
                     mf_barrier_drain();  // counters / thresholds / compacted buffers published
                 }
-            }
-        }
-        if constexpr (SEEDK) {
-            // wave 0's decision from its last poll (written before this K-step's barrier)
-            const int act = seed_adopted ? 0 : __builtin_amdgcn_readfirstlane(sst[0]);
-            if (act == 2) {  // every threshold published: adopt them
-                i8d_seed_adopt(sst, nqb, thr_key, thr_f, qrec);
-                seed_adopted = true;
-            } else if (act == 1) {  // every workgroup arrived: claim one selection
-                const int ctid = vtid_here();
-                if (ctid == 0) sst[2] = atomicAdd(lds_ptr(&((const SeedPtrs*)(sst + 8))->sync) + 2, 1);
-                __syncthreads();
-                const int c = __builtin_amdgcn_readfirstlane(sst[2]);
-                if (ctid == 0) sst[0] = 0;
-                if (c < nqb) i8d_seed_select(a, c, shist, sst);
-                else if (ctid == 0) sst[7] = 1;  // claims exhausted: wave 0 stops proposing them
-                __syncthreads();
             }
         }
         if constexpr (RES) {  // this tile's <mu_g, q> into qrec .w (read by the epilogue, K-steps later)
@@ -2119,72 +1924,6 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
                     for (int r = 0; r < 4; ++r)
                         acc[m][p][r] = __float_as_int(__int_as_float(acc[m][2 * p][r]) + __int_as_float(acc[m][2 * p + 1][r]));
         }
-        if constexpr (SEEDK) {
-            if (ti == t0) {  // the seed sample: publish its 16-row-group key maxima, set the provisional thresholds
-                float* gm = (float*)shist;  // [256 queries][16 groups] (the records' area, free here)
-                const int M = a.G * 16;
-                const SeedPtrs* sp = (const SeedPtrs*)(sst + 8);
-                unsigned* const smx = lds_ptr(&sp->maxima) + blk * 16;
-                const int stid = vtid_here();
-#pragma unroll
-                for (int n = 0; n < 16; ++n) {
-                    const float4 f = qrec[16 * n + qlane];
-#pragma unroll
-                    for (int m = 0; m < 2; ++m) {
-                        float mx = -INFINITY;
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            const int row = wid * 32 + 16 * m + (olane >> 4) * 4 + r;
-                            const uint32_t w = rx[row];
-                            float x = __builtin_fmaf(__uint_as_float(w & 0xFFFF0000u), f.y,
-                                                     (float)acc[m][n][r] * __uint_as_float(w << 16)) * f.x;
-                            if constexpr (L2) x = __builtin_fmaf(2.0f, x, -rq[row]);
-                            if constexpr (RES) x += f.w;  // + <mu_g, q>
-                            if (rowbase + row < a.n_valid) mx = fmaxf(mx, x);
-                        }
-                        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-                        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-                        if ((olane >> 4) == 0) {
-                            const int q = 16 * n + qlane, g = 2 * wid + m;
-                            gm[q * 16 + g] = mx;
-                            if (q < nqb)
-                                __hip_atomic_store(smx + (size_t)q * M + g, __float_as_uint(mx), __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT);
-                        }
-                    }
-                }
-                __syncthreads();
-                if (stid < nqb) {
-                    // provisional threshold: the seed_prov_rank-th largest of the sample's 16 group
-                    // maxima (a rank the published seed exceeds with near certainty; i8d_seed_adopt
-                    // accounts for it where it does not)
-                    const int pr = a.seed_prov_rank;
-                    float tp = -INFINITY;
-#pragma unroll
-                    for (int g = 0; g < 16; ++g) {
-                        const float x = gm[stid * 16 + g];
-                        int above = 0;  // maxima ahead of x: larger, or equal at a lower group
-#pragma unroll
-                        for (int h = 0; h < 16; ++h) {
-                            const float y = gm[stid * 16 + h];
-                            above += (y > x || (y == x && h < g)) ? 1 : 0;
-                        }
-                        if (above == pr - 1) tp = x;
-                    }
-                    if (tp > -INFINITY) {
-                        const u64 kp = (u64)ord_f32(tp) << 32;
-                        if (kp > thr_key[stid]) {
-                            thr_key[stid] = kp;
-                            thr_f[stid] = tp;
-                            qrec[stid].z = tp;
-                        }
-                    }
-                }
-                __threadfence();  // release this workgroup's maxima before counting it in
-                __syncthreads();
-                if (stid == 0) atomicAdd(lds_ptr(&sp->sync), 1);
-            }
-        }
         // the bound test of all columns first (straight-line VALU, one bit per column)
         uint32_t gomask = 0;
 #pragma unroll
@@ -2231,28 +1970,9 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
         }
         if (nrec) drain(nrec);
         check_pending = true;
-        if constexpr (SEEDK) {
-            if (!seed_adopted && wid == 0) {
-                // the poll: (arrivals, published) LDS-DMA'd into sst[5..6] one tile ago (its landing
-                // is covered by every K-step's counted wait since), so no register waits on it
-                if (ti > t0 && olane == 0) {  // (the first poll was issued after the seed tile)
-                    const int arr = sst[5], pub = sst[6];
-                    sst[0] = pub >= nqb ? 2 : (arr >= a.G && sst[7] == 0) ? 1 : 0;
-                }
-                if (olane < 2)
-                    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off sc1" ::"v"(lds_ptr(&((const SeedPtrs*)(sst + 8))->sync) + olane),
-                                 "s"(lds_addr((const uint8_t*)(sst + 5)))
-                                 : "memory", "m0");
-            }
-        }
     }
 #undef I8D_ISSUE
 #undef I8D_BODY
-    if constexpr (SEEDK) {
-        mf_barrier_drain();  // (the dummy steps' loads and the last poll)
-        if (!seed_adopted) i8d_seed_unadopted(sst, nqb, thr_key);
-        i8d_seed_help(a, nqb, shist, sst);
-    }
     // ---- flush: pool -> buffers, then the best <= Kp per query -> the query's survivor list ----
     mf_barrier_drain();  // (also drains the dummy steps' loads)
     {
@@ -2284,16 +2004,7 @@ __global__ void __launch_bounds__(512, 2) k_screen_i8d(ScreenArgs a, const uint8
 // ... over group-residual codes (a corpus stored cluster by cluster): every key + <mu_g, q>
 // (inner product; the seed pass adds the same terms to its maxima)
 __global__ void __launch_bounds__(512, 2) k_screen_i8d_res(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
-    screen_direct<DT_I8, METRIC_IP, false, 16, false, true>(a, qt, nqb);
-}
-// the same main pass with its threshold seeded in the kernel (no seed pass / select launches);
-// inner product (the L2 form's extra epilogue state leaves no registers for it: it keeps the pass)
-__global__ void __launch_bounds__(512, 2) k_screen_i8d_seeded(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
     screen_direct<DT_I8, METRIC_IP, false, 16, true>(a, qt, nqb);
-}
-// ... over group-residual codes (a corpus stored cluster by cluster): every key + <mu_g, q>
-__global__ void __launch_bounds__(512, 2) k_screen_i8d_seeded_res(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
-    screen_direct<DT_I8, METRIC_IP, false, 16, true, true>(a, qt, nqb);
 }
 template <int DT, int METRIC>
 __global__ void __launch_bounds__(512, 2) k_screen_d16(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
@@ -3846,9 +3557,9 @@ hipError_t launch_quant_rows(int dt, const uint8_t* data, int dpad, int64_t r0, 
 
 hipError_t launch_pack_qtile_i8(const float* q, int nqb, int d, int dpad8, uint8_t* qt, float2* qfac, float* qeps,
                                 const unsigned* maxes, int* gcnt, u64* drop, hipStream_t st, int* fails,
-                                const unsigned* l2max, float gamma, int* seed_sync) {
+                                const unsigned* l2max, float gamma) {
     hipLaunchKernelGGL(k_pack_qtile_i8, dim3(MFMA_QB / 4), dim3(256), 0, st, q, nqb, d, dpad8, qt, qfac, qeps, maxes,
-                       gcnt, drop, fails, l2max, gamma, seed_sync);
+                       gcnt, drop, fails, l2max, gamma);
     return hipGetLastError();
 }
 
@@ -3893,21 +3604,6 @@ static hipError_t launch_mfma_dt(int dt, const ScreenArgs& a, const uint8_t* qt,
         if (a.gT && (a.metric != METRIC_IP || !i8_direct_ok(a.dpad))) return hipErrorInvalidValue;
         if (!SEED && i8_direct_ok(a.dpad)) {  // the main pass: direct form (no seed-tile reuse)
             if (a.seed_acc || a.tile_stride != 0) return hipErrorInvalidValue;
-            if (a.seed_sync) {  // threshold seeded in the kernel (inner product; L2 keeps the seed pass)
-                if (a.metric != METRIC_IP || !a.seedmax || !a.thr_out || !a.drop || a.thr0 || a.seed_rank < 1 ||
-                    a.seed_prov_rank < 1 || a.seed_prov_rank > 16 ||
-                    a.G * 16 > kI8dSeedMaxima || (int64_t)a.tiles < 4 * (int64_t)a.G)
-                    return hipErrorInvalidValue;
-                if (a.gT) {  // group residuals
-                    set_lds_attr((const void*)k_screen_i8d_seeded_res, I8D_LDS + I8D_SEED_LDS + I8D_RES_LDS);
-                    hipLaunchKernelGGL(k_screen_i8d_seeded_res, dim3(a.G), dim3(MF_THREADS),
-                                       I8D_LDS + I8D_SEED_LDS + I8D_RES_LDS, st, a, qt, nqb);
-                    return hipGetLastError();
-                }
-                set_lds_attr((const void*)k_screen_i8d_seeded, I8D_LDS + I8D_SEED_LDS);
-                hipLaunchKernelGGL(k_screen_i8d_seeded, dim3(a.G), dim3(MF_THREADS), I8D_LDS + I8D_SEED_LDS, st, a, qt, nqb);
-                return hipGetLastError();
-            }
             if (a.gT) {  // group residuals (inner product)
                 if (a.metric != METRIC_IP) return hipErrorInvalidValue;
                 set_lds_attr((const void*)k_screen_i8d_res, I8D_LDS + I8D_RES_LDS);

@@ -52,10 +52,6 @@ def main() -> int:
         rc |= check(asm, metric, sym)
     # the main pass over group-residual codes (inner product; + <mu_g, q> per key)
     rc |= check(asm, "ip", "_ZN2vs16k_screen_i8d_resENS_10ScreenArgsEPKhi:", name="k_screen_i8d_res")
-    # the same main pass with its threshold seeded in the kernel (inner product)
-    rc |= check(asm, "ip", "_ZN2vs19k_screen_i8d_seededENS_10ScreenArgsEPKhi:", name="k_screen_i8d_seeded")
-    # ... over group-residual codes
-    rc |= check(asm, "ip", "_ZN2vs23k_screen_i8d_seeded_resENS_10ScreenArgsEPKhi:", name="k_screen_i8d_seeded_res")
     # the bf16 / f16 direct form (k_screen_d16): its corpus loads are global_load_dwordx4 with and
     # without the nt hint (the first half of each 128 B line keeps the default policy)
     for dt, dcode in (("bf16", 1), ("f16", 2)):

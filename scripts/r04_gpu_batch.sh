@@ -8,7 +8,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 PYT="python -u -m pytest -v --timeout 300 --timeout-method thread"
-TESTS=${TESTS:-"tests/test_gpu_int8_seeded.py tests/test_gpu_int8_clustered.py tests/test_gpu_multi_device.py tests/test_gpu_hnsw_build.py tests/test_gpu_hnsw.py tests/test_gpu_cfg1.py tests/test_gpu_int8_screen.py tests/test_gpu_distributed.py"}
+TESTS=${TESTS:-"tests/test_gpu_int8_direct.py tests/test_gpu_int8_clustered.py tests/test_gpu_multi_device.py tests/test_gpu_hnsw_build.py tests/test_gpu_hnsw.py tests/test_gpu_cfg1.py tests/test_gpu_int8_screen.py tests/test_gpu_distributed.py"}
 fatal() { [ "$1" -ge 124 ] && [ "$1" -ne 0 ]; }
 run() {  # name, seconds, command...
   local name=$1 secs=$2; shift 2

@@ -1,15 +1,15 @@
-"""The int8 direct main pass with its threshold seeded inside the kernel (k_screen_i8d_seeded,
-inner product, d a multiple of 256, >= 4 tiles per workgroup): each workgroup screens a sample
-tile first, publishes its 16-row-group maxima, and the workgroups select and adopt each query's
-seed themselves while they screen.  Results must be bit-exact against ``oracle.knn_exact`` on the
-stored values whatever the seed does: a provisional or a published threshold that lies only fails
-the certificate (the device fallback round re-searches), it never changes an answer.
+"""The int8 direct main pass (k_screen_i8d, inner product, d a multiple of 256) behind its seed
+pass (>= 4 tiles per workgroup: one sample tile per workgroup, 16-row-group maxima, the rank-r
+maximum per query as the starting threshold).  Results must be bit-exact against
+``oracle.knn_exact`` on the stored values whatever the seed does: a seed that lies only fails the
+certificate (the device fallback round re-searches), it never changes an answer.
 
 Cases: every storage dtype, k 1 / 10 / 100 / 1000, one and two query blocks, a partial last
-tile, near-copies of the queries planted in exactly the sample tiles (the selected seed sits
-among them), a sample tile holding a query's whole top-k
-(the provisional threshold lies), exact duplicates across the corpus (ties -> lower id), the
-device API with an id offset, and the two-phase sharded step's phase A / B.
+tile, near-copies of the queries planted in exactly the sampled tiles (the selected seed sits
+among them), a sampled tile holding a query's whole top-k, exact duplicates across the corpus
+(ties -> lower id), the device API with an id offset, and the two-phase sharded step's phase A / B.
+(Round 4 also ran these cases against a form that seeded inside the main pass; it measured slower
+and was removed, profiles/r04_seed_ab.txt.)
 """
 import numpy as np
 import pytest
@@ -40,13 +40,10 @@ def _exact(ix, q, k):
 
 
 def _sample_tiles(tiles, G):
-    """Each workgroup's seed tile (loop index 0 of k_screen_i8d_seeded): position
-    p = b * T_b // G of its interleaved set b, b + G, ..."""
-    out = []
-    for b in range(G):
-        tb = (tiles - b + G - 1) // G
-        out.append(b + (b * tb // G) * G)
-    return out
+    """The seed pass's tiles (vs_api.hip search_block_i8): workgroup b of min(G, 512) screens tile
+    b * (tiles // that)."""
+    g = min(G, 512)
+    return [b * (tiles // g) for b in range(g)]
 
 
 @pytest.mark.parametrize("dtype,d,nq,k,tpc", [
@@ -57,7 +54,7 @@ def _sample_tiles(tiles, G):
     ("bf16", 512, 300, 25, 6.1),   # two query blocks (256 + 44)
     ("bf16", 512, 32, 1000, 4.2),  # deep screens: compaction inside the K loop
 ])
-def test_seeded_direct_exact(FlatIndex, dtype, d, nq, k, tpc):
+def test_direct_direct_exact(FlatIndex, dtype, d, nq, k, tpc):
     G = _num_cu()
     N = int(256 * G * tpc) + 77  # a partial last tile
     ix = FlatIndex(d, "ip", dtype)
@@ -70,7 +67,7 @@ def test_seeded_direct_exact(FlatIndex, dtype, d, nq, k, tpc):
     ix.close()
 
 
-def test_seeded_native_and_int8_identical_at_cfg3_width(FlatIndex):
+def test_direct_native_and_int8_identical_at_cfg3_width(FlatIndex):
     G = _num_cu()
     N, d, nq, k = 256 * G * 5 + 1, 1536, 128, 100
     ix = FlatIndex(d, "ip", "bf16")
@@ -86,7 +83,7 @@ def test_seeded_native_and_int8_identical_at_cfg3_width(FlatIndex):
     ix.close()
 
 
-def test_seeded_planted_sample_tiles_exact(FlatIndex):
+def test_direct_planted_sample_tiles_exact(FlatIndex):
     # near-copies of 16 queries in exactly the sample tiles (4 rows per tile, ~64 per query, in one
     # 16-row group each): the selected seed lands among them, far above the rest of the corpus, so
     # the main pass lists almost nothing but the planted rows -- still enough for the certificate
@@ -113,10 +110,10 @@ def test_seeded_planted_sample_tiles_exact(FlatIndex):
     ix.close()
 
 
-def test_seeded_sample_tile_holding_the_top_k(FlatIndex):
-    # one sample tile holds 200 near-copies of query 0 spread over all 16 of its groups: its
-    # provisional threshold (4th group maximum) drops most of them in that tile's own epilogue --
-    # the drop bound must make the certificate fail rather than return a wrong answer
+def test_direct_sample_tile_holding_the_top_k(FlatIndex):
+    # one sampled tile holds 200 near-copies of query 0 spread over all 16 of its groups: the
+    # seed sits among them (the sample is not representative of the corpus), and the answer must
+    # stay exact (a lying seed fails the certificate; the fallback round re-searches)
     G = _num_cu()
     d, k, nq = 512, 100, 24
     tiles = 5 * G + 1
@@ -134,7 +131,7 @@ def test_seeded_sample_tile_holding_the_top_k(FlatIndex):
     ix.close()
 
 
-def test_seeded_exact_duplicates_tie_to_lower_id(FlatIndex):
+def test_direct_exact_duplicates_tie_to_lower_id(FlatIndex):
     G = _num_cu()
     d, k, nq = 512, 20, 40
     N = 256 * G * 4 + 300
@@ -153,7 +150,7 @@ def test_seeded_exact_duplicates_tie_to_lower_id(FlatIndex):
     ix.close()
 
 
-def test_seeded_device_api_with_offset_and_phases(FlatIndex):
+def test_direct_device_api_with_offset_and_phases(FlatIndex):
     import torch
     G = _num_cu()
     d, nq, k = 512, 64, 30
