@@ -555,12 +555,13 @@ void search_block_i8(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float
     r.ostride = ostride;
     if (phase == 1) {
         const int ka = KA1;
-        c->pa.ensure((size_t)nqb * ka * 12 + (size_t)nqb * 16);
+        const int kah = rfw_ka_hi(ka);  // (phase A keeps up to this many rows per query)
+        c->pa.ensure((size_t)nqb * kah * 12 + (size_t)nqb * 16);
         r.phase = 1;
-        r.pa_cap = ka;
+        r.pa_cap = kah;
         r.pa_sc = c->pa.as<double>();
-        r.pa_ids = (uint32_t*)(r.pa_sc + (size_t)nqb * ka);
-        r.pa_tA = (u64*)(r.pa_ids + (size_t)nqb * ka);
+        r.pa_ids = (uint32_t*)(r.pa_sc + (size_t)nqb * kah);
+        r.pa_tA = (u64*)(r.pa_ids + (size_t)nqb * kah);
         r.pa_n = (int*)(r.pa_tA + nqb);
         HIP_CHECK(launch_refine_wide(r, nqb, ka, st));
         if (keep) *keep = r;

@@ -192,27 +192,57 @@ __device__ __forceinline__ u64 wave_kth(const u64 (&keys)[E], int K) {
     return t;
 }
 
-// Same over a 256-thread block; red = 8 ints of LDS.
+// Over a whole block: a threshold t with Klo <= #(keys >= t) <= Khi (distinct keys, Klo <= #keys): the bit bisection of
+// block_kth, stopping at the first prefix whose count lands in the range (Khi = Klo: the Klo-th
+// largest key).  One barrier per step: the per-wave counts alternate between the two halves of
+// red[2 * waves] (a half is rewritten two steps later, after every wave has passed the barrier of
+// the step in between, i.e. after its reads).
 template <int E>
-__device__ __forceinline__ u64 block_kth(const u64 (&keys)[E], int K, int* red) {
+__device__ __forceinline__ u64 block_kth_range(const u64 (&keys)[E], int Klo, int Khi, int* red) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
     u64 t = 0;
-    for (int b = 63; b >= 0; --b) {
+    for (int b = 63, par = 0; b >= 0; --b, par ^= 1) {
         const u64 cand = t | (1ull << b);
         int c = 0;
 #pragma unroll
         for (int e = 0; e < E; ++e) c += keys[e] >= cand ? 1 : 0;
         c = wave_sum_i(c);
-        if (lane == 0) red[w] = c;
+        if (lane == 0) red[par * nw + w] = c;
         __syncthreads();
         int tot = 0;
-        for (int i = 0; i < nw; ++i) tot += red[i];
-        __syncthreads();
-        if (tot >= K) {
+        for (int i = 0; i < nw; ++i) tot += red[par * nw + i];
+        if (tot >= Klo) {
             t = cand;
-            if (tot == K) break;
+            if (tot <= Khi) break;
         }
     }
+    __syncthreads();  // (every wave has read red before its caller reuses it)
+    return t;
+}
+// The K-th largest of the block's keys (distinct keys, K <= #keys); red: 2 x waves ints
+template <int E>
+__device__ __forceinline__ u64 block_kth(const u64 (&keys)[E], int K, int* red) {
+    return block_kth_range<E>(keys, K, K, red);
+}
+// ... over keys in memory (lists longer than the registers hold)
+__device__ __forceinline__ u64 block_kth_range_mem(const u64* buf, int n, int Klo, int Khi, int* red) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    u64 t = 0;
+    for (int b = 63, par = 0; b >= 0; --b, par ^= 1) {
+        const u64 cand = t | (1ull << b);
+        int c = 0;
+        for (int idx = threadIdx.x; idx < n; idx += blockDim.x) c += buf[idx] >= cand ? 1 : 0;
+        c = wave_sum_i(c);
+        if (lane == 0) red[par * nw + w] = c;
+        __syncthreads();
+        int tot = 0;
+        for (int i = 0; i < nw; ++i) tot += red[par * nw + i];
+        if (tot >= Klo) {
+            t = cand;
+            if (tot <= Khi) break;
+        }
+    }
+    __syncthreads();  // (every wave has read red before its caller reuses it)
     return t;
 }
 
@@ -2695,7 +2725,7 @@ __device__ __forceinline__ void refine(const RefineArgs& a, int KP2) {
     __shared__ int nv_s;
     __shared__ u64 minkey_s, thr_s;
     __shared__ double qq_s;
-    __shared__ int red[RF_THREADS / 64];
+    __shared__ int red[2 * (RF_THREADS / 64)];
     const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     constexpr int NW = RF_THREADS / 64;
     // the best Kp keys of the candidate list, compacted into LDS (cq)
@@ -2909,7 +2939,6 @@ __global__ void __launch_bounds__(RF_THREADS) k_refine_redo(RefineArgs a, int KP
 //  drop) have true <= key_score(max(thr0, drop)) + qeps, which must be < T; and the rows scored
 //  must fit the block's RFW_CAP slots.
 // ------------------------------------------------------------------------------------------------
-constexpr int RFW_CAP = 8192;  // rows scored per query (fp64 score + id in LDS)
 
 // order-preserving block compaction of this thread's keys in [lo, hi) to ids[base + ...]; returns
 // the block total
@@ -2994,7 +3023,7 @@ __global__ void __launch_bounds__(RF_THREADS) k_refine_wide(RefineArgs a, int KA
     double* sc = (double*)smem;                                  // [RFW_CAP]
     uint32_t* ids = (uint32_t*)(smem + (size_t)RFW_CAP * 8);     // [RFW_CAP]
     double* qs = (double*)(smem + (size_t)RFW_CAP * 12);         // fp64 query, transposed groups
-    __shared__ int red[RF_THREADS / 64];
+    __shared__ int red[2 * (RF_THREADS / 64)];
     __shared__ int nb_s;
     __shared__ double qq_s;
     const int q = blockIdx.x, tid = threadIdx.x;
@@ -3038,7 +3067,12 @@ __global__ void __launch_bounds__(RF_THREADS) k_refine_wide(RefineArgs a, int KA
         const int j = tid + RF_THREADS * e;
         keys[e] = (inreg && j < n) ? src[j] : 0ull;
     }
-    if (n > KA) tA = inreg ? block_kth<RF_E>(keys, KA, red) : block_kth_mem(src, n, KA, red);
+    // phase A: the best KA..rfw_ka_hi(KA) keys (any count in that range serves: T' and the phase-B
+    // window follow from the rows actually scored, and the range stops the bisection early)
+    if (n > KA) {
+        const int Khi = rfw_ka_hi(KA);
+        tA = inreg ? block_kth_range<RF_E>(keys, KA, Khi, red) : block_kth_range_mem(src, n, KA, Khi, red);
+    }
     if (inreg) {
         nA = block_write_ids<RF_E>(keys, tA, ~0ull, ids, RFW_CAP, red);
     } else {  // very long lists: the phase-A set from memory (block_compact_mem writes keys)

@@ -39,6 +39,14 @@ for s in ${STEPS:-tests cfg3 shard8 mix03 micro multi}; do
     diagmix10m) run diag_mix03_10m 600 python scripts/diag_mixture.py --sorted --sigma 0.3 --rows 10000000 --batches 4 --check ;;
     diagmix) run diag_mix03 600 python scripts/diag_mixture.py --sorted --sigma 0.3 ;;
     multi) run multi_step 600 python scripts/multi_step_timing.py ;;
+    cfg5skew) run bench_cfg5_skew 900 python bench.py --workload cfg5 --skew 1.1 --steps 10 --warmup 2 ;;
+    cfg5skewpmc) mkdir -p gpurun_out/pmc5f gpurun_out/pmc5w && \
+      run pmc5_fetch 900 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmc5f -o p --output-format csv -- python bench.py --workload cfg5 --skew 1.1 --steps 3 --warmup 1 && \
+      run pmc5_write 900 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d gpurun_out/pmc5w -o p --output-format csv -- python bench.py --workload cfg5 --skew 1.1 --steps 3 --warmup 1 && \
+      run ivf_traffic 120 python scripts/ivf_traffic.py gpurun_out/pmc5f gpurun_out/pmc5w gpurun_out/traffic_cfg5_skew.json 1.1 50000000 && \
+      rm -rf gpurun_out/pmc5f gpurun_out/pmc5w ;;
+    trace8) mkdir -p gpurun_out/trace8 && run trace8 300 rocprofv3 --kernel-trace -d gpurun_out/trace8 -o t --output-format csv -- python bench.py --shard-of 8 --steps 10 --warmup 3 --no-cpu-baseline && \
+      python scripts/trace_tail.py $(ls gpurun_out/trace8/*/t_kernel_trace.csv gpurun_out/trace8/t_kernel_trace.csv 2>/dev/null | head -1) 80 "vs::|copyBuffer|nccl|rccl|Kernel" > gpurun_out/trace8_tail.txt && rm -rf gpurun_out/trace8 ;;
     hnsw) run hnsw_bench 900 python scripts/hnsw_bench.py ;;
     *) echo "unknown step $s" >> gpurun_out/steps.log; exit 2 ;;
   esac
