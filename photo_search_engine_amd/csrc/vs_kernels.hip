@@ -3793,7 +3793,10 @@ static void launch_refine_one(const RefineArgs& a, int nq, int KP2, size_t lds, 
 // per workgroup, at most 32 per query, the whole grid within one wave of the chip.
 int refine_split(int nq, int Kp, int dt, int num_cu) {
     const int per_round = (dt == DT_F32 ? 2 : 4) * (RF_THREADS / 64);
-    int ns = Kp / (2 * per_round);
+    // GEMV batches (<= 8 queries: the product's single-query call): one scoring round per
+    // workgroup -- a single query's Kp rows gathered by one CU were a chain of dependent rounds
+    // (cfg2: 42 us for ~100 fp32 rows); MFMA batches: two rounds per workgroup
+    int ns = nq <= GEMV_NQ_MAX ? (Kp + per_round - 1) / per_round : Kp / (2 * per_round);
     ns = std::min(ns, 32);
     ns = std::min(ns, num_cu / std::max(nq, 1));
     return ns >= 2 ? ns : 1;

@@ -47,6 +47,9 @@ for s in ${STEPS:-tests cfg3 shard8 mix03 micro multi}; do
       rm -rf gpurun_out/pmc5f gpurun_out/pmc5w ;;
     trace8) mkdir -p gpurun_out/trace8 && run trace8 300 rocprofv3 --kernel-trace -d gpurun_out/trace8 -o t --output-format csv -- python bench.py --shard-of 8 --steps 10 --warmup 3 --no-cpu-baseline && \
       python scripts/trace_tail.py $(ls gpurun_out/trace8/*/t_kernel_trace.csv gpurun_out/trace8/t_kernel_trace.csv 2>/dev/null | head -1) 80 "vs::|copyBuffer|nccl|rccl|Kernel" > gpurun_out/trace8_tail.txt && rm -rf gpurun_out/trace8 ;;
+    trace2) mkdir -p gpurun_out/trace2 && run trace2 300 rocprofv3 --kernel-trace -d gpurun_out/trace2 -o t --output-format csv -- python bench.py --workload cfg2 --steps 20 --warmup 3 --no-cpu-baseline && \
+      python scripts/trace_tail.py $(ls gpurun_out/trace2/*/t_kernel_trace.csv gpurun_out/trace2/t_kernel_trace.csv 2>/dev/null | head -1) 60 "vs::|copyBuffer|Kernel" > gpurun_out/trace2_tail.txt && rm -rf gpurun_out/trace2 ;;
+    product) run product_native 300 python scripts/product_latency.py && run product_int8 300 python scripts/product_latency.py --screen int8 ;;
     hnsw) run hnsw_bench 900 python scripts/hnsw_bench.py ;;
     *) echo "unknown step $s" >> gpurun_out/steps.log; exit 2 ;;
   esac
