@@ -106,4 +106,7 @@ def test_int8_group_residuals_incremental_adds(dtype):
     for _ in range(4):
         ix.search(q, 50)
     assert ix.uncertified_count() - u0 <= 96 // 16  # group residuals keep the int8 screen certifying
+    st = ix.screen_state()
+    assert st["screen"] == 1 and st["group_residuals"] == 1 and st["groups_with_mean"] >= N // 4096 - 1
+    assert 0.0 < st["max_mean_norm"] <= 1.0 and st["i8_routed_searches"] == 0
     ix.close()

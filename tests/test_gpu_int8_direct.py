@@ -64,6 +64,8 @@ def test_direct_direct_exact(FlatIndex, dtype, d, nq, k, tpc):
     _exact(ix, q, k)
     assert ix.uncertified_count() == 0
     assert ix.unresolved_count() == 0
+    st = ix.screen_state()  # isotropic rows: no group has a mean worth coding against
+    assert st["group_residuals"] == 0 and st["groups_with_mean"] == 0 and st["i8_union_log2"] == 0
     ix.close()
 
 
