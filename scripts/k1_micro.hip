@@ -8,7 +8,9 @@
 // Variants (template MODE): 0 = loads only (A loads + query DMA, no reads, no MFMA),
 // 1 = + B fragment reads, 2 = + MFMAs (full loop, column-max epilogue), 3/4 = dump accumulators
 // (correctness check on a small corpus against a host int32 GEMM), 5 = no barrier, 6 = loads issued
-// after the MFMAs, 8 = per-value float epilogue, 9 = bound epilogue (the product's), P = lead.
+// after the MFMAs, 8 = per-value float epilogue, 9 = bound epilogue (the product's), P = lead;
+// 10 / 11 = compiler-scheduled v_mfma_i32_32x32x32_i8 / 16x16x64_i8 over the same bytes (run ids
+// 20 / 21: does the 32x32 shape's half operand traffic per MAC lower the power-limited time?).
 // Results (MI355X, 10M x 1536, int8 codes of Gaussian rows): DESIGN.md §5.
 // Run: ./abtmp/k1_micro [N] [d] [iters] [data: 0 random, 1 zero, 2 Gaussian codes] [mode]
 //
@@ -80,6 +82,9 @@ __global__ void __launch_bounds__(THREADS, 2)
 
     intx4 A[U][2];
     intx4 acc[2][16];
+    intx16 acc32[8];  // MODE 10: 8 blocks of 32 rows x 32 queries (v_mfma_i32_32x32x32_i8)
+#pragma unroll
+    for (int n = 0; n < 8; ++n) acc32[n] = intx16{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
@@ -119,7 +124,27 @@ __global__ void __launch_bounds__(THREADS, 2)
                 if constexpr (MODE != 5) barrier_lgkm();
                 if constexpr (MODE != 6) ISSUE_STEP(s + P, (u + P) % U);
                 const uint8_t* slot = smem + (s % U) * KB + lane_off;
-                if constexpr (MODE == 2 || MODE >= 5 || MODE == 3 || MODE == 4) {
+                if constexpr (MODE == 10 || MODE == 11) {
+                    // compiler-scheduled MFMAs over the same bytes: 10 = 32x32x32 (16 per K-step, half
+                    // the operand reads per MAC), 11 = 16x16x64 (32 per K-step); the operand mapping
+                    // is not the product's (timing only)
+                    intx4 b[16];
+#pragma unroll
+                    for (int n = 0; n < 16; ++n) b[n] = *(const intx4*)(slot + n * 1024);
+                    if constexpr (MODE == 10) {
+#pragma unroll
+                        for (int h = 0; h < 2; ++h)
+#pragma unroll
+                            for (int n = 0; n < 8; ++n)
+                                acc32[n] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[u][h], b[8 * h + n], acc32[n], 0, 0, 0);
+                    } else {
+#pragma unroll
+                        for (int m = 0; m < 2; ++m)
+#pragma unroll
+                            for (int n = 0; n < 16; ++n)
+                                acc[m][n] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[u][m], b[n], acc[m][n], 0, 0, 0);
+                    }
+                } else if constexpr (MODE == 2 || MODE >= 5 || MODE == 3 || MODE == 4) {
                     // one asm block per K-step: 16 B-fragment reads RA = 4 ahead of their MFMA pairs
                     intx4 bt[4];
                     const uint32_t slot_lds = lds_addr(slot);
@@ -204,6 +229,15 @@ __global__ void __launch_bounds__(THREADS, 2)
                                 const float bound = fmaxf(smax * fm, smin * fm);
                                 nhit += __builtin_fmaf(bmax, f.y, bound) * f.x >= thr[q];
                             }
+                        }
+                    } else if constexpr (MODE == 10) {
+#pragma unroll
+                        for (int n = 0; n < 8; ++n) {
+                            int mx = INT32_MIN;
+#pragma unroll
+                            for (int r = 0; r < 16; ++r) mx = max(mx, acc32[n][r]);
+                            nhit += mx > 2000000;
+                            acc32[n] = intx16{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
                         }
                     } else if constexpr (MODE == 2 || MODE >= 5) {
 #pragma unroll
@@ -360,5 +394,7 @@ int main(int argc, char** argv) {
     run(k_micro<0, 7>, "loads only P=7", 13);
     run(k_micro<2, 7>, "full P=7", 14);
     run(k_micro<2>, "full (MFMA)", 2);
+    run(k_micro<10>, "MFMA 32x32x32 (builtins)", 20);
+    run(k_micro<11>, "MFMA 16x16x64 (builtins)", 21);
     return 0;
 }

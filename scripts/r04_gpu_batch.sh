@@ -30,6 +30,10 @@ for s in ${STEPS:-tests cfg3 shard8 mix03 micro multi}; do
     mix03) run bench_mix03 600 python bench.py --data mixture-sorted --sigma 0.3 --warmup 8 --no-cpu-baseline ;;
     mix05) run bench_mix05 600 python bench.py --data mixture-sorted --sigma 0.5 --warmup 8 --no-cpu-baseline ;;
     mix10) run bench_mix10 600 python bench.py --data mixture-sorted --sigma 1.0 --warmup 8 --no-cpu-baseline ;;
+    micro32) for m in 20 21 9; do for dt in 1 2; do
+             timeout -k 10 120 ./abtmp/k1_micro 10000000 1536 20 $dt $m >> gpurun_out/k1_micro32.txt 2>&1
+             rc=$?; if [ $rc -ne 0 ]; then echo "step micro32 rc=$rc" >> gpurun_out/steps.log; exit $rc; fi
+           done; done; echo "step micro32 rc=0" >> gpurun_out/steps.log ;;
     micro) for m in 0 2 9; do for dt in 1 2; do
              timeout -k 10 120 ./abtmp/k1_micro 10000000 1536 20 $dt $m >> gpurun_out/k1_micro.txt 2>&1
              rc=$?; if [ $rc -ne 0 ]; then echo "step micro rc=$rc" >> gpurun_out/steps.log; exit $rc; fi
@@ -50,6 +54,8 @@ for s in ${STEPS:-tests cfg3 shard8 mix03 micro multi}; do
     trace2) mkdir -p gpurun_out/trace2 && run trace2 300 rocprofv3 --kernel-trace -d gpurun_out/trace2 -o t --output-format csv -- python bench.py --workload cfg2 --steps 20 --warmup 3 --no-cpu-baseline && \
       python scripts/trace_tail.py $(ls gpurun_out/trace2/*/t_kernel_trace.csv gpurun_out/trace2/t_kernel_trace.csv 2>/dev/null | head -1) 60 "vs::|copyBuffer|Kernel" > gpurun_out/trace2_tail.txt && rm -rf gpurun_out/trace2 ;;
     product) run product_native 300 python scripts/product_latency.py && run product_int8 300 python scripts/product_latency.py --screen int8 ;;
+    cfg4) run bench_cfg4 1100 python bench.py --workload cfg4 --steps 10 --warmup 3 --no-cpu-baseline ;;
+    cfg5) run bench_cfg5 900 python bench.py --workload cfg5 --steps 10 --warmup 2 --no-cpu-baseline ;;
     hnsw) run hnsw_bench 900 python scripts/hnsw_bench.py ;;
     *) echo "unknown step $s" >> gpurun_out/steps.log; exit 2 ;;
   esac
