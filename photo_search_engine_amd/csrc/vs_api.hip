@@ -982,7 +982,9 @@ vs_pending* vs::search_phase_a(vs_index* ix, const float* q_dev, int64_t nq, int
     p->k = k;
     p->id_offset = id_offset;
     if (!two_phase_ok(ix, nq, k)) throw VsError(VS_ERR_ARG, "two-phase search: not applicable (vs_two_phase_ok)");
-    p->two = i8_allowed(ix);  // (routed to the native screen: phase A runs the whole search)
+    // (routed to the native screen, or group-residual codes on a shard too small for their seeded
+    // direct pass: phase A runs the whole search -- a per-rank choice, the exchanges are the same)
+    p->two = i8_allowed(ix) && use_i8(ix, (int)nq, k);
     c->cert.ensure((size_t)nq * sizeof(int));
     if (p->two) {
         // phase A's depth: twice a shard's expected share of the global top-k (+32), so the shards'

@@ -191,3 +191,29 @@ def test_int8_two_phase_concurrent_searches(Multi):
         np.testing.assert_array_equal(I, Ie)
         np.testing.assert_array_equal(D, S.astype(np.float32))
     ix.close()
+
+
+def test_int8_two_phase_group_residual_small_shards(Multi):
+    # cluster-sorted rows: every shard's int8 copy is coded against its group means, and each shard
+    # (100k rows: under 4 tiles per workgroup) is too small for the seeded direct pass those codes
+    # need -- phase A must run the native search on such a shard instead of the int8 one (a
+    # per-shard choice: the exchanges stay the same), and the answer stays exact
+    N, d, C, k = 300_000, 512, 32, 20
+    c = O.synth_rows(O.SEED_CORPUS + 900, 0, C, d, True)
+    g = O.synth_rows(O.SEED_CORPUS + 91, 0, N, d, True)
+    cid = np.sort(np.random.default_rng(91).integers(0, C, N))
+    x = c[cid] + np.float32(0.3) * g
+    x = (x / np.linalg.norm(x, axis=1, keepdims=True)).astype(np.float32)
+    qc = np.random.default_rng(92).integers(0, C, 64)
+    q = c[qc] + np.float32(0.3) * O.synth_rows(O.SEED_QUERIES + 91, 0, 64, d, True)
+    q = (q / np.linalg.norm(q, axis=1, keepdims=True)).astype(np.float32)
+    ix = Multi(d, "ip", "bf16", devices=[0, 0, 0])
+    ix.add(x)
+    ix.set_screen("int8")
+    xs = ix.reconstruct_n(0, N)
+    S, Ie = O.knn_exact(xs, q, k, "ip")
+    for _ in range(2):
+        D, I = ix.search(q, k)
+        np.testing.assert_array_equal(I, Ie)
+        np.testing.assert_array_equal(D, S.astype(np.float32))
+    ix.close()
