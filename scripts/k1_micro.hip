@@ -124,7 +124,7 @@ __global__ void __launch_bounds__(THREADS, 2)
                 if constexpr (MODE != 5) barrier_lgkm();
                 if constexpr (MODE != 6) ISSUE_STEP(s + P, (u + P) % U);
                 const uint8_t* slot = smem + (s % U) * KB + lane_off;
-                if constexpr (MODE == 10 || MODE == 11) {
+                if constexpr (MODE == 10 || MODE == 11 || MODE == 12) {
                     // compiler-scheduled MFMAs over the same bytes: 10 = 32x32x32 (16 per K-step, half
                     // the operand reads per MAC), 11 = 16x16x64 (32 per K-step); the operand mapping
                     // is not the product's (timing only)
@@ -137,11 +137,17 @@ __global__ void __launch_bounds__(THREADS, 2)
 #pragma unroll
                             for (int n = 0; n < 8; ++n)
                                 acc32[n] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[u][h], b[8 * h + n], acc32[n], 0, 0, 0);
-                    } else {
+                    } else if constexpr (MODE == 11) {  // corpus fragment held for 16 MFMAs in a row
 #pragma unroll
                         for (int m = 0; m < 2; ++m)
 #pragma unroll
                             for (int n = 0; n < 16; ++n)
+                                acc[m][n] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[u][m], b[n], acc[m][n], 0, 0, 0);
+                    } else {  // 12: MFMA pairs per query fragment (the product's order)
+#pragma unroll
+                        for (int n = 0; n < 16; ++n)
+#pragma unroll
+                            for (int m = 0; m < 2; ++m)
                                 acc[m][n] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[u][m], b[n], acc[m][n], 0, 0, 0);
                     }
                 } else if constexpr (MODE == 2 || MODE >= 5 || MODE == 3 || MODE == 4) {
@@ -396,5 +402,6 @@ int main(int argc, char** argv) {
     run(k_micro<2>, "full (MFMA)", 2);
     run(k_micro<10>, "MFMA 32x32x32 (builtins)", 20);
     run(k_micro<11>, "MFMA 16x16x64 (builtins)", 21);
+    run(k_micro<12>, "MFMA 16x16x64 pairs (builtins)", 22);
     return 0;
 }

@@ -30,7 +30,7 @@ for s in ${STEPS:-tests cfg3 shard8 mix03 micro multi}; do
     mix03) run bench_mix03 600 python bench.py --data mixture-sorted --sigma 0.3 --warmup 8 --no-cpu-baseline ;;
     mix05) run bench_mix05 600 python bench.py --data mixture-sorted --sigma 0.5 --warmup 8 --no-cpu-baseline ;;
     mix10) run bench_mix10 600 python bench.py --data mixture-sorted --sigma 1.0 --warmup 8 --no-cpu-baseline ;;
-    micro32) for m in 20 21 9; do for dt in 1 2; do
+    micro32) for m in 21 22 9; do for dt in 1 2; do
              timeout -k 10 120 ./abtmp/k1_micro 10000000 1536 20 $dt $m >> gpurun_out/k1_micro32.txt 2>&1
              rc=$?; if [ $rc -ne 0 ]; then echo "step micro32 rc=$rc" >> gpurun_out/steps.log; exit $rc; fi
            done; done; echo "step micro32 rc=0" >> gpurun_out/steps.log ;;
