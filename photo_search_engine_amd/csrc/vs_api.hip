@@ -567,7 +567,9 @@ void search_block_i8(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float
         if (keep) *keep = r;
         return;
     }
-    HIP_CHECK(launch_refine_wide(r, nqb, (int)round_up(2 * k + 32, 32), st));
+    // (phase-A depths just under a power of two: the phase-A selection may stop anywhere up to
+    // that power -- rfw_ka_hi -- instead of bisecting to an exact count)
+    HIP_CHECK(launch_refine_wide(r, nqb, (int)round_up(2 * k + 24, 8), st));
 }
 
 // Enqueue one query block through screen -> merge -> refine.  q: device fp32 [nqb][d].
@@ -811,7 +813,7 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
     // certificate needs a gap of 2 margins between the k-th and the Kp-th best
     if (wide) {
         const int ka = redo ? screen_depth(k) : Kp;  // (a fallback round's Kp is the listing depth)
-        HIP_CHECK(launch_refine_wide(r, nqb, (int)round_up(std::max(ka, k + 32), 32), st));
+        HIP_CHECK(launch_refine_wide(r, nqb, (int)round_up(std::max(ka - 8, k + 24), 8), st));
         if (!redo) health_note(ix, c, st, 2, nqb);
         return;
     }
@@ -987,10 +989,10 @@ vs_pending* vs::search_phase_a(vs_index* ix, const float* q_dev, int64_t nq, int
     p->two = i8_allowed(ix) && use_i8(ix, (int)nq, k);
     c->cert.ensure((size_t)nq * sizeof(int));
     if (p->two) {
-        // phase A's depth: twice a shard's expected share of the global top-k (+32), so the shards'
+        // phase A's depth: twice a shard's expected share of the global top-k (+24), so the shards'
         // lists together hold the global k-th best of what they scored
         const int share = (k + world - 1) / world;
-        p->ka = (int)std::min<int64_t>(round_up(2 * k + 32, 32), round_up(2 * share + 32, 32));
+        p->ka = (int)std::min<int64_t>(round_up(2 * k + 24, 8), round_up(2 * share + 24, 8));
         search_block_i8(ix, c, q_dev, (int)nq, k, nullptr, I_a, S_a, c->cert.as<int>(), id_offset, st, 1, p->ka,
                         &p->r, stride);
     } else {

@@ -50,8 +50,14 @@ inline int64_t tile_bytes(int dpad, int dt) { return (int64_t)TR * dpad * es_of(
 inline int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
 
 constexpr int RFW_CAP = 8192;  // k_refine_wide: rows scored per query (fp64 score + id in LDS)
-// k_refine_wide's phase A takes between KA and this many keys (the two-phase state holds as many)
-__host__ __device__ inline int rfw_ka_hi(int KA) { return KA + KA / 2 <= RFW_CAP / 2 ? KA + KA / 2 : (KA > RFW_CAP / 2 ? KA : RFW_CAP / 2); }
+// k_refine_wide's phase A takes between KA and this many keys (the two-phase state holds as many):
+// up to 1.5 KA, within KA's power of two (the phase-A sort's size stays what KA alone gives)
+__host__ __device__ inline int rfw_ka_hi(int KA) {
+    int p2 = 1;
+    while (p2 < KA) p2 <<= 1;
+    const int hi = KA + KA / 2 < p2 ? KA + KA / 2 : p2;
+    return hi > KA ? hi : KA;
+}
 
 // screening depth: k plus a margin that certifies exactness for all but pathological inputs
 inline int screen_depth(int k) {

@@ -169,6 +169,14 @@ __device__ __forceinline__ u64 wave_min_u64(u64 v) {
     }
     return v;
 }
+__device__ __forceinline__ u64 wave_max_u64(u64 v) {
+#pragma unroll
+    for (int s = 32; s > 0; s >>= 1) {
+        u64 o = __shfl_xor(v, s, 64);
+        v = o > v ? o : v;
+    }
+    return v;
+}
 __device__ __forceinline__ int lane_prefix(u64 mask) {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
@@ -200,8 +208,35 @@ __device__ __forceinline__ u64 wave_kth(const u64 (&keys)[E], int K) {
 template <int E>
 __device__ __forceinline__ u64 block_kth_range(const u64 (&keys)[E], int Klo, int Khi, int* red) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    // the bits every non-empty key shares (the scores' common exponent and leading mantissa) are
+    // the threshold's prefix: the bisection starts below them
+    __shared__ u64 mm[2 * 16];
+    u64 kmax = 0ull, kmin = ~0ull;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        kmax = keys[e] > kmax ? keys[e] : kmax;
+        kmin = (keys[e] != 0ull && keys[e] < kmin) ? keys[e] : kmin;
+    }
+    kmax = wave_max_u64(kmax);
+    kmin = wave_min_u64(kmin);
+    if (lane == 0) {
+        mm[w] = kmax;
+        mm[16 + w] = kmin;
+    }
+    __syncthreads();
+    kmax = 0ull;
+    kmin = ~0ull;
+    for (int i = 0; i < nw; ++i) {
+        kmax = mm[i] > kmax ? mm[i] : kmax;
+        kmin = mm[16 + i] < kmin ? mm[16 + i] : kmin;
+    }
     u64 t = 0;
-    for (int b = 63, par = 0; b >= 0; --b, par ^= 1) {
+    int bstart = 63;
+    if (kmin != ~0ull && kmax != kmin) {
+        bstart = 63 - __clzll((long long)(kmax ^ kmin));
+        t = kmax & ~((2ull << bstart) - 1ull);  // (bstart <= 62: 2 << bstart does not overflow)
+    }
+    for (int b = bstart, par = 0; b >= 0; --b, par ^= 1) {
         const u64 cand = t | (1ull << b);
         int c = 0;
 #pragma unroll
@@ -2628,6 +2663,73 @@ __device__ __forceinline__ bool better_exact(double sa, uint32_t ia, double sb, 
     return ia < ib;
 }
 
+// Bitonic sort of (sc, ids)[0, n2) best first (n2 a power of two, padding = worst), the whole
+// block taking part.  n2 <= blockDim.x: thread i keeps element i in registers; partners inside a
+// wave (stride < 64) are exchanged by shuffles, wider ones through LDS (one barrier each way) --
+// 3 barrier pairs for 256 elements instead of 36 barriers.  Larger n2: the LDS network.
+template <int METRIC>
+__device__ __forceinline__ void sort_best_first(double* sc, uint32_t* ids, int n2) {
+    const int tid = threadIdx.x;
+    if (n2 <= (int)blockDim.x) {
+        const bool act = tid < n2;
+        double s = act ? sc[tid] : 0.0;
+        uint32_t id = act ? ids[tid] : 0u;
+        for (int size = 2; size <= n2; size <<= 1) {
+            for (int stride = size >> 1; stride > 0; stride >>= 1) {
+                double ps;
+                uint32_t pid;
+                if (stride >= 64) {
+                    __syncthreads();  // (every thread's previous read of its partner is done)
+                    if (act) {
+                        sc[tid] = s;
+                        ids[tid] = id;
+                    }
+                    __syncthreads();
+                    ps = act ? sc[tid ^ stride] : 0.0;
+                    pid = act ? ids[tid ^ stride] : 0u;
+                } else {
+                    ps = __shfl_xor(s, stride, 64);
+                    pid = (uint32_t)__shfl_xor((int)id, stride, 64);
+                }
+                if (act) {
+                    const bool up = (tid & size) == 0, lower = (tid & stride) == 0;
+                    const bool pb = better_exact(ps, pid, s, id, METRIC);
+                    if (lower == up ? pb : !pb) {
+                        s = ps;
+                        id = pid;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        if (act) {
+            sc[tid] = s;
+            ids[tid] = id;
+        }
+        __syncthreads();
+        return;
+    }
+    for (int size = 2; size <= n2; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int i = tid; i < n2; i += blockDim.x) {
+                const int j = i ^ stride;
+                if (j > i) {
+                    const bool up = (i & size) == 0;
+                    const double si = sc[i], sj = sc[j];
+                    const uint32_t ii = ids[i], ij = ids[j];
+                    const bool jb = better_exact(sj, ij, si, ii, METRIC);
+                    if (up ? jb : !jb) {
+                        sc[i] = sj; sc[j] = si;
+                        ids[i] = ij; ids[j] = ii;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+
 // Exact canonical fp64 scores of R stored rows at once (row[i] < 0: absent), query staged in LDS as
 // fp64 (QLDS) or read from global fp32.  Lane l owns 8-element groups g = l, l+64, ... in ascending
 // order and accumulates them sequentially, then an xor-butterfly 32..1 -- the expression tree of the
@@ -2850,25 +2952,7 @@ __device__ __forceinline__ void refine(const RefineArgs& a, int KP2) {
         ids[j] = 0xFFFFFFFFu;
     }
     __syncthreads();
-    // bitonic sort, best first
-    for (int size = 2; size <= KP2; size <<= 1) {
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int i = tid; i < KP2; i += RF_THREADS) {
-                const int j = i ^ stride;
-                if (j > i) {
-                    const bool up = (i & size) == 0;
-                    const double si = sc[i], sj = sc[j];
-                    const uint32_t ii = ids[i], ij = ids[j];
-                    const bool jb = better_exact(sj, ij, si, ii, METRIC);
-                    if (up ? jb : !jb) {
-                        sc[i] = sj; sc[j] = si;
-                        ids[i] = ij; ids[j] = ii;
-                    }
-                }
-            }
-            __syncthreads();
-        }
-    }
+    sort_best_first<METRIC>(sc, ids, KP2);  // best first
     // exactness certificate: every non-candidate row has exact transformed score <= smin + eps
     if (tid == 0) {
         // rows outside the candidate set scored at most: the Kp-th best listed key (when the list
@@ -2996,26 +3080,8 @@ __device__ __forceinline__ void rfw_score(const RefineArgs& a, const uint32_t* i
 
 // bitonic sort of (sc, ids)[0, n2) best first (n2 a power of two, padding = worst)
 __device__ __forceinline__ void rfw_sort(double* sc, uint32_t* ids, int n2) {
-    for (int size = 2; size <= n2; size <<= 1) {
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int i = threadIdx.x; i < n2; i += blockDim.x) {
-                const int j = i ^ stride;
-                if (j > i) {
-                    const bool up = (i & size) == 0;
-                    const double si = sc[i], sj = sc[j];
-                    const uint32_t ii = ids[i], ij = ids[j];
-                    const bool jb = better_exact(sj, ij, si, ii, METRIC_IP);
-                    if (up ? jb : !jb) {
-                        sc[i] = sj; sc[j] = si;
-                        ids[i] = ij; ids[j] = ii;
-                    }
-                }
-            }
-            __syncthreads();
-        }
-    }
+    sort_best_first<METRIC_IP>(sc, ids, n2);
 }
-
 template <int DT, int METRIC, bool QLDS>
 __global__ void __launch_bounds__(RF_THREADS) k_refine_wide(RefineArgs a, int KA) {
     constexpr bool L2 = METRIC == METRIC_L2;

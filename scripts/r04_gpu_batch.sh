@@ -56,6 +56,7 @@ for s in ${STEPS:-tests cfg3 shard8 mix03 micro multi}; do
     product) run product_native 300 python scripts/product_latency.py && run product_int8 300 python scripts/product_latency.py --screen int8 ;;
     cfg4) run bench_cfg4 1100 python bench.py --workload cfg4 --steps 10 --warmup 3 --no-cpu-baseline ;;
     cfg5) run bench_cfg5 900 python bench.py --workload cfg5 --steps 10 --warmup 2 --no-cpu-baseline ;;
+    stamps) run stamps_1250k 300 python scripts/refine_stamps.py --run --rows 1250000 && run stamps_10m 300 python scripts/refine_stamps.py --run --rows 10000000 ;;
     hnsw) run hnsw_bench 900 python scripts/hnsw_bench.py ;;
     *) echo "unknown step $s" >> gpurun_out/steps.log; exit 2 ;;
   esac
