@@ -641,8 +641,11 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
         a.cap = (int)round_up(Kp + 2 * TR, 256);
         const int sdt = gemv_i8 ? DT_I8 : ix->dtype;
         const int dpadq = gemv_i8 ? ix->dpad8 : ix->dpad;
-        // work-queue tiles over exactly the resident blocks
-        a.G = (int)std::min<int64_t>(tiles, (int64_t)ix->num_cu * (gemv_dyn() ? gemv_blocks_per_cu(sdt, QB) : 8));
+        // work-queue tiles over exactly the resident blocks; a corpus of at most num_cu / 2 tiles
+        // (cfg1: 40) would leave most CUs idle: its work items are quarter tiles (GEMV_SPLIT)
+        const int64_t resident = (int64_t)ix->num_cu * (gemv_dyn() ? gemv_blocks_per_cu(sdt, QB) : 8);
+        a.gemv_split = tiles <= ix->num_cu / 2 ? GEMV_SPLIT : 1;
+        a.G = (int)std::min<int64_t>(tiles * a.gemv_split, resident);
         c->qpad.ensure((size_t)QB * dpadq * sizeof(float));
         int* ctr = nullptr;
         if (gemv_dyn()) {  // the work-queue counter is zeroed by the query pack (no separate memset)
@@ -759,11 +762,12 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
         r.cand_n = a.gcnt;
         r.lcap = a.lcap;
     } else {  // GEMV: merge the per-block lists down to [q][Kp] (qstride nqb, or part[0] with QB)
-        // one query (the product's call shape): stop the merge tree at <= 2048 keys, which the
-        // refine's one-wave selection takes directly (saves the last k_merge launch).  Needs >= Kp
-        // non-empty keys among them, which every round keeps when the shard has >= Kp rows.
+        // one query (the product's call shape): stop the merge tree at <= kRefineRegKeys keys,
+        // which the refine selects from in registers (one wave up to 2048; a k_merge launch costs
+        // more than the block-wide selection above that).  Needs >= Kp non-empty keys among them,
+        // which every round keeps when the shard has >= Kp rows.
         int nseg = a.G;
-        const int stop = (nqb == 1 && ix->ntotal >= Kp) ? kRefineOneWaveKeys : 0;
+        const int stop = (nqb == 1 && ix->ntotal >= Kp) ? kRefineRegKeys : 0;
         r.cand = merge_all(a.part, nseg, QB, stop);
         r.cand_n = nullptr;
         r.lcap = nseg * Kp;

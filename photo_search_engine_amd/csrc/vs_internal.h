@@ -36,6 +36,7 @@ constexpr int MFMA_KP_MAX = 512;  // per-(workgroup, query) screening depth of t
                                   // workgroup and certify against the workgroups' drop bounds
 static_assert(MFMA_KP_MAX + TR <= MFMA_CAP, "MFMA screen: compaction invariant cnt <= cap - TR");
 constexpr int GEMV_NQ_MAX = 8; // queries per GEMV screen launch
+constexpr int GEMV_SPLIT = 4;   // row blocks per tile of the GEMV screen's small-corpus work items
 constexpr int KP_MAX = 4096;   // largest screening depth (k <= 3276; k_refine sorts 4096 keys in LDS)
 constexpr int SELECT_E = 16;   // keys per thread in block selection (256 threads -> 4096 keys)
 
@@ -212,6 +213,8 @@ struct ScreenArgs {
     const int* wg_desc;      // mapped screen: per workgroup MAP_DESC ints {tile_map offset of its
                              // first tile, tiles, logical index of the first tile in its list
                              // segment, rows of that segment, query tile index, qmap offset, queries}
+    int gemv_split;          // GEMV screen: 1 (or 0) = work items of whole tiles, GEMV_SPLIT = of
+                             // 256 / GEMV_SPLIT rows (small corpora: more CUs)
     const float* gT;         // int8 group residuals: [group][QB] <mu_g, q> added to every key of the
                              // group's rows (the seed pass and k_screen_i8d_res), or null
 };
@@ -268,6 +271,7 @@ hipError_t launch_merge(const u64* in, int nseg, int qstride, int nq, int Kp, u6
                         hipStream_t st);
 
 constexpr int kRefineOneWaveKeys = 2048;  // = 64 * RF_WE: lists one wave of k_refine selects from
+constexpr int kRefineRegKeys = 16384;     // = RF_THREADS * RF_E: lists k_refine selects from in registers
 struct RefineArgs {
     const u64* cand;       // [nq][lcap] candidate keys: the first cand_n[q] (or, if cand_n is null,
     const int* cand_n;     //  all lcap, zero = empty) of each row; the refine keeps the best Kp

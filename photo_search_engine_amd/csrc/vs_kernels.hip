@@ -2121,7 +2121,9 @@ __global__ void __launch_bounds__(512, 2) k_screen_mfma_mapped(ScreenArgs a, con
 // wave-instruction is a contiguous 1 KiB piece.  int8: the fp32 dot of the codes with the fp32 query (no query
 // quantisation), key = s_x * dot + beta_x * ||q|| (an upper bound of the true score up to fp32
 // rounding, certified in k_refine).
-template <int DT, int NQ>
+// SPLIT: work items of 256 / SPLIT rows (a tile in SPLIT row blocks, each wave 64 / SPLIT rows of
+// it): corpora of fewer tiles than resident blocks reach more CUs (cfg1: 40 tiles)
+template <int DT, int NQ, int SPLIT = 1>
 __global__ void __launch_bounds__(256) k_screen_gemv(ScreenArgs a, const float* __restrict__ qp, int nqb) {
     constexpr bool I8 = DT == DT_I8;
     constexpr int ES = DT == DT_F32 ? 4 : I8 ? 1 : 2;
@@ -2130,7 +2132,8 @@ __global__ void __launch_bounds__(256) k_screen_gemv(ScreenArgs a, const float* 
     constexpr int LPR = CB / 16;
     constexpr int RPI = 64 / LPR;
     constexpr int EPU = 16 / ES;
-    constexpr int RG = 64 / RPI;
+    constexpr int RG = 64 / RPI / SPLIT;  // row groups per wave and item
+    static_assert(RG >= 1 && 64 % (RPI * SPLIT) == 0, "split");
     constexpr int RB0 = (NQ <= 2) ? 8 : 4;  // rows per pass (register budget)
     constexpr int RB = RB0 < RG ? RB0 : RG;
     static_assert(RG % RB == 0, "row groups");
@@ -2144,8 +2147,9 @@ __global__ void __launch_bounds__(256) k_screen_gemv(ScreenArgs a, const float* 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int unit = lane % LPR, rsub = lane / LPR;
     const int blk = blockIdx.x;
-    const int t0 = (int)((int64_t)a.tiles * blk / a.G);
-    const int t1 = (int)((int64_t)a.tiles * (blk + 1) / a.G);
+    const int items = a.tiles * SPLIT;
+    const int t0 = (int)((int64_t)items * blk / a.G);
+    const int t1 = (int)((int64_t)items * (blk + 1) / a.G);
     if (tid < NQ) {
         const bool real = tid < nqb;
         thr_key[tid] = real ? 0ull : ~0ull;
@@ -2162,17 +2166,19 @@ __global__ void __launch_bounds__(256) k_screen_gemv(ScreenArgs a, const float* 
     // tiles: a static contiguous range, or (next_tile) one at a time from a work queue with a grid
     // of exactly the resident blocks, so no second partial round of blocks idles the HBM stream
     for (int it = 0;; ++it) {
-        int ti;
+        int item;
         if (a.next_tile) {
             if (tid == 0) tile_s = atomicAdd(a.next_tile, 1);
             __syncthreads();
-            ti = tile_s;
-            __syncthreads();  // every thread has its tile before tile_s is reused
-            if (ti >= a.tiles) break;  // block-uniform
+            item = tile_s;
+            __syncthreads();  // every thread has its item before tile_s is reused
+            if (item >= items) break;  // block-uniform
         } else {
-            ti = t0 + it;
-            if (ti >= t1) break;
+            item = t0 + it;
+            if (item >= t1) break;
         }
+        const int ti = item / SPLIT;
+        const int wrow = (item % SPLIT) * (TR / SPLIT) + wid * (64 / SPLIT);  // the wave's first row
         const uint8_t* tb = a.corpus + (int64_t)ti * tbytes;
         const int64_t rowbase = (int64_t)ti * TR;
         for (int gb = 0; gb < RG / RB; ++gb) {
@@ -2200,7 +2206,7 @@ __global__ void __launch_bounds__(256) k_screen_gemv(ScreenArgs a, const float* 
                 uint4 raw[RB];
 #pragma unroll
                 for (int r = 0; r < RB; ++r) {
-                    const int rit = wid * 64 + (gb * RB + r) * RPI + rsub;
+                    const int rit = wrow + (gb * RB + r) * RPI + rsub;
                     // non-temporal: 1.04 -> 0.96-0.98 ms at cfg2 (74% -> 79-80% of HBM peak)
                     raw[r] = ld_nt16(tb + (int64_t)c * TR * CB + rit * CB + unit * 16);
                 }
@@ -2234,7 +2240,7 @@ __global__ void __launch_bounds__(256) k_screen_gemv(ScreenArgs a, const float* 
             if (unit == 0) {
 #pragma unroll
                 for (int r = 0; r < RB; ++r) {
-                    const int rit = wid * 64 + (gb * RB + r) * RPI + rsub;
+                    const int rit = wrow + (gb * RB + r) * RPI + rsub;
                     const int64_t gr = rowbase + rit;
                     if (gr >= a.n_valid) continue;
                     float sq = 0.0f, rbeta = 0.0f;
@@ -2817,6 +2823,7 @@ constexpr int RF_THREADS = 1024;  // 16 waves per query: Kp / 16 candidates per 
 constexpr int RF_E = 16;          // candidate keys per thread held in registers for the selection
 constexpr int RF_WE = 32;         // lists up to 64 * RF_WE keys: threshold found by one wave
 static_assert(64 * RF_WE == kRefineOneWaveKeys, "one-wave selection size");
+static_assert(RF_THREADS * RF_E == kRefineRegKeys, "register selection size");
 
 template <int DT, int METRIC, bool QLDS>
 __device__ __forceinline__ void refine(const RefineArgs& a, int KP2) {
@@ -3812,17 +3819,23 @@ int gemv_blocks_per_cu(int dt, int nqpad) {
     return v;
 }
 
+template <int DT, int SPLIT>
+static void launch_gemv_split(const ScreenArgs& a, const float* qp, int nqb, int nqpad, hipStream_t st) {
+    switch (nqpad) {
+        case 1: hipLaunchKernelGGL((k_screen_gemv<DT, 1, SPLIT>), dim3(a.G), dim3(256), 0, st, a, qp, nqb); break;
+        case 2: hipLaunchKernelGGL((k_screen_gemv<DT, 2, SPLIT>), dim3(a.G), dim3(256), 0, st, a, qp, nqb); break;
+        case 4: hipLaunchKernelGGL((k_screen_gemv<DT, 4, SPLIT>), dim3(a.G), dim3(256), 0, st, a, qp, nqb); break;
+        default: hipLaunchKernelGGL((k_screen_gemv<DT, 8, SPLIT>), dim3(a.G), dim3(256), 0, st, a, qp, nqb); break;
+    }
+}
 template <int DT>
 static void launch_gemv_dt(const ScreenArgs& a, const float* qp, int nqb, int nqpad, hipStream_t st) {
-    switch (nqpad) {
-        case 1: hipLaunchKernelGGL((k_screen_gemv<DT, 1>), dim3(a.G), dim3(256), 0, st, a, qp, nqb); break;
-        case 2: hipLaunchKernelGGL((k_screen_gemv<DT, 2>), dim3(a.G), dim3(256), 0, st, a, qp, nqb); break;
-        case 4: hipLaunchKernelGGL((k_screen_gemv<DT, 4>), dim3(a.G), dim3(256), 0, st, a, qp, nqb); break;
-        default: hipLaunchKernelGGL((k_screen_gemv<DT, 8>), dim3(a.G), dim3(256), 0, st, a, qp, nqb); break;
-    }
+    if (a.gemv_split == GEMV_SPLIT) launch_gemv_split<DT, GEMV_SPLIT>(a, qp, nqb, nqpad, st);
+    else launch_gemv_split<DT, 1>(a, qp, nqb, nqpad, st);
 }
 hipError_t launch_screen_gemv(int dt, const ScreenArgs& a, const float* qp, int nqb, int nqpad, hipStream_t st) {
     if (dt == DT_I8 && (!a.rsb || !a.qinfo || (a.metric == METRIC_L2 && !a.sqn))) return hipErrorInvalidValue;
+    if (a.gemv_split != 0 && a.gemv_split != 1 && a.gemv_split != GEMV_SPLIT) return hipErrorInvalidValue;
     if (dt == DT_F32) launch_gemv_dt<DT_F32>(a, qp, nqb, nqpad, st);
     else if (dt == DT_BF16) launch_gemv_dt<DT_BF16>(a, qp, nqb, nqpad, st);
     else if (dt == DT_I8) launch_gemv_dt<DT_I8>(a, qp, nqb, nqpad, st);

@@ -57,6 +57,9 @@ for s in ${STEPS:-tests cfg3 shard8 mix03 micro multi}; do
     cfg4) run bench_cfg4 1100 python bench.py --workload cfg4 --steps 10 --warmup 3 --no-cpu-baseline ;;
     cfg5) run bench_cfg5 900 python bench.py --workload cfg5 --steps 10 --warmup 2 --no-cpu-baseline ;;
     stamps) run stamps_1250k 300 python scripts/refine_stamps.py --run --rows 1250000 && run stamps_10m 300 python scripts/refine_stamps.py --run --rows 10000000 ;;
+    trace1) mkdir -p gpurun_out/trace1 && run trace1 300 rocprofv3 --kernel-trace --memory-copy-trace -d gpurun_out/trace1 -o t --output-format csv -- python bench.py --workload cfg1 --steps 200 --warmup 20 && \
+      python scripts/trace_tail.py $(ls gpurun_out/trace1/*/t_kernel_trace.csv gpurun_out/trace1/t_kernel_trace.csv 2>/dev/null | head -1) 40 "vs::|copyBuffer|Kernel" > gpurun_out/trace1_tail.txt && \
+      cp $(ls gpurun_out/trace1/*/t_memory_copy_trace.csv gpurun_out/trace1/t_memory_copy_trace.csv 2>/dev/null | head -1) gpurun_out/trace1_memcpy.csv; rm -rf gpurun_out/trace1 ;;
     hnsw) run hnsw_bench 900 python scripts/hnsw_bench.py ;;
     *) echo "unknown step $s" >> gpurun_out/steps.log; exit 2 ;;
   esac
