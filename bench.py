@@ -294,11 +294,11 @@ def main():
                "hbm_frac": round(bytes_n / (kn * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                "uncertified_first_pass": unc_n}
     elapsed, kms, kind, uncert, t_switch = timed(screen)
-    unresolved = ix.unresolved_count()  # queries the device fallback could not certify (must be 0)
+    full_scan = ix.full_scan_count()  # queries no bounded screen certified (answered by the full scan)
     if G > 1:
-        t = torch.tensor([unresolved], dtype=torch.int64, device=dev)
+        t = torch.tensor([full_scan], dtype=torch.int64, device=dev)
         dist.all_reduce(t)
-        unresolved = int(t.item())
+        full_scan = int(t.item())
     if alt is not None:  # both screens return the same exact answer
         if sh.floor_override is not None:
             # --shard-of: the two-phase rank returns its share of the GLOBAL top-k exactly (entries at
@@ -382,7 +382,7 @@ def main():
             },
             # first-pass certificate failures; every one was re-searched exactly (search_device_exact)
             "uncertified_first_pass": uncert,
-            "unresolved": unresolved,
+            "full_scan": full_scan,
             # group residuals, margins and the screen-health state after the timed steps (vs_screen_state)
             "screen_state": ix.screen_state(),
             "build_s": round(t_build, 2),

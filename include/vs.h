@@ -48,7 +48,8 @@ enum {
     VS_ERR_ARG = -1,          /* bad argument (dims, k, null pointer) */
     VS_ERR_DEVICE = -2,       /* no HIP device / HIP runtime failure */
     VS_ERR_OOM = -3,          /* device allocation failed */
-    VS_ERR_UNCERTIFIED = -4,  /* exactness certificate could not be established */
+    VS_ERR_UNCERTIFIED = -4,  /* exactness certificate could not be established (IVF list search
+                               * only: every flat search ends in the exact full scan instead) */
     VS_ERR_INTERNAL = -5
 };
 
@@ -74,7 +75,9 @@ int64_t vs_capacity(const vs_index* index);
 int vs_synthesize(int device, uint64_t seed, int64_t global_row0, int64_t n, int d, int normalize, int dtype,
                   float* out_dev, void* stream);
 
-/* ---- search (index.search, utils/vector_store.py:191) */
+/* ---- search (index.search, utils/vector_store.py:191).  Exact for every query: a failed
+ * certificate re-screens the query 4x deeper, and past the deepest screen (KP_MAX) the exact full
+ * scan answers it (faiss's k lowest ids among any number of tied rows). */
 int vs_search(vs_index* index, const float* q, int64_t nq, int32_t k, float* D, int64_t* I);
 /* All pointers device-resident; enqueued on `stream` (NULL = the legacy default stream, which is
  * torch's default stream: device calls are always ordered with the caller's stream), no host
@@ -87,10 +90,12 @@ int vs_search_device(vs_index* index, const float* q_dev, int64_t nq, int32_t k,
 /* Same outputs, but exact for every query (every dtype): each query block's first pass is
  * followed on the stream by a fallback round at the deepest screen (KP_MAX, proven seed; the MFMA
  * screen of the stored dtype, fp32 included) whose kernels do nothing unless a certificate of that
- * block failed, and which rewrites only the failed queries -- no host sync: the call returns with
- * the work queued.  A query even that round cannot certify (more near-tied rows than KP_MAX: where
- * vs_search returns VS_ERR_UNCERTIFIED) is counted in vs_unresolved_count.  The product's
- * multi-GPU layers (photo_search_engine_amd/distributed.py, vs_multi_search) use this one. */
+ * block failed, and which rewrites only the failed queries; a query even that round cannot certify
+ * (more near-tied rows than KP_MAX, e.g. thousands of identical embeddings) is answered by a gated
+ * exact full scan of the shard (every row scored, a running top-k: faiss's lowest ids among any
+ * number of ties; counted in vs_full_scan_count) -- no host sync: the call returns with the work
+ * queued.  The product's multi-GPU layers (photo_search_engine_amd/distributed.py,
+ * vs_multi_search) use this one. */
 int vs_search_device_exact(vs_index* index, const float* q_dev, int64_t nq, int32_t k, float* D_dev,
                            int64_t* I_dev, double* S64_dev, int64_t id_offset, void* stream);
 
@@ -170,8 +175,9 @@ const char* vs_version(void);
 int vs_set_timing(vs_index* index, int enable);
 int vs_timing_fetch(vs_index* index, float* ms, int cap, int* kernel_kind);
 int64_t vs_uncertified_count(vs_index* index);   /* first-pass certificate failures; synchronises */
-/* queries vs_search_device_exact's device fallback round could not certify (see there); synchronises */
-int64_t vs_unresolved_count(vs_index* index);
+/* queries answered by the exact full scan (no bounded screen could certify them; see
+ * vs_search_device_exact); synchronises */
+int64_t vs_full_scan_count(vs_index* index);
 /* pinned host bytes the index holds for vs_search's query / result staging (all contexts); each
  * context stages at most 8 MiB and loops over query chunks beyond that */
 int64_t vs_host_staging_bytes(vs_index* index);
@@ -283,6 +289,14 @@ void vs_hnsw_destroy(vs_hnsw* graph);
 int vs_hnsw_search(vs_hnsw* graph, const float* q, int64_t nq, int32_t k, int32_t ef_search, float* D,
                    int64_t* I);
 int64_t vs_hnsw_ntotal(const vs_hnsw* graph);
+/* Rewrite m neighbour slots (positions into the create call's neighbour array) and set the entry
+ * point / top level: the batched insertion of faiss IndexHNSWFlat.add (utils/vector_store.py:164)
+ * keeps ONE device graph laid out for the final node count -- nodes not inserted yet have empty
+ * lists and no links to them, so they are unreachable -- and patches in each batch's new lists
+ * and reverse links (photo_search_engine_amd/hnsw.py insert_rows).  Slots and ids are validated
+ * as in vs_hnsw_create. */
+int vs_hnsw_patch(vs_hnsw* graph, int64_t m, const uint64_t* pos, const int32_t* val, int32_t entry_point,
+                  int32_t max_level);
 
 /* HNSW graph build: faiss HNSW::shrink_neighbor_list (the neighbour-selection heuristic
  * IndexHNSWFlat.add applies to a new node's candidates and to a full list receiving a reverse link,

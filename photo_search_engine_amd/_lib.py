@@ -83,7 +83,7 @@ _SIGS = {
     "vs_set_timing": (ctypes.c_int, [_vp, ctypes.c_int]),
     "vs_timing_fetch": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
     "vs_uncertified_count": (_c_i64, [_vp]),
-    "vs_unresolved_count": (_c_i64, [_vp]),
+    "vs_full_scan_count": (_c_i64, [_vp]),
     "vs_host_staging_bytes": (_c_i64, [_vp]),
     "vs_screen_copy_bytes": (_c_i64, [_vp]),
     "vs_screen_state": (ctypes.c_int, [_vp, _vp, ctypes.c_int]),
@@ -130,6 +130,7 @@ _SIGS = {
     "vs_hnsw_destroy": (None, [_vp]),
     "vs_hnsw_search": (ctypes.c_int, [_vp, _vp, _c_i64, ctypes.c_int32, ctypes.c_int32, _vp, _vp]),
     "vs_hnsw_ntotal": (_c_i64, [_vp]),
+    "vs_hnsw_patch": (ctypes.c_int, [_vp, _c_i64, _vp, _vp, ctypes.c_int32, ctypes.c_int32]),
     "vs_hnsw_prune": (ctypes.c_int, [_vp, _c_i64, _vp, _vp, ctypes.c_int32, ctypes.c_int32, _vp]),
 }
 

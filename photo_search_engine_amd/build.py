@@ -11,7 +11,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libvs.so")
-SOURCES = ["vs_api.hip", "vs_hnsw.hip", "vs_io.hip", "vs_ivf.hip", "vs_kernels.hip", "vs_multi.hip"]
+SOURCES = ["vs_api.hip", "vs_fullscan.hip", "vs_hnsw.hip", "vs_io.hip", "vs_ivf.hip", "vs_kernels.hip", "vs_multi.hip"]
 ARCH = os.environ.get("VS_OFFLOAD_ARCH", "gfx950")
 
 

@@ -56,7 +56,9 @@ struct Ctx {
     bool pending = false;
     DevBuf qdev, qtile, qinfo, qpad, cand, part, merge_a, merge_b, outD, outI, outS, cert, thr0, seedmax, gcnt, gT;
     DevBuf qfac, qeps, drop;  // int8 screen: per-query code scale and norm, refine margin, drop bounds
-    DevBuf fails;             // the current query block's certificate-failure count (fallback gate)
+    DevBuf fails;             // the current query block's certificate-failure counts: [0] first pass (the
+                              // fallback round's gate), [1] fallback round (the full scan's gate)
+    DevBuf fsc, fdone;        // full scan: per-workgroup lists of the block's queries, done counters
     DevBuf rsc, rdone;        // split refine: per-query scores + ids of the kept rows, done counters
     DevBuf pa;       // two-phase (sharded) search: the refine's phase-1 state between the launches
     DevBuf rows[2];  // read_rows_host: unpacked fp32 chunks
@@ -66,11 +68,11 @@ struct Ctx {
     PinnedPair pin;  // read_rows_host: pinned landing chunks
     HostBuf hq;      // vs_search: the query batch, staged for the H2D copy
     HostBuf hout;    // vs_search: I (int64), D (fp32) and certificates land here; search_exact_device: certificates
-    unsigned* unres = nullptr;  // this call's unresolved-query counter (device), instead of the index's
+    unsigned* unres = nullptr;  // this call's full-scan counter (device), instead of the index's
     ~Ctx() {
         for (DevBuf* b : {&qdev, &qtile, &qinfo, &qpad, &cand, &part, &merge_a, &merge_b, &outD, &outI, &outS, &cert, &thr0,
                           &gT, &seedmax, &gcnt, &rows[0], &rows[1], &tilectr, &seedacc, &outAll, &qfac, &qeps, &drop, &fails, &rsc, &rdone,
-                          &pa})
+                          &pa, &fsc, &fdone})
             b->release();
         pin.release();
         hq.release();
@@ -92,7 +94,7 @@ struct vs_index {
     float* sqn = nullptr;
     unsigned* d_maxsq = nullptr;
     unsigned* d_uncert = nullptr;
-    unsigned* d_unres = nullptr;  // queries the device fallback round could not certify either
+    unsigned* d_unres = nullptr;  // queries answered by the exact full scan (no bounded screen certified them)
     float maxsq = 0.0f;
     // int8 screen copy (VS_SCREEN_I8): codes in row tiles of 64-element chunks + per-row scale and
     // error norm; d_maxsq[2..3] = max ||x_hat||, max error norm (fp32 bits, certificate margins)
@@ -279,6 +281,11 @@ void ensure_capacity_i8(vs_index* ix) {
 void quantize_rows(vs_index* ix, int64_t r0, int64_t n, hipStream_t st) {
     if (ix->screen != VS_SCREEN_I8 || n <= 0) return;
     if (ix->gmean) {
+        // rows already searchable get new codes, bounds and group means: searches still queued on
+        // other streams (device-API callers return before their kernels run) must finish first, or
+        // one could read a row's new code with the old <mu_g, q> and its key would no longer bound
+        // the score (the exclusive lock only orders host calls; vs_set_screen syncs likewise)
+        if (r0 % I8_GROUP_ROWS != 0) HIP_CHECK(hipDeviceSynchronize());
         const int64_t g0 = r0 / I8_GROUP_ROWS, g1 = (r0 + n + I8_GROUP_ROWS - 1) / I8_GROUP_ROWS;
         HIP_CHECK(launch_group_means(ix->dtype, ix->data, ix->dpad, ix->d, g0, g1 - g0, r0 + n, ix->dpad8, ix->gmean,
                                      ix->d_maxsq + 5, st));
@@ -456,7 +463,7 @@ void search_block_i8(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float
     c->qeps.ensure(sizeof(float) * MFMA_QB);
     c->drop.ensure(sizeof(u64) * MFMA_QB);
     c->gcnt.ensure(sizeof(int) * MFMA_QB);
-    c->fails.ensure(sizeof(int));
+    c->fails.ensure(2 * sizeof(int));
     // threshold seeding: a seed pass + select before the main pass (>= 4 tiles per workgroup).
     // (Round 4 measured the alternative -- each workgroup of the direct main pass screening a sample
     // tile first and the workgroups selecting and adopting the seed among themselves, no extra
@@ -577,7 +584,7 @@ void search_block_i8(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float
 // redo: the device fallback round of the block just searched (MFMA dtypes, unseeded screen): its
 // three launches (pack, screen, refine) are gated on the block's failure count (c->fails) and the
 // refine rewrites only the queries whose certificate failed; a query it cannot certify either
-// counts in d_unres
+// counts in c->fails[1], the gate of the block's full scan (full_scan_block)
 void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, float* D, int64_t* I, double* S64,
                   int* cert, int64_t id_offset, hipStream_t st, int seed_rank, bool redo = false,
                   bool allow_i8 = true, int ostride = 1) {
@@ -590,7 +597,7 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
     // (search_all makes blocks of > GEMV_NQ_MAX queries only where the MFMA screen serves them)
     const bool use_mfma = nqb > GEMV_NQ_MAX || redo;
     const int* gate = redo ? c->fails.as<int>() : nullptr;
-    if (!redo) c->fails.ensure(sizeof(int));
+    if (!redo) c->fails.ensure(2 * sizeof(int));
     // int8 screen, few queries: the GEMV streams the int8 copy (1 B per element) with the fp32
     // query; its keys carry the row error bound, so it screens deeper (first passes only)
     bool gemv_i8 = !use_mfma && seed_rank > 0 && ix->screen == VS_SCREEN_I8 && ix->data8 != nullptr && !ix->i8_res;
@@ -792,8 +799,8 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
     r.I = I;
     r.S64 = S64;
     r.cert = cert;
-    r.uncert = redo ? (c->unres ? c->unres : ix->d_unres) : ix->d_uncert;
-    r.fails = redo ? nullptr : c->fails.as<int>();
+    r.uncert = redo ? nullptr : ix->d_uncert;
+    r.fails = c->fails.as<int>() + (redo ? 1 : 0);  // (a fallback round's failures gate the full scan)
     r.redo = redo ? 1 : 0;
     r.gate = gate;
     r.ostride = ostride;
@@ -828,6 +835,49 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
 // the shard.
 int fallback_depth(const vs_index* ix) { return (int)std::min<int64_t>(KP_MAX, round_up(ix->ntotal, 16)); }
 
+// The last tier: an exact full scan of the shard (vs_fullscan.hip) for the block's queries with
+// cert[q] == 0 -- those no bounded screen could certify (more rows than KP_MAX tied within its
+// margin, e.g. thousands of identical embeddings).  Every row is scored canonically and streamed
+// through a running top-k, so the answer is faiss's (ties to the lowest ids) for any tie count.
+// gate: the fallback round's failure count (c->fails[1]; the launch returns at once while it is
+// 0), or null = run.  Scanned queries count in this call's counter or the index's d_unres.
+constexpr int64_t kFullScanScratch = 32ll << 20;  // per-workgroup lists of one block, at most
+void full_scan_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float* D, int64_t* I, double* S64,
+                     int* cert, int64_t id_offset, hipStream_t st, const int* gate, int ostride = 1) {
+    const int64_t tiles = (ix->ntotal + TR - 1) / TR;
+    const int64_t per_wg = (int64_t)nqb * k * 12;
+    const int G = (int)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(ix->num_cu, tiles),
+                                                               kFullScanScratch / per_wg));
+    c->fsc.ensure(full_scan_scratch_bytes(nqb, G, k));
+    if (c->fdone.bytes < sizeof(unsigned) * MFMA_QB) {  // zeroed once; each query's last workgroup re-zeroes
+        c->fdone.ensure(sizeof(unsigned) * MFMA_QB);
+        HIP_CHECK(hipMemsetAsync(c->fdone.p, 0, c->fdone.bytes, st));
+    }
+    FullScanArgs a{};
+    a.corpus = ix->data;
+    a.d = ix->d;
+    a.dpad = ix->dpad;
+    a.dt = ix->dtype;
+    a.metric = ix->metric;
+    a.n_valid = ix->ntotal;
+    a.q = q;
+    a.nq = nqb;
+    a.k = k;
+    a.cert = cert;
+    a.gate = gate;
+    a.id_offset = id_offset;
+    a.D = D;
+    a.I = I;
+    a.S64 = S64;
+    a.ostride = ostride;
+    a.gsc = c->fsc.as<double>();
+    a.gid = (uint32_t*)(a.gsc + (size_t)nqb * G * k);
+    a.gdone = c->fdone.as<unsigned>();
+    a.count = c->unres ? c->unres : ix->d_unres;
+    a.G = G;
+    HIP_CHECK(launch_full_scan(a, st));
+}
+
 // Full search of nq device queries; outputs device [nq][k].  device_fallback: every block's first
 // pass is followed by its gated fallback round (no host round trip; MFMA dtypes only).
 void search_all(vs_index* ix, Ctx* c, const float* q, int64_t nq, int k, int Kp, float* D, int64_t* I, double* S64,
@@ -847,9 +897,12 @@ void search_all(vs_index* ix, Ctx* c, const float* q, int64_t nq, int k, int Kp,
         else nqb = (int)std::min<int64_t>(rem, GEMV_NQ_MAX);
         search_block(ix, c, q + done * ix->d, nqb, k, Kp, D ? D + done * k : nullptr, I + done * k,
                      S64 ? S64 + done * k : nullptr, cert ? cert + done : nullptr, id_offset, st, seed_rank, false, i8);
-        if (device_fallback)
+        if (device_fallback) {
             search_block(ix, c, q + done * ix->d, nqb, k, std::max(Kp, fallback_depth(ix)), D ? D + done * k : nullptr,
                          I + done * k, S64 ? S64 + done * k : nullptr, cert + done, id_offset, st, 0, true);
+            full_scan_block(ix, c, q + done * ix->d, nqb, k, D ? D + done * k : nullptr, I + done * k,
+                            S64 ? S64 + done * k : nullptr, cert + done, id_offset, st, c->fails.as<int>() + 1);
+        }
         done += nqb;
     }
 }
@@ -858,7 +911,7 @@ void check_index(const vs_index* ix) {
     if (!ix) throw VsError(VS_ERR_ARG, "null index");
 }
 
-// Points a leased Ctx's unresolved-query counter at the caller's device word for one call, and
+// Points a leased Ctx's full-scan counter at the caller's device word for one call, and
 // clears it on every exit (exceptions included), before the Ctx returns to the pool: a later
 // lease must never count into a buffer it does not own.
 struct UnresScope {
@@ -874,9 +927,9 @@ struct UnresScope {
 // exact device search (vs_search_device_exact; the IVF coarse quantizer): like vs_search_device,
 // but certificate failures are re-searched on the device, by each query block's gated fallback
 // round at the deepest screen (KP_MAX, where vs_search's escalation ends; fp32 rows: the fp32 MFMA
-// screen).  async: no host round trip at all, the call returns with the work queued and a query
-// even the fallback cannot certify counts in vs_unresolved_count; otherwise the certificates are
-// read back and such a query raises VS_ERR_UNCERTIFIED, as in vs_search.
+// screen), and a query even that round cannot certify by the gated exact full scan of the shard
+// (full_scan_block; counted in vs_full_scan_count).  async: no host round trip at all, the call
+// returns with the work queued; otherwise the certificates are read back and checked.
 void vs::search_exact_device(vs_index* ix, const float* q_dev, int64_t nq, int k, int64_t* I_dev, double* S64_dev,
                              hipStream_t st, float* D_dev, int64_t id_offset, bool async, unsigned* unres) {
     check_index(ix);
@@ -898,28 +951,23 @@ void vs::search_exact_device(vs_index* ix, const float* q_dev, int64_t nq, int k
     int* cert_h = (int*)c->hout.p;
     HIP_CHECK(hipMemcpyAsync(cert_h, c->cert.p, (size_t)nq * sizeof(int), hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));
-    // a query even the fallback round left uncertified (scores denser than the bf16 query rounding
-    // in the MFMA keys, e.g. a tight cluster): re-screened alone on the GEMV screen, whose fp32
-    // query leaves only the accumulation error in its keys, 4x deeper each round (vs_search's
-    // escalation); its outputs are rewritten in place
+    // (every block's full scan has run behind its fallback round: a query left uncertified here
+    // would be a library error, so it is answered by a full scan of its own rather than trusted)
     for (int64_t qi = 0; qi < nq; ++qi) {
-        int Kr = Kp;
+        if (cert_h[qi]) continue;
         int* cq = c->cert.as<int>() + qi;
-        while (!cert_h[qi]) {
-            if (Kr >= KP_MAX || Kr >= ix->ntotal)
-                throw VsError(VS_ERR_UNCERTIFIED, "exactness certificate failed at maximum screening depth");
-            Kr = (int)std::min<int64_t>(std::min<int64_t>((int64_t)Kr * 4, KP_MAX), round_up(ix->ntotal, 16));
-            search_all(ix, c, q_dev + qi * ix->d, 1, k, Kr, (D_dev ? D_dev : c->outD.as<float>()) + qi * k,
-                       I_dev + qi * k, S64_dev ? S64_dev + qi * k : nullptr, cq, id_offset, st, /*safe seed*/ 0);
-            HIP_CHECK(hipMemcpyAsync(&cert_h[qi], cq, sizeof(int), hipMemcpyDeviceToHost, st));
-            HIP_CHECK(hipStreamSynchronize(st));
-        }
+        HIP_CHECK(hipMemsetAsync(cq, 0, sizeof(int), st));
+        full_scan_block(ix, c, q_dev + qi * ix->d, 1, k, (D_dev ? D_dev : c->outD.as<float>()) + qi * k, I_dev + qi * k,
+                        S64_dev ? S64_dev + qi * k : nullptr, cq, id_offset, st, nullptr);
+        HIP_CHECK(hipMemcpyAsync(&cert_h[qi], cq, sizeof(int), hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+        if (!cert_h[qi]) throw VsError(VS_ERR_INTERNAL, "full scan left a query uncertified");
     }
 }
 
 // S concurrent exact device searches over consecutive parts (whole query blocks) of one batch, each
 // on its own stream with its own leased workspace (leases held together, so no two parts share a
-// workspace and serialise on it); a part's unresolved queries count in unres[part].  The IVF
+// workspace and serialise on it); a part's full-scanned queries count in unres[part] (if given).  The IVF
 // coarse assignment: one 256-row block of a small quantizer fills only nlist / 256 workgroups.
 void vs::search_exact_device_parts(vs_index* ix, const float* q_dev, int64_t nq, int k, int64_t* I_dev,
                                    hipStream_t* streams, int S, unsigned* unres) {
@@ -938,7 +986,7 @@ void vs::search_exact_device_parts(vs_index* ix, const float* q_dev, int64_t nq,
         Ctx* c = leases[i]->c;
         c->outD.ensure((size_t)(q1 - q0) * k * sizeof(float));
         c->cert.ensure((size_t)(q1 - q0) * sizeof(int));
-        UnresScope us(c, unres + i);  // reset even if search_all throws
+        UnresScope us(c, unres ? unres + i : nullptr);  // reset even if search_all throws
         search_all(ix, c, q_dev + q0 * ix->d, q1 - q0, k, Kp, c->outD.as<float>(), I_dev + q0 * k, nullptr,
                    c->cert.as<int>(), 0, streams[i], kOptimisticSeedRank, true);
     }
@@ -1049,6 +1097,9 @@ void vs::search_phase_b(vs_pending* p, const double* floor_S, float* D, int64_t*
     UnresScope us(c, unres);
     search_block(ix, c, p->q, (int)nq, k, std::max(screen_depth(k), fallback_depth(ix)), D, I, S64,
                  c->cert.as<int>(), p->id_offset, st, 0, true, true, stride);
+    // and its gated full scan (the shard's own exact top-k; the floor is not needed for it)
+    full_scan_block(ix, c, p->q, (int)nq, k, D, I, S64, c->cert.as<int>(), p->id_offset, st, c->fails.as<int>() + 1,
+                    stride);
 }
 
 void vs::search_pending_free(vs_pending* p) { delete p; }
@@ -1174,7 +1225,7 @@ int vs_create(int d, int metric, int dtype, int device, vs_index** out) {
         try {
             HIP_CHECK(hipStreamCreateWithFlags(&ix->own, hipStreamNonBlocking));
             // [0] max ||x||^2, [1] uncertified counter, [2..3] int8 screen maxima (fp32 bits),
-            // [4] unresolved counter (device fallback), [5..6] group residuals (max ||mu_g||,
+            // [4] full-scan counter (vs_full_scan_count), [5..6] group residuals (max ||mu_g||,
             // groups with a mean), [7] max ||x - s c|| of the int8 codes
             HIP_CHECK(hipMalloc(&ix->d_maxsq, sizeof(unsigned) * 8));
             HIP_CHECK(hipMemset(ix->d_maxsq, 0, sizeof(unsigned) * 8));
@@ -1427,15 +1478,22 @@ int vs_search(vs_index* ix, const float* q, int64_t nq, int32_t k, float* D, int
             HIP_CHECK(hipMemcpyAsync(c->hout.p, c->outAll.p, obytes, hipMemcpyDeviceToHost, st));
             HIP_CHECK(hipStreamSynchronize(st));
             // exactness certificate failed for some queries (near-ties deeper than the margin):
-            // re-screen those queries one at a time with a 4x deeper candidate set.
+            // re-screen those queries one at a time with a 4x deeper candidate set; past the
+            // deepest screen (more than KP_MAX rows tied within its margin) the exact full scan
             for (int64_t qi = 0; qi < m; ++qi) {
                 int Kr = Kp;
                 while (!cert_h[qi]) {
-                    if (Kr >= KP_MAX || Kr >= ix->ntotal)
-                        throw VsError(VS_ERR_UNCERTIFIED, "exactness certificate failed at maximum screening depth");
-                    Kr = (int)std::min<int64_t>(std::min<int64_t>((int64_t)Kr * 4, KP_MAX), round_up(ix->ntotal, 16));
-                    search_all(ix, c, c->qdev.as<float>() + qi * ix->d, 1, kk, Kr, c->outD.as<float>(),
-                               c->outI.as<int64_t>(), nullptr, c->cert.as<int>(), 0, st, /*safe seed*/ 0);
+                    if (Kr < 0) throw VsError(VS_ERR_INTERNAL, "full scan left a query uncertified");
+                    if (Kr >= KP_MAX || Kr >= ix->ntotal) {
+                        HIP_CHECK(hipMemsetAsync(c->cert.p, 0, sizeof(int), st));
+                        full_scan_block(ix, c, c->qdev.as<float>() + qi * ix->d, 1, kk, c->outD.as<float>(),
+                                        c->outI.as<int64_t>(), nullptr, c->cert.as<int>(), 0, st, nullptr);
+                        Kr = -1;
+                    } else {
+                        Kr = (int)std::min<int64_t>(std::min<int64_t>((int64_t)Kr * 4, KP_MAX), round_up(ix->ntotal, 16));
+                        search_all(ix, c, c->qdev.as<float>() + qi * ix->d, 1, kk, Kr, c->outD.as<float>(),
+                                   c->outI.as<int64_t>(), nullptr, c->cert.as<int>(), 0, st, /*safe seed*/ 0);
+                    }
                     HIP_CHECK(hipMemcpyAsync(Dk + qi * kk, c->outD.p, kk * sizeof(float), hipMemcpyDeviceToHost, st));
                     HIP_CHECK(hipMemcpyAsync(Ik + qi * kk, c->outI.p, kk * sizeof(int64_t), hipMemcpyDeviceToHost, st));
                     HIP_CHECK(hipMemcpyAsync(&cert_h[qi], c->cert.p, sizeof(int), hipMemcpyDeviceToHost, st));
@@ -1586,7 +1644,7 @@ int vs_screen_state(vs_index* ix, double* out, int cap) {
     });
 }
 
-int64_t vs_unresolved_count(vs_index* ix) {
+int64_t vs_full_scan_count(vs_index* ix) {
     int64_t v = -1;
     int rc = guarded([&] {
         check_index(ix);

@@ -26,7 +26,9 @@ struct vs_hnsw {
     int device = 0;
     int64_t n = 0;
     int entry = -1, max_level = -1, nbmax = 1;
-    DevBuf offsets, neighbors, cum, vis, qdev, outD, outI;
+    DevBuf offsets, neighbors, cum, vis, qdev, outD, outI, ppos, pval;
+    std::vector<int32_t> levels_h, cum_h;  // host copies: vs_hnsw_patch validates against them
+    std::vector<uint64_t> offsets_h;
     hipStream_t st = nullptr;
     std::mutex mtx;  // searches on one handle are serialised (shared workspaces)
 };
@@ -82,6 +84,12 @@ std::vector<int32_t> checked_neighbors(int64_t n, const int32_t* levels, const u
     return out;
 }
 
+__global__ void __launch_bounds__(256) k_scatter_i32(int32_t* __restrict__ dst, const uint64_t* __restrict__ pos,
+                                                     const int32_t* __restrict__ val, int64_t m) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < m) dst[pos[i]] = val[i];
+}
+
 }  // namespace
 
 extern "C" {
@@ -106,6 +114,9 @@ int vs_hnsw_create(vs_index* index, int64_t n, const int32_t* levels, const uint
             h->entry = n ? entry_point : -1;
             h->max_level = n ? max_level : -1;
             h->nbmax = nbmax;
+            h->levels_h.assign(levels, levels + n);
+            h->offsets_h.assign(offsets, offsets + (n > 0 ? n + 1 : 0));
+            h->cum_h.assign(cum, cum + n_cum);
             HIP_CHECK(hipStreamCreateWithFlags(&h->st, hipStreamNonBlocking));
             if (n > 0) {
                 h->offsets.ensure((size_t)(n + 1) * 8);
@@ -130,13 +141,55 @@ void vs_hnsw_destroy(vs_hnsw* h) {
     {
         DeviceGuard g(h->device);
         if (h->st) (void)hipStreamSynchronize(h->st);
-        for (DevBuf* b : {&h->offsets, &h->neighbors, &h->cum, &h->vis, &h->qdev, &h->outD, &h->outI}) b->release();
+        for (DevBuf* b : {&h->offsets, &h->neighbors, &h->cum, &h->vis, &h->qdev, &h->outD, &h->outI, &h->ppos, &h->pval})
+            b->release();
         if (h->st) (void)hipStreamDestroy(h->st);
     }
     delete h;
 }
 
 int64_t vs_hnsw_ntotal(const vs_hnsw* h) { return h ? h->n : -1; }
+
+int vs_hnsw_patch(vs_hnsw* h, int64_t m, const uint64_t* pos, const int32_t* val, int32_t entry_point,
+                  int32_t max_level) {
+    return guarded([&] {
+        if (!h || m < 0 || (m > 0 && (!pos || !val))) throw VsError(VS_ERR_ARG, "vs_hnsw_patch: bad arguments");
+        const int64_t n = h->n;
+        if (n == 0) {
+            if (m > 0) fail("an empty graph has no neighbour slots");
+            return;
+        }
+        if (entry_point < 0 || entry_point >= n) fail("entry point out of range");
+        if (max_level != h->levels_h[entry_point] - 1) fail("max_level must be the entry point's top level");
+        const int nlev = (int)h->cum_h.size() - 1;
+        // every slot and id is checked here: the search kernel follows them
+        for (int64_t i = 0; i < m; ++i) {
+            if (pos[i] >= h->offsets_h[n]) fail("patch position out of range");
+            const int64_t node = (int64_t)(std::upper_bound(h->offsets_h.begin(), h->offsets_h.end(), pos[i]) -
+                                           h->offsets_h.begin()) - 1;
+            const uint64_t rel = pos[i] - h->offsets_h[node];
+            int l = 0;
+            while (l + 1 < nlev && rel >= (uint64_t)h->cum_h[l + 1]) ++l;
+            const int32_t v = val[i];
+            if (v < -1 || v >= n) fail("neighbour id out of range");
+            if (v >= 0 && h->levels_h[v] <= l) fail("a neighbour is listed on a level above its own");
+        }
+        std::lock_guard<std::mutex> lk(h->mtx);
+        DeviceGuard g(h->device);
+        if (m > 0) {
+            h->ppos.ensure((size_t)m * 8);
+            h->pval.ensure((size_t)m * 4);
+            HIP_CHECK(hipMemcpyAsync(h->ppos.p, pos, (size_t)m * 8, hipMemcpyHostToDevice, h->st));
+            HIP_CHECK(hipMemcpyAsync(h->pval.p, val, (size_t)m * 4, hipMemcpyHostToDevice, h->st));
+            hipLaunchKernelGGL(k_scatter_i32, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, h->st,
+                               h->neighbors.as<int32_t>(), h->ppos.as<uint64_t>(), h->pval.as<int32_t>(), m);
+            HIP_CHECK(hipGetLastError());
+            HIP_CHECK(hipStreamSynchronize(h->st));
+        }
+        h->entry = entry_point;
+        h->max_level = max_level;
+    });
+}
 
 int vs_hnsw_search(vs_hnsw* h, const float* q, int64_t nq, int32_t k, int32_t ef_search, float* D, int64_t* I) {
     return guarded([&] {

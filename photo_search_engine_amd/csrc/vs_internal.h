@@ -324,6 +324,30 @@ int refine_split(int nq, int Kp, int dt, int num_cu);
 hipError_t launch_refine(const RefineArgs& a, int nq, hipStream_t st);
 // exact refine behind the int8 screen: adaptive two-phase depth (KA keys first), IP only
 hipError_t launch_refine_wide(const RefineArgs& a, int nq, int KA, hipStream_t st);
+// exact full scan of a shard for the queries no bounded screen could certify (vs_fullscan.hip):
+// every row scored canonically, streamed through a running top-k (any number of ties)
+struct FullScanArgs {
+    const uint8_t* corpus;  // tiled shard
+    int d, dpad, dt, metric;
+    int64_t n_valid;
+    const float* q;         // [nq][d] fp32 queries of the block
+    int nq, k;
+    int* cert;              // [nq]: queries with cert[q] == 0 are scanned (and set to 1)
+    const int* gate;        // nothing at all while *gate == 0 (the fallback round's failure count), or null
+    int64_t id_offset;
+    float* D;               // [nq][k] (may be null)
+    int64_t* I;             // [nq][k]
+    double* S64;            // [nq][k] (may be null)
+    int ostride;            // I / S64 element stride, as RefineArgs::ostride
+    double* gsc;            // [nq][G][k] per-workgroup lists (full_scan_scratch_bytes)
+    uint32_t* gid;
+    unsigned* gdone;        // [nq] per-query completion counters, zero between launches
+    unsigned* count;        // queries scanned (device counter), or null
+    int G;                  // workgroups (row ranges)
+};
+size_t full_scan_scratch_bytes(int nq, int G, int k);
+hipError_t launch_full_scan(const FullScanArgs& a, hipStream_t st);
+
 constexpr int I8_GROUP_ROWS = 4096;  // rows per group of the int8 copy's group residuals (16 tiles)
 constexpr int I8_MAX_K = 1024;  // largest k the int8 screen serves (k_refine_wide: 2 * KA <= RFW_CAP)
 // int8 screen copy of stored rows [r0, r0 + n) (maxes[0..1]: running max ||x_hat||, max beta)

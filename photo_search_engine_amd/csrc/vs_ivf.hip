@@ -62,10 +62,9 @@ struct vs_ivf {
     std::vector<int> cert_h;
     hipStream_t own = nullptr;
     // coarse assignment of added rows: kAssignStreams concurrent exact searches (one 256-row block
-    // of the coarse quantizer fills only nlist / 256 workgroups) and their unresolved counters
+    // of the coarse quantizer fills only nlist / 256 workgroups)
     hipStream_t astream[8] = {};
     hipEvent_t aev[9] = {};
-    DevBuf aunres;
     std::shared_mutex rw;
     std::mutex search_mtx;
     std::atomic<bool> timing{false};
@@ -171,32 +170,25 @@ void assign_rows(vs_ivf* ix, int64_t n, Fill&& fill, int64_t* lists_host) {
         for (int i = 0; i < S; ++i) HIP_CHECK(hipStreamCreateWithFlags(&ix->astream[i], hipStreamNonBlocking));
         for (int i = 0; i <= S; ++i) HIP_CHECK(hipEventCreateWithFlags(&ix->aev[i], hipEventDisableTiming));
     }
-    ix->aunres.ensure(S * sizeof(unsigned));
-    unsigned* unres = ix->aunres.as<unsigned>();
     for (int64_t r0 = 0; r0 < n; r0 += rpc) {
         const int64_t m = std::min(rpc, n - r0);
         fill(r0, m, ix->tmp_rows.as<float>());
         // a row goes to the best centroid of its STORED values (the dtype-rounded row)
         HIP_CHECK(launch_round_f32(ix->dtype, ix->tmp_rows.as<float>(), m * ix->d, ix->own));
-        HIP_CHECK(hipMemsetAsync(unres, 0, S * sizeof(unsigned), ix->own));
         HIP_CHECK(hipEventRecord(ix->aev[S], ix->own));
         // the chunk in S parts of whole 256-row blocks, each an exact device search on its own
-        // stream (no host round trip; a query even the device fallback cannot certify counts in
-        // its part's counter, checked below)
+        // stream (no host round trip: every query certified by its first pass, the device fallback
+        // round or the full scan -- a row tied between centroids goes to the lowest id, as in faiss)
         for (int i = 0; i < S; ++i) HIP_CHECK(hipStreamWaitEvent(ix->astream[i], ix->aev[S], 0));
         search_exact_device_parts(ix->coarse, ix->tmp_rows.as<float>(), m, 1, ix->assign_ids.as<int64_t>(),
-                                  ix->astream, S, unres);
+                                  ix->astream, S, nullptr);
         for (int i = 0; i < S; ++i) {
             HIP_CHECK(hipEventRecord(ix->aev[i], ix->astream[i]));
             HIP_CHECK(hipStreamWaitEvent(ix->own, ix->aev[i], 0));
         }
-        unsigned unres_h[S];
-        HIP_CHECK(hipMemcpyAsync(unres_h, unres, S * sizeof(unsigned), hipMemcpyDeviceToHost, ix->own));
         HIP_CHECK(hipMemcpyAsync(lists_host + r0, ix->assign_ids.p, (size_t)m * sizeof(int64_t),
                                  hipMemcpyDeviceToHost, ix->own));
         HIP_CHECK(hipStreamSynchronize(ix->own));
-        for (int i = 0; i < S; ++i)
-            if (unres_h[i]) throw VsError(VS_ERR_UNCERTIFIED, "coarse assignment: exactness certificate failed at maximum screening depth");
     }
 }
 
@@ -635,7 +627,6 @@ void vs_ivf_destroy(vs_ivf* ix) {
             if (a) (void)hipStreamDestroy(a);
         for (hipEvent_t& e : ix->aev)
             if (e) (void)hipEventDestroy(e);
-        ix->aunres.release();
     }
     vs_destroy(ix->coarse);
     delete ix;

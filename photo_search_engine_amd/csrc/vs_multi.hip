@@ -120,10 +120,9 @@ void throw_rc(int rc) {
 // one search's resources on every device, leased per call
 struct MCtx {
     std::vector<hipStream_t> st;
-    std::vector<DevBuf> qdev, S, I, unres_d;  // per device: queries, per-shard lists, unresolved count
+    std::vector<DevBuf> qdev, S, I;           // per device: queries, per-shard lists
     std::vector<DevBuf> floor;                // per device: the two-phase floor (device 0's merged phase-A lists)
     std::vector<hipEvent_t> ready;            // per device: its lists landed on device 0
-    unsigned* unres_h = nullptr;              // pinned, per device: this call's unresolved queries
     DevBuf gS, gI, oS, oI, oD;                // device 0: gathered [G][nq][k] lists, merged outputs
     DevBuf fS, fI, fD;                        // device 0: the merged phase-A lists (two-phase step)
     hipEvent_t floor_ready = nullptr;         // device 0: the floor is merged
@@ -180,7 +179,7 @@ void destroy_ctx(vs_multi* m, MCtx* c) {
     for (int g = 0; g < (int)c->st.size(); ++g) {
         DeviceGuard dg(m->dev[g]);
         if (c->st[g]) (void)hipStreamSynchronize(c->st[g]);
-        for (DevBuf* b : {&c->qdev[g], &c->S[g], &c->I[g], &c->unres_d[g], &c->floor[g]}) b->release();
+        for (DevBuf* b : {&c->qdev[g], &c->S[g], &c->I[g], &c->floor[g]}) b->release();
         if (c->ready[g]) (void)hipEventDestroy(c->ready[g]);
         if (c->st[g]) (void)hipStreamDestroy(c->st[g]);
     }
@@ -189,7 +188,6 @@ void destroy_ctx(vs_multi* m, MCtx* c) {
         for (DevBuf* b : {&c->gS, &c->gI, &c->oS, &c->oI, &c->oD, &c->fS, &c->fI, &c->fD}) b->release();
         if (c->floor_ready) (void)hipEventDestroy(c->floor_ready);
     }
-    if (c->unres_h) (void)hipHostFree(c->unres_h);
     delete c;
 }
 
@@ -201,21 +199,17 @@ MCtx* make_ctx(vs_multi* m) {
     c->qdev.resize(G);
     c->S.resize(G);
     c->I.resize(G);
-    c->unres_d.resize(G);
     c->floor.resize(G);
     try {
         for (int g = 0; g < G; ++g) {
             DeviceGuard dg(m->dev[g]);
             HIP_CHECK(hipStreamCreateWithFlags(&c->st[g], hipStreamNonBlocking));
             HIP_CHECK(hipEventCreateWithFlags(&c->ready[g], hipEventDisableTiming));
-            c->unres_d[g].ensure(sizeof(unsigned));
         }
         {
             DeviceGuard dg(m->dev[0]);
             HIP_CHECK(hipEventCreateWithFlags(&c->floor_ready, hipEventDisableTiming));
         }
-        HIP_CHECK(hipHostMalloc((void**)&c->unres_h, sizeof(unsigned) * G, hipHostMallocDefault));
-        std::memset(c->unres_h, 0, sizeof(unsigned) * G);
         c->pool = new Pool(G);
     } catch (...) {
         destroy_ctx(m, c);
@@ -279,7 +273,6 @@ void multi_search_two_phase(vs_multi* m, MCtx* c, const float* q, int64_t nq, in
             c->S[g].ensure(lb * sizeof(double));
             c->I[g].ensure(lb * sizeof(int64_t));
             c->floor[g].ensure(lb * sizeof(double));
-            c->unres_h[g] = 0;
             HIP_CHECK(hipMemcpyAsync(c->qdev[g].p, q, (size_t)nq * m->d * sizeof(float), hipMemcpyHostToDevice, s));
             int64_t* Ig = c->I[g].as<int64_t>();
             pend[g] = search_phase_a(m->ix[g], c->qdev[g].as<float>(), nq, kk, G, 0, c->S[g].as<double>(), Ig, 1, s);
@@ -306,13 +299,10 @@ void multi_search_two_phase(vs_multi* m, MCtx* c, const float* q, int64_t nq, in
                 HIP_CHECK(hipMemcpyPeerAsync(c->floor[g].p, m->dev[g], c->fS.p, m->dev[0], lb * sizeof(double), s));
                 fl = c->floor[g].as<double>();
             }
-            unsigned* ud = c->unres_d[g].as<unsigned>();
-            HIP_CHECK(hipMemsetAsync(ud, 0, sizeof(unsigned), s));
             int64_t* Ig = c->I[g].as<int64_t>();
             vs_pending* p = pend[g];
             pend[g] = nullptr;  // (phase B frees it, on success and on every error)
-            search_phase_b(p, fl, nullptr, Ig, c->S[g].as<double>(), 1, s, ud);
-            HIP_CHECK(hipMemcpyAsync(&c->unres_h[g], ud, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+            search_phase_b(p, fl, nullptr, Ig, c->S[g].as<double>(), 1, s);
             hipLaunchKernelGGL(k_local_to_global, dim3((unsigned)((lb + 255) / 256)), dim3(256), 0, s, Ig, (int64_t)lb, G, g);
             HIP_CHECK(hipGetLastError());
             HIP_CHECK(hipMemcpyPeerAsync(c->gS.as<double>() + lb * g, m->dev[0], c->S[g].p, m->dev[g], lb * sizeof(double), s));
@@ -497,17 +487,11 @@ int vs_multi_search(vs_multi* m, const float* q, int64_t nq, int32_t k, float* D
             c->I[g].ensure(lb * sizeof(int64_t));
             double* Sg = c->S[g].as<double>();
             int64_t* Ig = c->I[g].as<int64_t>();
-            c->unres_h[g] = 0;
             HIP_CHECK(hipMemcpyAsync(c->qdev[g].p, q, (size_t)nq * m->d * sizeof(float), hipMemcpyHostToDevice, s));
             if (vs_ntotal(m->ix[g]) > 0) {
                 // exact per shard: uncertified screens are re-searched on this device, queued behind
-                // the first pass (no host round trip for bf16 / f16 shards); the queries even that
-                // round could not certify are counted in THIS call's counter and travel back with
-                // the results
-                unsigned* ud = c->unres_d[g].as<unsigned>();
-                HIP_CHECK(hipMemsetAsync(ud, 0, sizeof(unsigned), s));
-                search_exact_device(m->ix[g], c->qdev[g].as<float>(), nq, kk, Ig, Sg, s, nullptr, 0, /*async*/ true, ud);
-                HIP_CHECK(hipMemcpyAsync(&c->unres_h[g], ud, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+                // the first pass (no host round trip): the fallback round, then the full scan
+                search_exact_device(m->ix[g], c->qdev[g].as<float>(), nq, kk, Ig, Sg, s, nullptr, 0, /*async*/ true);
                 hipLaunchKernelGGL(k_local_to_global, dim3((unsigned)((lb + 255) / 256)), dim3(256), 0, s, Ig,
                                    (int64_t)lb, G, g);
                 HIP_CHECK(hipGetLastError());
@@ -533,11 +517,7 @@ int vs_multi_search(vs_multi* m, const float* q, int64_t nq, int32_t k, float* D
         std::vector<int64_t> Ik(lb);
         HIP_CHECK(hipMemcpyAsync(Dk.data(), c->oD.p, lb * sizeof(float), hipMemcpyDeviceToHost, s0));
         HIP_CHECK(hipMemcpyAsync(Ik.data(), c->oI.p, lb * sizeof(int64_t), hipMemcpyDeviceToHost, s0));
-        HIP_CHECK(hipStreamSynchronize(s0));  // (s0 waited for every shard's ready event, which follows its
-                                              //  counter copy)
-        for (int g = 0; g < G; ++g)
-            if (c->unres_h[g] != 0)
-                throw VsError(VS_ERR_UNCERTIFIED, "exactness certificate failed at maximum screening depth");
+        HIP_CHECK(hipStreamSynchronize(s0));  // (s0 waited for every shard's ready event)
         for (int64_t a = 0; a < nq; ++a)
             for (int j = 0; j < k; ++j) {
                 D[a * k + j] = j < kk ? Dk[a * kk + j] : fillD;

@@ -197,10 +197,11 @@ class ShardedFlatIndex:
     def n_local(self) -> int:
         return int(self.index.ntotal)
 
-    def unresolved_count(self) -> int:
-        """Queries this rank's device fallback could not certify so far (synchronising; 0 unless
-        more than KP_MAX rows tie within the screen's error margin -- see vs_unresolved_count)."""
-        f = getattr(self.index, "unresolved_count", None)
+    def full_scan_count(self) -> int:
+        """Queries this rank's shard answered by the exact full scan so far (synchronising; 0 unless
+        more than KP_MAX rows tie within the screen's error margin -- see vs_full_scan_count).  Their
+        shard lists are exact like every other's: nothing uncertified is ever merged."""
+        f = getattr(self.index, "full_scan_count", None)
         return int(f()) if f else 0
 
     # -- search --------------------------------------------------------------------------------

@@ -34,6 +34,10 @@ class HNSWGraph:
 
     def __init__(self, index, graph: dict, ef_search: Optional[int] = None) -> None:
         self._h = None
+        from .index import FlatIndex
+        if not isinstance(index, FlatIndex):  # (vs_hnsw_create reads a one-device vs_index)
+            raise TypeError("HNSWGraph indexes the rows of a FlatIndex; a multi-device index searches its "
+                            "graph through its own hnsw_search (a one-device copy of the rows)")
         L = _lib.load()
         levels = np.ascontiguousarray(graph["levels"], dtype=np.int32)
         n = int(levels.shape[0])
@@ -70,6 +74,16 @@ class HNSWGraph:
         I = np.empty((nq, k), dtype=np.int64)
         check(self._L.vs_hnsw_search(self._h, _ptr(q), nq, k, int(ef_search or self.efSearch), _ptr(D), _ptr(I)))
         return D, I
+
+    def patch(self, pos: np.ndarray, val: np.ndarray, entry_point: int, max_level: int) -> None:
+        """Rewrite neighbour slots ``pos`` (indices into the neighbour array) with ``val`` and set the
+        entry point / top level (include/vs.h ``vs_hnsw_patch``)."""
+        pos = np.ascontiguousarray(pos, dtype=np.uint64)
+        val = np.ascontiguousarray(val, dtype=np.int32)
+        if pos.shape != val.shape:
+            raise ValueError("pos and val must have the same length")
+        check(self._L.vs_hnsw_patch(self._h, int(pos.shape[0]), _ptr(pos), _ptr(val), int(entry_point),
+                                    int(max_level)))
 
     def close(self) -> None:
         if self._h is not None:
@@ -223,16 +237,15 @@ def insert_rows(index, graph: dict, n_old: int, n: int, ef_construction: int, ma
     exact best C new nodes of that level; the heuristic keeps its forward list
     (``vs_hnsw_prune``); every node it names gets the new sources appended (faiss ``add_link``),
     the list re-shrunk over the union when it would overflow.  A new node above the old top level
-    becomes the entry point.  Equal to ``oracle/hnsw_oracle.py insert_batch`` batch by batch."""
-    while n_old < n:
-        n1 = min(n, n_old + int(batch))
-        graph = _insert_batch(index, graph, n_old, n1, int(ef_construction), make_index, seed, cmax)
-        n_old = n1
-    return graph
+    becomes the entry point.  Equal to ``oracle/hnsw_oracle.py insert_batch`` batch by batch.
 
-
-def _insert_batch(index, graph: dict, n_old: int, n: int, ef_construction: int, make_index, seed: int,
-                  cmax: int) -> dict:
+    Cost: the node levels, offsets and the neighbour array are laid out ONCE for the final n (a
+    node's slots never move), and ONE device graph over them serves every batch's beams -- nodes
+    not inserted yet have empty lists and nothing links to them, so they are unreachable -- patched
+    after each batch with the slots it wrote (``vs_hnsw_patch``).  Each batch costs its own rows
+    and links, not the graph's size."""
+    if n_old >= n:
+        return graph
     probas = np.asarray(graph["assign_probas"])
     cum = np.asarray(graph["cum_nneighbor_per_level"]).astype(np.int64)
     # old nodes keep the graph's levels (a faiss-built graph's included); new node i gets entry i of
@@ -244,17 +257,72 @@ def _insert_batch(index, graph: dict, n_old: int, n: int, ef_construction: int, 
     old_off = np.asarray(graph["offsets"], dtype=np.uint64)
     nb = np.full(int(offsets[-1]), -1, dtype=np.int32)
     nb[:int(old_off[n_old])] = np.asarray(graph["neighbors"], dtype=np.int32)[:int(old_off[n_old])]
-    old = dict(graph, levels=(old_lev + 1).astype(np.int32), offsets=old_off[:n_old + 1],
-               neighbors=np.ascontiguousarray(np.asarray(graph["neighbors"], dtype=np.int32)[:int(old_off[n_old])]))
+    st = {"lev": lev, "offsets": offsets, "nb": nb, "cum": cum, "entry": int(graph["entry_point"]),
+          "top": int(graph["max_level"])}
+    full = dict(graph, levels=(lev + 1).astype(np.int32), offsets=offsets, neighbors=nb)
+    dev = None
+    try:
+        while n_old < n:
+            n1 = min(n, n_old + int(batch))
+            if n_old > 0 and dev is None:  # the beams' graph (nodes >= n_old unreachable until patched)
+                dev = _beam_graph(index, full, st, ef_construction)
+            pos = _insert_batch(index, st, n_old, n1, int(ef_construction), make_index, cmax, dev)
+            if dev is not None and n1 < n:
+                dev.patch(pos, nb[pos.astype(np.int64)], st["entry"], st["top"])
+            n_old = n1
+    finally:
+        if dev is not None:
+            dev.close()
+    out = dict(graph)
+    out.update({"levels": (lev + 1).astype(np.int32), "offsets": offsets, "neighbors": nb, "entry_point": st["entry"],
+                "max_level": st["top"], "efConstruction": int(ef_construction)})
+    return out
+
+
+class _IndexBeams:
+    """The beams of an index that searches a graph dict itself (``hnsw_search``: the test checker):
+    a snapshot of the in-place arrays, taken at creation and at every patch, as the device graph
+    sees them (nothing a batch writes is visible to its own beams)."""
+
+    def __init__(self, index, full: dict, st: dict) -> None:
+        self.index, self.full, self.st = index, full, st
+        self.patch(None, None, st["entry"], st["top"])
+
+    def search(self, q, k: int, ef: int):
+        return None, self.index.hnsw_search(self.g, q, k, ef)
+
+    def patch(self, pos, val, entry_point: int, max_level: int) -> None:
+        self.g = dict(self.full, neighbors=np.array(self.full["neighbors"], copy=True), entry_point=int(entry_point),
+                      max_level=int(max_level))
+
+    def close(self) -> None:
+        pass
+
+
+def _beam_graph(index, full: dict, st: dict, ef: int):
+    if hasattr(index, "_one_device_copy"):  # multi-device rows: the HNSW kernels read one device's HBM
+        return HNSWGraph(index._one_device_copy(), dict(full, entry_point=st["entry"], max_level=st["top"]), ef)
+    if hasattr(index, "hnsw_search"):
+        return _IndexBeams(index, full, st)
+    return HNSWGraph(index, dict(full, entry_point=st["entry"], max_level=st["top"]), ef)
+
+
+def _insert_batch(index, st: dict, n_old: int, n: int, ef_construction: int, make_index, cmax: int,
+                  dev) -> np.ndarray:
+    """Insert nodes [n_old, n) into the in-place arrays of ``st``; returns the neighbour slots it
+    wrote (for the device graph's patch).  ``dev``: the device graph of nodes [0, n_old)."""
+    lev, offsets, nb, cum = st["lev"], st["offsets"], st["nb"], st["cum"]
+    old_lev = lev[:n_old]
     new = np.arange(n_old, n, dtype=np.int64)
     top_new = int(lev[new].max()) if new.size else -1
+    written = []
     for level in range(top_new, -1, -1):
         width = int(cum[level + 1] - cum[level])
         C = min(max(ef_construction, width), cmax)
         nmem = new[lev[new] >= level]
         omem = np.nonzero(old_lev >= level)[0]
         if level == 0 and n_old > 0:
-            I = beam_search(index, old, np.ascontiguousarray(_rows(index, nmem)), C, ef_construction)
+            I = dev.search(np.ascontiguousarray(_rows(index, nmem)), C, ef_construction)[1]
             oc = [[int(v) for v in row if v >= 0] for row in I]
         else:
             oc = _exact_candidates(make_index, index, omem, nmem, C, exclude_self=False)
@@ -290,11 +358,8 @@ def _insert_batch(index, graph: dict, n_old: int, n: int, ef_construction: int, 
             base = int(offsets[v]) + int(cum[level])
             nb[base:base + width] = -1
             nb[base:base + len(L)] = L
-    entry, top = int(graph["entry_point"]), int(graph["max_level"])
-    if new.size and (top_new > top or entry < 0):
-        top = top_new
-        entry = int(new[lev[new] == top_new][0])
-    out = dict(graph)
-    out.update({"levels": (lev + 1).astype(np.int32), "offsets": offsets, "neighbors": nb, "entry_point": entry,
-                "max_level": top, "efConstruction": int(ef_construction)})
-    return out
+            written.append(np.arange(base, base + width, dtype=np.uint64))
+    if new.size and (top_new > st["top"] or st["entry"] < 0):
+        st["top"] = top_new
+        st["entry"] = int(new[lev[new] == top_new][0])
+    return np.concatenate(written) if written else np.zeros(0, dtype=np.uint64)

@@ -146,9 +146,10 @@ class FlatIndex:
 
     def search_device_exact(self, q_ptr: int, nq: int, k: int, D_ptr: Optional[int], I_ptr: int,
                             S64_ptr: Optional[int] = None, id_offset: int = 0, stream: Optional[int] = None) -> None:
-        """``search_device`` with certificate failures re-searched.  bf16/f16: by a fallback round
-        queued on the device (no host sync); a query it cannot certify counts in
-        :meth:`unresolved_count`.  fp32: certificates read back, host-driven re-search."""
+        """``search_device`` exact for every query: a failed certificate is re-searched by a fallback
+        round queued on the device (no host sync), and a query even that round cannot certify (more
+        near-tied rows than the deepest screen lists) by the exact full scan of the shard, counted in
+        :meth:`full_scan_count`."""
         check(self._L.vs_search_device_exact(self._h, q_ptr, int(nq), int(k), D_ptr or None, I_ptr, S64_ptr or None,
                                              int(id_offset), stream or None))
 
@@ -199,9 +200,10 @@ class FlatIndex:
                 "max_row_error", "i8_union_log2", "i8_routed_searches", "native_seed_log2")
         return {k: (float(buf[i]) if "max" in k else int(buf[i])) for i, k in enumerate(keys)}
 
-    def unresolved_count(self) -> int:
-        """Queries ``search_device_exact``'s device fallback could not certify either (must stay 0)."""
-        return int(check(self._L.vs_unresolved_count(self._h)))
+    def full_scan_count(self) -> int:
+        """Queries answered by the exact full scan so far: no bounded screen could certify them (more
+        rows than KP_MAX tied within its margin).  Synchronises."""
+        return int(check(self._L.vs_full_scan_count(self._h)))
 
     def host_staging_bytes(self) -> int:
         """Pinned host bytes held for ``search``'s query / result staging (bounded per context)."""
@@ -315,12 +317,10 @@ class MultiDeviceFlatIndex:
     def reconstruct(self, i: int) -> np.ndarray:
         return self.reconstruct_n(int(i), 1)[0]
 
-    def hnsw_prune(self, nodes, cand, W: int) -> np.ndarray:
-        """:meth:`FlatIndex.hnsw_prune` on a one-device copy of the rows on ``devices[0]`` (the
-        kernel gathers rows by id from one device's HBM).  The copy is made once and kept until the
-        rows change (a graph build calls this twice per level)."""
-        if len(nodes) == 0:
-            return np.full((0, int(W)), -1, dtype=np.int32)
+    def _one_device_copy(self) -> "FlatIndex":
+        """A one-device copy of the rows on ``devices[0]`` for the HNSW kernels (they gather rows by
+        id from one device's HBM).  Made once and kept until the rows change (a graph build calls
+        the kernels several times per level)."""
         n = self.ntotal
         if self._prune_copy is None or self._prune_copy[0] != n:
             self._drop_prune_copy()
@@ -333,7 +333,23 @@ class MultiDeviceFlatIndex:
                 tmp.close()
                 raise
             self._prune_copy = (n, tmp)
-        return self._prune_copy[1].hnsw_prune(nodes, cand, W)
+        return self._prune_copy[1]
+
+    def hnsw_prune(self, nodes, cand, W: int) -> np.ndarray:
+        """:meth:`FlatIndex.hnsw_prune` on the one-device copy of the rows."""
+        if len(nodes) == 0:
+            return np.full((0, int(W)), -1, dtype=np.int32)
+        return self._one_device_copy().hnsw_prune(nodes, cand, W)
+
+    def hnsw_search(self, graph: dict, q: np.ndarray, k: int, ef: int) -> np.ndarray:
+        """Ids (nq x k, -1 padded) of faiss's HNSW search over ``graph`` on the one-device copy of
+        the rows (``hnsw.beam_search``: the insertion beam of a graph save)."""
+        from .hnsw import HNSWGraph
+        g = HNSWGraph(self._one_device_copy(), graph, ef)
+        try:
+            return g.search(q, k, ef)[1]
+        finally:
+            g.close()
 
     def _drop_prune_copy(self) -> None:
         pc, self._prune_copy = getattr(self, "_prune_copy", None), None

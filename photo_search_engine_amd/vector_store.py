@@ -400,8 +400,8 @@ class VectorStore:
         ``_GRAPH_REBUILD_GROWTH`` since it was built; rows added behind it meanwhile are searched
         exactly (a flat index of those rows) and merged with the graph's results, so alternating
         ``add_item`` / ``search`` does not pay a whole-graph build per search.  Stores above
-        ``VECTOR_HNSW_GRAPH_MAX_ROWS`` (no graph is saved for them either), beams wider than the GPU
-        search takes (max(efSearch, k) > 2048) and multi-GPU indexes search exactly."""
+        ``VECTOR_HNSW_GRAPH_MAX_ROWS`` (their graph is still saved: :meth:`save`), beams wider than
+        the GPU search takes (max(efSearch, k) > 2048) and multi-GPU indexes search exactly."""
         n = int(self.index.ntotal)
         if (self.index_type != "hnsw" or not _hnsw_graph_search() or not isinstance(self.index, FlatIndex)
                 or max(k, self.hnsw_ef_search) > _HNSW_EF_MAX or n > _hnsw_graph_max_rows()):

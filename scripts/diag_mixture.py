@@ -1,6 +1,6 @@
 """Screen health on clustered corpora, batch by batch: bench.py's mixture rows (64 unit centroids,
 normalise(c + sigma g), inserted cluster by cluster with --sorted), d=1536 bf16, batch 256, k=100,
-the int8 screen.  Per search: wall time, first-pass certificate failures, unresolved queries and
+the int8 screen.  Per search: wall time, first-pass certificate failures, full-scanned queries and
 the index's screen state (group residuals, margins, union depth, native routing).
 python scripts/diag_mixture.py [--rows 2000000] [--sigma 0.3] [--sorted] [--batches 12]"""
 import argparse
@@ -82,7 +82,7 @@ for screen in ("native", "int8"):
     ix.set_screen(screen)
     print(json.dumps({"screen": screen, "state": ix.screen_state()}), flush=True)
     for b in range(args.batches):
-        u0, r0 = ix.uncertified_count(), ix.unresolved_count()
+        u0, r0 = ix.uncertified_count(), ix.full_scan_count()
         t = time.perf_counter()
         ix.search_device_exact(q.data_ptr(), nq, k, D.data_ptr(), I.data_ptr(), S.data_ptr(), 0, st)
         torch.cuda.synchronize()
@@ -96,7 +96,7 @@ for screen in ("native", "int8"):
                 if set(got[qi].tolist()) != set(exact_I[qi].tolist()):
                     bad.append(qi)
         print(json.dumps({"screen": screen, "batch": b, "ms": round(ms, 3),
-                          "uncertified": ix.uncertified_count() - u0, "unresolved": ix.unresolved_count() - r0,
+                          "uncertified": ix.uncertified_count() - u0, "full_scan": ix.full_scan_count() - r0,
                           "identical_to_native": bool((got == ref).all()), "inexact_queries": bad,
                           "state": ix.screen_state()}), flush=True)
 ix.close()

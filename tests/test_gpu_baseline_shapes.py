@@ -156,7 +156,7 @@ def _cfg4_worker(rank, world, port, N, d, nq, k, outdir):
         D8, I8, S8 = sh.search(q, k)
         torch.cuda.synchronize()
         np.savez(os.path.join(outdir, f"r{rank}.npz"), D=D.cpu().numpy(), I=I.cpu().numpy(), S=S.cpu().numpy(),
-                 I8=I8.cpu().numpy(), S8=S8.cpu().numpy(), n=sh.n_local, unres=sh.unresolved_count())
+                 I8=I8.cpu().numpy(), S8=S8.cpu().numpy(), n=sh.n_local, full_scan=sh.full_scan_count())
         sh.close()
     finally:
         dist.destroy_process_group()
@@ -172,10 +172,10 @@ def test_cfg4_shape_sharded_four_ranks(tmp_path):
         np.testing.assert_array_equal(o["I"], outs[0]["I"])
         np.testing.assert_array_equal(o["S"], outs[0]["S"])
     D, I, S = outs[0]["D"], outs[0]["I"], outs[0]["S"]
-    for o in outs:  # int8 screen on every shard: identical merged answer, nothing unresolved
+    for o in outs:  # int8 screen on every shard: identical merged answer, no full scan
         np.testing.assert_array_equal(o["I8"], I)
         np.testing.assert_array_equal(o["S8"], S)
-        assert int(o["unres"]) == 0
+        assert int(o["full_scan"]) == 0
     x = O.synth_rows(O.SEED_CORPUS, 0, N, d, True, "f16")
     q = O.synth_rows(O.SEED_QUERIES, 0, nq, d, True, "f16")
     np.testing.assert_array_equal(D, S.astype(np.float32))

@@ -40,7 +40,7 @@ def _worker(rank, world, port, N, d, dtype, nq, k, metric, outdir, screen="nativ
         torch.cuda.synchronize()
         np.savez(os.path.join(outdir, f"r{rank}.npz"), D=D.cpu().numpy(), I=I.cpu().numpy(), S=S.cpu().numpy(),
                  row0=sh.row0, n=sh.n_local, two=sh.index.two_phase_ok(nq, k),
-                 unres=sh.unresolved_count())
+                 full_scan=sh.full_scan_count())
         sh.close()
     finally:
         dist.destroy_process_group()
@@ -92,7 +92,7 @@ def test_two_phase_int8_ranks_one_gpu_match_oracle(tmp_path, world, metric, dtyp
              nprocs=world, join=True)
     outs = [np.load(tmp_path / f"r{r}.npz") for r in range(world)]
     assert all(bool(o["two"]) for o in outs)
-    assert sum(int(o["unres"]) for o in outs) == 0
+    assert sum(int(o["full_scan"]) for o in outs) == 0
     x = O.synth_rows(O.SEED_CORPUS, 0, N, d, True, dtype)
     q = O.synth_rows(O.SEED_QUERIES, 0, nq, d, True, dtype)
     Se, Ie = O.knn_exact(x, q, k, metric)
@@ -140,7 +140,7 @@ def test_two_phase_single_index_with_external_floor(metric):
         mine = [(s, i) for s, i in zip(Sg[qi], Ig[qi]) if lo <= i < hi]
         got = list(zip(Sh[qi][:len(mine)], Ih[qi][:len(mine)]))
         assert got == mine, qi
-    assert ix.unresolved_count() == 0
+    assert ix.full_scan_count() == 0
     # (3) a pending search dropped without phase B releases the index (an add must not block)
     p = ix.search_phase_a(qd.data_ptr(), nq, k, 2, Sa.data_ptr(), Ia.data_ptr(), lo)
     ix.search_pending_free(p)
@@ -187,3 +187,54 @@ def test_rccl_backend_one_rank_exchange_and_merge(tmp_path):
         np.testing.assert_array_equal(o["I" + sfx], Ie, err_msg="I" + sfx)
         np.testing.assert_array_equal(o["S" + sfx], Se, err_msg="S" + sfx)
         np.testing.assert_array_equal(o["D" + sfx], Se.astype(np.float32), err_msg="D" + sfx)
+
+
+def _tie_worker(rank, world, port, N, d, dtype, copies, nq, k, metric, screen, outdir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from photo_search_engine_amd.distributed import ShardedFlatIndex, shard_range
+        x, q = _tie_corpus(N, d, dtype, copies, nq)
+        sh = ShardedFlatIndex(d, metric, dtype, device=0)
+        row0, n = shard_range(N, rank, world)
+        sh.add_shard(x[row0:row0 + n], row0, N)
+        sh.index.set_screen(screen)
+        D, I, S = sh.search(torch.from_numpy(q).cuda(), k)
+        torch.cuda.synchronize()
+        np.savez(os.path.join(outdir, f"r{rank}.npz"), D=D.cpu().numpy(), I=I.cpu().numpy(), S=S.cpu().numpy(),
+                 full_scan=sh.full_scan_count())
+        sh.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def _tie_corpus(N, d, dtype, copies, nq):
+    x = O.synth_rows(O.SEED_CORPUS, 0, N, d, True, dtype)
+    v = x[N // 2 + 5].copy()
+    pos = np.random.default_rng(5).choice(N, copies, replace=False)  # spread over every shard
+    x[pos] = v
+    q = np.concatenate([np.repeat(v[None], nq - 1, axis=0), O.synth_rows(O.SEED_QUERIES, 0, 1, d, True, dtype)])
+    return x, q
+
+
+@pytest.mark.parametrize("screen,metric,nq,copies", [("native", "ip", 3, 9000), ("native", "l2", 3, 20000),
+                                                     ("int8", "ip", 12, 20000)])
+def test_two_ranks_ties_split_across_shards(tmp_path, screen, metric, nq, copies):
+    # thousands of identical rows spread over both shards (more per shard than any bounded screen
+    # lists): each shard's device path ends in its exact full scan, the exchange merges exact shard
+    # lists, and every rank returns faiss's answer -- the k lowest ids of the tie
+    N, d, k, dtype = 2 * 24_000, 64, 10, "bf16"
+    mp.spawn(_tie_worker, args=(2, _free_port(), N, d, dtype, copies, nq, k, metric, screen, str(tmp_path)),
+             nprocs=2, join=True)
+    outs = [np.load(tmp_path / f"r{r}.npz") for r in range(2)]
+    x, q = _tie_corpus(N, d, dtype, copies, nq)
+    x = O.round_dtype(x, dtype)
+    Se, Ie = O.knn_exact(x, O.round_dtype(q, dtype), k, metric)
+    for o in outs:
+        np.testing.assert_array_equal(o["I"], Ie)
+        np.testing.assert_array_equal(o["S"], Se)
+        np.testing.assert_array_equal(o["D"], Se.astype(np.float32))
+    if copies // 2 > 8192:  # (beyond the adaptive refine's 8192 rows: only the full scan certifies)
+        assert sum(int(o["full_scan"]) for o in outs) >= 1

@@ -79,7 +79,8 @@ def test_store_graph_mode_search_save_load_add(tmp_path, monkeypatch):
 
 
 def test_store_graph_mode_above_row_cap_searches_exactly(tmp_path, monkeypatch):
-    """Above VECTOR_HNSW_GRAPH_MAX_ROWS the store neither saves nor searches a graph: exact search."""
+    """Above VECTOR_HNSW_GRAPH_MAX_ROWS the store searches exactly (no graph build per search; its
+    graph is still saved, see test_multi_device_store_saves_graph_above_row_cap)."""
     monkeypatch.setenv("VECTOR_HNSW_SEARCH", "graph")
     monkeypatch.setenv("VECTOR_HNSW_GRAPH_MAX_ROWS", "500")
     n, d = 800, 32
@@ -111,3 +112,31 @@ def test_store_graph_mode_on_the_reference_file(tmp_path, monkeypatch):
     assert np.array_equal(I, I_ref) and np.array_equal(D, S_ref.astype(np.float32))
     res = store.search(x[7].tolist(), 3)
     assert res[0]["metadata"]["photo_path"] == "/photos/7.jpg"
+
+
+def test_multi_device_store_saves_graph_above_row_cap(tmp_path, monkeypatch):
+    """A multi-GPU store (VECTOR_DEVICES) of index_type hnsw above the exact-build size: save()
+    inserts the rows past the cap into the graph by beams over it (hnsw.insert_rows), which run on a
+    one-device copy of the multi-device index's rows.  The saved graph equals the one-device
+    store's, and a reload searches it."""
+    monkeypatch.setenv("VECTOR_HNSW_GRAPH_MAX_ROWS", "300")
+    n, d = 700, 32
+    rows = O.synth_rows(O.SEED_CORPUS + 51, 0, n, d, False)
+    meta = [{"photo_path": f"/p/{i}.jpg"} for i in range(n)]
+    one = _store(tmp_path / "one", d)
+    one.add(rows, meta)
+    one.save()
+    monkeypatch.setenv("VECTOR_DEVICES", "0,0")
+    multi = _store(tmp_path / "multi", d)
+    multi.add(rows, meta)
+    from photo_search_engine_amd.index import MultiDeviceFlatIndex
+    assert isinstance(multi.index, MultiDeviceFlatIndex)
+    multi.save()
+    g1 = faiss_format.read_hnsw_graph(one.index_path)
+    g2 = faiss_format.read_hnsw_graph(multi.index_path)
+    for key in ("levels", "offsets", "neighbors"):
+        assert np.array_equal(np.asarray(g1[key]), np.asarray(g2[key])), key
+    assert int(g1["entry_point"]) == int(g2["entry_point"])
+    assert open(one.index_path, "rb").read() == open(multi.index_path, "rb").read()
+    multi.index.close()
+    one.index.close()

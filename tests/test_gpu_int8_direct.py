@@ -63,7 +63,7 @@ def test_direct_direct_exact(FlatIndex, dtype, d, nq, k, tpc):
     q = O.synth_rows(O.SEED_QUERIES + 9, 0, nq, d, True, "f32")
     _exact(ix, q, k)
     assert ix.uncertified_count() == 0
-    assert ix.unresolved_count() == 0
+    assert ix.full_scan_count() == 0
     st = ix.screen_state()  # isotropic rows: no group has a mean worth coding against
     assert st["group_residuals"] == 0 and st["groups_with_mean"] == 0 and st["i8_union_log2"] == 0
     ix.close()
@@ -108,7 +108,7 @@ def test_direct_planted_sample_tiles_exact(FlatIndex):
     _, I = _exact(ix, np.concatenate([qb, qb]), k)  # 32 queries: the MFMA path
     planted = {t * 256 + 3 + r for t in _sample_tiles(tiles, G) for r in range(4)}
     assert all(int(i) in planted for i in I.ravel())
-    assert ix.unresolved_count() == 0
+    assert ix.full_scan_count() == 0
     ix.close()
 
 
@@ -129,7 +129,7 @@ def test_direct_sample_tile_holding_the_top_k(FlatIndex):
     ix.add(x)
     ix.set_screen("int8")
     _exact(ix, q, k)
-    assert ix.unresolved_count() == 0
+    assert ix.full_scan_count() == 0
     ix.close()
 
 
@@ -179,5 +179,5 @@ def test_direct_device_api_with_offset_and_phases(FlatIndex):
     ix.search_phase_b(p, Sa.data_ptr(), D.data_ptr(), I.data_ptr(), S.data_ptr(), stream)
     np.testing.assert_array_equal(I.cpu().numpy(), Ie)
     np.testing.assert_array_equal(S.cpu().numpy(), Se)
-    assert ix.unresolved_count() == 0
+    assert ix.full_scan_count() == 0
     ix.close()

@@ -298,52 +298,82 @@ def test_device_exact_search_re_searches_uncertified_queries(FlatIndex, nq, dtyp
     np.testing.assert_array_equal(S.cpu().numpy(), Se)
     np.testing.assert_array_equal(D.cpu().numpy(), Se.astype(np.float32))
     assert ix.uncertified_count() > 0
-    assert ix.unresolved_count() == 0
+    assert ix.full_scan_count() == 0
 
 
+@pytest.mark.parametrize("metric", ["ip", "l2"])
 @pytest.mark.parametrize("dtype", ["bf16", "f32"])
-@pytest.mark.parametrize("nq,copies", [(1, 5000), (20, 12000)])
-def test_ties_beyond_max_depth_are_reported(FlatIndex, nq, copies, dtype):
-    # `copies` identical rows tie with the query's best score: more than vs_search's deepest screen
-    # (KP_MAX = 4096 rows) can certify that no unlisted copy wins: it raises VS_ERR_UNCERTIFIED.
-    # The device API's fallback round (no host sync) lists up to
-    # MFMA_KP_MAX rows per workgroup and scores every listed row within one margin of T' (up to the
-    # adaptive refine's 8192): 5000 copies it certifies -- the k lowest ids of the tie --, 12000 it
-    # counts in unresolved_count (the multi-device handle, whose shards run that path, likewise
-    # answers the first and raises on the second).
+@pytest.mark.parametrize("nq,copies", [(1, 5000), (20, 12000), (3, 20000)])
+def test_ties_beyond_max_depth_full_scan(FlatIndex, nq, copies, dtype, metric):
+    # `copies` identical rows tie with the query's best score: more than the deepest bounded screen
+    # (KP_MAX = 4096 rows, the adaptive refine's 8192) can certify.  faiss answers with the k lowest
+    # ids of the tie (/root/reference/utils/vector_store.py:191); so must every entry point: the
+    # host API (escalation, then the exact full scan), the device API (fallback round, then the gated
+    # full scan, no host sync) and the multi-device handle whose shards run the device path.
     import torch
-    from photo_search_engine_amd._lib import VsError
     from photo_search_engine_amd.index import MultiDeviceFlatIndex
-    d, k = 64, 10
-    x = O.synth_rows(O.SEED_CORPUS, 0, 25_000, d, True, dtype)
+    d, k, N = 64, 10, 25_000
+    x = O.synth_rows(O.SEED_CORPUS, 0, N, d, True, dtype)
     v = x[123].copy()
-    pos = np.random.default_rng(3).choice(25_000, copies, replace=False)
+    pos = np.random.default_rng(3).choice(N, copies, replace=False)
     x[pos] = v
-    tie = np.unique(np.concatenate([pos, [123]]))
     q = np.repeat(v[None], nq, axis=0)
-    ix = FlatIndex(d, "ip", dtype)
+    ix = FlatIndex(d, metric, dtype)
     ix.add(x)
-    with pytest.raises(VsError) as e:
-        ix.search(q, k)
-    assert e.value.code == -4
+    xs = ix.reconstruct_n(0, N)
+    Se, Ie = O.knn_exact(xs, q, k, metric)
+    tie = np.unique(np.concatenate([pos, [123]]))
+    np.testing.assert_array_equal(Ie, np.repeat(tie[None, :k], nq, axis=0))  # (the checker itself)
+    D, I = ix.search(q, k)
+    np.testing.assert_array_equal(I, Ie)
+    np.testing.assert_array_equal(D, Se.astype(np.float32))
+    fs0 = ix.full_scan_count()
+    assert fs0 >= 1  # the bounded screens could not certify it
     qd = torch.from_numpy(q).cuda()
-    I = torch.empty((nq, k), dtype=torch.int64, device="cuda")
-    ix.search_device_exact(qd.data_ptr(), nq, k, None, I.data_ptr(), None, 0, 0)
-    if copies <= 7000:
-        assert ix.unresolved_count() == 0
-        np.testing.assert_array_equal(I.cpu().numpy(), np.repeat(tie[None, :k], nq, axis=0))
-    else:
-        assert ix.unresolved_count() == nq
-    m = MultiDeviceFlatIndex(d, "ip", dtype, devices=[0, 0])  # (its shards run the device path)
+    I2 = torch.empty((nq, k), dtype=torch.int64, device="cuda")
+    S2 = torch.empty((nq, k), dtype=torch.float64, device="cuda")
+    D2 = torch.empty((nq, k), dtype=torch.float32, device="cuda")
+    ix.search_device_exact(qd.data_ptr(), nq, k, D2.data_ptr(), I2.data_ptr(), S2.data_ptr(), 7, 0)
+    np.testing.assert_array_equal(I2.cpu().numpy(), Ie + 7)
+    np.testing.assert_array_equal(S2.cpu().numpy(), Se)
+    np.testing.assert_array_equal(D2.cpu().numpy(), Se.astype(np.float32))
+    assert ix.full_scan_count() >= fs0 + (nq if copies > 8192 else 0)
+    m = MultiDeviceFlatIndex(d, metric, dtype, devices=[0, 0])  # (its shards run the device path)
     m.add(x)
-    if copies <= 7000:
-        _, Im = m.search(q, k)
-        np.testing.assert_array_equal(Im, np.repeat(tie[None, :k], nq, axis=0))
-    else:
-        with pytest.raises(VsError) as e:
-            m.search(q, k)
-        assert e.value.code == -4
+    Dm, Im = m.search(q, k)
+    np.testing.assert_array_equal(Im, Ie)
+    np.testing.assert_array_equal(Dm, Se.astype(np.float32))
     m.close()
+    ix.close()
+
+
+@pytest.mark.parametrize("metric", ["ip", "l2"])
+def test_full_scan_near_ties_and_k_beyond_rows(FlatIndex, metric):
+    # The full scan's own ordering: rows tied to the last bit mixed with rows one ulp apart (bf16),
+    # every row scanned by a workgroup whose range starts mid-tie, and k larger than the index
+    # (padding).  Forced through the host API on a tie the screens cannot list.
+    d, N = 64, 9000
+    x = O.synth_rows(O.SEED_CORPUS, 0, N, d, True, "bf16")
+    v = x[7].copy()
+    rng = np.random.default_rng(11)
+    pos = rng.choice(N, 6000, replace=False)
+    x[pos] = v
+    near = rng.choice(pos, 300, replace=False)
+    x[near, 0] = v[0] + np.float32(2.0 ** -8) * np.sign(v[0] if v[0] != 0 else 1.0)  # near-ties
+    ix = FlatIndex(d, metric, "bf16")
+    ix.add(x)
+    xs = ix.reconstruct_n(0, N)
+    for k in (1, 64, 1000):
+        D, I = ix.search(v[None], k)
+        Se, Ie = O.knn_exact(xs, v[None].astype(np.float32), k, metric)
+        np.testing.assert_array_equal(I, Ie)
+        np.testing.assert_array_equal(D, Se.astype(np.float32))
+    # k beyond the rows present: faiss pads (host API searches min(k, ntotal) and pads)
+    small = FlatIndex(d, metric, "bf16")
+    small.add(np.repeat(v[None], 50, axis=0))
+    D, I = small.search(v[None], 60)
+    assert I[0, :50].tolist() == list(range(50)) and (I[0, 50:] == -1).all()
+    small.close()
     ix.close()
 
 
@@ -366,7 +396,7 @@ def test_batch_refine_certifies_ties_within_its_depth(FlatIndex, d):
     np.testing.assert_array_equal(I, Ie)
     np.testing.assert_array_equal(D, S.astype(np.float32))
     assert set(I[0].tolist()) <= set(dup.tolist()) | {123}
-    assert ix.unresolved_count() == 0
+    assert ix.full_scan_count() == 0
     ix.close()
 
 

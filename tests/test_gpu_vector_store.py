@@ -245,3 +245,29 @@ def test_device_search_context_reuse_across_streams_is_ordered():
         np.testing.assert_array_equal(I.cpu().numpy(), Ie)
         np.testing.assert_array_equal(S.cpu().numpy(), Se)
     ix.close()
+
+
+@pytest.mark.parametrize("metric", ["cosine", "l2"])
+@pytest.mark.parametrize("copies", [5000, 20000])
+def test_store_search_thousands_of_identical_embeddings(VS, tmp_path, metric, copies):
+    # A photo library with thousands of identical embeddings (the same picture imported many
+    # times): faiss returns the k lowest ids of the tie (/root/reference/utils/vector_store.py:191,
+    # tie order pinned by /root/reference/tests/test_searcher.py:323-350); so does the drop-in, for
+    # any tie count -- beyond the deepest bounded screen the exact full scan answers.
+    d, n, k = 64, 25_000, 10
+    x = O.synth_rows(O.SEED_CORPUS, 0, n, d, True, "f32")
+    v = x[4321].copy()
+    pos = np.random.default_rng(9).choice(n, copies, replace=False)
+    x[pos] = v
+    store = VS(dimension=d, index_path=str(tmp_path / "t.index"), metadata_path=str(tmp_path / "t.json"),
+               metric=metric)
+    store.add(x, [{"photo_path": f"p{i}.jpg"} for i in range(n)])
+    xs = store._normalize_rows(x)
+    qn = store._normalize_query(v.tolist())
+    Se, Ie = O.knn_exact(xs, np.asarray(qn, dtype=np.float32), k, "ip" if metric == "cosine" else "l2")
+    tie = np.unique(np.concatenate([pos, [4321]]))
+    assert Ie[0].tolist() == tie[:k].tolist()
+    res = store.search(v.tolist(), k)
+    assert [r["metadata"]["photo_path"] for r in res] == [f"p{i}.jpg" for i in tie[:k]]
+    assert [r["distance"] for r in res] == [float(np.float32(s)) for s in Se[0]]
+    store.index.close()
