@@ -78,8 +78,6 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal only: every rank on cuda:0 (with --dist-backend gloo on a 1-GPU box)")
-    ap.add_argument("--zero-corpus", action="store_true",
-                    help="diagnostic only: all-zero corpus rows (the DVFS/power test of DESIGN §5; results meaningless)")
     ap.add_argument("--no-recall", action="store_true", help="cfg5: skip the exact ground truth (profiling runs)")
     ap.add_argument("--skew", type=float, default=0.0,
                     help="cfg5: Zipf exponent of the cluster sizes (0 = equal-sized clusters; 1.1 = a heavy head)")
@@ -210,13 +208,6 @@ def main():
             sh.index.add_device(xr.data_ptr(), m, torch.cuda.current_stream(dev).cuda_stream)
             torch.cuda.synchronize()
             del xr
-    elif args.zero_corpus:
-        zeros = torch.zeros((1 << 20, d), dtype=torch.float32, device=dev)
-        sh.row0, sh.n_total = row0, N
-        for r in range(0, n_local, zeros.shape[0]):
-            m = min(zeros.shape[0], n_local - r)
-            sh.index.add_device(zeros.data_ptr(), m, torch.cuda.current_stream(dev).cuda_stream)
-        del zeros
     elif args.shard_of > 1:
         sh.row0, sh.n_total = row0, N
         sh.index.add_synthetic(SEED_CORPUS, row0, n_local, True)
@@ -378,7 +369,11 @@ def main():
                 "mfma_tflops": round(alg_flops / (kavg * 1e-3) / 1e12, 1),
                 "mfma_frac": round(alg_flops / (kavg * 1e-3) / 1e12 / peak_flops, 4),
                 "mfma_peak_tflops": peak_flops,
-                **_power_ceiling(kind, args.workload, alg_bytes, n_local, N),
+                # the same box's zero / real operand pair of the main screen kernels (vs_screen_probe)
+                "power_pair": _power_pair(ix, q, nq, kind, alg_bytes,
+                                          n_local * d * es + nq * d * es + nq * k * 12 +
+                                          (n_local * 4 if args.metric == "l2" else 0),
+                                          torch.cuda.current_stream(dev).cuda_stream),
             },
             # first-pass certificate failures; every one was re-searched exactly (search_device_exact)
             "uncertified_first_pass": uncert,
@@ -409,25 +404,30 @@ def main():
         dist.destroy_process_group()
 
 
-def _power_ceiling(kind: str, workload: str, alg_bytes: int, n_local: int, N: int) -> dict:
-    """The int8 K1 loop's own bound on this board (profiles/r04_k1_power_pair.json, from
-    scripts/k1_micro.hip mode 9 at the cfg3 shape): the same loop (loads + query-fragment reads + MFMAs +
-    the product's bound epilogue) on int8 codes of Gaussian rows vs on an all-zero corpus -- equal cycles, but the board holds a
-    lower clock under the MFMAs on random operands.  ``power_ceiling_ms`` is that loop's time on
-    random codes scaled to this launch's rows: no schedule of the same MFMA work goes below it on
-    this board, so ``frac`` cannot exceed ``power_ceiling_frac``."""
-    if kind != "mfma_i8" or workload != "cfg3":  # (the micro ran at cfg3's d = 1536)
+def _power_pair(ix, q, nq: int, kind: str, alg_bytes: int, alg_bytes_native: int, stream: int) -> dict:
+    """The box's own zero / real operand pair, measured in this process after the timed steps
+    (include/vs.h ``vs_screen_probe``): one launch of each main screen kernel over the same rows with
+    every threshold at +inf (the K loop + the epilogue's bound test, no survivors), once with the real
+    query tile and once with the tile zeroed (one MFMA operand all zeros).  Same code, same bytes,
+    same cycles per K-step: what differs is the clock the board holds under the MFMAs on real
+    operands (DESIGN §6 "Power").  A reference beside ``frac``, not a bound: boards differ by up
+    to ~12 % (MI355X_MICROARCH DVFS), and the product kernel also inserts survivors."""
+    if kind != "mfma_i8":
         return {}
-    try:
-        with open(os.path.join(REPO, "profiles", "r04_k1_power_pair.json")) as f:
-            pp = json.load(f)
-    except (OSError, ValueError):
-        return {}
-    ms = float(pp["full_random_codes_ms"]) * n_local / float(pp["rows"])
-    return {"power_ceiling_ms": round(ms, 4),
-            "power_ceiling_frac": round(alg_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-            "power_ceiling_zero_operands_ms": round(float(pp["full_zero_ms"]) * n_local / float(pp["rows"]), 4),
-            "power_ceiling_source": "profiles/r04_k1_power_pair.json (scripts/k1_micro.hip)"}
+    out = {}
+    for scr, ab in (("int8", alg_bytes), ("native", alg_bytes_native)):
+        try:
+            real = ix.screen_probe(q.data_ptr(), nq, scr, False, stream)
+            zero = ix.screen_probe(q.data_ptr(), nq, scr, True, stream)
+        except Exception as e:  # (the probe needs the direct screens: d a multiple of 256)
+            out[scr] = {"skipped": str(e)[:120]}
+            continue
+        out[scr] = {"loop_ms": round(real, 4), "zero_query_ms": round(zero, 4),
+                    "loop_frac": round(ab / (real * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                    "zero_query_frac": round(ab / (zero * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    out["note"] = ("five launches back to back per form, the fastest; thresholds at +inf (no survivors); "
+                   "zero_query = the packed query tile zeroed; same process and box as the timed steps")
+    return out
 
 
 def _gather_rows(row, G, dev, backend, torch, dist):

@@ -173,6 +173,14 @@ const char* vs_version(void);
  * the stream it is launched on.  vs_timing_fetch synchronises those events and returns up to
  * `cap` per-launch durations (ms), oldest first, then clears them. */
 int vs_set_timing(vs_index* index, int enable);
+/* One launch of the main screen kernel (screen = VS_SCREEN_I8: the int8 direct screen; NATIVE: the
+ * bf16 / f16 direct screen) over the whole index for 9..256 device queries, every query's threshold
+ * at +inf (the bound test passes nothing: the K loop + epilogue test, no survivors); zero_queries
+ * zeroes the packed query tile first, so one MFMA operand is all zeros.  Five launches back to
+ * back; *ms = the fastest one's duration (HIP events on `stream`, synchronised).  bench.py runs both forms in the same process as the timed
+ * steps: the box's own zero / real operand pair behind the power note of its roofline. */
+int vs_screen_probe(vs_index* index, const float* q_dev, int64_t nq, int32_t screen, int32_t zero_queries,
+                    void* stream, float* ms);
 int vs_timing_fetch(vs_index* index, float* ms, int cap, int* kernel_kind);
 int64_t vs_uncertified_count(vs_index* index);   /* first-pass certificate failures; synchronises */
 /* queries answered by the exact full scan (no bounded screen could certify them; see

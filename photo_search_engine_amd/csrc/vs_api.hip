@@ -1579,6 +1579,96 @@ int vs_set_screen(vs_index* ix, int screen) {
 
 int vs_screen(const vs_index* ix) { return ix ? ix->screen : -1; }
 
+int vs_screen_probe(vs_index* ix, const float* q_dev, int64_t nq, int32_t screen, int32_t zero_queries, void* stream,
+                    float* ms) {
+    return guarded([&] {
+        check_index(ix);
+        if (!q_dev || !ms || nq <= GEMV_NQ_MAX || nq > MFMA_QB) throw VsError(VS_ERR_ARG, "vs_screen_probe: 9..256 device queries");
+        std::shared_lock<std::shared_mutex> lk(ix->rw);
+        DeviceGuard dg(ix->device);
+        const bool i8 = screen == VS_SCREEN_I8;
+        if (i8 && (ix->screen != VS_SCREEN_I8 || !ix->data8 || ix->i8_res || !i8_direct_ok(ix->dpad8)))
+            throw VsError(VS_ERR_ARG, "vs_screen_probe: the int8 probe needs the int8 direct screen (no group residuals)");
+        if (!i8 && !((ix->dtype == DT_BF16 || ix->dtype == DT_F16) && d16_direct_ok(ix->dpad)))
+            throw VsError(VS_ERR_ARG, "vs_screen_probe: the native probe needs bf16 / f16 rows of the direct screen");
+        if (ix->ntotal == 0) throw VsError(VS_ERR_ARG, "index is empty");
+        hipStream_t st = (hipStream_t)stream;
+        CtxLease L(ix, st, false);
+        Ctx* c = L.c;
+        const int nqb = (int)nq;
+        const int64_t tiles = (ix->ntotal + TR - 1) / TR;
+        ScreenArgs a{};
+        a.n_valid = ix->ntotal;
+        a.tiles = (int)tiles;
+        a.d = ix->d;
+        a.metric = ix->metric;
+        a.sqn = ix->sqn;
+        a.Kp = MFMA_KP_MAX;
+        a.cap = MFMA_CAP;
+        a.G = (int)std::max<int64_t>(1, std::min<int64_t>(tiles, ix->num_cu));
+        a.lcap = a.G * a.Kp;
+        c->gcnt.ensure(sizeof(int) * MFMA_QB);
+        c->drop.ensure(sizeof(u64) * MFMA_QB);
+        c->fails.ensure(2 * sizeof(int));
+        if (i8) {
+            c->qtile.ensure((size_t)MFMA_QB * ix->dpad8);
+            c->qfac.ensure(sizeof(float2) * MFMA_QB);
+            c->qeps.ensure(sizeof(float) * MFMA_QB);
+            HIP_CHECK(launch_pack_qtile_i8(q_dev, nqb, ix->d, ix->dpad8, c->qtile.as<uint8_t>(), c->qfac.as<float2>(),
+                                           c->qeps.as<float>(), ix->d_maxsq + 2, c->gcnt.as<int>(), c->drop.as<u64>(), st,
+                                           c->fails.as<int>(), ix->metric == METRIC_L2 ? ix->d_maxsq : nullptr,
+                                           gamma_of(ix->d)));
+            a.corpus = ix->data8;
+            a.dpad = ix->dpad8;
+            a.rsb = ix->rsb;
+            a.qfac = c->qfac.as<float2>();
+        } else {
+            c->qtile.ensure((size_t)MFMA_QB * ix->dpad * ix->es);
+            c->qinfo.ensure(sizeof(float) * 2 * MFMA_QB);
+            HIP_CHECK(launch_pack_qtile(ix->dtype, q_dev, nqb, ix->d, ix->dpad, c->qtile.as<uint8_t>(),
+                                        c->qinfo.as<float>(), c->gcnt.as<int>(), c->drop.as<u64>(), st));
+            a.corpus = ix->data;
+            a.dpad = ix->dpad;
+        }
+        if (zero_queries) HIP_CHECK(hipMemsetAsync(c->qtile.p, 0, c->qtile.bytes, st));
+        // every query's threshold at the key of +inf: the bound test rejects every column, so the
+        // launch is the K loop + the epilogue's bound test with no survivor to insert
+        c->thr0.ensure(sizeof(u64) * MFMA_QB);
+        std::vector<u64> thr(MFMA_QB, 0xFF80000000000000ull);
+        HIP_CHECK(hipMemcpyAsync(c->thr0.p, thr.data(), sizeof(u64) * MFMA_QB, hipMemcpyHostToDevice, st));
+        a.thr0 = c->thr0.as<u64>();
+        a.drop = c->drop.as<u64>();
+        c->cand.ensure((size_t)a.G * MFMA_QB * a.cap * sizeof(u64));
+        c->part.ensure((size_t)MFMA_QB * a.lcap * sizeof(u64));
+        a.cand = c->cand.as<u64>();
+        a.glist = c->part.as<u64>();
+        a.gcnt = c->gcnt.as<int>();
+        // kProbeReps launches back to back (the cadence of the timed steps, no host gap between
+        // them), each between its own events; the fastest one is reported
+        constexpr int kProbeReps = 5;
+        hipEvent_t ev[kProbeReps + 1];
+        for (hipEvent_t& e : ev) HIP_CHECK(hipEventCreate(&e));
+        hipError_t le = hipSuccess;
+        HIP_CHECK(hipEventRecord(ev[0], st));
+        for (int i = 0; i < kProbeReps && le == hipSuccess; ++i) {
+            le = launch_screen_mfma(i8 ? DT_I8 : ix->dtype, a, c->qtile.as<uint8_t>(), nqb, st);
+            HIP_CHECK(hipEventRecord(ev[i + 1], st));
+        }
+        HIP_CHECK(hipEventSynchronize(ev[kProbeReps]));  // (also keeps the host threshold array alive)
+        float best = 0.0f;
+        hipError_t te = hipSuccess;
+        for (int i = 0; i < kProbeReps && te == hipSuccess; ++i) {
+            float t = 0.0f;
+            te = hipEventElapsedTime(&t, ev[i], ev[i + 1]);
+            if (i == 0 || t < best) best = t;
+        }
+        for (hipEvent_t& e : ev) (void)hipEventDestroy(e);
+        HIP_CHECK(le);
+        HIP_CHECK(te);
+        *ms = best;
+    });
+}
+
 int vs_set_timing(vs_index* ix, int enable) {
     return guarded([&] {
         check_index(ix);

@@ -295,28 +295,115 @@ void search_core(vs_ivf* ix, const float* q_dev, int64_t nq, int k, int nprobe, 
     }
     // (algorithmic bytes above: every probed list read once; the GEMV scan re-reads a list per
     // query group, the MFMA scan per 128-query block -- that extra traffic is not algorithmic)
-    // The MFMA scans run as ONE launch: each scan's pages are cut into workgroup chunks of about
-    // the same size (~2 workgroups per CU in all), heaviest chunks dispatched first, so small and
-    // large lists share the chip without per-list launches or an idle tail.
+    // The MFMA scans run as ONE launch of ~2 workgroups per CU (one resident per CU, LDS-bound), each
+    // over a chunk of one scan's pages with that scan's query tile -- re-read from L2 once per page.
+    // XCD grouping: workgroups b and b + 8 share an XCD and its 4 MB L2 (blocks are dealt round-robin
+    // over the 8 XCDs; observed placement, used for speed only), so the scans are dealt to 8 groups
+    // in order of size, each group filled to 1/8 of the pages (a scan larger than that spans groups),
+    // and group x's W chunks take descriptor slots x, x + 8, x + 16, ...: an XCD then holds the query
+    // tiles of ~1/8 of the scans instead of all of them (mapped-scan traffic 1.116x -> see DESIGN §7c).
     std::vector<int>& desc = ix->desc_h;
     desc.clear();
     if (!mscans.empty()) {
-        const int64_t chunk = std::min<int64_t>(MFMA_MAP_TILES, std::max<int64_t>(1, (mtiles + 2 * ix->num_cu - 1) /
-                                                                                         (2 * ix->num_cu)));
-        struct Wg { int nt, tm_off, t0, nvalid, qti, qoff, nqb; };
-        std::vector<Wg> wgs;
-        for (int si = 0; si < (int)mscans.size(); ++si) {
-            const MScan& m = mscans[si];
-            const int64_t np = (int64_t)ix->pages[m.l].size();
-            const int64_t G = (np + chunk - 1) / chunk;
-            for (int64_t i = 0; i < G; ++i) {
-                const int64_t t0 = np * i / G, t1 = np * (i + 1) / G;
-                wgs.push_back({(int)(t1 - t0), ix->page_off_h[m.l] + (int)t0, (int)t0, (int)ix->list_n[m.l], si, m.q0,
-                               m.nqb});
+        constexpr int NX = 8;
+        struct Seg { int si, p0, p1; };  // pages [p0, p1) of scan si
+        std::vector<int> order((size_t)mscans.size());
+        for (size_t i = 0; i < order.size(); ++i) order[i] = (int)i;
+        std::stable_sort(order.begin(), order.end(), [&](int x, int y) {
+            return ix->pages[mscans[x].l].size() > ix->pages[mscans[y].l].size();
+        });
+        std::vector<std::vector<Seg>> grp(NX);
+        std::vector<int64_t> gp(NX, 0);
+        {
+            const int64_t target = (mtiles + NX - 1) / NX;
+            int x = 0;
+            for (int si : order) {
+                const int np = (int)ix->pages[mscans[si].l].size();
+                int p0 = 0;
+                while (p0 < np) {
+                    if (x < NX - 1 && gp[x] >= target) ++x;
+                    const int take = x < NX - 1 ? (int)std::min<int64_t>(np - p0, std::max<int64_t>(1, target - gp[x])) : np - p0;
+                    grp[x].push_back({si, p0, p0 + take});
+                    gp[x] += take;
+                    p0 += take;
+                }
             }
-            for (int j = 0; j < m.nqb; ++j) per_q[mq[m.q0 + j]] += G * Kp;
         }
-        std::stable_sort(wgs.begin(), wgs.end(), [](const Wg& x, const Wg& y) { return x.nt > y.nt; });
+        // W chunks per group: ~2 workgroups per CU in all, at most MFMA_MAP_TILES pages each, at least
+        // one per segment
+        int W = std::max(1, (2 * ix->num_cu + NX - 1) / NX);
+        for (int x = 0; x < NX; ++x) {
+            W = std::max<int>(W, (int)grp[x].size());
+            W = std::max<int>(W, (int)((gp[x] + MFMA_MAP_TILES - 1) / MFMA_MAP_TILES));
+        }
+        struct Wg { int nt, tm_off, t0, nvalid, qti, qoff, nqb; };
+        std::vector<std::vector<Wg>> gw(NX);
+        for (int x = 0; x < NX; ++x) {
+            if (grp[x].empty()) continue;
+            // chunks per segment: proportional to its pages (>= 1, <= its pages, <= 256 pages each)
+            const int nseg = (int)grp[x].size();
+            std::vector<int> w(nseg);
+            int sum = 0;
+            for (int i = 0; i < nseg; ++i) {
+                const int64_t len = grp[x][i].p1 - grp[x][i].p0;
+                const int64_t lo = (len + MFMA_MAP_TILES - 1) / MFMA_MAP_TILES;
+                w[i] = (int)std::min<int64_t>(len, std::max<int64_t>(lo, (int64_t)std::llround((double)W * len / (double)gp[x])));
+                sum += w[i];
+            }
+            for (bool grew = true; sum < W && grew;) {  // top up (largest pages per chunk first)
+                grew = false;
+                int best = -1;
+                double bpc = 0.0;
+                for (int i = 0; i < nseg; ++i) {
+                    const int len = grp[x][i].p1 - grp[x][i].p0;
+                    if (w[i] < len && (double)len / w[i] > bpc) {
+                        bpc = (double)len / w[i];
+                        best = i;
+                    }
+                }
+                if (best >= 0) {
+                    ++w[best];
+                    ++sum;
+                    grew = true;
+                }
+            }
+            for (bool shrank = true; sum > W && shrank;) {  // trim (smallest pages per chunk first)
+                shrank = false;
+                int best = -1;
+                double bpc = 1e300;
+                for (int i = 0; i < nseg; ++i) {
+                    const int len = grp[x][i].p1 - grp[x][i].p0;
+                    const int lo = (len + MFMA_MAP_TILES - 1) / MFMA_MAP_TILES;
+                    if (w[i] > std::max(1, lo) && (double)len / w[i] < bpc) {
+                        bpc = (double)len / w[i];
+                        best = i;
+                    }
+                }
+                if (best >= 0) {
+                    --w[best];
+                    --sum;
+                    shrank = true;
+                }
+            }
+            for (int i = 0; i < nseg; ++i) {
+                const Seg& g = grp[x][i];
+                const MScan& m = mscans[g.si];
+                const int64_t len = g.p1 - g.p0;
+                for (int c = 0; c < w[i]; ++c) {
+                    const int t0 = g.p0 + (int)(len * c / w[i]), t1 = g.p0 + (int)(len * (c + 1) / w[i]);
+                    gw[x].push_back({t1 - t0, ix->page_off_h[m.l] + t0, t0, (int)ix->list_n[m.l], g.si, m.q0, m.nqb});
+                }
+                for (int j = 0; j < m.nqb; ++j) per_q[mq[m.q0 + j]] += w[i] * Kp;
+            }
+            std::stable_sort(gw[x].begin(), gw[x].end(), [](const Wg& a_, const Wg& b_) { return a_.nt > b_.nt; });
+        }
+        // slot 8 j + x <- group x's j-th chunk (a group short of chunks: the others close ranks)
+        std::vector<Wg> wgs;
+        size_t maxlen = 0;
+        for (auto& v : gw) maxlen = std::max(maxlen, v.size());
+        for (size_t j = 0; j < maxlen; ++j)
+            for (int x = 0; x < NX; ++x)
+                if (j < gw[x].size()) wgs.push_back(gw[x][j]);
         ix->n_mdesc = (int)wgs.size();
         const int64_t tmap_len = ix->page_off_h.back();
         for (const Wg& w : wgs) {

@@ -200,6 +200,14 @@ class FlatIndex:
                 "max_row_error", "i8_union_log2", "i8_routed_searches", "native_seed_log2")
         return {k: (float(buf[i]) if "max" in k else int(buf[i])) for i, k in enumerate(keys)}
 
+    def screen_probe(self, q_ptr: int, nq: int, screen: str, zero_queries: bool, stream: Optional[int] = None) -> float:
+        """ms of one main-screen launch over the index with every threshold at +inf (no survivors),
+        the query tile zeroed when ``zero_queries`` (include/vs.h ``vs_screen_probe``)."""
+        ms = ctypes.c_float(0.0)
+        check(self._L.vs_screen_probe(self._h, q_ptr, int(nq), FlatIndex.SCREENS[screen], int(bool(zero_queries)),
+                                      stream or None, ctypes.byref(ms)))
+        return float(ms.value)
+
     def full_scan_count(self) -> int:
         """Queries answered by the exact full scan so far: no bounded screen could certify them (more
         rows than KP_MAX tied within its margin).  Synchronises."""
