@@ -489,6 +489,29 @@ void search_core(vs_ivf* ix, const float* q_dev, int64_t nq, int k, int nprobe, 
         HIP_CHECK(hipEventCreate(&e1));
         HIP_CHECK(hipEventRecord(e0, st));
     }
+    // Both scans at once when both have work: the GEMV scan (HBM-bound, 8 small workgroups per CU)
+    // on a side stream beside the MFMA scan (power-bound, one LDS-heavy workgroup per CU), so the
+    // chip streams the GEMV lists while the MFMAs run instead of after them; they share only the
+    // per-query list counters (atomics) and write disjoint candidate slots.
+    const int n_dyn_items = (int)(total_ints / IVF_ITEM_INTS);
+    const bool concurrent = dyn && !mscans.empty() && n_dyn_items > 0;
+    hipStream_t dst = st;
+    if (concurrent) {
+        if (!ix->astream[0]) {
+            for (int i = 0; i < 8; ++i) HIP_CHECK(hipStreamCreateWithFlags(&ix->astream[i], hipStreamNonBlocking));
+            for (int i = 0; i <= 8; ++i) HIP_CHECK(hipEventCreateWithFlags(&ix->aev[i], hipEventDisableTiming));
+        }
+        dst = ix->astream[0];
+        ix->next_item.ensure(sizeof(int));
+        HIP_CHECK(hipMemsetAsync(ix->next_item.p, 0, sizeof(int), st));
+        HIP_CHECK(hipEventRecord(ix->aev[0], st));  // fork: queries packed, list counters zeroed
+        HIP_CHECK(hipStreamWaitEvent(dst, ix->aev[0], 0));
+        a.next_item = ix->next_item.as<int>();
+        a.items = ix->items.as<int>();
+        a.n_items = n_dyn_items;
+        HIP_CHECK(launch_ivf_scan_dyn(ix->dtype, a, std::min(a.n_items, max_grid), dst));
+        HIP_CHECK(hipEventRecord(ix->aev[1], dst));
+    }
     // lists probed by many queries: the MFMA screen over their pages (unseeded; every workgroup
     // appends its best Kp per query to the query's list, which the refine cuts to Kp)
     if (!mscans.empty()) {
@@ -519,7 +542,9 @@ void search_core(vs_ivf* ix, const float* q_dev, int64_t nq, int k, int nprobe, 
         HIP_CHECK(launch_screen_mfma_mapped(ix->dtype, sa, ix->mqtile.as<uint8_t>(), st));
     }
     size_t off = 0;
-    if (dyn) {
+    if (concurrent) {
+        HIP_CHECK(hipStreamWaitEvent(st, ix->aev[1], 0));  // join
+    } else if (dyn) {
         ix->next_item.ensure(sizeof(int));
         HIP_CHECK(hipMemsetAsync(ix->next_item.p, 0, sizeof(int), st));
         a.next_item = ix->next_item.as<int>();
