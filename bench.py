@@ -444,6 +444,8 @@ def _kernel_name(kind: str, dtype: str, d: int, n_local: int = 0, metric: str = 
     int8 codes taken against group means (``residual``) run the inner-product form that adds
     <mu_g, q> to every key."""
     dpad = max(-(-d // 64) * 64, 64)
+    if kind == "full_scan":
+        return "k_full_scan"
     if kind == "mfma_i8" and dpad % 256 == 0 and dpad >= 512:
         return "k_screen_i8d_res" if residual and metric == "ip" else "k_screen_i8d"
     if kind == "mfma" and dtype in ("bf16", "f16") and dpad % 128 == 0 and dpad >= 256:
@@ -644,8 +646,9 @@ def _mixture_rows(seed, r0, m, d, centroids, sigma, dev, stream, cdf=None):
 def run_cfg1(args):
     """BASELINE cfg1 end to end through the drop-in: ``VectorStore(dimension=1536)`` over 10k raw
     rows (bulk ``add``; the store normalises them as the reference does), one step = ONE
-    ``store.search(query_list, 10)`` call -- host normalisation, the C-ABI call (H2D query, GEMV
-    screen + exact refine, D2H) and the result dicts -- over a cycle of 256 distinct queries.
+    ``store.search(query_list, 10)`` call -- host normalisation, the C-ABI call (H2D query, the
+    exact full scan of the 61 MB corpus in one launch, D2H) and the result dicts -- over a cycle of
+    256 distinct queries.
     value = calls per second; the dominant kernel's time comes from the library's HIP events.
     Beside it: the faiss IndexFlatIP sequential scan (nq < 20) restated on one host thread, the
     per-call latency faiss-cpu gives the reference at this config, and the ids of every timed call

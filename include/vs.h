@@ -173,6 +173,12 @@ const char* vs_version(void);
  * the stream it is launched on.  vs_timing_fetch synchronises those events and returns up to
  * `cap` per-launch durations (ms), oldest first, then clears them. */
 int vs_set_timing(vs_index* index, int enable);
+/* Calls of 1-2 queries with k <= 64 over an index of at most 65536 rows and at most `bytes` stored
+ * bytes (rows x padded d x element size; default 192 MiB) skip the screen: one launch scores every
+ * row exactly and selects the top-k (the full scan of vs_search_device_exact's last tier, run
+ * first) -- the product's single-query call on a photo library, BASELINE cfg1.  0 = always screen
+ * (tests of the screen kernels).  Results are the same bits either way. */
+int vs_set_scan_limit(vs_index* index, int64_t bytes);
 /* One launch of the main screen kernel (screen = VS_SCREEN_I8: the int8 direct screen; NATIVE: the
  * bf16 / f16 direct screen) over the whole index for 9..256 device queries, every query's threshold
  * at +inf (the bound test passes nothing: the K loop + epilogue test, no survivors); zero_queries

@@ -84,6 +84,7 @@ _SIGS = {
     "vs_timing_fetch": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
     "vs_uncertified_count": (_c_i64, [_vp]),
     "vs_full_scan_count": (_c_i64, [_vp]),
+    "vs_set_scan_limit": (ctypes.c_int, [_vp, _c_i64]),
     "vs_screen_probe": (ctypes.c_int, [_vp, _vp, _c_i64, ctypes.c_int32, ctypes.c_int32, _vp, _vp]),
     "vs_host_staging_bytes": (_c_i64, [_vp]),
     "vs_screen_copy_bytes": (_c_i64, [_vp]),

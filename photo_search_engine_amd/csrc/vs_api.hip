@@ -86,6 +86,8 @@ struct Ctx {
 
 void vs::set_last_error(const std::string& msg) { g_err = msg; }
 
+constexpr int64_t kDefaultScanLimit = 192ll << 20;  // (the MALL holds such a corpus between calls)
+
 struct vs_index {
     int d = 0, dpad = 0, metric = 0, dtype = 0, device = 0, es = 4;
     int num_cu = 256;
@@ -121,7 +123,10 @@ struct vs_index {
     std::atomic<bool> timing{false};
     std::mutex tmtx;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> tev;
-    int last_kernel_kind = 0;  // 1 = mfma, 2 = gemv, 3 = int8 mfma
+    // corpora of at most this many stored bytes answer calls of 1-2 queries with the exact full scan
+    // alone (vs_set_scan_limit; 0 = never)
+    std::atomic<int64_t> scan_limit{kDefaultScanLimit};
+    int last_kernel_kind = 0;  // 1 = mfma, 2 = gemv, 3 = int8 mfma, 4 = int8 gemv, 5 = exact full scan
     // Screen health (first passes of MFMA batches): the certificate-failure count of a batch is read
     // back without a host wait (pinned word + event, observed by a later search).  A failed query
     // costs its block a full fallback round, so the index adapts to its corpus:
@@ -807,8 +812,7 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
     r.optimistic = optimistic ? 1 : 0;
     r.nsplit = redo ? 1 : refine_split(nqb, Kp, ix->dtype, ix->num_cu);
     if (r.nsplit > 1) {
-        int KP2 = 1;
-        while (KP2 < Kp) KP2 <<= 1;
+        const int KP2 = refine_kp2(Kp);
         c->rsc.ensure((size_t)nqb * KP2 * 12);
         r.gsc = c->rsc.as<double>();
         r.gids = (uint32_t*)(r.gsc + (size_t)nqb * KP2);
@@ -842,11 +846,13 @@ int fallback_depth(const vs_index* ix) { return (int)std::min<int64_t>(KP_MAX, r
 // gate: the fallback round's failure count (c->fails[1]; the launch returns at once while it is
 // 0), or null = run.  Scanned queries count in this call's counter or the index's d_unres.
 constexpr int64_t kFullScanScratch = 32ll << 20;  // per-workgroup lists of one block, at most
+// rows_per_wg: each workgroup's row range is at least this long (G = rows / rows_per_wg, <= CUs)
 void full_scan_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float* D, int64_t* I, double* S64,
-                     int* cert, int64_t id_offset, hipStream_t st, const int* gate, int ostride = 1) {
-    const int64_t tiles = (ix->ntotal + TR - 1) / TR;
+                     int* cert, int64_t id_offset, hipStream_t st, const int* gate, int ostride = 1,
+                     int rows_per_wg = TR, bool fallback = true) {
+    const int64_t ranges = (ix->ntotal + rows_per_wg - 1) / rows_per_wg;
     const int64_t per_wg = (int64_t)nqb * k * 12;
-    const int G = (int)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(ix->num_cu, tiles),
+    const int G = (int)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(ix->num_cu, ranges),
                                                                kFullScanScratch / per_wg));
     c->fsc.ensure(full_scan_scratch_bytes(nqb, G, k));
     if (c->fdone.bytes < sizeof(unsigned) * MFMA_QB) {  // zeroed once; each query's last workgroup re-zeroes
@@ -873,17 +879,53 @@ void full_scan_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float
     a.gsc = c->fsc.as<double>();
     a.gid = (uint32_t*)(a.gsc + (size_t)nqb * G * k);
     a.gdone = c->fdone.as<unsigned>();
-    a.count = c->unres ? c->unres : ix->d_unres;
+    a.count = !fallback ? nullptr : c->unres ? c->unres : ix->d_unres;  // (a first pass is counted nowhere)
     a.G = G;
     HIP_CHECK(launch_full_scan(a, st));
 }
 
 // Full search of nq device queries; outputs device [nq][k].  device_fallback: every block's first
 // pass is followed by its gated fallback round (no host round trip; MFMA dtypes only).
+// (measured against the GEMV screen + refine, scripts/small_scan_timing.py: the scan wins up to
+// ~190 MB at d >= 1536 and k = 10; more rows, smaller d or deeper k favour the screen)
+constexpr int kSmallScanQ = 2;           // queries per call
+constexpr int kSmallScanMaxK = 64;
+constexpr int64_t kSmallScanMaxRows = 65536;
+constexpr int kSmallScanRows = 64;       // rows per workgroup range
+bool small_scan(const vs_index* ix, int64_t nq, int k) {
+    return nq <= kSmallScanQ && k <= kSmallScanMaxK && ix->ntotal <= kSmallScanMaxRows &&
+           (int64_t)ix->ntotal * ix->dpad * ix->es <= ix->scan_limit.load();
+}
+
 void search_all(vs_index* ix, Ctx* c, const float* q, int64_t nq, int k, int Kp, float* D, int64_t* I, double* S64,
                 int* cert, int64_t id_offset, hipStream_t st, int seed_rank, bool device_fallback = false) {
-    const int64_t tiles = (ix->ntotal + TR - 1) / TR;
-    (void)tiles;
+    // One or two queries over a small corpus (the product's single-query call, BASELINE cfg1): the
+    // exact full scan alone -- every row scored canonically in one launch, no screen, no refine, no
+    // certificate to fail (measured: DESIGN §5 "Small corpora").  First passes only (seed_rank > 0):
+    // a re-search of a certificate failure never reaches here, since this path has none.
+    if (seed_rank > 0 && small_scan(ix, nq, k)) {
+        int* cq = cert;
+        if (!cq) {
+            c->cert.ensure((size_t)nq * sizeof(int));
+            cq = c->cert.as<int>();
+        }
+        HIP_CHECK(hipMemsetAsync(cq, 0, (size_t)nq * sizeof(int), st));
+        const bool timing = ix->timing.load();
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (timing) {
+            HIP_CHECK(hipEventCreate(&e0));
+            HIP_CHECK(hipEventCreate(&e1));
+            HIP_CHECK(hipEventRecord(e0, st));
+        }
+        full_scan_block(ix, c, q, (int)nq, k, D, I, S64, cq, id_offset, st, nullptr, 1, kSmallScanRows, false);
+        if (timing) {
+            HIP_CHECK(hipEventRecord(e1, st));
+            std::lock_guard<std::mutex> g(ix->tmtx);
+            ix->tev.emplace_back(e0, e1);
+            ix->last_kernel_kind = 5;
+        }
+        return;
+    }
     const bool i8 = seed_rank > 0 && i8_allowed(ix);  // (int8 screen on, and not routed away)
     const bool mfma_ok = (i8 && k <= I8_MAX_K) || ix->dtype != DT_F32;
     int64_t done = 0;
@@ -1666,6 +1708,14 @@ int vs_screen_probe(vs_index* ix, const float* q_dev, int64_t nq, int32_t screen
         HIP_CHECK(le);
         HIP_CHECK(te);
         *ms = best;
+    });
+}
+
+int vs_set_scan_limit(vs_index* ix, int64_t bytes) {
+    return guarded([&] {
+        check_index(ix);
+        if (bytes < 0) throw VsError(VS_ERR_ARG, "scan limit must be >= 0");
+        ix->scan_limit.store(bytes);
     });
 }
 

@@ -185,6 +185,54 @@ __device__ __forceinline__ u64 wave_kth(const u64 (&keys)[E], int K) {
     return t;
 }
 
+// ... any threshold t with Klo <= #(keys >= t) <= Khi (the bisection stops at the first prefix
+// whose count lands in the range; starts below the keys' common prefix)
+template <int E>
+__device__ __forceinline__ u64 wave_kth_range(const u64 (&keys)[E], int Klo, int Khi) {
+    u64 kmax = 0ull, kmin = ~0ull;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        kmax = keys[e] > kmax ? keys[e] : kmax;
+        kmin = (keys[e] != 0ull && keys[e] < kmin) ? keys[e] : kmin;
+    }
+    kmax = wave_max_u64(kmax);
+    kmin = wave_min_u64(kmin);
+    u64 t = 0;
+    int bstart = 63;
+    if (kmin != ~0ull && kmax != kmin) {
+        bstart = 63 - __clzll((long long)(kmax ^ kmin));
+        t = kmax & ~((2ull << bstart) - 1ull);
+    }
+    for (int b = bstart; b >= 0; --b) {
+        const u64 cand = t | (1ull << b);
+        int c = 0;
+#pragma unroll
+        for (int e = 0; e < E; ++e) c += keys[e] >= cand ? 1 : 0;
+        c = wave_sum_i(c);
+        if (c >= Klo) {
+            t = cand;
+            if (c <= Khi) break;
+        }
+    }
+    return t;
+}
+// K-th largest of n distinct keys in LDS / memory by ONE wave (no block barriers)
+__device__ __forceinline__ u64 wave_kth_buf(const u64* buf, int n, int K) {
+    const int lane = threadIdx.x & 63;
+    u64 t = 0;
+    for (int b = 63; b >= 0; --b) {
+        const u64 cand = t | (1ull << b);
+        int c = 0;
+        for (int i = lane; i < n; i += 64) c += buf[i] >= cand ? 1 : 0;
+        c = wave_sum_i(c);
+        if (c >= K) {
+            t = cand;
+            if (c == K) break;
+        }
+    }
+    return t;
+}
+
 // Over a whole block: a threshold t with Klo <= #(keys >= t) <= Khi (distinct keys, Klo <= #keys): the bit bisection of
 // block_kth, stopping at the first prefix whose count lands in the range (Khi = Klo: the Klo-th
 // largest key).  One barrier per step: the per-wave counts alternate between the two halves of

@@ -81,6 +81,32 @@ __device__ __forceinline__ void fs_merge(const FsLists& L, int& cur, int& nl, in
     nl = min(k, nl + nb);
 }
 
+// sort the batch's nb entries (bitonic over the next power of two, worst-padded) and merge them in
+__device__ __forceinline__ void fs_sort_merge(const FsLists& L, int& cur, int& nl, int nb, int k) {
+    int n2 = 1;
+    while (n2 < nb) n2 <<= 1;
+    for (int j = nb + (int)threadIdx.x; j < n2; j += FS_THREADS) {
+        L.bsc[j] = -INFINITY;
+        L.bid[j] = 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    sort_best_first<METRIC_IP>(L.bsc, L.bid, n2);
+    fs_merge(L, cur, nl, nb, k);
+}
+
+// rows per wave in flight: twice the refine's (one workgroup per CU here, so the registers are there)
+template <int DT>
+constexpr int fs_rows() { return DT == DT_F32 ? 4 : 8; }
+
+// agent-scope relaxed stores / loads (global_store / global_load ... sc1): the hand-off of the
+// workgroups' lists to the last one needs no cache fence (MI355X_MICROARCH "valid forms": every byte
+// stored and loaded sc1, every storing wave's vmcnt(0) before ONE lane's agent-scope counter add,
+// the last adder told by the value its add returned, its waves loading after a barrier)
+template <typename T>
+__device__ __forceinline__ void st_agent(T* p, T v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+template <typename T>
+__device__ __forceinline__ T ld_agent(const T* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
 template <int DT, int METRIC, bool QLDS>
 __global__ void __launch_bounds__(FS_THREADS) k_full_scan(FullScanArgs a, int KL) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -96,8 +122,9 @@ __global__ void __launch_bounds__(FS_THREADS) k_full_scan(FullScanArgs a, int KL
     L.lid[0] = (uint32_t*)(qs + (QLDS ? (size_t)ng * 8 : 0));
     L.lid[1] = L.lid[0] + KL;
     L.bid = L.lid[1] + KL;
-    __shared__ int go_s, nb_s, cnt_s, last_s;
-    constexpr int RR = refine_rows<DT>();
+    __shared__ int go_s, nb_s, last_s;
+    __shared__ int red_s[FS_NW];
+    constexpr int RR = fs_rows<DT>();
     const int k = a.k;
     const int64_t r0 = a.n_valid * b / G, r1 = a.n_valid * (b + 1) / G;
     for (int q = 0; q < a.nq; ++q) {
@@ -143,15 +170,7 @@ __global__ void __launch_bounds__(FS_THREADS) k_full_scan(FullScanArgs a, int KL
             __syncthreads();
             const int nb = nb_s;
             if (nb > FS_B - FS_NW * RR || base + FS_NW * RR >= r1) {
-                if (nb > 0) {
-                    for (int j = nb + tid; j < FS_B; j += FS_THREADS) {
-                        L.bsc[j] = -INFINITY;
-                        L.bid[j] = 0xFFFFFFFFu;
-                    }
-                    __syncthreads();
-                    sort_best_first<METRIC_IP>(L.bsc, L.bid, FS_B);
-                    fs_merge(L, cur, nl, nb, k);
-                }
+                if (nb > 0) fs_sort_merge(L, cur, nl, nb, k);
                 if (tid == 0) nb_s = 0;
                 __syncthreads();
             }
@@ -160,44 +179,102 @@ __global__ void __launch_bounds__(FS_THREADS) k_full_scan(FullScanArgs a, int KL
         double* gs = a.gsc + ((size_t)q * G + b) * k;
         uint32_t* gi = a.gid + ((size_t)q * G + b) * k;
         for (int j = tid; j < k; j += FS_THREADS) {
-            gs[j] = j < nl ? L.lsc[cur][j] : -INFINITY;
-            gi[j] = j < nl ? L.lid[cur][j] : 0xFFFFFFFFu;
+            st_agent(gs + j, j < nl ? L.lsc[cur][j] : -INFINITY);
+            st_agent(gi + j, j < nl ? L.lid[cur][j] : 0xFFFFFFFFu);
         }
-        __threadfence();  // release (device scope: the other XCDs' L2s)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (every storing wave, before the add)
         __syncthreads();
-        if (tid == 0) last_s = atomicAdd(a.gdone + q, 1u) == (unsigned)(G - 1) ? 1 : 0;
+        if (tid == 0)
+            last_s = __hip_atomic_fetch_add(a.gdone + q, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                             (unsigned)(G - 1) ? 1 : 0;
         __syncthreads();
         if (!last_s) continue;
-        __threadfence();  // acquire the other workgroups' lists
-        for (int g = 0; g < G; ++g) {
-            if (g == b) continue;
-            const volatile double* vs_ = a.gsc + ((size_t)q * G + g) * k;
-            const volatile uint32_t* vi = a.gid + ((size_t)q * G + g) * k;
-            for (int c0 = 0; c0 < k; c0 += FS_B) {
-                const int j = c0 + tid;
+        // The other lists as one flat array [G][k].  First a floor: the k-th best of the G lists'
+        // heads (k distinct rows at least that good, so no entry below it can be in the top-k).  Then
+        // FS_B entries at a time (the next chunk's loads in flight): entries at least as good as the
+        // floor that beat the running k-th best are appended to the batch; a batch that would
+        // overflow, and the last one, are sorted and merged (few entries pass the floor).
+        {
+            const double* vs_ = a.gsc + (size_t)q * G * k;
+            const uint32_t* vi = a.gid + (size_t)q * G * k;
+            const int total = G * k;
+            // every load of the first FS_PF chunks (and the heads) issued before any is used
+            constexpr int FS_PF = 8;
+            auto fetch = [&](int j, double& s, uint32_t& id) {
+                s = -INFINITY;
+                id = 0xFFFFFFFFu;
+                if (j < total && j / k != b) {
+                    s = ld_agent(vs_ + j);
+                    id = ld_agent(vi + j);
+                }
+            };
+            double ps[FS_PF];
+            uint32_t pi[FS_PF];
+#pragma unroll
+            for (int c = 0; c < FS_PF; ++c) fetch(c * FS_B + tid, ps[c], pi[c]);
+            int h2 = 1;
+            while (h2 < G) h2 <<= 1;
+            for (int g = tid; g < h2; g += FS_THREADS) {
                 double s = -INFINITY;
                 uint32_t id = 0xFFFFFFFFu;
-                if (j < k) {
-                    s = vs_[j];
-                    id = vi[j];
+                if (g < G) {
+                    if (g == b) {
+                        if (nl > 0) {
+                            s = L.lsc[cur][0];
+                            id = L.lid[cur][0];
+                        }
+                    } else {
+                        s = ld_agent(vs_ + (size_t)g * k);
+                        id = ld_agent(vi + (size_t)g * k);
+                    }
                 }
-                // a sorted list: the entries that beat the running k-th best form a prefix
-                const bool full = nl >= k;
-                bool ok = j < k && id != 0xFFFFFFFFu;
-                if (ok && full) ok = fs_better(s, id, L.lsc[cur][k - 1], L.lid[cur][k - 1]);
-                if (tid == 0) cnt_s = FS_B;
-                __syncthreads();
-                if (!ok) atomicMin(&cnt_s, tid);
-                __syncthreads();
-                const int cnt = cnt_s;
-                if (tid < cnt) {
-                    L.bsc[tid] = s;
-                    L.bid[tid] = id;
-                }
-                __syncthreads();
-                if (cnt > 0) fs_merge(L, cur, nl, cnt, k);
-                if (cnt < FS_B) break;  // (block-uniform)
+                L.bsc[g] = s;
+                L.bid[g] = id;
             }
+            __syncthreads();
+            sort_best_first<METRIC_IP>(L.bsc, L.bid, h2);
+            const bool has_floor = G >= k && L.bid[k - 1] != 0xFFFFFFFFu;
+            const double fs = has_floor ? L.bsc[k - 1] : -INFINITY;
+            const uint32_t fi = has_floor ? L.bid[k - 1] : 0xFFFFFFFFu;
+            __syncthreads();  // (every thread has the floor before the batch is reused)
+            int nb = 0;  // entries waiting in the batch (block-uniform)
+            for (int c0 = 0, ci = 0; c0 < total; c0 += FS_B, ++ci) {
+                const int slot = ci % FS_PF;
+                double s = 0.0;
+                uint32_t id = 0u;
+#pragma unroll
+                for (int c = 0; c < FS_PF; ++c)
+                    if (c == slot) {
+                        s = ps[c];
+                        id = pi[c];
+                    }
+                if (slot == FS_PF - 1)  // this group of chunks is in registers: fetch the next group
+#pragma unroll
+                    for (int c = 0; c < FS_PF; ++c) fetch(c0 + (c + 1) * FS_B + tid, ps[c], pi[c]);
+                bool ok = id != 0xFFFFFFFFu;
+                if (ok && has_floor) ok = !fs_better(fs, fi, s, id);  // not below the floor
+                if (ok && nl >= k) ok = fs_better(s, id, L.lsc[cur][k - 1], L.lid[cur][k - 1]);
+                const u64 m = __ballot(ok);
+                if (lane == 0) red_s[wid] = __popcll(m);
+                __syncthreads();
+                int wb = 0, cnt = 0;
+                for (int i = 0; i < FS_NW; ++i) {
+                    if (i < wid) wb += red_s[i];
+                    cnt += red_s[i];
+                }
+                if (nb + cnt > FS_B) {  // (block-uniform) make room
+                    fs_sort_merge(L, cur, nl, nb, k);
+                    nb = 0;
+                }
+                if (ok) {
+                    const int pos = nb + wb + lane_prefix(m);
+                    L.bsc[pos] = s;
+                    L.bid[pos] = id;
+                }
+                nb += cnt;
+                __syncthreads();
+            }
+            if (nb > 0) fs_sort_merge(L, cur, nl, nb, k);
         }
         const size_t ost = a.ostride > 1 ? (size_t)a.ostride : 1;
         for (int j = tid; j < k; j += FS_THREADS) {
@@ -215,7 +292,7 @@ __global__ void __launch_bounds__(FS_THREADS) k_full_scan(FullScanArgs a, int KL
         }
         if (tid == 0) {
             a.cert[q] = 1;
-            a.gdone[q] = 0u;  // ready for the next launch (kernel boundary orders it)
+            st_agent(a.gdone + q, 0u);  // ready for the next launch
             if (a.count) atomicAdd(a.count, 1u);
         }
     }
@@ -223,8 +300,7 @@ __global__ void __launch_bounds__(FS_THREADS) k_full_scan(FullScanArgs a, int KL
 
 template <int DT, int METRIC, bool QLDS>
 static void launch_full_scan_one(const FullScanArgs& a, int KL, size_t lds, hipStream_t st) {
-    (void)hipFuncSetAttribute((const void*)k_full_scan<DT, METRIC, QLDS>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              152 * 1024);
+    set_lds_attr((const void*)k_full_scan<DT, METRIC, QLDS>, 152 * 1024);
     hipLaunchKernelGGL((k_full_scan<DT, METRIC, QLDS>), dim3(a.G), dim3(FS_THREADS), lds, st, a, KL);
 }
 
@@ -242,7 +318,7 @@ static void launch_full_scan_dt(const FullScanArgs& a, int KL, size_t lds, bool 
 size_t full_scan_scratch_bytes(int nq, int G, int k) { return (size_t)nq * G * k * 12; }
 
 hipError_t launch_full_scan(const FullScanArgs& a, hipStream_t st) {
-    if (a.nq <= 0 || a.k <= 0 || a.k > KP_MAX || a.G <= 0 || a.n_valid <= 0 || !a.cert || !a.I || !a.gsc || !a.gid ||
+    if (a.nq <= 0 || a.k <= 0 || a.k > KP_MAX || a.G <= 0 || a.G > FS_B || a.n_valid <= 0 || !a.cert || !a.I || !a.gsc || !a.gid ||
         !a.gdone || !a.q || !a.corpus)
         return hipErrorInvalidValue;
     int KL = 64;

@@ -319,6 +319,14 @@ struct RefineArgs {
     int tfloor_k;
     int ostride;           // I / S64 element stride (0/1 = separate arrays; 2 = interleaved (score bits, id))
 };
+// k_refine's kept-row capacity: a power of two >= 1.5 Kp (<= KP_MAX, >= Kp): its selection stops at
+// any count of the best keys in [Kp, refine_kp2(Kp)], which ends the bisection early
+inline int refine_kp2(int Kp) {
+    const int want = std::max(Kp, std::min(KP_MAX, Kp + Kp / 2));
+    int p = 1;
+    while (p < want) p <<= 1;
+    return p;
+}
 // workgroups per query of k_refine for a Kp-deep refine of nq queries (1 = no split)
 int refine_split(int nq, int Kp, int dt, int num_cu);
 hipError_t launch_refine(const RefineArgs& a, int nq, hipStream_t st);
@@ -346,6 +354,7 @@ struct FullScanArgs {
     int G;                  // workgroups (row ranges)
 };
 size_t full_scan_scratch_bytes(int nq, int G, int k);
+void set_lds_attr(const void* fn, int bytes);  // max dynamic LDS of a kernel, set once per device
 hipError_t launch_full_scan(const FullScanArgs& a, hipStream_t st);
 
 constexpr int I8_GROUP_ROWS = 4096;  // rows per group of the int8 copy's group residuals (16 tiles)

@@ -2362,8 +2362,10 @@ __device__ __forceinline__ void refine(const RefineArgs& a, int KP2) {
             const int j = tid + RF_THREADS * e;
             keys[e] = j < n ? src[j] : 0ull;
         }
+        // the best Kp..KP2 keys (any count in that range: the bisection stops early; every kept key
+        // is scored, and the certificate uses the Kp-th best key below)
         u64 t = 1ull;
-        if (n > a.Kp) {
+        if (n > KP2) {
             if (n <= 64 * RF_WE) {  // typical seeded list: one wave finds the threshold, no block barriers
                 if (wid == 0) {
                     u64 wk[RF_WE];
@@ -2372,21 +2374,28 @@ __device__ __forceinline__ void refine(const RefineArgs& a, int KP2) {
                         const int j = lane + 64 * e;
                         wk[e] = j < n ? src[j] : 0ull;
                     }
-                    const u64 tw = wave_kth<RF_WE>(wk, a.Kp);
+                    const u64 tw = wave_kth_range<RF_WE>(wk, a.Kp, KP2);
                     if (lane == 0) thr_s = tw;
                 }
                 __syncthreads();
                 t = thr_s;
             } else {
-                t = block_kth<RF_E>(keys, a.Kp, red);
+                t = block_kth_range<RF_E>(keys, a.Kp, KP2, red);
             }
         }
         nkept = block_write_kept<RF_E>(keys, t, cq, red);
     } else {  // very long lists (unseeded screens of many workgroups): selection from memory
-        const u64 t = block_kth_mem(src, n, a.Kp, red);
+        const u64 t = block_kth_range_mem(src, n, a.Kp, KP2, red);
         nkept = block_compact_mem(src, cq, n, t, red);
     }
     __syncthreads();
+    // the Kp-th best listed key bounds every listed row not kept and every row a screen block
+    // dropped below its own Kp-th (a block's Kp-th key is at most the Kp-th over all lists); with
+    // more than Kp kept it is found among the kept keys by one wave
+    if (nkept > a.Kp && wid == 0) {
+        const u64 kk = wave_kth_buf(cq, nkept, a.Kp);
+        if (lane == 0) thr_s = kk;
+    }
     int myv = 0;
     u64 mymin = ~0ull;
     for (int j = tid; j < nkept; j += RF_THREADS) {
@@ -2468,7 +2477,7 @@ __device__ __forceinline__ void refine(const RefineArgs& a, int KP2) {
         // rows outside the candidate set scored at most: the Kp-th best listed key (when the list
         // was cut to Kp), or a workgroup's compaction bound (deep searches keep MFMA_KP_MAX per
         // workgroup), whichever is larger
-        u64 th = nv >= a.Kp ? minkey_s : 0ull;
+        u64 th = nv > a.Kp ? thr_s : nv == a.Kp ? minkey_s : 0ull;
         if (a.drop && a.drop[q] > th) th = a.drop[q];
         int cert = 1;
         if (a.optimistic && nv < a.Kp) cert = 0;  // an optimistic seed may have cut real candidates
@@ -3182,7 +3191,7 @@ hipError_t launch_pack_qf32(const float* q, int nqb, int nqpad, int d, int dpad,
 
 // Dynamic-LDS limit of a kernel, set once per (kernel, device) -- the attribute is per device, and
 // several threads may launch at once (vs_multi runs one worker per device); thread-safe.
-static void set_lds_attr(const void* fn, int bytes) {
+void set_lds_attr(const void* fn, int bytes) {  // (once per kernel and device)
     static std::mutex mu;
     static std::set<std::pair<const void*, int>> done;
     int dev = 0;
@@ -3398,8 +3407,7 @@ static void launch_refine_dt(const RefineArgs& a, int nq, int KP2, size_t lds, b
 hipError_t launch_refine(const RefineArgs& a, int nq, hipStream_t st) {
     if (a.redo && (!a.gate || !a.cert)) return hipErrorInvalidValue;
     if (a.nsplit > 1 && (a.redo || !a.gsc || !a.gids || !a.gdone)) return hipErrorInvalidValue;
-    int KP2 = 1;
-    while (KP2 < a.Kp) KP2 <<= 1;
+    const int KP2 = refine_kp2(a.Kp);
     const size_t base = (size_t)KP2 * 12 + 8 + (size_t)KP2 * 8;  // scores, ids, (query), kept keys
     const size_t qbytes = (size_t)((a.d + 7) >> 3) * 64;    // fp64 query, transposed 8-element groups
     const bool qlds = base + qbytes <= 148 * 1024;  // query as fp64 in LDS when it fits

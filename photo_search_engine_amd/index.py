@@ -185,7 +185,7 @@ class FlatIndex:
         buf = (ctypes.c_float * cap)()
         kind = ctypes.c_int(0)
         n = check(self._L.vs_timing_fetch(self._h, buf, cap, ctypes.byref(kind)))
-        return [float(buf[i]) for i in range(n)], {1: "mfma", 2: "gemv", 3: "mfma_i8", 4: "gemv_i8"}.get(kind.value, "none")
+        return [float(buf[i]) for i in range(n)], {1: "mfma", 2: "gemv", 3: "mfma_i8", 4: "gemv_i8", 5: "full_scan"}.get(kind.value, "none")
 
     def uncertified_count(self) -> int:
         """First-pass certificate failures so far (each one was re-searched)."""
@@ -207,6 +207,11 @@ class FlatIndex:
         check(self._L.vs_screen_probe(self._h, q_ptr, int(nq), FlatIndex.SCREENS[screen], int(bool(zero_queries)),
                                       stream or None, ctypes.byref(ms)))
         return float(ms.value)
+
+    def set_scan_limit(self, nbytes: int) -> None:
+        """Single-query calls over at most ``nbytes`` of stored rows use the exact full scan instead of
+        a screen (include/vs.h ``vs_set_scan_limit``; 0 = always screen)."""
+        check(self._L.vs_set_scan_limit(self._h, int(nbytes)))
 
     def full_scan_count(self) -> int:
         """Queries answered by the exact full scan so far: no bounded screen could certify them (more

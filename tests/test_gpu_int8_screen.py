@@ -18,8 +18,15 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(scope="module")
 def FlatIndex():
+    # the screen kernels under test: single-query calls on small corpora would otherwise take the
+    # exact full scan (vs_set_scan_limit), which tests/test_gpu_parity.py covers on its own
     from photo_search_engine_amd.index import FlatIndex as FI
-    return FI
+
+    class Screened(FI):
+        def __init__(self, *a, **kw):
+            super().__init__(*a, **kw)
+            self.set_scan_limit(0)
+    return Screened
 
 
 def _num_cu():

@@ -17,8 +17,15 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(scope="module")
 def FlatIndex():
+    # the screen kernels under test: single-query calls on small corpora would otherwise take the
+    # exact full scan (vs_set_scan_limit), which tests/test_gpu_parity.py covers on its own
     from photo_search_engine_amd.index import FlatIndex as FI
-    return FI
+
+    class Screened(FI):
+        def __init__(self, *a, **kw):
+            super().__init__(*a, **kw)
+            self.set_scan_limit(0)
+    return Screened
 
 
 def _check_exact(ix, q, k, metric):
@@ -599,3 +606,64 @@ def test_few_query_deep_refine_split_exact(FlatIndex, dtype, metric, nq, k, N):
     for i in range(3):
         q = O.synth_rows(O.SEED_QUERIES, 500 + 10 * i, nq, 96, True, "f32")
         _check_exact(ix, q, k, metric)
+
+
+@pytest.fixture(scope="module")
+def PlainFlatIndex():
+    from photo_search_engine_amd.index import FlatIndex as FI
+    return FI
+
+
+@pytest.mark.parametrize("metric", ["ip", "l2"])
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16"])
+@pytest.mark.parametrize("N,nq,k", [(10_000, 1, 10), (777, 2, 1), (4_099, 1, 64), (50, 1, 60), (65_536, 2, 33)])
+def test_small_scan_exact(PlainFlatIndex, metric, dtype, N, nq, k):
+    # calls of 1-2 queries (k <= 64) over a corpus under the scan limits (<= 65536 rows, default 192 MiB) skip
+    # the screen: one launch scores every row canonically and selects the top-k (k_full_scan, the
+    # timed kernel); ids and scores bit-exact, k beyond the rows padded, nothing counted as a
+    # fallback full scan
+    d = 136
+    ix = PlainFlatIndex(d, metric, dtype)
+    ix.add_synthetic(O.SEED_CORPUS, 0, N, True)
+    q = O.synth_rows(O.SEED_QUERIES, 5, nq, d, True, "f32")
+    ix.set_timing(True)
+    _check_exact(ix, q, k, metric)
+    ix.set_timing(False)
+    assert ix.timing_fetch()[1] == "full_scan"
+    assert ix.full_scan_count() == 0 and ix.uncertified_count() == 0
+    # the device API (exact path), with an id offset: the same answer
+    import torch
+    qd = torch.from_numpy(q).cuda()
+    I = torch.empty((nq, k), dtype=torch.int64, device="cuda")
+    S = torch.empty((nq, k), dtype=torch.float64, device="cuda")
+    ix.search_device_exact(qd.data_ptr(), nq, k, None, I.data_ptr(), S.data_ptr(), 11, 0)
+    Se, Ie = O.knn_exact(ix.reconstruct_n(0, N), q, k, metric)
+    np.testing.assert_array_equal(I.cpu().numpy(), np.where(Ie >= 0, Ie + 11, -1))
+    valid = Ie >= 0
+    np.testing.assert_array_equal(S.cpu().numpy()[valid], Se[valid])
+    # a limit of 0: the screen path, same bits
+    D1, I1 = ix.search(q, k)
+    ix.set_scan_limit(0)
+    D2, I2 = ix.search(q, k)
+    np.testing.assert_array_equal(I1, I2)
+    np.testing.assert_array_equal(D1, D2)
+    ix.close()
+
+
+def test_small_scan_ties_and_zero_rows(PlainFlatIndex):
+    # 20000 identical rows and zero vectors in a small corpus: the single-query call's full scan
+    # returns faiss's lowest ids of the tie directly
+    d, N, k = 64, 25_000, 10
+    x = O.synth_rows(O.SEED_CORPUS, 0, N, d, True, "bf16")
+    v = x[77].copy()
+    pos = np.random.default_rng(1).choice(N, 20_000, replace=False)
+    x[pos] = v
+    x[:5] = 0.0
+    ix = PlainFlatIndex(d, "ip", "bf16")
+    ix.add(x)
+    for qv in (v, np.zeros(d, np.float32)):
+        D, I = ix.search(qv[None], k)
+        S, Ie = O.knn_exact(ix.reconstruct_n(0, N), qv[None].astype(np.float32), k, "ip")
+        np.testing.assert_array_equal(I, Ie)
+        np.testing.assert_array_equal(D, S.astype(np.float32))
+    ix.close()
