@@ -849,7 +849,7 @@ constexpr int64_t kFullScanScratch = 32ll << 20;  // per-workgroup lists of one 
 // rows_per_wg: each workgroup's row range is at least this long (G = rows / rows_per_wg, <= CUs)
 void full_scan_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float* D, int64_t* I, double* S64,
                      int* cert, int64_t id_offset, hipStream_t st, const int* gate, int ostride = 1,
-                     int rows_per_wg = TR, bool fallback = true) {
+                     int rows_per_wg = TR, bool fallback = true, bool all_queries = false) {
     const int64_t ranges = (ix->ntotal + rows_per_wg - 1) / rows_per_wg;
     const int64_t per_wg = (int64_t)nqb * k * 12;
     const int G = (int)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(ix->num_cu, ranges),
@@ -881,6 +881,7 @@ void full_scan_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float
     a.gdone = c->fdone.as<unsigned>();
     a.count = !fallback ? nullptr : c->unres ? c->unres : ix->d_unres;  // (a first pass is counted nowhere)
     a.G = G;
+    a.all_queries = all_queries ? 1 : 0;
     HIP_CHECK(launch_full_scan(a, st));
 }
 
@@ -909,7 +910,6 @@ void search_all(vs_index* ix, Ctx* c, const float* q, int64_t nq, int k, int Kp,
             c->cert.ensure((size_t)nq * sizeof(int));
             cq = c->cert.as<int>();
         }
-        HIP_CHECK(hipMemsetAsync(cq, 0, (size_t)nq * sizeof(int), st));
         const bool timing = ix->timing.load();
         hipEvent_t e0 = nullptr, e1 = nullptr;
         if (timing) {
@@ -917,7 +917,7 @@ void search_all(vs_index* ix, Ctx* c, const float* q, int64_t nq, int k, int Kp,
             HIP_CHECK(hipEventCreate(&e1));
             HIP_CHECK(hipEventRecord(e0, st));
         }
-        full_scan_block(ix, c, q, (int)nq, k, D, I, S64, cq, id_offset, st, nullptr, 1, kSmallScanRows, false);
+        full_scan_block(ix, c, q, (int)nq, k, D, I, S64, cq, id_offset, st, nullptr, 1, kSmallScanRows, false, true);
         if (timing) {
             HIP_CHECK(hipEventRecord(e1, st));
             std::lock_guard<std::mutex> g(ix->tmtx);

@@ -130,7 +130,7 @@ __global__ void __launch_bounds__(FS_THREADS) k_full_scan(FullScanArgs a, int KL
     for (int q = 0; q < a.nq; ++q) {
         __syncthreads();  // (the previous query's readers of qs / the lists are done)
         if (tid == 0) {
-            go_s = a.cert[q] == 0 ? 1 : 0;
+            go_s = (a.all_queries || a.cert[q] == 0) ? 1 : 0;
             nb_s = 0;
         }
         __syncthreads();

@@ -352,6 +352,7 @@ struct FullScanArgs {
     unsigned* gdone;        // [nq] per-query completion counters, zero between launches
     unsigned* count;        // queries scanned (device counter), or null
     int G;                  // workgroups (row ranges)
+    int all_queries;        // 1: scan every query of the block (cert is only written), no memset first
 };
 size_t full_scan_scratch_bytes(int nq, int G, int k);
 void set_lds_attr(const void* fn, int bytes);  // max dynamic LDS of a kernel, set once per device

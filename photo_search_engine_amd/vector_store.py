@@ -34,6 +34,7 @@ from __future__ import annotations
 
 import json
 import os
+import struct
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -180,9 +181,19 @@ class VectorStore:
     def _normalize_query(self, vector) -> np.ndarray:
         """``np.array([_normalize_vector(vector)], dtype="float32")`` without the Python-list round trip
         (~0.19 ms of a 0.5 ms call at d=4096): fp32 -> Python float -> fp32 is exact, so the bits
-        are the same.  Anything but a flat vector takes the reference's own expression (whose
-        extra axes the index then rejects, as faiss does)."""
-        array = np.array(vector, dtype="float32")
+        are the same.  A list of Python numbers is converted by ``struct`` (the same C double ->
+        float cast as numpy's, ~3x faster than ``np.array`` on a list: ~24 vs ~70 us at d=1536); a
+        value beyond the fp32 range (numpy makes it inf) or anything else takes ``np.array``.
+        Anything but a flat vector takes the reference's own expression (whose extra axes the index
+        then rejects, as faiss does)."""
+        array = None
+        if type(vector) is list:
+            try:
+                array = np.frombuffer(struct.pack(f"{len(vector)}f", *vector), dtype=np.float32)
+            except (struct.error, OverflowError, TypeError):
+                array = None
+        if array is None:
+            array = np.array(vector, dtype="float32")
         if array.ndim != 1:
             return np.array([self._normalize_vector(vector)], dtype="float32")
         if self._normalize:

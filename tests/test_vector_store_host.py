@@ -270,6 +270,31 @@ def test_query_normalisation_float64_and_l2_bit_identical(d, normalize):
             assert got.shape == want.shape and got.tobytes() == want.tobytes()
 
 
+@pytest.mark.parametrize("normalize", [True, False])
+def test_query_list_conversion_edge_values_bit_identical(normalize):
+    # the struct fast path of a list query: subnormals, fp64 values between fp32 neighbours (round
+    # to nearest even), values beyond the fp32 range (numpy: inf -- the fallback), ints, bools,
+    # numpy scalars and strings of numbers (numpy parses them -- the fallback) give the reference's bits
+    store = vsmod.VectorStore.__new__(vsmod.VectorStore)
+    store._normalize = normalize
+    rng = np.random.default_rng(9)
+    base = (rng.standard_normal(64) * 1e-3).tolist()
+    cases = [
+        base,
+        [1e-45, 3e-41, -2e-40] + base[3:],
+        [1.0 + 2.0 ** -24, 1.0 + 3 * 2.0 ** -25, -(1.0 + 2.0 ** -24)] + base[3:],
+        [3.5e38, -1e39] + base[2:],
+        [1, 2, True] + base[3:],
+        [np.float32(0.5), np.float64(0.25), np.int64(3)] + base[3:],
+        ["1.5", "-2"] + base[2:],
+    ]
+    for v in cases:
+        with np.errstate(all="ignore"):
+            want = np.array([store._normalize_vector(v)], dtype="float32")
+            got = store._normalize_query(v)
+        assert got.shape == want.shape and got.tobytes() == want.tobytes(), v[:3]
+
+
 def test_query_with_extra_axis_is_rejected_like_the_reference():
     # a (d, 1) array passes the reference's len() check but its np.array([...]) is 3-D, which the
     # index rejects; it must not be silently flattened into a valid (1, d) query
