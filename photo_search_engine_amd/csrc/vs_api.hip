@@ -658,6 +658,21 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
         const int64_t resident = (int64_t)ix->num_cu * (gemv_dyn() ? gemv_blocks_per_cu(sdt, QB) : 8);
         a.gemv_split = tiles <= ix->num_cu / 2 ? GEMV_SPLIT : 1;
         a.G = (int)std::min<int64_t>(tiles * a.gemv_split, resident);
+        // one query: each block keeps only Kb < Kp keys and publishes the key below which it dropped
+        // rows (ScreenArgs::drop, the refine's certificate bound for them), so the G lists together
+        // hold at most kRefineRegKeys keys -- the refine selects the best Kp from them in registers
+        // and no k_merge launch runs (cfg2: 1024 blocks x 176 keys took a merge of 15 us).  A block
+        // that drops a row the query needs fails the certificate (-> the full scan); with ~Kp / G of
+        // the best rows per block and Kb >= 16 that does not happen in practice.
+        if (nqb == 1 && ix->ntotal >= Kp) {
+            const int kb = (int)std::max<int64_t>(16, (kRefineRegKeys / std::max(a.G, 1)) / 16 * 16);
+            if (kb < Kp && (int64_t)a.G * kb <= kRefineRegKeys) {
+                a.Kp = kb;
+                a.cap = (int)round_up(kb + 2 * TR, 256);
+                c->drop.ensure(sizeof(u64) * MFMA_QB);
+                a.drop = c->drop.as<u64>();
+            }
+        }
         c->qpad.ensure((size_t)QB * dpadq * sizeof(float));
         int* ctr = nullptr;
         if (gemv_dyn()) {  // the work-queue counter is zeroed by the query pack (no separate memset)
@@ -665,7 +680,7 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
             ctr = c->tilectr.as<int>();
         }
         HIP_CHECK(launch_pack_qf32(q, nqb, QB, ix->d, dpadq, c->qpad.as<float>(), c->qinfo.as<float>(), st, ctr,
-                                   c->fails.as<int>()));
+                                   c->fails.as<int>(), a.drop));
         if (gemv_i8) {
             a.corpus = ix->data8;
             a.dpad = ix->dpad8;
@@ -691,16 +706,18 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
     // merge partial lists [nseg][qstride][Kp] down to one list per query (or, with stop_keys, to
     // the first round whose nseg * Kp <= stop_keys: one query's lists are then contiguous and the
     // refine selects the best Kp itself); returns it, nseg updated
+    // (segments of a.Kp keys: the screen's per-block depth, = Kp whenever a merge runs)
     auto merge_all = [&](const u64* src, int& nseg, int qstride, int stop_keys) -> const u64* {
-        const int spb = (256 * (Kp > 2048 ? 32 : 16)) / Kp;  // k_merge: 4096 / 8192 keys per block
-        const size_t mbytes = (size_t)std::max(1, (nseg + spb - 1) / spb) * nqb * Kp * sizeof(u64);
+        const int W = a.Kp;
+        const int spb = (256 * (W > 2048 ? 32 : 16)) / W;  // k_merge: 4096 / 8192 keys per block
+        const size_t mbytes = (size_t)std::max(1, (nseg + spb - 1) / spb) * nqb * W * sizeof(u64);
         c->merge_a.ensure(mbytes);
         c->merge_b.ensure(mbytes);
         u64* bufs[2] = {c->merge_a.as<u64>(), c->merge_b.as<u64>()};
         int which = 0;
-        while (nseg > 1 && (int64_t)nseg * Kp > stop_keys) {
+        while (nseg > 1 && (int64_t)nseg * W > stop_keys) {
             int nout = 0;
-            HIP_CHECK(launch_merge(src, nseg, qstride, nqb, Kp, bufs[which], &nout, st));
+            HIP_CHECK(launch_merge(src, nseg, qstride, nqb, W, bufs[which], &nout, st));
             src = bufs[which];
             which ^= 1;
             nseg = nout;
@@ -782,7 +799,7 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
         const int stop = (nqb == 1 && ix->ntotal >= Kp) ? kRefineRegKeys : 0;
         r.cand = merge_all(a.part, nseg, QB, stop);
         r.cand_n = nullptr;
-        r.lcap = nseg * Kp;
+        r.lcap = nseg * a.Kp;
     }
     r.Kp = Kp;
     r.drop = a.drop;
@@ -939,7 +956,13 @@ void search_all(vs_index* ix, Ctx* c, const float* q, int64_t nq, int k, int Kp,
         else nqb = (int)std::min<int64_t>(rem, GEMV_NQ_MAX);
         search_block(ix, c, q + done * ix->d, nqb, k, Kp, D ? D + done * k : nullptr, I + done * k,
                      S64 ? S64 + done * k : nullptr, cert ? cert + done : nullptr, id_offset, st, seed_rank, false, i8);
-        if (device_fallback) {
+        if (device_fallback && nqb <= GEMV_NQ_MAX) {
+            // a GEMV block (1-8 queries): a failed certificate goes straight to the full scan -- one
+            // pass over the rows per failed query, about what the fallback round's MFMA screen costs
+            // the block -- in ONE gated launch instead of four (the single-query step, cfg2)
+            full_scan_block(ix, c, q + done * ix->d, nqb, k, D ? D + done * k : nullptr, I + done * k,
+                            S64 ? S64 + done * k : nullptr, cert + done, id_offset, st, c->fails.as<int>());
+        } else if (device_fallback) {
             search_block(ix, c, q + done * ix->d, nqb, k, std::max(Kp, fallback_depth(ix)), D ? D + done * k : nullptr,
                          I + done * k, S64 ? S64 + done * k : nullptr, cert + done, id_offset, st, 0, true);
             full_scan_block(ix, c, q + done * ix->d, nqb, k, D ? D + done * k : nullptr, I + done * k,

@@ -166,6 +166,15 @@ __device__ __forceinline__ int lane_prefix(u64 mask) {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
+// agent-scope relaxed stores / loads (global_store / global_load ... sc1): hand-offs between the
+// workgroups of one launch without cache fences (MI355X_MICROARCH "valid forms": every handed-off
+// byte stored and loaded sc1, every storing wave's vmcnt(0) before ONE lane's agent-scope counter
+// add, the last adder told by the value its add returned, its waves loading after a barrier)
+template <typename T>
+__device__ __forceinline__ void st_agent(T* p, T v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+template <typename T>
+__device__ __forceinline__ T ld_agent(const T* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
 // K-th largest key among the wave's keys (keys unique, 0 = empty, at least K non-empty).
 // Bit-serial bisection with early exit once exactly K keys are >= the prefix.
 template <int E>

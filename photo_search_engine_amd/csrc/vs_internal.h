@@ -244,7 +244,7 @@ hipError_t launch_pack_qtile(int dt, const float* q, int nqb, int d, int dpad, u
                              const int* qidx = nullptr);
 hipError_t launch_pack_qf32(const float* q, int nqb, int nqpad, int d, int dpad, float* qp, float* qinfo,
                             hipStream_t st, int* ctr = nullptr,  // ctr: zeroed (a screen's tile queue)
-                            int* fails = nullptr);
+                            int* fails = nullptr, u64* drop = nullptr);  // drop: zeroed [nqpad]
 
 hipError_t launch_screen_mfma(int dt, const ScreenArgs& a, const uint8_t* qt, int nqb, hipStream_t st);
 // the int8 main pass runs the direct form (k_screen_i8d) for this int8 row stride (K-steps per tile

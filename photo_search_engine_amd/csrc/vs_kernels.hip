@@ -570,9 +570,11 @@ __global__ void __launch_bounds__(256) k_pack_qtile_i8(const float* __restrict__
 // GEMV queries: fp32, [nqpad][dpad] zero padded; q_hat = q
 __global__ void __launch_bounds__(256) k_pack_qf32(const float* __restrict__ q, int nqb, int nqpad, int d, int dpad,
                                                     float* __restrict__ qp, float* __restrict__ qinfo,
-                                                    int* __restrict__ ctr, int* __restrict__ fails) {
+                                                    int* __restrict__ ctr, int* __restrict__ fails,
+                                                    u64* __restrict__ drop) {
     const int lane = threadIdx.x & 63;
     const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (drop && r < nqpad && lane == 0) drop[r] = 0ull;  // the GEMV screen's block drop bounds
     if (ctr && blockIdx.x == 0 && threadIdx.x == 0) *ctr = 0;  // the GEMV screen's tile queue that follows
     if (fails && blockIdx.x == 0 && threadIdx.x == 0) fails[0] = fails[1] = 0;  // the block's certificate-failure counts
     if (r >= nqpad) return;
@@ -1957,13 +1959,18 @@ __global__ void __launch_bounds__(256) k_screen_gemv(ScreenArgs a, const float* 
         u64* pq = a.part + ((size_t)blk * NQ + qi) * a.Kp;
         u64* buf = cand + (size_t)qi * a.cap;
         int n = qi < nqb ? cnt[qi] : 0;
+        u64 dropped = qi < nqb ? thr_key[qi] : 0ull;  // (rows below a compaction threshold were dropped)
         if (n > a.Kp) {
             const u64 t = block_kth_mem(buf, n, a.Kp, red);
             n = block_compact_mem(buf, pq, n, t, red);
+            // keys below the Kp-th are dropped: its key bounds them (the refine's certificate
+            // takes the largest such bound over blocks, ScreenArgs::drop)
+            dropped = t > dropped ? t : dropped;
         } else {
             for (int j = tid; j < n; j += 256) pq[j] = buf[j];
         }
         for (int j = n + tid; j < a.Kp; j += 256) pq[j] = 0ull;
+        if (a.drop && tid == 0 && dropped != 0ull) atomicMax(a.drop + qi, dropped);
         __syncthreads();
     }
 }
@@ -2444,26 +2451,33 @@ __device__ __forceinline__ void refine(const RefineArgs& a, int KP2) {
 #pragma unroll
             for (int i = 0; i < RR; ++i)
                 if (rr[i] >= 0) {
-                    scw[j + i * NW] = s4[i];
-                    idw[j + i * NW] = a.idmap ? a.idmap[rr[i]] : (uint32_t)rr[i];
+                    const uint32_t uid = a.idmap ? a.idmap[rr[i]] : (uint32_t)rr[i];
+                    if (split) {  // (handed to the query's last workgroup: sc1 stores)
+                        st_agent(scw + j + i * NW, s4[i]);
+                        st_agent(idw + j + i * NW, uid);
+                    } else {
+                        scw[j + i * NW] = s4[i];
+                        idw[j + i * NW] = uid;
+                    }
                 }
         }
     }
     if (split) {
+        // the last of the query's workgroups takes over: sc1 stores above, every storing wave's
+        // vmcnt(0), one agent-scope counter add per workgroup, sc1 loads (no cache fences)
         __shared__ int last_s;
-        __threadfence();  // release this workgroup's scores (device scope: other XCDs' L2s)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (tid == 0) last_s = atomicAdd(a.gdone + q, 1u) == (unsigned)(a.nsplit - 1) ? 1 : 0;
+        if (tid == 0)
+            last_s = __hip_atomic_fetch_add(a.gdone + q, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                             (unsigned)(a.nsplit - 1) ? 1 : 0;
         __syncthreads();
         if (!last_s) return;
-        __threadfence();  // acquire the other workgroups' scores
-        const volatile double* vsc = scw;
-        const volatile uint32_t* vid = idw;
         for (int j = tid; j < nv; j += RF_THREADS) {
-            sc[j] = vsc[j];
-            ids[j] = vid[j];
+            sc[j] = ld_agent(scw + j);
+            ids[j] = ld_agent(idw + j);
         }
-        if (tid == 0) a.gdone[q] = 0u;  // ready for the next launch (kernel boundary orders it)
+        if (tid == 0) st_agent(a.gdone + q, 0u);  // ready for the next launch
     }
     const double worst = METRIC == METRIC_IP ? -INFINITY : INFINITY;
     for (int j = nv + tid; j < KP2; j += RF_THREADS) {
@@ -3183,9 +3197,9 @@ hipError_t launch_pack_qtile_i8(const float* q, int nqb, int d, int dpad8, uint8
 }
 
 hipError_t launch_pack_qf32(const float* q, int nqb, int nqpad, int d, int dpad, float* qp, float* qinfo,
-                            hipStream_t st, int* ctr, int* fails) {
+                            hipStream_t st, int* ctr, int* fails, u64* drop) {
     hipLaunchKernelGGL(k_pack_qf32, dim3(blocks4(nqpad)), dim3(256), 0, st, q, nqb, nqpad, d, dpad, qp, qinfo, ctr,
-                       fails);
+                       fails, drop);
     return hipGetLastError();
 }
 

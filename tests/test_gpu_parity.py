@@ -384,6 +384,30 @@ def test_full_scan_near_ties_and_k_beyond_rows(FlatIndex, metric):
     ix.close()
 
 
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_gemv_block_failure_goes_to_full_scan(FlatIndex, dtype):
+    # a GEMV first pass (1-8 queries) whose certificate fails -- 300 copies of the query's best row
+    # tie beyond its Kp-deep lists -- is answered on the device by the gated full scan alone (no
+    # MFMA fallback round for GEMV blocks); exact, and counted in full_scan_count
+    import torch
+    d, k, N, nq = 64, 10, 30_000, 4
+    x = O.synth_rows(O.SEED_CORPUS, 0, N, d, True, dtype)
+    v = x[4242].copy()
+    x[np.random.default_rng(2).choice(N, 300, replace=False)] = v
+    ix = FlatIndex(d, "ip", dtype)  # (screened fixture: no small scan)
+    ix.add(x)
+    q = np.concatenate([np.repeat(v[None], 2, axis=0), O.synth_rows(O.SEED_QUERIES, 0, nq - 2, d, True, dtype)])
+    qd = torch.from_numpy(q).cuda()
+    I = torch.empty((nq, k), dtype=torch.int64, device="cuda")
+    S = torch.empty((nq, k), dtype=torch.float64, device="cuda")
+    ix.search_device_exact(qd.data_ptr(), nq, k, None, I.data_ptr(), S.data_ptr(), 0, 0)
+    Se, Ie = O.knn_exact(ix.reconstruct_n(0, N), q, k, "ip")
+    np.testing.assert_array_equal(I.cpu().numpy(), Ie)
+    np.testing.assert_array_equal(S.cpu().numpy(), Se)
+    assert ix.uncertified_count() >= 2 and ix.full_scan_count() >= 2
+    ix.close()
+
+
 @pytest.mark.parametrize("d", [64, 512])
 def test_batch_refine_certifies_ties_within_its_depth(FlatIndex, d):
     """5000 exact ties (beyond KP_MAX = 4096) in a 20-query batch: the adaptive refine lists and
