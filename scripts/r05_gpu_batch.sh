@@ -62,6 +62,8 @@ for s in ${STEPS:-tests cfg3 shard8 mix03 micro multi}; do
       cp $(ls gpurun_out/trace1/*/t_memory_copy_trace.csv gpurun_out/trace1/t_memory_copy_trace.csv 2>/dev/null | head -1) gpurun_out/trace1_memcpy.csv; rm -rf gpurun_out/trace1 ;;
     hnsw) run hnsw_bench 900 python scripts/hnsw_bench.py ;;
     smallscan) run small_scan 600 python scripts/small_scan_timing.py ;;
+    tracemulti) mkdir -p gpurun_out/tracem && run tracemulti 600 rocprofv3 --kernel-trace --memory-copy-trace -d gpurun_out/tracem -o t --output-format csv -- python scripts/multi_step_timing.py --reps 3 && \
+      python scripts/trace_merge.py gpurun_out/tracem 140 > gpurun_out/tracem_tail.txt && rm -rf gpurun_out/tracem ;;
     trace3) mkdir -p gpurun_out/trace3 && run trace3 300 rocprofv3 --kernel-trace -d gpurun_out/trace3 -o t --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline && \
       python scripts/trace_tail.py $(ls gpurun_out/trace3/*/t_kernel_trace.csv gpurun_out/trace3/t_kernel_trace.csv 2>/dev/null | head -1) 60 "vs::|copyBuffer|Kernel" > gpurun_out/trace3_tail.txt && rm -rf gpurun_out/trace3 ;;
     prof3) mkdir -p gpurun_out/prof3 && run prof3 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof3 -o run --output-format csv -- python bench.py --steps 30 --warmup 1 --no-cpu-baseline ;;
