@@ -228,6 +228,7 @@ def main():
     t_build = time.time() - t_build
     result = {}
     per_rank = {}
+    host_ms = {}
 
     def step():
         result["D"], result["I"], result["S"] = sh.search(q, k)
@@ -262,6 +263,16 @@ def main():
         sh.exchange_timing = False
         km, kd = ix.timing_fetch()
         xm = sh.exchange_times_fetch()
+        # host time to enqueue one step with the device idle (untimed diagnostic: a step whose host
+        # side exceeds its device time leaves the device waiting on the host)
+        hs = []
+        for _ in range(3):
+            torch.cuda.synchronize()
+            th = time.perf_counter()
+            step()
+            hs.append((time.perf_counter() - th) * 1e3)
+        torch.cuda.synchronize()
+        host_ms[scr] = float(np.median(hs))
         per_rank[scr] = [float(np.mean(km)) if km else float("nan"), sum(xm) / args.steps, len(xm) / args.steps,
                          el * 1e3 / args.steps, float(n_local)]
         if G > 1:
@@ -338,6 +349,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
+            "host_enqueue_ms": round(host_ms.get(screen, float("nan")), 4),
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,

@@ -134,6 +134,12 @@ void vs_search_pending_free(vs_pending* pending);
 int vs_merge_shards_device(int metric, const double* S_in, const int64_t* I_in, int32_t in_stride, int G,
                            int64_t nq, int32_t k, double* S_out, int64_t* I_out, float* D_out, void* stream);
 
+/* ---- the int8 / native MFMA screens' threshold seed, exposed for verification: for each of nq
+ * queries, the rank-th largest of its M sampled maxima (device fp32 [nq][M]) as a starting key
+ * (ordered fp32 << 32) in thr_dev[q] (device u64 [nq]); 0 when M < rank.  M <= 8192, rank >= 1. */
+int vs_seed_select_device(int device, const float* maxima_dev, int32_t M, int64_t nq, int32_t rank,
+                          uint64_t* thr_dev, void* stream);
+
 /* ---- reconstruct (index.reconstruct, utils/vector_store.py:207) */
 int vs_reconstruct(vs_index* index, int64_t id, float* out);
 int vs_reconstruct_n(vs_index* index, int64_t i0, int64_t n, float* out); /* host n x d */

@@ -6,6 +6,7 @@ There is no CPU fallback anywhere in ``photo_search_engine_amd``.
 from __future__ import annotations
 
 import ctypes
+from typing import Optional
 import os
 import re
 import sys
@@ -67,6 +68,7 @@ _SIGS = {
     "vs_search_pending_free": (None, [_vp]),
     "vs_merge_shards_device": (ctypes.c_int, [ctypes.c_int, _vp, _vp, ctypes.c_int32, ctypes.c_int, _c_i64,
                                               ctypes.c_int32, _vp, _vp, _vp, _vp]),
+    "vs_seed_select_device": (ctypes.c_int, [ctypes.c_int, _vp, ctypes.c_int32, _c_i64, ctypes.c_int32, _vp, _vp]),
     "vs_add_from_file": (ctypes.c_int, [_vp, ctypes.c_char_p, _c_i64, _c_i64]),
     "vs_write_rows_to_file": (ctypes.c_int, [_vp, ctypes.c_char_p, _c_i64, _c_i64, _c_i64]),
     "vs_reconstruct": (ctypes.c_int, [_vp, _c_i64, _vp]),
@@ -144,12 +146,14 @@ def header_functions(path: str = HEADER_PATH):
     return sorted(set(re.findall(r"\b(vs_[a-z0-9_]+)\s*\(", text)))
 
 
-def load(path: str = LIB_PATH) -> ctypes.CDLL:
-    """Load libvs.so and bind every entry point; raises if the library is absent."""
+def load(path: Optional[str] = None) -> ctypes.CDLL:
+    """Load libvs.so and bind every entry point; raises if the library is absent.  (VS_LIB_PATH:
+    another build of the same library, for A/B measurements.)"""
     global _lib
     with _lock:
         if _lib is not None:
             return _lib
+        path = path or os.environ.get("VS_LIB_PATH") or LIB_PATH
         # One HIP runtime per process: torch wheels bundle their own libamdhip64.so.7 /
         # libhsa-runtime64.so.1.  If torch is importable, load it first so libvs binds to the
         # SAME runtime (same SONAME) instead of /opt/rocm's copy; two HSA runtimes in one process
@@ -165,6 +169,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
                 "build it with `python -m photo_search_engine_amd.build` (hipcc, gfx950)")
         L = ctypes.CDLL(path)
         for name, (res, args) in _SIGS.items():
+            if path != LIB_PATH and not hasattr(L, name):
+                continue  # (an A/B build from before an entry point was added)
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

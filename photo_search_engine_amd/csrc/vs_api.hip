@@ -65,6 +65,11 @@ struct Ctx {
     DevBuf tilectr;  // GEMV screen: tile work-queue counter
     DevBuf seedacc;  // MFMA seed pass: raw accumulators of each workgroup's seed tile
     DevBuf outAll;   // vs_search: I (int64), D (fp32), certificates in one block: ONE D2H copy
+    // the device fallback round's query tile, packed ahead by the block's first pass: 0 none (the
+    // round packs it), 1 the native first pass's own tile (qtile), 2 the int8 pass's native copy
+    // (qtile_n); the round's list counters are gcnt2 / drop2, zeroed by the same pack
+    DevBuf qtile_n, gcnt2, drop2;
+    int prepacked = 0;
     PinnedPair pin;  // read_rows_host: pinned landing chunks
     HostBuf hq;      // vs_search: the query batch, staged for the H2D copy
     HostBuf hout;    // vs_search: I (int64), D (fp32) and certificates land here; search_exact_device: certificates
@@ -449,7 +454,7 @@ double i8_union_target(int k, double sampled, double n) {
 // returns its arguments in *keep for vs_search_device_phase_b
 void search_block_i8(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float* D, int64_t* I, double* S64,
                      int* cert, int64_t id_offset, hipStream_t st, int phase = 0, int KA1 = 0,
-                     RefineArgs* keep = nullptr, int ostride = 1) {
+                     RefineArgs* keep = nullptr, int ostride = 1, bool prepack = false) {
     const int64_t tiles = (ix->ntotal + TR - 1) / TR;
     ScreenArgs a{};
     a.corpus = ix->data8;
@@ -484,10 +489,22 @@ void search_block_i8(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float
         HIP_CHECK(launch_group_dots(ix->gmean, ng, ix->dpad8, q, nqb, ix->d, c->gT.as<float>(), st));
         a.gT = c->gT.as<float>();
     }
+    // (a device fallback round follows: its native tile is packed here too, from the same loads)
+    NativeTile nat{};
+    c->prepacked = 0;
+    if (prepack && (ix->dtype == DT_BF16 || ix->dtype == DT_F16)) {
+        c->qtile_n.ensure((size_t)MFMA_QB * ix->dpad * ix->es);
+        c->qinfo.ensure(sizeof(float) * 2 * MFMA_QB);
+        c->gcnt2.ensure(sizeof(int) * MFMA_QB);
+        c->drop2.ensure(sizeof(u64) * MFMA_QB);
+        nat = NativeTile{ix->dtype, (int)ix->dpad, c->qtile_n.as<uint8_t>(), c->qinfo.as<float>(), c->gcnt2.as<int>(),
+                         c->drop2.as<u64>()};
+    }
     HIP_CHECK(launch_pack_qtile_i8(q, nqb, ix->d, ix->dpad8, c->qtile.as<uint8_t>(), c->qfac.as<float2>(),
                                    c->qeps.as<float>(), ix->d_maxsq + 2, c->gcnt.as<int>(), c->drop.as<u64>(), st,
                                    c->fails.as<int>(), ix->metric == METRIC_L2 ? ix->d_maxsq : nullptr,
-                                   gamma_of(ix->d)));
+                                   gamma_of(ix->d), nat.qt ? &nat : nullptr));
+    if (nat.qt) c->prepacked = 2;
     a.qfac = c->qfac.as<float2>();
     a.drop = c->drop.as<u64>();
     a.lcap = a.G * a.Kp;
@@ -590,11 +607,14 @@ void search_block_i8(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float
 // three launches (pack, screen, refine) are gated on the block's failure count (c->fails) and the
 // refine rewrites only the queries whose certificate failed; a query it cannot certify either
 // counts in c->fails[1], the gate of the block's full scan (full_scan_block)
+// prepack (first passes followed by their device fallback round): the round's native query tile
+// and zeroed list counters are prepared by this pass's query pack (Ctx::prepacked)
 void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, float* D, int64_t* I, double* S64,
                   int* cert, int64_t id_offset, hipStream_t st, int seed_rank, bool redo = false,
-                  bool allow_i8 = true, int ostride = 1) {
+                  bool allow_i8 = true, int ostride = 1, bool prepack = false) {
+    if (!redo) c->prepacked = 0;
     if (seed_rank > 0 && allow_i8 && use_i8(ix, nqb, k)) {
-        search_block_i8(ix, c, q, nqb, k, D, I, S64, cert, id_offset, st);
+        search_block_i8(ix, c, q, nqb, k, D, I, S64, cert, id_offset, st, 0, 0, nullptr, 1, prepack);
         health_note(ix, c, st, 1, nqb);
         return;
     }
@@ -638,6 +658,13 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
                     : Kp;
     int QB;
     c->qinfo.ensure(sizeof(float) * 2 * MFMA_QB);
+    // the screen's query tile and survivor-list counters (a fallback round prepared by its first pass:
+    // the prepacked tile, counters gcnt2 / drop2, no pack launch)
+    const int pre = redo ? c->prepacked : 0;
+    c->prepacked = 0;
+    const uint8_t* qtile = c->qtile.as<uint8_t>();
+    int* gcnt = nullptr;
+    u64* dropb = nullptr;
     if (use_mfma) {
         QB = MFMA_QB;
         a.cap = MFMA_CAP;
@@ -645,9 +672,26 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
         c->qtile.ensure((size_t)MFMA_QB * ix->dpad * ix->es);
         c->gcnt.ensure(sizeof(int) * MFMA_QB);
         c->drop.ensure(sizeof(u64) * MFMA_QB);
-        HIP_CHECK(launch_pack_qtile(ix->dtype, q, nqb, ix->d, ix->dpad, c->qtile.as<uint8_t>(), c->qinfo.as<float>(),
-                                    c->gcnt.as<int>(), c->drop.as<u64>(), st, redo ? nullptr : c->fails.as<int>(),
-                                    gate));
+        qtile = c->qtile.as<uint8_t>();
+        gcnt = c->gcnt.as<int>();
+        dropb = c->drop.as<u64>();
+        if (pre) {
+            if (pre == 2) qtile = c->qtile_n.as<uint8_t>();
+            gcnt = c->gcnt2.as<int>();
+            dropb = c->drop2.as<u64>();
+        } else {
+            // a first pass whose fallback round follows zeroes that round's counters too
+            const bool pp = prepack && !redo;
+            if (pp) {
+                c->gcnt2.ensure(sizeof(int) * MFMA_QB);
+                c->drop2.ensure(sizeof(u64) * MFMA_QB);
+            }
+            HIP_CHECK(launch_pack_qtile(ix->dtype, q, nqb, ix->d, ix->dpad, c->qtile.as<uint8_t>(),
+                                        c->qinfo.as<float>(), gcnt, dropb, st, redo ? nullptr : c->fails.as<int>(),
+                                        gate, nullptr, pp ? c->gcnt2.as<int>() : nullptr,
+                                        pp ? c->drop2.as<u64>() : nullptr));
+            if (pp) c->prepacked = 1;
+        }
     } else {
         QB = nqb <= 1 ? 1 : nqb <= 2 ? 2 : nqb <= 4 ? 4 : 8;
         a.cap = (int)round_up(Kp + 2 * TR, 256);
@@ -698,9 +742,9 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
     if (!use_mfma && gemv_dyn()) a.next_tile = c->tilectr.as<int>();
     if (use_mfma) {
         a.glist = c->part.as<u64>();
-        a.gcnt = c->gcnt.as<int>();
+        a.gcnt = gcnt;
         a.lcap = a.G * a.Kp;
-        a.drop = c->drop.as<u64>();
+        a.drop = dropb;
     }
 
     // merge partial lists [nseg][qstride][Kp] down to one list per query (or, with stop_keys, to
@@ -777,7 +821,7 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
         HIP_CHECK(hipEventCreate(&e1));
         HIP_CHECK(hipEventRecord(e0, st));
     }
-    if (use_mfma) HIP_CHECK(launch_screen_mfma(ix->dtype, a, c->qtile.as<uint8_t>(), nqb, st));
+    if (use_mfma) HIP_CHECK(launch_screen_mfma(ix->dtype, a, qtile, nqb, st));
     else HIP_CHECK(launch_screen_gemv(gemv_i8 ? DT_I8 : ix->dtype, a, c->qpad.as<float>(), nqb, QB, st));
     if (timing) {
         HIP_CHECK(hipEventRecord(e1, st));
@@ -955,7 +999,8 @@ void search_all(vs_index* ix, Ctx* c, const float* q, int64_t nq, int k, int Kp,
             nqb = (int)std::min<int64_t>(rem, MFMA_QB);
         else nqb = (int)std::min<int64_t>(rem, GEMV_NQ_MAX);
         search_block(ix, c, q + done * ix->d, nqb, k, Kp, D ? D + done * k : nullptr, I + done * k,
-                     S64 ? S64 + done * k : nullptr, cert ? cert + done : nullptr, id_offset, st, seed_rank, false, i8);
+                     S64 ? S64 + done * k : nullptr, cert ? cert + done : nullptr, id_offset, st, seed_rank, false, i8,
+                     1, device_fallback && nqb > GEMV_NQ_MAX);
         if (device_fallback && nqb <= GEMV_NQ_MAX) {
             // a GEMV block (1-8 queries): a failed certificate goes straight to the full scan -- one
             // pass over the rows per failed query, about what the fallback round's MFMA screen costs
@@ -1111,7 +1156,7 @@ vs_pending* vs::search_phase_a(vs_index* ix, const float* q_dev, int64_t nq, int
         const int share = (k + world - 1) / world;
         p->ka = (int)std::min<int64_t>(round_up(2 * k + 24, 8), round_up(2 * share + 24, 8));
         search_block_i8(ix, c, q_dev, (int)nq, k, nullptr, I_a, S_a, c->cert.as<int>(), id_offset, st, 1, p->ka,
-                        &p->r, stride);
+                        &p->r, stride, true);
     } else {
         c->outS.ensure((size_t)nq * k * sizeof(double));
         c->outI.ensure((size_t)nq * k * sizeof(int64_t));
@@ -1589,6 +1634,16 @@ int vs_merge_shards_device(int metric, const double* S_in, const int64_t* I_in, 
         if (nq == 0) return;
         HIP_CHECK(launch_merge_shards(metric, S_in, I_in, G, nq, k, S_out, I_out, D_out, (hipStream_t)stream,
                                       in_stride));
+    });
+}
+
+int vs_seed_select_device(int device, const float* maxima, int32_t M, int64_t nq, int32_t rank, uint64_t* thr,
+                          void* stream) {
+    return guarded([&] {
+        if (M <= 0 || M > 8192 || rank < 1 || nq < 0) throw VsError(VS_ERR_ARG, "bad M / rank / nq");
+        if (nq == 0) return;
+        DeviceGuard dg(device);
+        HIP_CHECK(launch_seed_select(maxima, M, (int)nq, rank, (u64*)thr, (hipStream_t)stream));
     });
 }
 

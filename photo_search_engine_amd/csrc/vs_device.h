@@ -242,17 +242,21 @@ __device__ __forceinline__ u64 wave_kth_buf(const u64* buf, int n, int K) {
     return t;
 }
 
-// Over a whole block: a threshold t with Klo <= #(keys >= t) <= Khi (distinct keys, Klo <= #keys): the bit bisection of
-// block_kth, stopping at the first prefix whose count lands in the range (Khi = Klo: the Klo-th
-// largest key).  One barrier per step: the per-wave counts alternate between the two halves of
-// red[2 * waves] (a half is rewritten two steps later, after every wave has passed the barrier of
-// the step in between, i.e. after its reads).
+// Over a whole block: a threshold t with Klo <= #(keys >= t) <= Khi (distinct keys, 0 = empty slot,
+// Klo <= #keys; Khi = Klo: the Klo-th largest key).  Radix select over the keys' RANGE: w = key -
+// min, rounds of 8 bits from the top bit of max - min (an LDS histogram of the digit among the keys
+// matching the prefix so far; one wave scans the 256 bins from the top for the bin where the count
+// reaches Klo), stopping at the first bin whose lower edge leaves at most Khi keys at or above it.
+// The keys of a refine list span a narrow score range, so one or two rounds (3 barriers each)
+// replace the ~25 one-barrier steps of a bit bisection (13 us of a phase-A refine at the 8-shard
+// step).
 template <int E>
 __device__ __forceinline__ u64 block_kth_range(const u64 (&keys)[E], int Klo, int Khi, int* red) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    // the bits every non-empty key shares (the scores' common exponent and leading mantissa) are
-    // the threshold's prefix: the bisection starts below them
     __shared__ u64 mm[2 * 16];
+    __shared__ unsigned hist[256];
+    __shared__ int s_bin, s_above, s_cnt;
+    (void)red;
     u64 kmax = 0ull, kmin = ~0ull;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
@@ -272,28 +276,64 @@ __device__ __forceinline__ u64 block_kth_range(const u64 (&keys)[E], int Klo, in
         kmax = mm[i] > kmax ? mm[i] : kmax;
         kmin = mm[16 + i] < kmin ? mm[16 + i] : kmin;
     }
-    u64 t = 0;
-    int bstart = 63;
+    u64 t = kmin;
     if (kmin != ~0ull && kmax != kmin) {
-        bstart = 63 - __clzll((long long)(kmax ^ kmin));
-        t = kmax & ~((2ull << bstart) - 1ull);  // (bstart <= 62: 2 << bstart does not overflow)
-    }
-    for (int b = bstart, par = 0; b >= 0; --b, par ^= 1) {
-        const u64 cand = t | (1ull << b);
-        int c = 0;
+        const u64 span = kmax - kmin;
+        const int bits = 64 - __clzll((long long)span);
+        u64 prefix = 0ull;
+        int above = 0;  // keys above the prefix's range (counted in earlier rounds)
+        for (int sh = bits - 8; sh > -8; sh -= 8) {
+            const u64 hmask = sh + 8 >= 64 ? 0ull : ~0ull << (sh + 8);
+            for (int i = threadIdx.x; i < 256; i += blockDim.x) hist[i] = 0u;
+            __syncthreads();
 #pragma unroll
-        for (int e = 0; e < E; ++e) c += keys[e] >= cand ? 1 : 0;
-        c = wave_sum_i(c);
-        if (lane == 0) red[par * nw + w] = c;
-        __syncthreads();
-        int tot = 0;
-        for (int i = 0; i < nw; ++i) tot += red[par * nw + i];
-        if (tot >= Klo) {
-            t = cand;
-            if (tot <= Khi) break;
+            for (int e = 0; e < E; ++e) {
+                const u64 x = keys[e] - kmin;
+                if (keys[e] != 0ull && (x & hmask) == prefix)
+                    atomicAdd(&hist[(unsigned)((sh >= 0 ? x >> sh : x << -sh) & 255ull)], 1u);
+            }
+            __syncthreads();
+            if (w == 0) {  // lane l: bins 255-4l .. 252-4l (descending)
+                unsigned c[4], sum = 0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    c[i] = hist[255 - 4 * lane - i];
+                    sum += c[i];
+                }
+                unsigned incl = sum;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const unsigned v = __shfl_up(incl, o, 64);
+                    if (lane >= o) incl += v;
+                }
+                const unsigned excl = incl - sum;
+                const unsigned need = (unsigned)(Klo - above);
+                const bool here = excl < need && incl >= need;
+                if (here) {
+                    unsigned cum = excl;
+                    int i = 0;
+                    while (cum + c[i] < need) cum += c[i++];
+                    s_bin = 255 - 4 * lane - i;
+                    s_above = above + (int)cum;
+                    s_cnt = (int)c[i];
+                }
+                if (__ballot(here) == 0ull && lane == 0) {  // (fewer than Klo keys: the lowest bin)
+                    s_bin = 0;
+                    s_above = above;
+                    s_cnt = 0;
+                }
+            }
+            __syncthreads();
+            const u64 b = (u64)s_bin;
+            prefix |= sh >= 0 ? b << sh : b >> -sh;
+            t = kmin + prefix;  // the bin's lower edge: s_above + s_cnt keys at or above it
+            const int at = s_above + s_cnt;
+            above = s_above;
+            __syncthreads();  // (every wave has read the words before the next round rewrites them)
+            if (at <= Khi || sh <= 0) break;
         }
     }
-    __syncthreads();  // (every wave has read red before its caller reuses it)
+    __syncthreads();  // (every wave has read the shared words before the caller reuses them)
     return t;
 }
 // The K-th largest of the block's keys (distinct keys, K <= #keys); red: 2 x waves ints

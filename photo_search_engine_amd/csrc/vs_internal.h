@@ -241,7 +241,8 @@ hipError_t launch_gather_rows(int dt, const uint8_t* data, const int64_t* ids, i
 // qidx (optional): tile row r packs query qidx[r] of q; qinfo is then indexed by qidx and max-combined
 hipError_t launch_pack_qtile(int dt, const float* q, int nqb, int d, int dpad, uint8_t* qt, float* qinfo, int* gcnt,
                              u64* drop, hipStream_t st, int* fails = nullptr, const int* gate = nullptr,
-                             const int* qidx = nullptr);
+                             const int* qidx = nullptr,
+                             int* gcnt2 = nullptr, u64* drop2 = nullptr);
 hipError_t launch_pack_qf32(const float* q, int nqb, int nqpad, int d, int dpad, float* qp, float* qinfo,
                             hipStream_t st, int* ctr = nullptr,  // ctr: zeroed (a screen's tile queue)
                             int* fails = nullptr, u64* drop = nullptr);  // drop: zeroed [nqpad]
@@ -370,9 +371,21 @@ hipError_t launch_group_means(int dt, const uint8_t* data, int dpad, int d, int6
                               int dpad8, uint16_t* gmean, unsigned* maxes, hipStream_t st);
 hipError_t launch_group_dots(const uint16_t* gmean, int64_t ngroups, int dpad8, const float* q, int nq, int d, float* T,
                              hipStream_t st);
+// The device fallback round's native query tile, packed ahead by the first pass's query pack (so
+// the gated round needs no pack launch of its own): the tile in the corpus dtype (bf16 / f16), its
+// qinfo, and zeroed survivor-list lengths / drop bounds of the round's screen.
+struct NativeTile {
+    int dt;
+    int dpad;
+    uint8_t* qt;
+    float* qinfo;
+    int* gcnt;
+    u64* drop;
+};
 hipError_t launch_pack_qtile_i8(const float* q, int nqb, int d, int dpad8, uint8_t* qt, float2* qfac, float* qeps,
                                 const unsigned* maxes, int* gcnt, u64* drop, hipStream_t st, int* fails = nullptr,
-                                const unsigned* l2max = nullptr, float gamma = 0.0f);
+                                const unsigned* l2max = nullptr, float gamma = 0.0f,
+                                const NativeTile* nat = nullptr);
 
 // ---- IVF-Flat (vs_ivf.hip) ---------------------------------------------------------------------
 // Inverted lists are chains of pages: a page is one row tile (TR rows, the flat layout above) of

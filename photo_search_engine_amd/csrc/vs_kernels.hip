@@ -186,7 +186,8 @@ __global__ void __launch_bounds__(256) k_pack_qtile(const float* __restrict__ q,
                                                      uint8_t* __restrict__ qt, float* __restrict__ qinfo,
                                                      int* __restrict__ gcnt, u64* __restrict__ drop,
                                                      int* __restrict__ fails, const int* __restrict__ gate,
-                                                     const int* __restrict__ qidx) {
+                                                     const int* __restrict__ qidx, int* __restrict__ gcnt2,
+                                                     u64* __restrict__ drop2) {
     if (gate && *gate == 0) return;  // device fallback round with nothing to re-search
     const int lane = threadIdx.x & 63;
     const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -194,6 +195,10 @@ __global__ void __launch_bounds__(256) k_pack_qtile(const float* __restrict__ q,
     if (fails && r == 0 && lane == 0) fails[0] = fails[1] = 0;  // the block's certificate-failure counts
     if (gcnt && lane == 0) gcnt[r] = 0;  // survivor-list lengths of the screen that follows ...
     if (drop && lane == 0) drop[r] = 0ull;  // ... and its workgroups' drop bounds
+    if (gcnt2 && lane == 0) {  // (and those of the device fallback round, which reuses this tile)
+        gcnt2[r] = 0;
+        drop2[r] = 0ull;
+    }
     double n2 = 0.0, e2 = 0.0;
     const int64_t qr = (qidx && r < nqb) ? (int64_t)qidx[r] : (int64_t)r;
     constexpr int KE = DT == DT_F32 ? 16 : 32;  // elements per K-step (64 B per query row)
@@ -479,12 +484,16 @@ __global__ void __launch_bounds__(256) k_group_dots(const uint16_t* __restrict__
 //   true <x, q> <= s_x t_q <c_x, c_q> + ||x - s_x c_x|| ||q|| + ||s_x c_x|| ||q - t_q c_q|| + rounding
 //               <= key + max ||s_x c_x|| max(0, ||q - t_q c_q|| - eps_q ||q||) + rounding <= key_score + qeps.
 // Also zeroes the survivor-list lengths and the workgroup drop bounds of the screen that follows.
+// NDT (bf16 / f16; 0 = none): also the device fallback round's native tile (NativeTile, the layout
+// and qinfo of k_pack_qtile<NDT>), from the same loaded values -- the round's gated pack launch
+// is then not needed.
+template <int NDT>
 __global__ void __launch_bounds__(256) k_pack_qtile_i8(const float* __restrict__ q, int nqb, int d, int dpad8,
                                                         uint8_t* __restrict__ qt, float2* __restrict__ qfac,
                                                         float* __restrict__ qeps, const unsigned* __restrict__ maxes,
                                                         int* __restrict__ gcnt, u64* __restrict__ drop,
                                                         int* __restrict__ fails, const unsigned* __restrict__ l2max,
-                                                        float gamma) {
+                                                        float gamma, NativeTile nat) {
     const int lane = threadIdx.x & 63;
     const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= MFMA_QB) return;
@@ -492,6 +501,10 @@ __global__ void __launch_bounds__(256) k_pack_qtile_i8(const float* __restrict__
     if (lane == 0) {
         gcnt[r] = 0;
         drop[r] = 0ull;
+        if constexpr (NDT != 0) {
+            nat.gcnt[r] = 0;
+            nat.drop[r] = 0ull;
+        }
     }
     // The codes need not be the nearest (the error norm below is measured from the codes chosen), so
     // v * (1 / t) replaces the division; d <= 2048 (the common case): the lane's values are loaded
@@ -531,6 +544,30 @@ __global__ void __launch_bounds__(256) k_pack_qtile_i8(const float* __restrict__
         }
     } else {
         for (int i = lane; i < dpad8; i += 64) one(i, (r < nqb && i < d) ? q[(int64_t)r * d + i] : 0.0f);
+    }
+    if constexpr (NDT != 0) {  // the native tile (k_pack_qtile<NDT>'s layout and qinfo)
+        double n2n = 0.0, e2n = 0.0;
+        auto nat_one = [&](int i, float v) {
+            const float st = round_store<NDT>(v, nat.qt + (int64_t)(i >> 5) * MFMA_QB * 64 + (int64_t)r * 64 + (i & 31) * 2);
+            n2n += (double)st * st;
+            const double df = (double)st - (double)v;
+            e2n += df * df;
+        };
+        if (cached && nat.dpad <= 64 * PL) {
+#pragma unroll
+            for (int j = 0; j < PL; ++j) {
+                const int i = lane + 64 * j;
+                if (i < nat.dpad) nat_one(i, i < d ? vv[j] : 0.0f);
+            }
+        } else {
+            for (int i = lane; i < nat.dpad; i += 64) nat_one(i, (r < nqb && i < d) ? q[(int64_t)r * d + i] : 0.0f);
+        }
+        n2n = wave_sum_f64(n2n);
+        e2n = wave_sum_f64(e2n);
+        if (lane == 0 && r < nqb) {
+            nat.qinfo[2 * r] = (float)(sqrt(n2n) * (1.0 + 1e-6)) + 1e-30f;
+            nat.qinfo[2 * r + 1] = (float)(sqrt(e2n) * (1.0 + 1e-6));
+        }
     }
     e2 = wave_sum_f64(e2);
     n2 = wave_sum_f64(n2);
@@ -2387,7 +2424,9 @@ __device__ __forceinline__ void refine(const RefineArgs& a, int KP2) {
                 __syncthreads();
                 t = thr_s;
             } else {
-                t = block_kth_range<RF_E>(keys, a.Kp, KP2, red);
+                // (the radix select takes exactly Kp at about the cost of a range: the one-wave
+                // Kp-th search below is then not needed, and only Kp rows are scored)
+                t = block_kth<RF_E>(keys, a.Kp, red);
             }
         }
         nkept = block_write_kept<RF_E>(keys, t, cq, red);
@@ -2856,9 +2895,12 @@ __global__ void __launch_bounds__(RF_THREADS) k_refine_wide(RefineArgs a, int KA
 // has `rank` DISTINCT rows scoring >= T, so T never exceeds the true rank-th best screen score and
 // the key just below every score >= T, (ord(T) << 32) | 0, is a valid starting threshold
 // (rank = Kp: proven; rank < Kp: optimistic, checked by the refine certificate).
-// 8-bit radix select, one 256-thread block per query, maxima held in registers (VPT per thread):
-// four rounds of (LDS histogram of the next digit among values matching the prefix so far, one
-// wave scans the 256 bins from the top) give the exact rank-th largest orderable value.
+// Radix select over the block's value RANGE, one 256-thread block per query, maxima held in
+// registers (VPT per thread): w = ord(v) - min, rounds of 8 bits from the top bit of max - min down
+// (LDS histogram of the digit among the values matching the prefix so far, one wave scans the 256
+// bins from the top) give the exact rank-th largest.  (Digits of the raw orderable value put all
+// ~4k maxima -- one or two float exponents -- into one or two bins of the first two rounds, whose
+// LDS atomics then serialise on a single address: 13 us per launch at the 8-shard step.)
 constexpr int SEED_VPT = 16;  // up to 256 * 16 = 4096 maxima per query (2x / 4x variants below)
 template <int VPT>
 __global__ void __launch_bounds__(256) k_seed_select(const float* __restrict__ seedmax, int M, int nq, int rank,
@@ -2866,21 +2908,51 @@ __global__ void __launch_bounds__(256) k_seed_select(const float* __restrict__ s
     __shared__ unsigned hist[256];
     __shared__ unsigned s_digit;
     __shared__ int s_rank;
+    __shared__ unsigned s_mn[4], s_mx[4];
     const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
     uint32_t v[VPT];
+    unsigned mn = ~0u, mx = 0u;
 #pragma unroll
     for (int e = 0; e < VPT; ++e) {
         const int j = tid + 256 * e;
-        v[e] = j < M ? ord_f32(seedmax[(size_t)q * M + j]) : 0u;  // 0 = padding (below every value)
+        v[e] = j < M ? ord_f32(seedmax[(size_t)q * M + j]) : 0u;
+        if (j < M) {
+            mn = min(mn, v[e]);
+            mx = max(mx, v[e]);
+        }
     }
-    uint32_t prefix = 0u, mask = 0u;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        mn = min(mn, (unsigned)__shfl_xor((int)mn, o, 64));
+        mx = max(mx, (unsigned)__shfl_xor((int)mx, o, 64));
+    }
+    if (lane == 0) {
+        s_mn[tid >> 6] = mn;
+        s_mx[tid >> 6] = mx;
+    }
+    __syncthreads();
+    mn = min(min(s_mn[0], s_mn[1]), min(s_mn[2], s_mn[3]));
+    mx = max(max(s_mx[0], s_mx[1]), max(s_mx[2], s_mx[3]));
+    if (M < rank) {  // fewer than `rank` values: no threshold
+        if (tid == 0) thr0[q] = 0ull;
+        return;
+    }
+#pragma unroll
+    for (int e = 0; e < VPT; ++e) v[e] -= mn;  // (padding: excluded by index below)
+    const unsigned span = mx - mn;
+    const int bits = span ? 32 - __builtin_clz(span) : 0;
+    uint32_t prefix = 0u;
     int r = rank;
-    for (int shift = 24; shift >= 0; shift -= 8) {
+    for (int sh = bits - 8; sh > -8; sh -= 8) {
+        // digit = bits [sh, sh + 8) of w (sh < 0: the low sh + 8 bits, left-aligned); the prefix
+        // fixes the bits above sh + 8
+        const uint32_t hmask = sh + 8 >= 32 ? 0u : ~0u << (sh + 8);
         hist[tid] = 0u;
         __syncthreads();
 #pragma unroll
         for (int e = 0; e < VPT; ++e)
-            if ((v[e] & mask) == prefix) atomicAdd(&hist[(v[e] >> shift) & 255u], 1u);
+            if (tid + 256 * e < M && (v[e] & hmask) == prefix)
+                atomicAdd(&hist[(sh >= 0 ? v[e] >> sh : v[e] << -sh) & 255u], 1u);
         __syncthreads();
         if (tid < 64) {  // lane l holds bins 255-4l .. 252-4l (descending)
             unsigned c[4], sum = 0;
@@ -2904,24 +2976,16 @@ __global__ void __launch_bounds__(256) k_seed_select(const float* __restrict__ s
                 s_digit = 255u - 4u * lane - (unsigned)i;
                 s_rank = r - (int)cum;
             }
-            if (__ballot(here) == 0ull && lane == 0) {  // fewer than `rank` values in total
-                s_digit = 0u;
-                s_rank = 0;
-            }
         }
         __syncthreads();
-        if (s_rank == 0) {  // not enough values: no threshold
-            prefix = 0u;
-            break;
-        }
-        prefix |= s_digit << shift;
-        mask |= 255u << shift;
+        prefix |= sh >= 0 ? s_digit << sh : s_digit >> -sh;
         r = s_rank;
         __syncthreads();
     }
     if (tid == 0) {
-        const float T = unord_f32(prefix);
-        thr0[q] = (prefix == 0u || T == -INFINITY) ? 0ull : ((u64)prefix << 32);
+        const uint32_t o = mn + prefix;
+        const float T = unord_f32(o);
+        thr0[q] = (o == 0u || T == -INFINITY) ? 0ull : ((u64)o << 32);
     }
 }
 
@@ -3132,16 +3196,18 @@ hipError_t launch_gather_rows(int dt, const uint8_t* data, const int64_t* ids, i
 }
 
 hipError_t launch_pack_qtile(int dt, const float* q, int nqb, int d, int dpad, uint8_t* qt, float* qinfo, int* gcnt,
-                             u64* drop, hipStream_t st, int* fails, const int* gate, const int* qidx) {
+                             u64* drop, hipStream_t st, int* fails, const int* gate, const int* qidx, int* gcnt2,
+                             u64* drop2) {
+    if ((gcnt2 == nullptr) != (drop2 == nullptr)) return hipErrorInvalidValue;
     if (dt == DT_F32)
         hipLaunchKernelGGL(k_pack_qtile<DT_F32>, dim3(MFMA_QB / 4), dim3(256), 0, st, q, nqb, d, dpad, qt, qinfo,
-                           gcnt, drop, fails, gate, qidx);
+                           gcnt, drop, fails, gate, qidx, gcnt2, drop2);
     else if (dt == DT_BF16)
         hipLaunchKernelGGL(k_pack_qtile<DT_BF16>, dim3(MFMA_QB / 4), dim3(256), 0, st, q, nqb, d, dpad, qt, qinfo,
-                           gcnt, drop, fails, gate, qidx);
+                           gcnt, drop, fails, gate, qidx, gcnt2, drop2);
     else
         hipLaunchKernelGGL(k_pack_qtile<DT_F16>, dim3(MFMA_QB / 4), dim3(256), 0, st, q, nqb, d, dpad, qt, qinfo,
-                           gcnt, drop, fails, gate, qidx);
+                           gcnt, drop, fails, gate, qidx, gcnt2, drop2);
     return hipGetLastError();
 }
 
@@ -3190,9 +3256,22 @@ hipError_t launch_quant_rows(int dt, const uint8_t* data, int dpad, int64_t r0, 
 
 hipError_t launch_pack_qtile_i8(const float* q, int nqb, int d, int dpad8, uint8_t* qt, float2* qfac, float* qeps,
                                 const unsigned* maxes, int* gcnt, u64* drop, hipStream_t st, int* fails,
-                                const unsigned* l2max, float gamma) {
-    hipLaunchKernelGGL(k_pack_qtile_i8, dim3(MFMA_QB / 4), dim3(256), 0, st, q, nqb, d, dpad8, qt, qfac, qeps, maxes,
-                       gcnt, drop, fails, l2max, gamma);
+                                const unsigned* l2max, float gamma, const NativeTile* nat) {
+    const NativeTile none{};
+    if (!nat) {
+        hipLaunchKernelGGL(k_pack_qtile_i8<0>, dim3(MFMA_QB / 4), dim3(256), 0, st, q, nqb, d, dpad8, qt, qfac, qeps,
+                           maxes, gcnt, drop, fails, l2max, gamma, none);
+        return hipGetLastError();
+    }
+    if (!nat->qt || !nat->qinfo || !nat->gcnt || !nat->drop || nat->dpad % 32 != 0) return hipErrorInvalidValue;
+    if (nat->dt == DT_BF16)
+        hipLaunchKernelGGL(k_pack_qtile_i8<DT_BF16>, dim3(MFMA_QB / 4), dim3(256), 0, st, q, nqb, d, dpad8, qt, qfac,
+                           qeps, maxes, gcnt, drop, fails, l2max, gamma, *nat);
+    else if (nat->dt == DT_F16)
+        hipLaunchKernelGGL(k_pack_qtile_i8<DT_F16>, dim3(MFMA_QB / 4), dim3(256), 0, st, q, nqb, d, dpad8, qt, qfac,
+                           qeps, maxes, gcnt, drop, fails, l2max, gamma, *nat);
+    else
+        return hipErrorInvalidValue;
     return hipGetLastError();
 }
 
