@@ -465,12 +465,14 @@ __device__ __forceinline__ void sort_best_first(double* sc, uint32_t* ids, int n
     const int tid = threadIdx.x;
     if (n2 <= (int)blockDim.x) {
         const bool act = tid < n2;
+        // (waves holding no element skip the shuffles -- they still meet every barrier)
+        const bool wact = (tid & ~63) < n2;
         double s = act ? sc[tid] : 0.0;
         uint32_t id = act ? ids[tid] : 0u;
         for (int size = 2; size <= n2; size <<= 1) {
             for (int stride = size >> 1; stride > 0; stride >>= 1) {
-                double ps;
-                uint32_t pid;
+                double ps = 0.0;
+                uint32_t pid = 0u;
                 if (stride >= 64) {
                     __syncthreads();  // (every thread's previous read of its partner is done)
                     if (act) {
@@ -480,7 +482,7 @@ __device__ __forceinline__ void sort_best_first(double* sc, uint32_t* ids, int n
                     __syncthreads();
                     ps = act ? sc[tid ^ stride] : 0.0;
                     pid = act ? ids[tid ^ stride] : 0u;
-                } else {
+                } else if (wact) {
                     ps = __shfl_xor(s, stride, 64);
                     pid = (uint32_t)__shfl_xor((int)id, stride, 64);
                 }
@@ -522,6 +524,72 @@ __device__ __forceinline__ void sort_best_first(double* sc, uint32_t* ids, int n
     }
 }
 
+
+// (sc, ids)[0, n) best first in place by rank (n <= blockDim.x; entries [n, n2) -- the caller's
+// worst-score padding -- stay where they are): each entry's rank is the number of entries ahead of
+// it under better_exact's order (IEEE compare, so -0 == +0; NaN ranked as the worst score; then
+// the id; then the position, so equal entries keep distinct ranks), counted by NG groups of
+// threads over a share of the entries each (8 broadcast LDS reads at a time, branch-free) and
+// summed in LDS; then every entry moves to its rank.  A wave64 VALU op takes 4 cycles, so the
+// count is spread over the whole block instead of one thread per entry (and ~log^2 n bitonic
+// stages).  Larger n: the bitonic sort of all n2.
+template <int METRIC>
+__device__ __forceinline__ void sort_valid_best_first(double* sc, uint32_t* ids, int n, int n2) {
+    if (n > (int)blockDim.x) {
+        sort_best_first<METRIC>(sc, ids, n2);
+        return;
+    }
+    __shared__ int rk[256];
+    const int tid = threadIdx.x;
+    int T = 64;  // threads per group: one per entry
+    while (T < n) T <<= 1;
+    const int NG = T <= 256 ? (int)blockDim.x / T : 1;
+    const int e = tid & (T - 1), g = tid / T;
+    const double worst = METRIC == METRIC_L2 ? INFINITY : -INFINITY;
+    if (NG > 1) {
+        for (int i = tid; i < T; i += blockDim.x) rk[i] = 0;
+        __syncthreads();
+    }
+    double ms = 0.0;
+    uint32_t mid = 0u;
+    int rank = 0;
+    const bool mine = e < n && g < NG;
+    if (mine) {
+        ms = sc[e];
+        mid = ids[e];
+        const double mk = ms == ms ? ms : worst;
+        const int j0 = (int)((int64_t)n * g / NG), j1 = (int)((int64_t)n * (g + 1) / NG);
+        for (int jb = j0; jb < j1; jb += 8) {
+            double sv[8];
+            uint32_t iv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int j = min(jb + u, j1 - 1);
+                sv[u] = sc[j];
+                iv[u] = ids[j];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int j = jb + u;
+                const double k = sv[u] == sv[u] ? sv[u] : worst;
+                const int gt = METRIC == METRIC_L2 ? (int)(k < mk) : (int)(k > mk);
+                const int ahead = gt | ((int)(k == mk) & ((int)(iv[u] < mid) | ((int)(iv[u] == mid) & (int)(j < e))));
+                rank += ahead & (int)(j < j1);
+            }
+        }
+    }
+    if (NG > 1) {
+        if (mine && rank) atomicAdd(&rk[e], rank);
+        __syncthreads();
+        if (mine && g == 0) rank = rk[e];
+    }
+    __syncthreads();  // (every read of sc / ids is done)
+    if (mine && g == 0) {
+        sc[rank] = ms;
+        ids[rank] = mid;
+    }
+    __syncthreads();
+}
 
 // Exact canonical fp64 scores of R stored rows at once (row[i] < 0: absent), query staged in LDS as
 // fp64 (QLDS) or read from global fp32.  Lane l owns 8-element groups g = l, l+64, ... in ascending

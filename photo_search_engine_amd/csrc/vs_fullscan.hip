@@ -81,7 +81,8 @@ __device__ __forceinline__ void fs_merge(const FsLists& L, int& cur, int& nl, in
     nl = min(k, nl + nb);
 }
 
-// sort the batch's nb entries (bitonic over the next power of two, worst-padded) and merge them in
+// sort the batch's nb entries (by rank; the bitonic network over the next power of two, worst-padded,
+// past one entry per thread) and merge them in
 __device__ __forceinline__ void fs_sort_merge(const FsLists& L, int& cur, int& nl, int nb, int k) {
     int n2 = 1;
     while (n2 < nb) n2 <<= 1;
@@ -90,7 +91,7 @@ __device__ __forceinline__ void fs_sort_merge(const FsLists& L, int& cur, int& n
         L.bid[j] = 0xFFFFFFFFu;
     }
     __syncthreads();
-    sort_best_first<METRIC_IP>(L.bsc, L.bid, n2);
+    sort_valid_best_first<METRIC_IP>(L.bsc, L.bid, nb, n2);
     fs_merge(L, cur, nl, nb, k);
 }
 
@@ -225,7 +226,7 @@ __global__ void __launch_bounds__(FS_THREADS) k_full_scan(FullScanArgs a, int KL
                 L.bid[g] = id;
             }
             __syncthreads();
-            sort_best_first<METRIC_IP>(L.bsc, L.bid, h2);
+            sort_valid_best_first<METRIC_IP>(L.bsc, L.bid, G, h2);
             const bool has_floor = G >= k && L.bid[k - 1] != 0xFFFFFFFFu;
             const double fs = has_floor ? L.bsc[k - 1] : -INFINITY;
             const uint32_t fi = has_floor ? L.bid[k - 1] : 0xFFFFFFFFu;

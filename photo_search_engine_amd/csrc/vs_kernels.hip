@@ -2524,7 +2524,7 @@ __device__ __forceinline__ void refine(const RefineArgs& a, int KP2) {
         ids[j] = 0xFFFFFFFFu;
     }
     __syncthreads();
-    sort_best_first<METRIC>(sc, ids, KP2);  // best first
+    sort_valid_best_first<METRIC>(sc, ids, nv, KP2);  // best first
     // exactness certificate: every non-candidate row has exact transformed score <= smin + eps
     if (tid == 0) {
         // rows outside the candidate set scored at most: the Kp-th best listed key (when the list
@@ -2650,10 +2650,6 @@ __device__ __forceinline__ void rfw_score(const RefineArgs& a, const uint32_t* i
     }
 }
 
-// bitonic sort of (sc, ids)[0, n2) best first (n2 a power of two, padding = worst)
-__device__ __forceinline__ void rfw_sort(double* sc, uint32_t* ids, int n2) {
-    sort_best_first<METRIC_IP>(sc, ids, n2);
-}
 template <int DT, int METRIC, bool QLDS>
 __global__ void __launch_bounds__(RF_THREADS) k_refine_wide(RefineArgs a, int KA) {
     constexpr bool L2 = METRIC == METRIC_L2;
@@ -2743,7 +2739,7 @@ __global__ void __launch_bounds__(RF_THREADS) k_refine_wide(RefineArgs a, int KA
         ids[j] = 0xFFFFFFFFu;
     }
     __syncthreads();
-    rfw_sort(sc, ids, nA2);  // phase A best first (nA2 <= RFW_CAP: KA <= RFW_CAP / 2)
+    sort_valid_best_first<METRIC_IP>(sc, ids, nA, nA2);  // phase A best first (nA2 <= RFW_CAP: KA <= RFW_CAP / 2)
     } else {  // phase 2: resume from the phase-1 state
         nA = a.pa_n[q];
         tA = a.pa_tA[q];
@@ -2859,7 +2855,7 @@ __global__ void __launch_bounds__(RF_THREADS) k_refine_wide(RefineArgs a, int KA
         ids[j] = 0xFFFFFFFFu;
     }
     __syncthreads();
-    if (nb_s > 0) rfw_sort(sc, ids, nF2);
+    if (nb_s > 0) sort_valid_best_first<METRIC_IP>(sc, ids, nF, nF2);
     // ---- certificate ----
     if (tid == 0) {
         u64 th = a.drop ? a.drop[q] : 0ull;

@@ -60,6 +60,7 @@ for s in ${STEPS:-tests cfg3 shard8 mix03 micro multi}; do
     trace1) mkdir -p gpurun_out/trace1 && run trace1 300 rocprofv3 --kernel-trace --memory-copy-trace -d gpurun_out/trace1 -o t --output-format csv -- python bench.py --workload cfg1 --steps 200 --warmup 20 && \
       python scripts/trace_tail.py $(ls gpurun_out/trace1/*/t_kernel_trace.csv gpurun_out/trace1/t_kernel_trace.csv 2>/dev/null | head -1) 40 "vs::|copyBuffer|Kernel" > gpurun_out/trace1_tail.txt && \
       cp $(ls gpurun_out/trace1/*/t_memory_copy_trace.csv gpurun_out/trace1/t_memory_copy_trace.csv 2>/dev/null | head -1) gpurun_out/trace1_memcpy.csv; rm -rf gpurun_out/trace1 ;;
+    stamps1) run stamps1_1m 300 python scripts/refine_stamps.py --run --rows 1000000 --single ;;
     stamps2) run stamps2_1250k 300 python scripts/refine_stamps.py --run --rows 1250000 --two-phase 8 ;;
     ab8) for i in 1 2; do for lib in diag/libvs_base.so photo_search_engine_amd/libvs.so; do
            VS_LIB_PATH=$lib timeout -k 10 300 python bench.py --shard-of 8 --steps 30 --no-cpu-baseline > gpurun_out/ab8.tmp 2>&1
@@ -71,6 +72,11 @@ for s in ${STEPS:-tests cfg3 shard8 mix03 micro multi}; do
            rc=$?; echo "$lib $(tail -1 gpurun_out/ab3.tmp)" >> gpurun_out/ab3.txt
            if [ $rc -ne 0 ]; then echo "step ab3 rc=$rc" >> gpurun_out/steps.log; exit $rc; fi
          done; done; echo "step ab3 rc=0" >> gpurun_out/steps.log ;;
+    ab) for i in 1 2; do for lib in $ABLIBS; do
+           VS_LIB_PATH=$lib timeout -k 10 300 python bench.py $ABARGS --no-cpu-baseline > gpurun_out/ab.tmp 2>&1
+           rc=$?; echo "$lib $(tail -1 gpurun_out/ab.tmp)" >> gpurun_out/ab_$ABNAME.txt
+           if [ $rc -ne 0 ]; then echo "step ab rc=$rc" >> gpurun_out/steps.log; exit $rc; fi
+         done; done; echo "step ab rc=0" >> gpurun_out/steps.log ;;
     ab2) for i in 1 2; do for lib in diag/libvs_base.so photo_search_engine_amd/libvs.so; do
            VS_LIB_PATH=$lib timeout -k 10 300 python bench.py --workload cfg2 --no-cpu-baseline > gpurun_out/ab2.tmp 2>&1
            rc=$?; echo "$lib $(tail -1 gpurun_out/ab2.tmp)" >> gpurun_out/ab2.txt
