@@ -3473,10 +3473,12 @@ static void launch_refine_one(const RefineArgs& a, int nq, int KP2, size_t lds, 
 // per workgroup, at most 32 per query, the whole grid within one wave of the chip.
 int refine_split(int nq, int Kp, int dt, int num_cu) {
     const int per_round = (dt == DT_F32 ? 2 : 4) * (RF_THREADS / 64);
-    // GEMV batches (<= 8 queries: the product's single-query call): one scoring round per
+    // GEMV batches (<= 8 queries: the product's single-query call): half a scoring round per
     // workgroup -- a single query's Kp rows gathered by one CU were a chain of dependent rounds
-    // (cfg2: 42 us for ~100 fp32 rows); MFMA batches: two rounds per workgroup
-    int ns = nq <= GEMV_NQ_MAX ? (Kp + per_round - 1) / per_round : Kp / (2 * per_round);
+    // (cfg2: 42 us for ~100 fp32 rows), and the gathers of a round still wait on their page
+    // walks and lines for ~10 us, so more CUs each take fewer rows (one round: 3-4 us slower per
+    // cfg2 step in the in-box A/B); MFMA batches: two rounds per workgroup
+    int ns = nq <= GEMV_NQ_MAX ? (2 * Kp + per_round - 1) / per_round : Kp / (2 * per_round);
     ns = std::min(ns, 32);
     ns = std::min(ns, num_cu / std::max(nq, 1));
     return ns >= 2 ? ns : 1;
