@@ -82,6 +82,7 @@ for s in ${STEPS:-tests cfg3 shard8 mix03 micro multi}; do
            rc=$?; echo "$lib $(tail -1 gpurun_out/ab2.tmp)" >> gpurun_out/ab2.txt
            if [ $rc -ne 0 ]; then echo "step ab2 rc=$rc" >> gpurun_out/steps.log; exit $rc; fi
          done; done; echo "step ab2 rc=0" >> gpurun_out/steps.log ;;
+    hnswins) run hnsw_insert 900 python scripts/hnsw_insert_timing.py ;;
     hnsw) run hnsw_bench 900 python scripts/hnsw_bench.py ;;
     smallscan) run small_scan 600 python scripts/small_scan_timing.py ;;
     tracemulti) mkdir -p gpurun_out/tracem && run tracemulti 600 rocprofv3 --kernel-trace --memory-copy-trace -d gpurun_out/tracem -o t --output-format csv -- python scripts/multi_step_timing.py --reps 3 && \

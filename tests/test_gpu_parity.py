@@ -691,3 +691,30 @@ def test_small_scan_ties_and_zero_rows(PlainFlatIndex):
         np.testing.assert_array_equal(I, Ie)
         np.testing.assert_array_equal(D, S.astype(np.float32))
     ix.close()
+
+
+@pytest.mark.parametrize("screen", ["native", "int8"])
+@pytest.mark.parametrize("metric", ["ip", "l2"])
+def test_zero_query_in_batch_ties_to_lowest_ids(FlatIndex, screen, metric):
+    # zero queries inside an MFMA batch: every inner-product score is exactly 0 (all rows tie), so
+    # the refines' selections and rank sorts must return the lowest ids in order; half the rows
+    # are all-negative (their products with 0 are -0.0) and a few rows are zero vectors
+    rng = np.random.default_rng(11)
+    d, N, nq, k = 96, 20_000, 256, 50
+    x = rng.standard_normal((N, d)).astype(np.float32)
+    x[::2] = -np.abs(x[::2])
+    x /= np.linalg.norm(x, axis=1, keepdims=True)  # (unit rows: distances ~2, the fp32 check's scale)
+    x[5:9] = 0.0
+    q = rng.standard_normal((nq, d)).astype(np.float32)
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    q[[0, 100, 255]] = 0.0
+    ix = FlatIndex(d, metric, "bf16")
+    ix.add(x)
+    if screen == "int8":
+        ix.set_screen("int8")
+    D, I = _check_exact(ix, O.round_dtype(q, "bf16"), k, metric)
+    if metric == "ip":
+        for r in (0, 100, 255):
+            np.testing.assert_array_equal(I[r], np.arange(k))
+            assert (D[r] == 0.0).all()
+    ix.close()
