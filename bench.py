@@ -229,6 +229,7 @@ def main():
     result = {}
     per_rank = {}
     host_ms = {}
+    host_in_loop = {}
 
     def step():
         result["D"], result["I"], result["S"] = sh.search(q, k)
@@ -253,8 +254,11 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
+        t_in = 0.0  # host time inside the step calls (diagnostic: ~ elapsed means host-bound)
         for _ in range(args.steps):
+            ts = time.perf_counter()
             step()
+            t_in += time.perf_counter() - ts
         torch.cuda.synchronize()
         if G > 1:
             dist.barrier()
@@ -273,6 +277,7 @@ def main():
             hs.append((time.perf_counter() - th) * 1e3)
         torch.cuda.synchronize()
         host_ms[scr] = float(np.median(hs))
+        host_in_loop[scr] = t_in * 1e3 / max(args.steps, 1)
         per_rank[scr] = [float(np.mean(km)) if km else float("nan"), sum(xm) / args.steps, len(xm) / args.steps,
                          el * 1e3 / args.steps, float(n_local)]
         if G > 1:
@@ -350,6 +355,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "host_enqueue_ms": round(host_ms.get(screen, float("nan")), 4),
+            "host_ms_in_loop": round(host_in_loop.get(screen, float("nan")), 4),
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
