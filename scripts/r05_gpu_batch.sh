@@ -26,6 +26,8 @@ for s in ${STEPS:-tests cfg3 shard8 mix03 micro multi}; do
     cfg3) run bench_cfg3 600 python bench.py ;;
     cfg1) run bench_cfg1 300 python bench.py --workload cfg1 --steps 1000 --warmup 50 ;;
     shard8) run bench_shard8 300 python bench.py --shard-of 8 --steps 30 --no-cpu-baseline ;;
+    shard2) run bench_shard2 300 python bench.py --shard-of 2 --steps 20 --no-cpu-baseline ;;
+    shard4) run bench_shard4 300 python bench.py --shard-of 4 --steps 30 --no-cpu-baseline ;;
     spawn2) run bench_spawn2 600 python bench.py --gpus 2 --same-device --dist-backend gloo --rows 2000000 --steps 10 --no-cpu-baseline ;;
     mix03) run bench_mix03 600 python bench.py --data mixture-sorted --sigma 0.3 --warmup 8 --no-cpu-baseline ;;
     mix05) run bench_mix05 600 python bench.py --data mixture-sorted --sigma 0.5 --warmup 8 --no-cpu-baseline ;;
