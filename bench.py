@@ -91,6 +91,8 @@ def parse():
     ap.add_argument("--sigma", type=float, default=1.0, help="--data mixture: cluster spread")
     ap.add_argument("--iso-data", action="store_true",
                     help="cfg5: isotropic rows (the flat bench's data) instead of the Gaussian mixture")
+    ap.add_argument("--k1-schedule", type=int, default=None, choices=[0, 1, 2],
+                    help="the direct K1 screens' K-step schedule (include/vs.h vs_set_k1_schedule; default: the library's)")
     ap.add_argument("--traffic-file", default=None,
                     help="rocprofv3 PMC summary giving HBM bytes per launch (default profiles/traffic_<workload>.json)")
     return ap.parse_args()
@@ -152,8 +154,10 @@ def main():
     import torch.distributed as dist
 
     from photo_search_engine_amd.distributed import ShardedFlatIndex, shard_range
-    from photo_search_engine_amd.index import synthesize_device
+    from photo_search_engine_amd.index import set_k1_schedule, synthesize_device
 
+    if args.k1_schedule is not None:
+        set_k1_schedule(args.k1_schedule)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -193,6 +193,31 @@ int vs_set_scan_limit(vs_index* index, int64_t bytes);
  * steps: the box's own zero / real operand pair behind the power note of its roofline. */
 int vs_screen_probe(vs_index* index, const float* q_dev, int64_t nq, int32_t screen, int32_t zero_queries,
                     void* stream, float* ms);
+/* Diagnostic forms of the direct screen's loop (csrc/vs_k1probe.hip; DESIGN §5 "Where K1 int8's time
+ * goes"), over the whole index like vs_screen_probe (thresholds at +inf, 9..256 device queries,
+ * zero_queries as there).  screen = VS_SCREEN_I8 (inner-product int8 direct screen; variants
+ * LOADS, LDS, MFMA, FULL, FULL_MS, FULL_PRIO, FULL_MS_PRIO) or VS_SCREEN_NATIVE (bf16 direct screen;
+ * LOADS, MFMA, FULL, FULL_MS).  `reps` launches back to back, each between its own HIP events:
+ * ms[r] = launch r's duration; stamps[(r * G + b) * 4 + {0,1,2,3}] = workgroup b's s_memtime at the
+ * loop's start and end, and its s_memrealtime (100 MHz) at the same points (host array of
+ * reps * 256 * 4); *G_out = the launch's workgroups.  Synchronises. */
+/* The direct K1 screens' K-step schedule, process-wide: 0 = one barrier at the head of every K-step;
+ * 1 (default) = the mid-step barrier on the int8 inner-product direct screen; 2 = also
+ * on the bf16 / f16 direct screen.  The same keys, survivors and results under every schedule. */
+int vs_set_k1_schedule(int32_t schedule);
+int vs_k1_schedule(void);
+enum {
+    VS_K1P_LOADS = 0,        /* corpus loads + query LDS-DMAs + the per-K-step barriers */
+    VS_K1P_LDS = 1,          /* + the query-fragment LDS reads */
+    VS_K1P_MFMA = 2,         /* + the MFMAs (no tile epilogue) */
+    VS_K1P_FULL = 3,         /* the whole loop with the epilogue's bound test (the product's schedule) */
+    VS_K1P_FULL_MS = 4,      /* the same under the mid-step-barrier schedule */
+    VS_K1P_FULL_PRIO = 5,    /* FULL with static priority 1 for waves 4-7 */
+    VS_K1P_FULL_MS_PRIO = 6  /* FULL_MS with static priority 1 for waves 4-7 */
+};
+int vs_k1_probe(vs_index* index, const float* q_dev, int64_t nq, int32_t screen, int32_t variant,
+                int32_t zero_queries, int32_t reps, void* stream, float* ms, unsigned long long* stamps,
+                int32_t* G_out);
 int vs_timing_fetch(vs_index* index, float* ms, int cap, int* kernel_kind);
 int64_t vs_uncertified_count(vs_index* index);   /* first-pass certificate failures; synchronises */
 /* queries answered by the exact full scan (no bounded screen could certify them; see
@@ -314,7 +339,8 @@ int64_t vs_hnsw_ntotal(const vs_hnsw* graph);
  * keeps ONE device graph laid out for the final node count -- nodes not inserted yet have empty
  * lists and no links to them, so they are unreachable -- and patches in each batch's new lists
  * and reverse links (photo_search_engine_amd/hnsw.py insert_rows).  Slots and ids are validated
- * as in vs_hnsw_create. */
+ * as in vs_hnsw_create, and a patch must rewrite whole (node, level) lists -- every slot of each list
+ * it touches -- each as distinct ids followed by -1s (VS_ERR_ARG otherwise, the graph unchanged). */
 int vs_hnsw_patch(vs_hnsw* graph, int64_t m, const uint64_t* pos, const int32_t* val, int32_t entry_point,
                   int32_t max_level);
 

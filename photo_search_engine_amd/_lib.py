@@ -88,6 +88,10 @@ _SIGS = {
     "vs_full_scan_count": (_c_i64, [_vp]),
     "vs_set_scan_limit": (ctypes.c_int, [_vp, _c_i64]),
     "vs_screen_probe": (ctypes.c_int, [_vp, _vp, _c_i64, ctypes.c_int32, ctypes.c_int32, _vp, _vp]),
+    "vs_k1_probe": (ctypes.c_int, [_vp, _vp, _c_i64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                   _vp, _vp, _vp, _vp]),
+    "vs_set_k1_schedule": (ctypes.c_int, [ctypes.c_int32]),
+    "vs_k1_schedule": (ctypes.c_int, []),
     "vs_host_staging_bytes": (_c_i64, [_vp]),
     "vs_screen_copy_bytes": (_c_i64, [_vp]),
     "vs_screen_state": (ctypes.c_int, [_vp, _vp, ctypes.c_int]),

@@ -11,7 +11,8 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libvs.so")
-SOURCES = ["vs_api.hip", "vs_fullscan.hip", "vs_hnsw.hip", "vs_io.hip", "vs_ivf.hip", "vs_kernels.hip", "vs_multi.hip"]
+SOURCES = ["vs_kernels.hip", "vs_api.hip", "vs_fullscan.hip", "vs_hnsw.hip", "vs_io.hip", "vs_ivf.hip", "vs_k1probe.hip",
+           "vs_multi.hip"]
 ARCH = os.environ.get("VS_OFFLOAD_ARCH", "gfx950")
 
 
@@ -48,7 +49,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(obj_dir, exist_ok=True)
     headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
     headers.append(os.path.join(HERE, "..", "include", "vs.h"))
-    objs = []
+    objs, jobs = [], []
     for src in SOURCES:
         spath = os.path.join(CSRC, src)
         obj = os.path.join(obj_dir, src.replace(".hip", ".o"))
@@ -57,9 +58,15 @@ def build(force: bool = False, verbose: bool = False) -> str:
                    "-Wno-unused-value", "-Wno-inline-asm", "-c", spath, "-o", obj + ".tmp.o"]
             if verbose:
                 print(" ".join(cmd), file=sys.stderr)
-            subprocess.run(cmd, check=True)
-            os.replace(obj + ".tmp.o", obj)
+            jobs.append((cmd, obj))
         objs.append(obj)
+    # the sources compile concurrently (vs_kernels.hip alone takes ~3 minutes)
+    procs = [(subprocess.Popen(cmd), obj) for cmd, obj in jobs]
+    failed = [obj for p, obj in procs if p.wait() != 0]
+    if failed:
+        raise subprocess.CalledProcessError(1, "hipcc " + " ".join(os.path.basename(o) for o in failed))
+    for _, obj in jobs:
+        os.replace(obj + ".tmp.o", obj)
     tmp = os.path.join(HERE, "libvs.tmp.so")  # a .so suffix keeps hipcc from emitting bundle side files
     cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
     subprocess.run(cmd, check=True)

@@ -706,9 +706,11 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
         // rows (ScreenArgs::drop, the refine's certificate bound for them), so the G lists together
         // hold at most kRefineRegKeys keys -- the refine selects the best Kp from them in registers
         // and no k_merge launch runs (cfg2: 1024 blocks x 176 keys took a merge of 15 us).  A block
-        // that drops a row the query needs fails the certificate (-> the full scan); with ~Kp / G of
-        // the best rows per block and Kb >= 16 that does not happen in practice.
-        if (nqb == 1 && ix->ntotal >= Kp) {
+        // that drops a row the query needs fails the certificate; with ~Kp / G of the best rows per
+        // block and Kb >= 16 that does not happen in practice.  First passes only (seed_rank > 0):
+        // Kb does not grow with Kp, so the host API's 4x-deeper re-searches of a failed query (a
+        // burst of near-duplicates in one block) keep whole Kp-deep lists and can certify it.
+        if (nqb == 1 && seed_rank > 0 && ix->ntotal >= Kp) {
             const int kb = (int)std::max<int64_t>(16, (kRefineRegKeys / std::max(a.G, 1)) / 16 * 16);
             if (kb < Kp && (int64_t)a.G * kb <= kRefineRegKeys) {
                 a.Kp = kb;
@@ -906,6 +908,7 @@ int fallback_depth(const vs_index* ix) { return (int)std::min<int64_t>(KP_MAX, r
 // through a running top-k, so the answer is faiss's (ties to the lowest ids) for any tie count.
 // gate: the fallback round's failure count (c->fails[1]; the launch returns at once while it is
 // 0), or null = run.  Scanned queries count in this call's counter or the index's d_unres.
+constexpr int64_t kFullScanScratchMax = 512ll << 20;
 constexpr int64_t kFullScanScratch = 32ll << 20;  // per-workgroup lists of one block, at most
 // rows_per_wg: each workgroup's row range is at least this long (G = rows / rows_per_wg, <= CUs)
 void full_scan_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float* D, int64_t* I, double* S64,
@@ -913,8 +916,12 @@ void full_scan_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float
                      int rows_per_wg = TR, bool fallback = true, bool all_queries = false) {
     const int64_t ranges = (ix->ntotal + rows_per_wg - 1) / rows_per_wg;
     const int64_t per_wg = (int64_t)nqb * k * 12;
-    const int G = (int)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(ix->num_cu, ranges),
-                                                               kFullScanScratch / per_wg));
+    // scratch: per workgroup one k-list per query of the block.  32 MiB serves ~100 workgroups at
+    // 256 queries x k 100; deep lists (k in the thousands) may take up to kFullScanScratchMax so the
+    // scan still reaches a quarter of the CUs (at 32 MiB, k = 3276 left it 3 workgroups)
+    const int64_t budget = std::max<int64_t>(kFullScanScratch, std::min<int64_t>(kFullScanScratchMax,
+                                                                                 per_wg * (ix->num_cu / 4)));
+    const int G = (int)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(ix->num_cu, ranges), budget / per_wg));
     c->fsc.ensure(full_scan_scratch_bytes(nqb, G, k));
     if (c->fdone.bytes < sizeof(unsigned) * MFMA_QB) {  // zeroed once; each query's last workgroup re-zeroes
         c->fdone.ensure(sizeof(unsigned) * MFMA_QB);
@@ -1102,7 +1109,7 @@ void vs::search_exact_device_parts(vs_index* ix, const float* q_dev, int64_t nq,
     }
 }
 
-unsigned* vs::unresolved_counter(vs_index* ix) { return ix->d_unres; }
+unsigned* vs::full_scan_counter(vs_index* ix) { return ix->d_unres; }
 
 // ---- two-phase exact device search (the sharded step with a global T' exchange) ----
 // Phase A of every shard scores the best KA keys of each query's survivor list; the shards exchange
@@ -1699,70 +1706,86 @@ int vs_set_screen(vs_index* ix, int screen) {
 
 int vs_screen(const vs_index* ix) { return ix ? ix->screen : -1; }
 
+// the shared setup of the screen probes: the packed query tile (zeroed on request), every threshold at
+// +inf, the candidate buffers; the caller holds the lease and the read lock
+static ScreenArgs probe_setup(vs_index* ix, Ctx* c, const float* q_dev, int64_t nq, bool i8, bool zero_queries,
+                              hipStream_t st, std::vector<u64>& thr) {
+    const int nqb = (int)nq;
+    const int64_t tiles = (ix->ntotal + TR - 1) / TR;
+    ScreenArgs a{};
+    a.n_valid = ix->ntotal;
+    a.tiles = (int)tiles;
+    a.d = ix->d;
+    a.metric = ix->metric;
+    a.sqn = ix->sqn;
+    a.Kp = MFMA_KP_MAX;
+    a.cap = MFMA_CAP;
+    a.G = (int)std::max<int64_t>(1, std::min<int64_t>(tiles, ix->num_cu));
+    a.lcap = a.G * a.Kp;
+    c->gcnt.ensure(sizeof(int) * MFMA_QB);
+    c->drop.ensure(sizeof(u64) * MFMA_QB);
+    c->fails.ensure(2 * sizeof(int));
+    if (i8) {
+        c->qtile.ensure((size_t)MFMA_QB * ix->dpad8);
+        c->qfac.ensure(sizeof(float2) * MFMA_QB);
+        c->qeps.ensure(sizeof(float) * MFMA_QB);
+        HIP_CHECK(launch_pack_qtile_i8(q_dev, nqb, ix->d, ix->dpad8, c->qtile.as<uint8_t>(), c->qfac.as<float2>(),
+                                       c->qeps.as<float>(), ix->d_maxsq + 2, c->gcnt.as<int>(), c->drop.as<u64>(), st,
+                                       c->fails.as<int>(), ix->metric == METRIC_L2 ? ix->d_maxsq : nullptr,
+                                       gamma_of(ix->d)));
+        a.corpus = ix->data8;
+        a.dpad = ix->dpad8;
+        a.rsb = ix->rsb;
+        a.qfac = c->qfac.as<float2>();
+    } else {
+        c->qtile.ensure((size_t)MFMA_QB * ix->dpad * ix->es);
+        c->qinfo.ensure(sizeof(float) * 2 * MFMA_QB);
+        HIP_CHECK(launch_pack_qtile(ix->dtype, q_dev, nqb, ix->d, ix->dpad, c->qtile.as<uint8_t>(),
+                                    c->qinfo.as<float>(), c->gcnt.as<int>(), c->drop.as<u64>(), st));
+        a.corpus = ix->data;
+        a.dpad = ix->dpad;
+    }
+    if (zero_queries) HIP_CHECK(hipMemsetAsync(c->qtile.p, 0, c->qtile.bytes, st));
+    // every query's threshold at the key of +inf: the bound test rejects every column, so the
+    // launch is the K loop + the epilogue's bound test with no survivor to insert
+    c->thr0.ensure(sizeof(u64) * MFMA_QB);
+    thr.assign(MFMA_QB, 0xFF80000000000000ull);
+    HIP_CHECK(hipMemcpyAsync(c->thr0.p, thr.data(), sizeof(u64) * MFMA_QB, hipMemcpyHostToDevice, st));
+    a.thr0 = c->thr0.as<u64>();
+    a.drop = c->drop.as<u64>();
+    c->cand.ensure((size_t)a.G * MFMA_QB * a.cap * sizeof(u64));
+    c->part.ensure((size_t)MFMA_QB * a.lcap * sizeof(u64));
+    a.cand = c->cand.as<u64>();
+    a.glist = c->part.as<u64>();
+    a.gcnt = c->gcnt.as<int>();
+    return a;
+}
+
+static void probe_checks(vs_index* ix, const float* q_dev, int64_t nq, int32_t screen, const void* out) {
+    check_index(ix);
+    if (!q_dev || !out || nq <= GEMV_NQ_MAX || nq > MFMA_QB) throw VsError(VS_ERR_ARG, "screen probe: 9..256 device queries");
+    const bool i8 = screen == VS_SCREEN_I8;
+    if (i8 && (ix->screen != VS_SCREEN_I8 || !ix->data8 || ix->i8_res || !i8_direct_ok(ix->dpad8)))
+        throw VsError(VS_ERR_ARG, "screen probe: the int8 probe needs the int8 direct screen (no group residuals)");
+    if (!i8 && !((ix->dtype == DT_BF16 || ix->dtype == DT_F16) && d16_direct_ok(ix->dpad)))
+        throw VsError(VS_ERR_ARG, "screen probe: the native probe needs bf16 / f16 rows of the direct screen");
+    if (ix->ntotal == 0) throw VsError(VS_ERR_ARG, "index is empty");
+}
+
 int vs_screen_probe(vs_index* ix, const float* q_dev, int64_t nq, int32_t screen, int32_t zero_queries, void* stream,
                     float* ms) {
     return guarded([&] {
         check_index(ix);
-        if (!q_dev || !ms || nq <= GEMV_NQ_MAX || nq > MFMA_QB) throw VsError(VS_ERR_ARG, "vs_screen_probe: 9..256 device queries");
+        probe_checks(ix, q_dev, nq, screen, ms);
         std::shared_lock<std::shared_mutex> lk(ix->rw);
         DeviceGuard dg(ix->device);
         const bool i8 = screen == VS_SCREEN_I8;
-        if (i8 && (ix->screen != VS_SCREEN_I8 || !ix->data8 || ix->i8_res || !i8_direct_ok(ix->dpad8)))
-            throw VsError(VS_ERR_ARG, "vs_screen_probe: the int8 probe needs the int8 direct screen (no group residuals)");
-        if (!i8 && !((ix->dtype == DT_BF16 || ix->dtype == DT_F16) && d16_direct_ok(ix->dpad)))
-            throw VsError(VS_ERR_ARG, "vs_screen_probe: the native probe needs bf16 / f16 rows of the direct screen");
-        if (ix->ntotal == 0) throw VsError(VS_ERR_ARG, "index is empty");
         hipStream_t st = (hipStream_t)stream;
         CtxLease L(ix, st, false);
         Ctx* c = L.c;
         const int nqb = (int)nq;
-        const int64_t tiles = (ix->ntotal + TR - 1) / TR;
-        ScreenArgs a{};
-        a.n_valid = ix->ntotal;
-        a.tiles = (int)tiles;
-        a.d = ix->d;
-        a.metric = ix->metric;
-        a.sqn = ix->sqn;
-        a.Kp = MFMA_KP_MAX;
-        a.cap = MFMA_CAP;
-        a.G = (int)std::max<int64_t>(1, std::min<int64_t>(tiles, ix->num_cu));
-        a.lcap = a.G * a.Kp;
-        c->gcnt.ensure(sizeof(int) * MFMA_QB);
-        c->drop.ensure(sizeof(u64) * MFMA_QB);
-        c->fails.ensure(2 * sizeof(int));
-        if (i8) {
-            c->qtile.ensure((size_t)MFMA_QB * ix->dpad8);
-            c->qfac.ensure(sizeof(float2) * MFMA_QB);
-            c->qeps.ensure(sizeof(float) * MFMA_QB);
-            HIP_CHECK(launch_pack_qtile_i8(q_dev, nqb, ix->d, ix->dpad8, c->qtile.as<uint8_t>(), c->qfac.as<float2>(),
-                                           c->qeps.as<float>(), ix->d_maxsq + 2, c->gcnt.as<int>(), c->drop.as<u64>(), st,
-                                           c->fails.as<int>(), ix->metric == METRIC_L2 ? ix->d_maxsq : nullptr,
-                                           gamma_of(ix->d)));
-            a.corpus = ix->data8;
-            a.dpad = ix->dpad8;
-            a.rsb = ix->rsb;
-            a.qfac = c->qfac.as<float2>();
-        } else {
-            c->qtile.ensure((size_t)MFMA_QB * ix->dpad * ix->es);
-            c->qinfo.ensure(sizeof(float) * 2 * MFMA_QB);
-            HIP_CHECK(launch_pack_qtile(ix->dtype, q_dev, nqb, ix->d, ix->dpad, c->qtile.as<uint8_t>(),
-                                        c->qinfo.as<float>(), c->gcnt.as<int>(), c->drop.as<u64>(), st));
-            a.corpus = ix->data;
-            a.dpad = ix->dpad;
-        }
-        if (zero_queries) HIP_CHECK(hipMemsetAsync(c->qtile.p, 0, c->qtile.bytes, st));
-        // every query's threshold at the key of +inf: the bound test rejects every column, so the
-        // launch is the K loop + the epilogue's bound test with no survivor to insert
-        c->thr0.ensure(sizeof(u64) * MFMA_QB);
-        std::vector<u64> thr(MFMA_QB, 0xFF80000000000000ull);
-        HIP_CHECK(hipMemcpyAsync(c->thr0.p, thr.data(), sizeof(u64) * MFMA_QB, hipMemcpyHostToDevice, st));
-        a.thr0 = c->thr0.as<u64>();
-        a.drop = c->drop.as<u64>();
-        c->cand.ensure((size_t)a.G * MFMA_QB * a.cap * sizeof(u64));
-        c->part.ensure((size_t)MFMA_QB * a.lcap * sizeof(u64));
-        a.cand = c->cand.as<u64>();
-        a.glist = c->part.as<u64>();
-        a.gcnt = c->gcnt.as<int>();
+        std::vector<u64> thr;
+        ScreenArgs a = probe_setup(ix, c, q_dev, nq, i8, zero_queries != 0, st, thr);
         // kProbeReps launches back to back (the cadence of the timed steps, no host gap between
         // them), each between its own events; the fastest one is reported
         constexpr int kProbeReps = 5;
@@ -1788,6 +1811,58 @@ int vs_screen_probe(vs_index* ix, const float* q_dev, int64_t nq, int32_t screen
         *ms = best;
     });
 }
+
+int vs_k1_probe(vs_index* ix, const float* q_dev, int64_t nq, int32_t screen, int32_t variant, int32_t zero_queries,
+                int32_t reps, void* stream, float* ms, unsigned long long* stamps, int32_t* G_out) {
+    return guarded([&] {
+        check_index(ix);
+        probe_checks(ix, q_dev, nq, screen, ms);
+        if (!stamps || !G_out || reps < 1 || reps > 64) throw VsError(VS_ERR_ARG, "vs_k1_probe: 1..64 reps, stamps, G_out");
+        std::shared_lock<std::shared_mutex> lk(ix->rw);
+        DeviceGuard dg(ix->device);
+        const bool i8 = screen == VS_SCREEN_I8;
+        if (ix->metric != METRIC_IP) throw VsError(VS_ERR_ARG, "vs_k1_probe: inner-product indexes");
+        hipStream_t st = (hipStream_t)stream;
+        CtxLease L(ix, st, false);
+        Ctx* c = L.c;
+        const int nqb = (int)nq;
+        std::vector<u64> thr;
+        ScreenArgs a = probe_setup(ix, c, q_dev, nq, i8, zero_queries != 0, st, thr);
+        struct Stamps {  // (DevBuf frees nothing itself)
+            DevBuf b;
+            ~Stamps() { b.release(); }
+        } stb;
+        DevBuf& sbuf = stb.b;
+        sbuf.ensure(sizeof(unsigned long long) * 4 * (size_t)a.G * (size_t)reps);
+        std::vector<hipEvent_t> ev((size_t)reps + 1);
+        for (hipEvent_t& e : ev) HIP_CHECK(hipEventCreate(&e));
+        hipError_t le = hipSuccess;
+        HIP_CHECK(hipEventRecord(ev[0], st));
+        for (int r = 0; r < reps && le == hipSuccess; ++r) {
+            a.stamps = sbuf.as<unsigned long long>() + (size_t)r * a.G * 4;
+            le = launch_k1_probe(variant, i8 ? DT_I8 : ix->dtype, a, c->qtile.as<uint8_t>(), nqb, st);
+            HIP_CHECK(hipEventRecord(ev[(size_t)r + 1], st));
+        }
+        HIP_CHECK(hipEventSynchronize(ev[(size_t)reps]));
+        hipError_t te = hipSuccess;
+        for (int r = 0; r < reps && te == hipSuccess && le == hipSuccess; ++r)
+            te = hipEventElapsedTime(&ms[r], ev[(size_t)r], ev[(size_t)r + 1]);
+        for (hipEvent_t& e : ev) (void)hipEventDestroy(e);
+        if (le != hipSuccess) throw VsError(VS_ERR_ARG, "vs_k1_probe: variant not available for this screen / index");
+        HIP_CHECK(te);
+        HIP_CHECK(hipMemcpy(stamps, sbuf.p, sizeof(unsigned long long) * 4 * (size_t)a.G * (size_t)reps,
+                            hipMemcpyDeviceToHost));
+        *G_out = a.G;
+    });
+}
+
+int vs_set_k1_schedule(int32_t schedule) {
+    return guarded([&] {
+        if (schedule < 0 || schedule > 2) throw VsError(VS_ERR_ARG, "K1 schedule: 0, 1 or 2");
+        set_k1_schedule(schedule);
+    });
+}
+int vs_k1_schedule(void) { return k1_schedule(); }
 
 int vs_set_scan_limit(vs_index* ix, int64_t bytes) {
     return guarded([&] {

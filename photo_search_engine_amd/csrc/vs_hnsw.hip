@@ -162,17 +162,52 @@ int vs_hnsw_patch(vs_hnsw* h, int64_t m, const uint64_t* pos, const int32_t* val
         if (entry_point < 0 || entry_point >= n) fail("entry point out of range");
         if (max_level != h->levels_h[entry_point] - 1) fail("max_level must be the entry point's top level");
         const int nlev = (int)h->cum_h.size() - 1;
-        // every slot and id is checked here: the search kernel follows them
+        // every slot and id is checked here: the search kernel follows them.  A patch rewrites whole
+        // (node, level) lists -- every slot of each list it touches (a slot given twice must carry
+        // the same id) -- and each list in the form vs_hnsw_create leaves: distinct ids, then -1s
+        std::vector<std::pair<uint64_t, int32_t>> pv((size_t)m);
         for (int64_t i = 0; i < m; ++i) {
             if (pos[i] >= h->offsets_h[n]) fail("patch position out of range");
-            const int64_t node = (int64_t)(std::upper_bound(h->offsets_h.begin(), h->offsets_h.end(), pos[i]) -
+            pv[(size_t)i] = {pos[i], val[i]};
+        }
+        std::sort(pv.begin(), pv.end());
+        size_t w = 0;
+        for (size_t i = 0; i < pv.size(); ++i) {
+            if (w > 0 && pv[w - 1].first == pv[i].first) {
+                if (pv[w - 1].second != pv[i].second) fail("one neighbour slot patched with two ids");
+                continue;
+            }
+            pv[w++] = pv[i];
+        }
+        pv.resize(w);
+        std::vector<int32_t> ids;
+        for (size_t i = 0; i < pv.size();) {
+            const uint64_t p0 = pv[i].first;
+            const int64_t node = (int64_t)(std::upper_bound(h->offsets_h.begin(), h->offsets_h.end(), p0) -
                                            h->offsets_h.begin()) - 1;
-            const uint64_t rel = pos[i] - h->offsets_h[node];
+            const uint64_t rel = p0 - h->offsets_h[node];
             int l = 0;
             while (l + 1 < nlev && rel >= (uint64_t)h->cum_h[l + 1]) ++l;
-            const int32_t v = val[i];
-            if (v < -1 || v >= n) fail("neighbour id out of range");
-            if (v >= 0 && h->levels_h[v] <= l) fail("a neighbour is listed on a level above its own");
+            const uint64_t lo = h->offsets_h[node] + (uint64_t)h->cum_h[l];
+            const uint64_t hi = h->offsets_h[node] + (uint64_t)h->cum_h[l + 1];
+            if (p0 != lo || i + (hi - lo) > pv.size() || pv[i + (hi - lo) - 1].first != hi - 1)
+                fail("a patch must rewrite whole neighbour lists");
+            ids.clear();
+            bool ended = false;
+            for (uint64_t j = 0; j < hi - lo; ++j) {
+                const int32_t v = pv[i + j].second;
+                if (v < -1 || v >= n) fail("neighbour id out of range");
+                if (v == -1) {
+                    ended = true;
+                    continue;
+                }
+                if (ended) fail("a neighbour id after the list's -1 terminator");
+                if (h->levels_h[v] <= l) fail("a neighbour is listed on a level above its own");
+                ids.push_back(v);
+            }
+            std::sort(ids.begin(), ids.end());
+            if (std::adjacent_find(ids.begin(), ids.end()) != ids.end()) fail("a neighbour listed twice in one list");
+            i += hi - lo;
         }
         std::lock_guard<std::mutex> lk(h->mtx);
         DeviceGuard g(h->device);
@@ -181,6 +216,7 @@ int vs_hnsw_patch(vs_hnsw* h, int64_t m, const uint64_t* pos, const int32_t* val
             h->pval.ensure((size_t)m * 4);
             HIP_CHECK(hipMemcpyAsync(h->ppos.p, pos, (size_t)m * 8, hipMemcpyHostToDevice, h->st));
             HIP_CHECK(hipMemcpyAsync(h->pval.p, val, (size_t)m * 4, hipMemcpyHostToDevice, h->st));
+            // (the synchronisation below keeps the caller's pos / val alive for the copies)
             hipLaunchKernelGGL(k_scatter_i32, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, h->st,
                                h->neighbors.as<int32_t>(), h->ppos.as<uint64_t>(), h->pval.as<int32_t>(), m);
             HIP_CHECK(hipGetLastError());

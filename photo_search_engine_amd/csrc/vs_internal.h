@@ -217,6 +217,8 @@ struct ScreenArgs {
                              // 256 / GEMV_SPLIT rows (small corpora: more CUs)
     const float* gT;         // int8 group residuals: [group][QB] <mu_g, q> added to every key of the
                              // group's rows (the seed pass and k_screen_i8d_res), or null
+    unsigned long long* stamps;  // diagnostic probe forms only (vs_k1probe.hip): per workgroup
+                                 // {s_memtime, s_memrealtime} around the loop; null in the product
 };
 constexpr int MAP_DESC = 8;
 constexpr int MFMA_MAP_TILES = 256;  // mapped screen: logical tiles per workgroup (its LDS page table)
@@ -248,6 +250,11 @@ hipError_t launch_pack_qf32(const float* q, int nqb, int nqpad, int d, int dpad,
                             int* fails = nullptr, u64* drop = nullptr);  // drop: zeroed [nqpad]
 
 hipError_t launch_screen_mfma(int dt, const ScreenArgs& a, const uint8_t* qt, int nqb, hipStream_t st);
+// the direct K1 screens' schedule: 0 = barrier at the head of every K-step, 1 = mid-step barrier
+void set_k1_schedule(int s);
+int k1_schedule();
+// diagnostic forms of the direct screen (vs_k1probe.hip): variant = VS_K1P_* (include/vs.h)
+hipError_t launch_k1_probe(int variant, int dt, const ScreenArgs& a, const uint8_t* qt, int nqb, hipStream_t st);
 // the int8 main pass runs the direct form (k_screen_i8d) for this int8 row stride (K-steps per tile
 // a multiple of 4); it takes no seed-tile accumulators (ScreenArgs::seed_acc must be null)
 bool i8_direct_ok(int dpad8);
@@ -447,27 +454,28 @@ void read_rows_host(vs_index* ix, int64_t i0, int64_t n,
                     const std::function<void(int64_t, int64_t, const float*)>& sink);
 int64_t stream_chunk_rows(int d);  // rows per pinned chunk (32 MiB of fp32)
 
-// Exact top-k of device queries over a flat index, certificate failures re-searched (bf16/f16: by
-// a gated fallback round on the device; async = no host sync, unresolved queries counted in
-// vs_unresolved_count instead of raising).  I_dev [nq][k], S64_dev optional.
-// unres (optional): a device counter of this call's queries even the fallback round could not
-// certify (default: the index's counter behind vs_unresolved_count)
+// Exact top-k of device queries over a flat index, certificate failures re-searched (MFMA dtypes: by
+// a gated fallback round on the device, then the gated exact full scan; async = no host sync).
+// I_dev [nq][k], S64_dev optional.
+// unres (optional): a device counter of this call's queries answered by the full scan, i.e. even
+// the fallback round could not certify them (default: the index's counter behind vs_full_scan_count)
 void search_exact_device(vs_index* ix, const float* q_dev, int64_t nq, int k, int64_t* I_dev, double* S64_dev,
                          hipStream_t st, float* D_dev = nullptr, int64_t id_offset = 0, bool async = false,
                          unsigned* unres = nullptr);
 // drop rows [n, ntotal) of a flat index (rows are append-only: a failed multi-device add rolls back
 // the shards that took their rows); the running maxima stay (they only widen certificate margins)
 void truncate_rows(vs_index* ix, int64_t n);
-unsigned* unresolved_counter(vs_index* ix);  // device word behind vs_unresolved_count
+unsigned* full_scan_counter(vs_index* ix);  // device word behind vs_full_scan_count
 // S concurrent exact device searches over parts of one batch (own streams and workspaces;
-// unres[i] counts part i's unresolved queries)
+// unres[i] counts part i's full-scanned queries)
 void search_exact_device_parts(vs_index* ix, const float* q_dev, int64_t nq, int k, int64_t* I_dev,
                                hipStream_t* streams, int S, unsigned* unres);
 // two-phase exact device search (vs_search_device_phase_a / _b)
 bool two_phase_ok(const vs_index* ix, int64_t nq, int k);
 vs_pending* search_phase_a(vs_index* ix, const float* q_dev, int64_t nq, int k, int world, int64_t id_offset,
                            double* S_a, int64_t* I_a, int stride, hipStream_t st);
-// (unres: this call's counter of queries the fallback round cannot certify; null = the index's)
+// (unres: this call's counter of full-scanned queries, the fallback round could not certify them;
+// null = the index's)
 void search_phase_b(vs_pending* p, const double* floor_S, float* D, int64_t* I, double* S64, int stride,
                     hipStream_t st, unsigned* unres = nullptr);
 void search_pending_free(vs_pending* p);

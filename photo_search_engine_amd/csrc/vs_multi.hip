@@ -333,12 +333,17 @@ int vs_multi_create(int d, int metric, int dtype, int n_dev, const int* dev_ids,
                 vs_index* x = nullptr;
                 throw_rc(vs_create(d, metric, dtype, dev_ids[g], &x));
                 m->ix.push_back(x);
-                if (dev_ids[g] != dev_ids[0]) {  // xGMI peer path to device 0 (best effort: copies work either way)
-                    DeviceGuard dg(dev_ids[g]);
-                    int can = 0;
-                    if (hipDeviceCanAccessPeer(&can, dev_ids[g], dev_ids[0]) == hipSuccess && can)
-                        (void)hipDeviceEnablePeerAccess(dev_ids[0], 0);
-                    (void)hipGetLastError();
+                if (dev_ids[g] != dev_ids[0]) {
+                    // xGMI peer paths both ways (best effort: copies work either way): the lists go
+                    // device g -> device 0, the two-phase floor device 0 -> device g
+                    for (int dir = 0; dir < 2; ++dir) {
+                        const int from = dir == 0 ? dev_ids[g] : dev_ids[0], to = dir == 0 ? dev_ids[0] : dev_ids[g];
+                        DeviceGuard dg(from);
+                        int can = 0;
+                        if (hipDeviceCanAccessPeer(&can, from, to) == hipSuccess && can)
+                            (void)hipDeviceEnablePeerAccess(to, 0);  // (already enabled: ignored)
+                        (void)hipGetLastError();
+                    }
                 }
             }
             m->pool = new Pool(n_dev);

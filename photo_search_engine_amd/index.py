@@ -208,6 +208,24 @@ class FlatIndex:
                                       stream or None, ctypes.byref(ms)))
         return float(ms.value)
 
+    K1_PROBES = {"loads": 0, "lds": 1, "mfma": 2, "full": 3, "full_ms": 4, "full_prio": 5, "full_ms_prio": 6}
+
+    def k1_probe(self, q_ptr: int, nq: int, screen: str, variant: str, zero_queries: bool, reps: int = 5,
+                 stream: Optional[int] = None):
+        """Diagnostic forms of the direct screen's loop (include/vs.h ``vs_k1_probe``): ``reps`` launches
+        back to back -> (ms per launch, stamps [reps][G][4] uint64: s_memtime at the loop's start and
+        end, s_memrealtime at the same points)."""
+        import numpy as np
+        ms = (ctypes.c_float * reps)()
+        st = np.zeros((reps, 256, 4), dtype=np.uint64)
+        G = ctypes.c_int32(0)
+        check(self._L.vs_k1_probe(self._h, q_ptr, int(nq), FlatIndex.SCREENS[screen], FlatIndex.K1_PROBES[variant],
+                                  int(bool(zero_queries)), int(reps), stream or None, ms, st.ctypes.data,
+                                  ctypes.byref(G)))
+        g = int(G.value)
+        flat = st.reshape(-1)[: reps * g * 4].reshape(reps, g, 4)
+        return [float(x) for x in ms], flat
+
     def set_scan_limit(self, nbytes: int) -> None:
         """Single-query calls over at most ``nbytes`` of stored rows use the exact full scan instead of
         a screen (include/vs.h ``vs_set_scan_limit``; 0 = always screen)."""
@@ -247,6 +265,17 @@ def merge_shards_device(metric_type: int, S_ptr: int, I_ptr: int, G: int, nq: in
     L = _lib.load()
     check(L.vs_merge_shards_device(int(metric_type), S_ptr, I_ptr, int(in_stride), int(G), int(nq), int(k), S_out,
                                    I_out, D_out or None, stream or None))
+
+
+def set_k1_schedule(schedule: int) -> None:
+    """The direct K1 screens' K-step schedule, process-wide (include/vs.h ``vs_set_k1_schedule``):
+    0 = a barrier at the head of every K-step, 1 (default) = the mid-step barrier on the int8 screen,
+    2 = also on bf16 / f16 rows.  Results are identical."""
+    check(_lib.load().vs_set_k1_schedule(int(schedule)))
+
+
+def k1_schedule() -> int:
+    return int(_lib.load().vs_k1_schedule())
 
 
 def synthesize_device(device: int, seed: int, global_row0: int, n: int, d: int, out_ptr: int, normalize: bool = True,

@@ -155,6 +155,9 @@ class VectorStore:
         self._graph_arrays: Optional[Dict[str, Any]] = None
         self._hnsw: Optional[HNSWGraph] = None
         self._graph_tail: Optional[FlatIndex] = None  # rows added behind the graph, searched exactly
+        # a flat-configured store loaded from an HNSW file: the reference's index object stays an
+        # IndexHNSWFlat (utils/vector_store.py:249), so its save() writes an HNSW file again
+        self._file_hnsw = False
 
     # ------------------------------------------------------------------ internals
     def _rebuild_path_index(self) -> None:
@@ -236,19 +239,23 @@ class VectorStore:
         return payload
 
     def _validate_loaded_index(self, payload: Dict[str, Any], loaded: "faiss_format.FaissFile") -> None:
-        # utils/vector_store.py:125-140; an HNSW config accepts a flat or an HNSW file (both are
-        # served exactly), the metric of the payload must match the configured metric.
+        # utils/vector_store.py:125-140, rule for rule: the sidecar's index_type and metric must match
+        # the configuration; an HNSW configuration needs an HNSW file (IndexHNSWFlat, :137-138) and
+        # never checks the file's metric; a flat configuration checks only the file's metric_type
+        # (:139-143), so an HNSW file of the configured metric loads too.
         index_type = str(payload.get("index_type") or "").strip().lower()
         metric = str(payload.get("metric") or "").strip().lower()
         if index_type != self.index_type:
             raise ValueError("索引类型与配置不一致，请重新构建索引")
         if metric != self.metric:
             raise ValueError("索引度量与配置不一致，请重新构建索引")
-        if self.index_type == "flat" and loaded.kind != "flat":
-            raise ValueError("索引结构与配置不一致，请重新构建索引")
-        want = METRIC_INNER_PRODUCT if self.metric == "cosine" else METRIC_L2
-        if loaded.metric_type != want:
-            raise ValueError("索引度量与配置不一致，请重新构建索引")
+        if self.index_type == "hnsw":
+            if loaded.kind != "hnsw":
+                raise ValueError("索引结构与配置不一致，请重新构建索引")
+        elif self.index_type == "flat":
+            want = METRIC_INNER_PRODUCT if self.metric == "cosine" else METRIC_L2
+            if loaded.metric_type != want:
+                raise ValueError("索引度量与配置不一致，请重新构建索引")
 
     # ------------------------------------------------------------------ reference API
     # 内部接口：仅允许indexer模块调用，禁止直接暴露给前端
@@ -324,13 +331,19 @@ class VectorStore:
         # written -- the bytes are identical to a full rewrite.  Payload bytes stream HBM -> file.
         n, d, mt = int(self.index.ntotal), int(self.index.d), int(self.index.metric_type)
         old = self._appendable_rows(d, mt)
-        if self.index_type == "hnsw":
+        if self.index_type == "hnsw" or self._file_hnsw:
             # an IHNf file the reference's faiss can load (rollback), at every size; a graph loaded
             # from file is kept (rows added since are inserted into it), with efSearch as configured
-            # (the reference sets hnsw.efSearch after every load, utils/vector_store.py:135, and faiss
-            # writes it back)
-            graph = (dict(self._graph_arrays, efSearch=self.hnsw_ef_search) if self._graph_covers(n) else
-                     self._build_graph(n))
+            # (the reference sets hnsw.efSearch after every load of an HNSW configuration,
+            # utils/vector_store.py:135, and faiss writes it back; a flat configuration keeps the
+            # file's)
+            ef = self.hnsw_ef_search if self.index_type == "hnsw" else None
+            if self._graph_covers(n):
+                graph = dict(self._graph_arrays)
+                if ef is not None:
+                    graph["efSearch"] = ef
+            else:
+                graph = self._build_graph(n)
             faiss_format.write_hnsw(self.index_path, graph, d, n, mt, lambda path, off: self.index.write_rows(path, off, 0, n))
             self._graph_arrays = graph
             self._persisted = None
@@ -362,10 +375,13 @@ class VectorStore:
         self.index = index
         self._persisted = (self._file_state(loaded.ntotal, loaded.d, loaded.metric_type)
                            if loaded.kind == "flat" else None)
-        if loaded.kind == "hnsw" and self.index_type == "hnsw" and _hnsw_graph_search():
-            self._graph_arrays = faiss_format.read_hnsw_graph(self.index_path)
         payload = self._load_index_meta()
         self._validate_loaded_index(payload, loaded)
+        # a flat configuration keeps an HNSW file's graph: save() writes it back (extended by the
+        # rows added since), as the reference's IndexHNSWFlat would be
+        self._file_hnsw = loaded.kind == "hnsw" and self.index_type == "flat"
+        if loaded.kind == "hnsw" and (self._file_hnsw or _hnsw_graph_search()):
+            self._graph_arrays = faiss_format.read_hnsw_graph(self.index_path)
 
         with open(self.metadata_path, "r", encoding="utf-8") as file:
             self.metadata = json.load(file)
@@ -389,6 +405,7 @@ class VectorStore:
     def clear(self) -> None:
         """清空索引与元数据."""
         self._drop_graph()
+        self._file_hnsw = False
         self.index = self._create_index(self.dimension) if self.dimension else None
         self.metadata = []
         self._embeddings = {}
@@ -462,8 +479,10 @@ class VectorStore:
         g = self._graph_arrays
         make = lambda: self._create_index(self.dimension)  # noqa: E731
         if g is not None and 0 < int(np.asarray(g["levels"]).shape[0]) < n:
-            return hnsw_mod.insert_rows(self.index, g, int(np.asarray(g["levels"]).shape[0]), n,
-                                        int(self.hnsw_ef_construction), make)
+            # (a flat configuration over an HNSW file inserts with the file's efConstruction, as the
+            # reference's loaded IndexHNSWFlat would)
+            efc = int(g["efConstruction"]) if self._file_hnsw else int(self.hnsw_ef_construction)
+            return hnsw_mod.insert_rows(self.index, g, int(np.asarray(g["levels"]).shape[0]), n, efc, make)
         n0 = min(n, max(1, _hnsw_graph_max_rows()))
         g = self._build_graph_exact(n0)
         if n0 < n:

@@ -50,6 +50,12 @@ def main() -> int:
     for metric, sym in (("ip", "_ZN2vs12k_screen_i8dILi0EEEvNS_10ScreenArgsEPKhi:"),
                         ("l2", "_ZN2vs12k_screen_i8dILi1EEEvNS_10ScreenArgsEPKhi:")):
         rc |= check(asm, metric, sym)
+    # the mid-step-barrier form (SCHED 1, the default int8 main pass): its corpus loads and query
+    # DMAs sit inside the K-step asm blocks, and the next step's first query fragments are read at
+    # the end of a block (in flight across the loop code between blocks)
+    # (inner product only: the L2 form keeps the head-barrier schedule)
+    rc |= check(asm, "ip", "_ZN2vs15k_screen_i8d_msILi0EEEvNS_10ScreenArgsEPKhi:", name="k_screen_i8d_ms",
+                frag_reads=True)
     # the main pass over group-residual codes (inner product; + <mu_g, q> per key)
     rc |= check(asm, "ip", "_ZN2vs16k_screen_i8d_resENS_10ScreenArgsEPKhi:", name="k_screen_i8d_res")
     # the bf16 / f16 direct form (k_screen_d16): its corpus loads are global_load_dwordx4 with and
@@ -65,11 +71,21 @@ def main() -> int:
     return rc
 
 
-def check(asm: str, metric: str, sym: str, name: str = "k_screen_i8d", any_policy: bool = False) -> int:
+def check(asm: str, metric: str, sym: str, name: str = "k_screen_i8d", any_policy: bool = False,
+          frag_reads: bool = False) -> int:
     start = asm.index(sym)
     end = asm.index(".Lfunc_end", start)
     raw = asm[start:end].split("\n")
-    code = [f"{l}  ;#L{i}" for i, l in enumerate(raw) if l.strip() and not l.strip().startswith((";", "."))]
+    code, in_asm, inasm = [], [], False  # in_asm: the instruction comes from an inline-asm block
+    for i, l in enumerate(raw):
+        t = l.strip()
+        if t.startswith(";;#ASMSTART"):
+            inasm = True
+        elif t.startswith(";;#ASMEND"):
+            inasm = False
+        if t and not t.startswith((";", ".")):
+            code.append(f"{l}  ;#L{i}")
+            in_asm.append(inasm)
     bad = []
     if any("scratch_" in l for l in code):
         bad.append("scratch (spill) instructions present")
@@ -109,6 +125,25 @@ def check(asm: str, metric: str, sym: str, name: str = "k_screen_i8d", any_polic
                 break
             if dst2 & dst:
                 break
+    if frag_reads:
+        # every query-fragment read (ds_read_b128) is consumed by an MFMA before any other
+        # instruction reads its registers without an lgkmcnt(0) wait in between (a copy of a
+        # prefetched fragment would read the register before the read lands)
+        for i, l in enumerate(code):
+            op, dst, _ = parsed[i]
+            if op != "ds_read_b128" or i < first_bar or not in_asm[i]:
+                continue  # (the compiler's own LDS reads are waited for by the compiler)
+            for j in range(i + 1, len(code)):
+                op2, dst2, src2 = parsed[j]
+                if "lgkmcnt(0)" in code[j]:
+                    break
+                if op2.startswith("v_mfma") and src2 & dst:
+                    break
+                if src2 & dst:
+                    bad.append(f"query fragment {sorted(dst)[0]}.. read before its wait by: {code[j].strip()}")
+                    break
+                if dst2 & dst:
+                    break
     nmfma = sum(1 for l in code if l.strip().startswith("v_mfma"))
     nbar = sum(1 for l in code if l.strip().startswith("s_barrier"))
     print(f"{name}<{metric}>: {len(code)} instructions, {nmfma} MFMA, {nbar} s_barrier, "

@@ -13,6 +13,18 @@ touches the corpus fragments between their load and their use.
   (v_mfma_f32_16x16x32_bf16 / _f16: 32 elements per K-step, fp32 accumulators in the same VGPRs)
   *_N4: 4 query column groups instead of 16 (narrow query tiles: 8 MFMAs per K-step)
 
+  I8D_LDSONLY: the 16 query-fragment reads and their waits alone (no MFMA; the K-loop probe)
+
+Mid-step-barrier schedule (SCHED 1 of screen_direct): one asm block per K-step that also holds the
+step's barrier and the issue of the K-step 3 ahead, so no wave leaves the matrix pipe idle around a
+barrier:
+  MS_<I8|BF|HF>_<F|N><O|P><P|N>: [4 own fragment reads (O) | the 4 prefetched by the previous step
+  (P)] MFMA pairs 0-7 (reads 4 ahead) -> s_waitcnt vmcnt(6) + s_barrier (the next step's query
+  slot has landed in every wave; every wave is done with the slot the issue below refills) -> MFMA
+  pairs 8-15, the 2 query LDS-DMAs and 2 corpus loads of the K-step 3 ahead between them -> [the
+  next step's first 4 fragment reads from its slot (P) | none (N)].  F = first K-step of a tile
+  (src2 = 0).
+
 Usage: python scripts/gen_i8_asm.py > photo_search_engine_amd/csrc/vs_i8_asm.h
 """
 RA = 4  # query-fragment reads in flight
@@ -33,6 +45,60 @@ def body(first: bool, last: bool, op: str = "v_mfma_i32_16x16x64_i8", ng: int = 
     if last:
         lines += ["s_nop 7", "s_nop 7", "s_nop 7"]
     return "\\n\\t".join(lines)
+
+
+def lds_only() -> str:
+    lines = []
+    for n in range(RA):
+        lines.append(f"ds_read_b128 %[b{n % RA}], %[addr] offset:{n * 1024}")
+    for n in range(16):
+        issued = min(16, n + RA)
+        lines.append(f"s_waitcnt lgkmcnt({issued - (n + 1)})")
+        if n + RA < 16:
+            lines.append(f"ds_read_b128 %[b{n % RA}], %[addr] offset:{(n + RA) * 1024}")
+    outs = ", ".join(f'[b{i}] "=&v"(bt[{i}])' for i in range(RA))
+    body_ = "\\n\\t".join(lines)
+    return f'#define I8D_LDSONLY() asm volatile("{body_}" : {outs} : [addr] "v"(slot_lds) : "memory")'
+
+
+def ms_step(op: str, first: bool, own: bool, pre: bool, nt: bool) -> str:
+    """One K-step of the mid-step-barrier schedule (module docstring)."""
+    ld = "global_load_dwordx4 %[an{}], %[cs], off" + (" offset:{}" ) + (" nt" if nt else "")
+    vmem = [["s_mov_b32 m0, %[ql0]", "s_nop 0", "global_load_lds_dwordx4 %[qs0], off"],
+            ["s_mov_b32 m0, %[ql1]", "s_nop 0", "global_load_lds_dwordx4 %[qs1], off"],
+            [ld.format(0, 0).replace(" offset:0", "")],
+            [ld.format(1, "%[a2off]").replace("%[a2off]", "{A2}")]]
+    lines = []
+    if own:
+        for n in range(RA):
+            lines.append(f"ds_read_b128 %[b{n}], %[addr] offset:{n * 1024}")
+    for n in range(16):
+        if n == 8:
+            lines += ["s_waitcnt vmcnt(6)", "s_barrier"]
+        # fragment reads in flight before pair n: min(16, n + RA) issued (+ the prefetch lines come last)
+        issued = min(16, n + RA)
+        lines.append(f"s_waitcnt lgkmcnt({issued - (n + 1)})")
+        for m in range(2):
+            src2 = "0" if first else f"%[c{m}_{n}]"
+            lines.append(f"{op} %[c{m}_{n}], %[a{m}], %[b{n % RA}], {src2}")
+        if n + RA < 16:
+            lines.append(f"ds_read_b128 %[b{n % RA}], %[addr] offset:{(n + RA) * 1024}")
+        if 8 <= n < 12:
+            lines += vmem[n - 8]
+    if pre:
+        for n in range(RA):
+            lines.append(f"ds_read_b128 %[b{n}], %[naddr] offset:{n * 1024}")
+    return "\\n\\t".join(lines)
+
+
+def ms_macro(name: str, op: str, first: bool, own: bool, pre: bool, nt: bool, a2: int) -> str:
+    outs = ", ".join([f'[c{m}_{n}] "+v"(acc[{m}][{n}])' for m in range(2) for n in range(16)] +
+                     [f'[b{i}] "+v"(bt[{i}])' for i in range(RA)] + ['[an0] "+v"(AN0_)', '[an1] "+v"(AN1_)'])
+    ins = ('[a0] "v"(A0_), [a1] "v"(A1_), [addr] "v"(slot_lds), [naddr] "v"(next_lds), [qs0] "v"(QS0_), '
+           '[qs1] "v"(QS1_), [ql0] "s"(QL0_), [ql1] "s"(QL1_), [cs] "v"(CS_)')
+    body_ = ms_step(op, first, own, pre, nt).replace("{A2}", str(a2))
+    return (f'#define {name}(A0_, A1_, AN0_, AN1_, QS0_, QS1_, QL0_, QL1_, CS_) asm volatile("{body_}" : {outs} : '
+            f'{ins} : "memory", "m0")')
 
 
 def macro(name: str, first: bool, last: bool, op: str = "v_mfma_i32_16x16x64_i8", ng: int = 16) -> str:
@@ -62,3 +128,15 @@ if __name__ == "__main__":
     print(macro("BFD_STEP0_N4", True, False, "v_mfma_f32_16x16x32_bf16", 4))
     print(macro("HFD_STEP_N4", False, False, "v_mfma_f32_16x16x32_f16", 4))
     print(macro("HFD_STEP0_N4", True, False, "v_mfma_f32_16x16x32_f16", 4))
+    print(lds_only())
+    # mid-step-barrier K-steps: int8 (corpus loads nt, fragments 1 KiB apart) and bf16 / f16 (the
+    # K-step reads one half of each row's 128 B line: the first half default policy, the second nt;
+    # fragments 16 rows x 128 B = 2 KiB apart)
+    for tag, op, a2, nts in (("I8", "v_mfma_i32_16x16x64_i8", 1024, (True,)),
+                             ("BF", "v_mfma_f32_16x16x32_bf16", 2048, (False, True)),
+                             ("HF", "v_mfma_f32_16x16x32_f16", 2048, (False, True))):
+        for nt in nts:
+            pol = "" if tag == "I8" else ("_NT" if nt else "_DF")
+            for first, own, pre in ((True, True, False), (False, True, True), (False, False, True), (False, False, False)):
+                nm = f"MS_{tag}{pol}_{'F' if first else 'N'}{'O' if own else 'P'}{'P' if pre else 'N'}"
+                print(ms_macro(nm, op, first, own, pre, nt, a2))

@@ -1,0 +1,45 @@
+#!/bin/bash
+# One GPU call of round-6 steps (STEPS="..." bash scripts/r06_gpu_batch.sh).  Every step runs under
+# its own time limit; a crash, abort, fault or time limit (rc >= 124) ends the call there.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+PYT="python -u -m pytest -v --timeout 300 --timeout-method thread"
+fatal() { [ "$1" -ge 124 ] && [ "$1" -ne 0 ]; }
+run() {  # name, seconds, command...
+  local name=$1 secs=$2; shift 2
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "step $name rc=$rc" >> gpurun_out/steps.log
+  if fatal $rc; then echo "fatal rc=$rc in $name: stopping" >> gpurun_out/steps.log; exit $rc; fi
+  return 0
+}
+abloop() {  # name, reps, args... : bench.py with --k1-schedule 0 / 1 alternating
+  local name=$1 reps=$2; shift 2
+  for i in $(seq 1 $reps); do for s in 0 1; do
+    timeout -k 10 300 python bench.py --k1-schedule $s "$@" --no-cpu-baseline > gpurun_out/ab.tmp 2>&1
+    local rc=$?
+    echo "sched$s $(tail -1 gpurun_out/ab.tmp)" >> gpurun_out/ab_$name.txt
+    if [ $rc -ne 0 ]; then cp gpurun_out/ab.tmp gpurun_out/ab_${name}_fail.log; echo "step ab_$name rc=$rc" >> gpurun_out/steps.log; exit $rc; fi
+  done; done
+  echo "step ab_$name rc=0" >> gpurun_out/steps.log
+}
+for s in ${STEPS:-decomp}; do
+  case $s in
+    full) run pytest_gpu 900 $PYT tests -m gpu ;;
+    full1) VS_TEST_K1_SCHEDULE=1 run pytest_gpu_sched1 900 $PYT tests -m gpu ;;
+    direct1) VS_TEST_K1_SCHEDULE=1 run pytest_direct_sched1 600 $PYT tests/test_gpu_int8_direct.py tests/test_gpu_baseline_shapes.py -m gpu ;;
+    smoke) run smoke 300 python __graft_entry__.py --smoke ;;
+    decomp) run k1_decompose 600 python scripts/k1_decompose.py --out gpurun_out/k1_decomposition.json ;;
+    cfg3) run bench_cfg3 600 python bench.py ;;
+    ab3) abloop cfg3 2 --steps 20 --warmup 3 ;;
+    ab3n) abloop cfg3n 2 --screen native --steps 10 --warmup 3 ;;
+    full2) VS_TEST_K1_SCHEDULE=2 run pytest_gpu_sched2 900 $PYT tests -m gpu ;;
+    ab8) abloop shard8 2 --shard-of 8 --steps 30 ;;
+    shard8) run bench_shard8 300 python bench.py --shard-of 8 --steps 30 --no-cpu-baseline ;;
+    cfg2) run bench_cfg2 300 python bench.py --workload cfg2 --no-cpu-baseline ;;
+    prof3) mkdir -p gpurun_out/prof3 && run prof3 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof3 -o run --output-format csv -- python bench.py --steps 30 --warmup 1 --no-cpu-baseline ;;
+    *) echo "unknown step $s" >> gpurun_out/steps.log; exit 2 ;;
+  esac
+done

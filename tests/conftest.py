@@ -20,6 +20,12 @@ GOLDEN = os.path.join(TESTS, "golden")
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) and libvs.so")
+    # VS_TEST_K1_SCHEDULE=0|1: run the GPU suite under that K1 schedule (include/vs.h
+    # vs_set_k1_schedule); unset = the library's default
+    sched = os.environ.get("VS_TEST_K1_SCHEDULE")
+    if sched is not None:
+        from photo_search_engine_amd.index import set_k1_schedule
+        set_k1_schedule(int(sched))
 
 
 @pytest.fixture(scope="session")

@@ -300,6 +300,33 @@ def scenarios():
     sc.append({"name": "load_type_mismatch", "ctor": {"dimension": d},
                "ops": [{"op": "add_item", "embedding": [0.1] * d, "metadata": {"id": 1}}, {"op": "save"}],
                "reload_ctor": {"dimension": d, "index_type": "hnsw"}, "reload": [{"op": "load"}]})
+    # --- the file's structure and metric against the configuration (utils/vector_store.py:125-143):
+    # a sidecar rewritten so it matches the configuration while the file does not
+    meta = lambda it, m: json.dumps({"index_type": it, "metric": m, "dimension": d, "hnsw_m": 32,  # noqa: E731
+                                     "hnsw_ef_construction": 200, "hnsw_ef_search": 96})
+    two = [{"op": "add_item", "embedding": fake_embedding("photo a"), "metadata": {"photo_path": "/a.jpg"}},
+           {"op": "add_item", "embedding": fake_embedding("photo bb"), "metadata": {"photo_path": "/b.jpg"}},
+           {"op": "add_item", "embedding": fake_embedding("photo ccc"), "metadata": {"photo_path": "/c.jpg"}}]
+    probe = [{"op": "total"}, {"op": "search", "query": fake_embedding("photo bb"), "top_k": 3},
+             {"op": "has_photo_path", "photo_path": "/c.jpg"}]
+    sc.append({"name": "load_hnsw_sidecar_over_flat_file", "ctor": {"dimension": d},
+               "ops": two + [{"op": "save"}, {"op": "write_file", "dir": "{dir}", "name": "index.bin.meta.json",
+                                              "text": meta("hnsw", "cosine")}],
+               "reload_ctor": {"dimension": d, "index_type": "hnsw"}, "reload": [{"op": "load"}] + probe})
+    sc.append({"name": "load_flat_sidecar_over_hnsw_file_ip", "ctor": {"dimension": d, "index_type": "hnsw"},
+               "ops": two + [{"op": "save"}, {"op": "write_file", "dir": "{dir}", "name": "index.bin.meta.json",
+                                              "text": meta("flat", "cosine")}],
+               "reload_ctor": {"dimension": d}, "reload": [{"op": "load"}] + probe})
+    sc.append({"name": "load_flat_sidecar_over_hnsw_file_l2_mismatch", "ctor": {"dimension": d, "index_type": "hnsw",
+                                                                                "metric": "l2"},
+               "ops": two + [{"op": "save"}, {"op": "write_file", "dir": "{dir}", "name": "index.bin.meta.json",
+                                              "text": meta("flat", "cosine")}],
+               "reload_ctor": {"dimension": d}, "reload": [{"op": "load"}]})
+    sc.append({"name": "load_hnsw_config_file_metric_unchecked", "ctor": {"dimension": d, "index_type": "hnsw",
+                                                                          "metric": "l2"},
+               "ops": two + [{"op": "save"}, {"op": "write_file", "dir": "{dir}", "name": "index.bin.meta.json",
+                                              "text": meta("hnsw", "cosine")}],
+               "reload_ctor": {"dimension": d, "index_type": "hnsw"}, "reload": [{"op": "load"}] + probe})
     sc.append({"name": "clear", "ctor": {"dimension": d}, "ops": [
         {"op": "add_item", "embedding": [0.1] * d, "metadata": {"photo_path": "/a.jpg"}}, {"op": "clear"},
         {"op": "total"}, {"op": "has_photo_path", "photo_path": "/a.jpg"},

@@ -186,6 +186,83 @@ def test_cfg4_shape_sharded_four_ranks(tmp_path):
     np.testing.assert_array_equal(S[:16], Se)
 
 
+def test_cfg4_full_shape_eight_shards_one_gpu(FlatIndex):
+    # cfg4 at its own size: 100M x 768 fp16 rows as the 8-GPU run shards them (8 contiguous shards of
+    # 12.5M rows, each searched with its global id offset, the lists merged by the sharded step's
+    # device merge), all 8 shards on the box's one GPU (230 GB of rows + int8 copies in 288 GB).
+    # Checked: native == int8 screen bit for bit, no full scan; every query's returned scores are
+    # the canonical scores of its ids, sorted; and on a 32-query slice the tie-tolerant rule against
+    # the faiss fp32 restatement over all 100M rows (streamed in chunks: 307 GB of fp32 rows does
+    # not fit the host)
+    import torch
+    from photo_search_engine_amd.distributed import shard_range, _device_merge
+    from photo_search_engine_amd.index import synthesize_device
+    N, d, nq, k, G, nslice = 100_000_000, 768, 256, 10, 8, 32
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    q = torch.empty((nq, d), dtype=torch.float32, device=dev)
+    synthesize_device(0, O.SEED_QUERIES, 0, nq, d, q.data_ptr(), True, "f16", stream)
+    shards = []
+    for g in range(G):
+        r0, n = shard_range(N, g, G)
+        ix = FlatIndex(d, "ip", "f16")
+        ix.reserve(n)
+        ix.add_synthetic(O.SEED_CORPUS, r0, n, True)
+        shards.append((ix, r0))
+    out = {}
+    for screen in ("native", "int8"):
+        Sg = torch.empty((G, nq, k), dtype=torch.float64, device=dev)
+        Ig = torch.empty((G, nq, k), dtype=torch.int64, device=dev)
+        for g, (ix, r0) in enumerate(shards):
+            ix.set_screen(screen)
+            ix.search_device_exact(q.data_ptr(), nq, k, None, Ig[g].data_ptr(), Sg[g].data_ptr(), r0, stream)
+        S, I, D = _device_merge(0, Sg, Ig, k)
+        torch.cuda.synchronize()
+        out[screen] = (S.cpu().numpy(), I.cpu().numpy(), D.cpu().numpy())
+    assert sum(ix.full_scan_count() for ix, _ in shards) == 0
+    for ix, _ in shards:
+        ix.close()
+    del shards
+    S, I, D = out["native"]
+    np.testing.assert_array_equal(out["int8"][1], I)
+    np.testing.assert_array_equal(out["int8"][0], S)
+    np.testing.assert_array_equal(D, S.astype(np.float32))
+    qh = q.cpu().numpy()
+    # every query: the returned scores are the canonical scores of the returned ids, in order
+    for a in range(nq):
+        rows = np.concatenate([O.synth_rows(O.SEED_CORPUS, int(i), 1, d, True, "f16") for i in I[a]])
+        np.testing.assert_array_equal(O.canon_scores(rows, qh[a:a + 1], "ip")[0], S[a])
+        key = list(zip((-S[a]).tolist(), I[a].tolist()))
+        assert key == sorted(key)
+    # the slice: faiss fp32 over every row, streamed in chunks generated on the device (the same
+    # counter-hash generator as the oracle's, bit-identical) and merged by (fp32 score desc, id asc)
+    Dc = np.full((nslice, k), -np.inf, dtype=np.float32)
+    Ic = np.full((nslice, k), -1, dtype=np.int64)
+    chunk = 5_000_000
+    buf = torch.empty((chunk, d), dtype=torch.float32, device=dev)
+    for r0 in range(0, N, chunk):
+        n = min(chunk, N - r0)
+        synthesize_device(0, O.SEED_CORPUS, r0, n, d, buf.data_ptr(), True, "f16", stream)
+        torch.cuda.synchronize()
+        Dp, Ip = O.knn_faiss_fp32(buf[:n].cpu().numpy(), qh[:nslice], k, "ip", THREADS)
+        Dm = np.concatenate([Dc, Dp], axis=1)
+        Im = np.concatenate([Ic, np.where(Ip >= 0, Ip + r0, -1)], axis=1)
+        order = np.lexsort((Im, -Dm.astype(np.float64)), axis=1)[:, :k]
+        Dc, Ic = np.take_along_axis(Dm, order, 1), np.take_along_axis(Im, order, 1)
+    del buf
+    assert np.max(np.abs(D[:nslice].astype(np.float64) - Dc)) <= 1e-5
+    for a in range(nslice):
+        miss = np.setdiff1d(Ic[a], I[a])
+        if miss.size == 0:
+            continue
+        rows = np.concatenate([O.synth_rows(O.SEED_CORPUS, int(i), 1, d, True, "f16") for i in miss])
+        sm = O.canon_scores(rows, qh[a:a + 1], "ip")[0]
+        for s_, i in zip(sm.tolist(), miss.tolist()):
+            assert not (s_ > S[a, k - 1] or (s_ == S[a, k - 1] and i < I[a, k - 1])), \
+                f"query {a}: faiss candidate {i} beats the k-th result"
+    assert float(np.mean(I[:nslice] == Ic)) >= 0.99
+
+
 # ------------------------------------------------------------------------------------------------
 # cfg5: IVF-Flat nlist=4096 nprobe=32 d=1536 bf16, batch 256, top-10 (reduced N, skewed lists)
 # ------------------------------------------------------------------------------------------------

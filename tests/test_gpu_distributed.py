@@ -22,14 +22,18 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, N, d, dtype, nq, k, metric, outdir, screen="native"):
+def _worker(rank, world, port, N, d, dtype, nq, k, metric, outdir, screen="native", backend="gloo"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    torch.cuda.set_device(0)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = rank if backend == "nccl" else 0  # nccl (RCCL over xGMI): one GPU per rank
+    torch.cuda.set_device(dev)
+    if backend == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", dev))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from photo_search_engine_amd.distributed import ShardedFlatIndex
-        sh = ShardedFlatIndex(d, metric, dtype, device=0)
+        sh = ShardedFlatIndex(d, metric, dtype, device=dev)
         sh.add_synthetic(O.SEED_CORPUS, N, True)
         sh.index.set_screen(screen)
         q = torch.from_numpy(O.synth_rows(O.SEED_QUERIES, 0, nq, d, True, dtype)).cuda()
@@ -61,6 +65,27 @@ def test_two_ranks_one_gpu_match_oracle(tmp_path, metric, dtype, nq, k, N):
         valid = Ie >= 0
         np.testing.assert_array_equal(o["S"][valid], Se[valid])
         np.testing.assert_array_equal(o["D"][valid], Se[valid].astype(np.float32))
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs >= 2 GPUs (one rank per GPU over RCCL); "
+                    "the one-GPU box runs the same path over gloo above")
+@pytest.mark.parametrize("screen,metric,dtype,nq,k,N", [("native", "ip", "bf16", 40, 25, 40011),
+                                                        ("int8", "ip", "bf16", 64, 20, 40011),
+                                                        ("native", "l2", "f32", 3, 10, 20011)])
+def test_ranks_on_distinct_gpus_nccl_match_oracle(tmp_path, screen, metric, dtype, nq, k, N):
+    # the driver's multi-GPU shape: one process per GPU, the exchanges over RCCL / xGMI
+    world, d = min(torch.cuda.device_count(), 4), 256
+    mp.spawn(_worker, args=(world, _free_port(), N, d, dtype, nq, k, metric, str(tmp_path), screen, "nccl"),
+             nprocs=world, join=True)
+    outs = [np.load(tmp_path / f"r{r}.npz") for r in range(world)]
+    assert sum(int(o["n"]) for o in outs) == N
+    x = O.synth_rows(O.SEED_CORPUS, 0, N, d, True, dtype)
+    q = O.synth_rows(O.SEED_QUERIES, 0, nq, d, True, dtype)
+    Se, Ie = O.knn_exact(x, q, k, metric)
+    for o in outs:
+        np.testing.assert_array_equal(o["I"], Ie)
+        np.testing.assert_array_equal(o["S"], Se)
+        assert int(o["full_scan"]) == 0
 
 
 def test_four_ranks_one_gpu_match_oracle(tmp_path):

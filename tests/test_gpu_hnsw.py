@@ -127,3 +127,45 @@ def test_hnsw_graph_validation_and_staleness():
     ix.reset()  # fewer rows than the graph covers: refused
     with pytest.raises(_lib.VsError):
         hg.search(q, 5, 20)
+
+
+def test_hnsw_patch_validates_whole_lists():
+    # vs_hnsw_patch takes whole (node, level) lists, each as vs_hnsw_create leaves them
+    # (distinct ids, then -1s); partial lists, duplicates and ids after the terminator are refused
+    # and leave the graph unchanged
+    n, d = 200, 16
+    ix, x = _index(n, d, "f32", "l2", seed=8)
+    g = H.layered_knn_graph(x, 4, "l2", seed=3)
+    hg = HNSWGraph(ix, g)
+    cum = np.asarray(g["cum_nneighbor_per_level"]).astype(np.int64)
+    lo = int(g["offsets"][7])
+    width = int(cum[1] - cum[0])
+    pos = np.arange(lo, lo + width, dtype=np.uint64)
+    cur = g["neighbors"][lo:lo + width].copy()
+    ep, top = int(g["entry_point"]), int(g["max_level"])
+    q = O.synth_rows(O.SEED_QUERIES + 8, 0, 6, d, True)
+    D0, I0 = hg.search(q, 5, 20)
+    bad_dup = cur.copy()
+    bad_dup[1] = bad_dup[0]
+    bad_after = cur.copy()
+    bad_after[1] = -1  # (ids 2.. follow the terminator)
+    for p_, v_ in ((pos[:-1], cur[:-1]), (pos, bad_dup), (pos, bad_after),
+                   (np.concatenate([pos, pos[:1]]), np.concatenate([cur, cur[1:2]]))):
+        with pytest.raises(_lib.VsError):
+            hg.patch(p_, v_, ep, top)
+    D1, I1 = hg.search(q, 5, 20)
+    assert np.array_equal(I0, I1) and np.array_equal(D0, D1)
+    # a whole list, rewritten compacted (its last id dropped, -1 padded): accepted, and the search
+    # equals the oracle's over the patched graph
+    new = np.full(width, -1, dtype=np.int32)
+    kept = cur[cur >= 0][:-1]
+    new[:kept.shape[0]] = kept
+    hg.patch(np.concatenate([pos, pos[:2]]), np.concatenate([new, new[:2]]), ep, top)  # (repeats agree)
+    g2 = dict(g)
+    g2["neighbors"] = g["neighbors"].copy()
+    g2["neighbors"][lo:lo + width] = new
+    D2, I2 = hg.search(q, 5, 20)
+    S_ref, I_ref = H.search(x, g2, q, 5, 20, "l2")
+    _check(D2, I2, S_ref, I_ref)
+    hg.close()
+    ix.close()

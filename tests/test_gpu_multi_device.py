@@ -217,3 +217,23 @@ def test_int8_two_phase_group_residual_small_shards(Multi):
         np.testing.assert_array_equal(I, Ie)
         np.testing.assert_array_equal(D, S.astype(np.float32))
     ix.close()
+
+
+@pytest.mark.skipif(__import__("torch").cuda.device_count() < 2,
+                    reason="needs >= 2 GPUs; the one-GPU box runs the same path with every shard on device 0")
+@pytest.mark.parametrize("dtype,metric,screen", [("bf16", "ip", "int8"), ("bf16", "l2", "int8"),
+                                                 ("f32", "ip", "native")])
+def test_shards_on_distinct_gpus(Multi, dtype, metric, screen):
+    # peer copies across physical devices both ways: the lists device g -> devices[0], the two-phase
+    # floor devices[0] -> device g (int8 screen on bf16 shards)
+    import torch
+    G = min(torch.cuda.device_count(), 4)
+    N, d = 300_000, 256
+    x = O.synth_rows(O.SEED_CORPUS, 0, N, d, True, dtype)
+    ix = Multi(d, metric, dtype, devices=list(range(G)))
+    ix.add(x)
+    ix.set_screen(screen)
+    for nq, k in ((64, 20), (1, 10), (256, 100)):
+        q = O.synth_rows(O.SEED_QUERIES, 0, nq, d, True, "f32")
+        _exact(ix, x, q, k, metric)
+    ix.close()

@@ -354,6 +354,31 @@ def test_ties_beyond_max_depth_full_scan(FlatIndex, nq, copies, dtype, metric):
     ix.close()
 
 
+@pytest.mark.parametrize("dtype,screen", [("f32", "native"), ("bf16", "native"), ("bf16", "int8")])
+def test_single_query_duplicate_burst_certified_by_research(FlatIndex, dtype, screen):
+    # a single query's GEMV first pass keeps only Kb keys per block; a burst of a few
+    # hundred contiguous duplicates (photos imported one after another) sits in one block and fails
+    # that pass.  The host API's deeper re-search keeps whole lists, so it certifies the query
+    # without the full scan (a truncated re-search would fail the same way at every depth).
+    d, k, N, copies = 128, 10, 120_000, 300
+    x = O.synth_rows(O.SEED_CORPUS, 0, N, d, True, dtype)
+    x[60_000:60_000 + copies] = x[60_000]
+    q = x[60_000:60_001].copy()
+    ix = FlatIndex(d, "ip", dtype)
+    ix.set_scan_limit(0)
+    ix.add(x)
+    ix.set_screen(screen)
+    xs = ix.reconstruct_n(0, N)
+    Se, Ie = O.knn_exact(xs, q, k, "ip")
+    np.testing.assert_array_equal(Ie[0], np.arange(60_000, 60_000 + k))
+    D, I = ix.search(q, k)
+    np.testing.assert_array_equal(I, Ie)
+    np.testing.assert_array_equal(D, Se.astype(np.float32))
+    assert ix.uncertified_count() >= 1  # the truncated first pass could not certify it
+    assert ix.full_scan_count() == 0    # the re-search did
+    ix.close()
+
+
 @pytest.mark.parametrize("metric", ["ip", "l2"])
 def test_full_scan_near_ties_and_k_beyond_rows(FlatIndex, metric):
     # The full scan's own ordering: rows tied to the last bit mixed with rows one ulp apart (bf16),

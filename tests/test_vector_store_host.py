@@ -201,6 +201,45 @@ def test_reference_hnsw_fixture_rewrites_byte_identical(tmp_path):
     assert open(out, "rb").read() == open(src, "rb").read()
 
 
+def test_flat_config_over_reference_hnsw_file_loads_and_saves_hnsw(VS, tmp_path):
+    # utils/vector_store.py:125-143: a flat configuration checks only the file's metric_type, so the
+    # reference's own IP HNSW file loads under a "flat" sidecar; its faiss index object stays an
+    # IndexHNSWFlat, so save() writes the HNSW file back: unchanged rows -> the same bytes
+    import json
+    import shutil
+    from photo_search_engine_amd import faiss_format as F
+    idx = tmp_path / "photo_search.index"
+    shutil.copy(os.path.join(GOLDEN, "ref_photo_search.index"), idx)
+    meta = json.load(open(os.path.join(GOLDEN, "ref_photo_search.index.meta.json")))
+    meta["index_type"] = "flat"
+    (tmp_path / "photo_search.index.meta.json").write_text(json.dumps(meta))
+    (tmp_path / "metadata.json").write_text(json.dumps([{"photo_path": f"/p/{i}"} for i in range(77)]))
+    store = VS(dimension=4096, index_path=str(idx), metadata_path=str(tmp_path / "metadata.json"))
+    assert store.load() and store.get_total_items() == 77
+    ref = F.read_index(str(idx)).vectors.copy()
+    res = store.search(ref[5].tolist(), 3)  # exact search: a stored row finds itself first
+    assert res[0]["metadata"] == {"photo_path": "/p/5"}
+    before = open(idx, "rb").read()
+    store.save()
+    assert open(idx, "rb").read() == before
+    assert json.load(open(str(idx) + ".meta.json"))["index_type"] == "flat"
+    # a row added after the load is inserted into the file's graph (its M = 48, its efConstruction)
+    store.add_item([float(v) for v in ref[3]], {"photo_path": "/p/new"})
+    store.save()
+    ff = F.read_index(str(idx))
+    g = F.read_hnsw_graph(str(idx))
+    assert ff.kind == "hnsw" and ff.ntotal == 78 and g["levels"].shape[0] == 78
+    probas, cum = F.hnsw_default_probas(48)
+    assert np.array_equal(g["cum_nneighbor_per_level"], cum) and g["efConstruction"] == 320
+    s2 = VS(dimension=4096, index_path=str(idx), metadata_path=str(tmp_path / "metadata.json"))
+    assert s2.load() and s2.get_total_items() == 78
+    # clear() starts a flat index again (the reference's clear() creates a fresh flat index)
+    s2.clear()
+    s2.add_item([float(v) for v in ref[0]], {"photo_path": "/p/0"})
+    s2.save()
+    assert F.read_index(str(idx)).kind == "flat"
+
+
 def test_hnsw_store_beyond_exact_build_inserts_and_saves_ihnf(VS, tmp_path, monkeypatch):
     # every size saves an IHNf file (rollback to the reference's faiss): the first
     # VECTOR_HNSW_GRAPH_MAX_ROWS rows get the exact-candidate build, the rest are inserted the way
