@@ -349,8 +349,9 @@ def main():
             "metric": (METRICS[args.workload] if not args.rows else
                        METRICS[args.workload].split(",")[0] + f" (rows override: N={N}, not the BASELINE config)") +
                       ("" if args.metric == "ip" else " [L2 metric, not the BASELINE config]") +
-                      (f" [one rank of a {args.shard_of}-shard step: {n_local} rows, both exchanges over a "
-                       "one-rank group, the G-shard floor precomputed; not the BASELINE line]"
+                      (f" [one rank of a {args.shard_of}-shard step: {n_local} rows, both merges on the "
+                       "rank's own lists (a one-rank group exchanges nothing: the G-rank run adds two RCCL "
+                       "all-gathers), the G-shard floor precomputed; not the BASELINE line]"
                        if args.shard_of > 1 else ""),
             "value": round(qps, 2),
             "unit": "queries/s",

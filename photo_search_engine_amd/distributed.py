@@ -206,6 +206,8 @@ class ShardedFlatIndex:
 
     # -- search --------------------------------------------------------------------------------
     def _gather(self, t: torch.Tensor) -> torch.Tensor:
+        if self.world == 1:  # a one-rank group has nothing to exchange (bench --shard-of G: the
+            return t.unsqueeze(0)  # measured rank's own lists; the G-rank run adds RCCL's latency)
         out = torch.empty((self.world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
         ev = None
         if self.exchange_timing and t.is_cuda:

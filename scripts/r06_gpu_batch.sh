@@ -15,9 +15,9 @@ run() {  # name, seconds, command...
   if fatal $rc; then echo "fatal rc=$rc in $name: stopping" >> gpurun_out/steps.log; exit $rc; fi
   return 0
 }
-abloop() {  # name, reps, args... : bench.py with --k1-schedule 0 / 1 alternating
+abloop() {  # name, reps, args... : bench.py with --k1-schedule $ABS (default "0 1") alternating
   local name=$1 reps=$2; shift 2
-  for i in $(seq 1 $reps); do for s in 0 1; do
+  for i in $(seq 1 $reps); do for s in ${ABS:-0 1}; do
     timeout -k 10 300 python bench.py --k1-schedule $s "$@" --no-cpu-baseline > gpurun_out/ab.tmp 2>&1
     local rc=$?
     echo "sched$s $(tail -1 gpurun_out/ab.tmp)" >> gpurun_out/ab_$name.txt
@@ -36,6 +36,9 @@ for s in ${STEPS:-decomp}; do
     ab3) abloop cfg3 2 --steps 20 --warmup 3 ;;
     ab3n) abloop cfg3n 2 --screen native --steps 10 --warmup 3 ;;
     full2) VS_TEST_K1_SCHEDULE=2 run pytest_gpu_sched2 900 $PYT tests -m gpu ;;
+    direct2) VS_TEST_K1_SCHEDULE=2 run pytest_direct_sched2 600 $PYT tests/test_gpu_int8_direct.py tests/test_gpu_int8_screen.py tests/test_gpu_baseline_shapes.py -k "not cfg4_full" -m gpu ;;
+    ab12) ABS="1 2" abloop cfg3_12 2 --steps 20 --warmup 3 ;;
+    ab812) ABS="1 2" abloop shard8_12 2 --shard-of 8 --steps 30 ;;
     ab8) abloop shard8 2 --shard-of 8 --steps 30 ;;
     shard8) run bench_shard8 300 python bench.py --shard-of 8 --steps 30 --no-cpu-baseline ;;
     cfg2) run bench_cfg2 300 python bench.py --workload cfg2 --no-cpu-baseline ;;
