@@ -91,7 +91,7 @@ def parse():
     ap.add_argument("--sigma", type=float, default=1.0, help="--data mixture: cluster spread")
     ap.add_argument("--iso-data", action="store_true",
                     help="cfg5: isotropic rows (the flat bench's data) instead of the Gaussian mixture")
-    ap.add_argument("--k1-schedule", type=int, default=None, choices=[0, 1, 2],
+    ap.add_argument("--k1-schedule", type=int, default=None, choices=[0, 1],
                     help="the direct K1 screens' K-step schedule (include/vs.h vs_set_k1_schedule; default: the library's)")
     ap.add_argument("--traffic-file", default=None,
                     help="rocprofv3 PMC summary giving HBM bytes per launch (default profiles/traffic_<workload>.json)")

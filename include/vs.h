@@ -196,15 +196,14 @@ int vs_screen_probe(vs_index* index, const float* q_dev, int64_t nq, int32_t scr
 /* Diagnostic forms of the direct screen's loop (csrc/vs_k1probe.hip; DESIGN §5 "Where K1 int8's time
  * goes"), over the whole index like vs_screen_probe (thresholds at +inf, 9..256 device queries,
  * zero_queries as there).  screen = VS_SCREEN_I8 (inner-product int8 direct screen; variants
- * LOADS, LDS, MFMA, FULL, FULL_MS, FULL_PRIO, FULL_MS_PRIO, FULL_MSIL) or VS_SCREEN_NATIVE (bf16
- * direct screen; LOADS, MFMA, FULL).  `reps` launches back to back, each between its own HIP events:
+ * LOADS, LDS, MFMA, FULL, FULL_MS, FULL_PRIO, FULL_MS_PRIO) or VS_SCREEN_NATIVE (bf16 direct
+ * screen; LOADS, MFMA, FULL).  `reps` launches back to back, each between its own HIP events:
  * ms[r] = launch r's duration; stamps[(r * G + b) * 4 + {0,1,2,3}] = workgroup b's s_memtime at the
  * loop's start and end, and its s_memrealtime (100 MHz) at the same points (host array of
  * reps * 256 * 4); *G_out = the launch's workgroups.  Synchronises. */
 /* The K-step schedule of the int8 inner-product direct screen (K1), process-wide: 0 = one barrier at
- * the head of every K-step; 1 (default) = the mid-step barrier; 2 = the mid-step barrier
- * with each tile's epilogue interleaved into the next tile's first K-step.  The same keys, survivors
- * and results under every schedule. */
+ * the head of every K-step; 1 (default) = the mid-step barrier.  The same keys,
+ * survivors and results under either schedule. */
 int vs_set_k1_schedule(int32_t schedule);
 int vs_k1_schedule(void);
 enum {
@@ -214,8 +213,7 @@ enum {
     VS_K1P_FULL = 3,         /* the whole loop with the epilogue's bound test (the product's schedule) */
     VS_K1P_FULL_MS = 4,      /* the same under the mid-step-barrier schedule */
     VS_K1P_FULL_PRIO = 5,    /* FULL with static priority 1 for waves 4-7 */
-    VS_K1P_FULL_MS_PRIO = 6, /* FULL_MS with static priority 1 for waves 4-7 */
-    VS_K1P_FULL_MSIL = 7     /* FULL_MS with the tile epilogue interleaved into the next tile's step 0 */
+    VS_K1P_FULL_MS_PRIO = 6  /* FULL_MS with static priority 1 for waves 4-7 */
 };
 int vs_k1_probe(vs_index* index, const float* q_dev, int64_t nq, int32_t screen, int32_t variant,
                 int32_t zero_queries, int32_t reps, void* stream, float* ms, unsigned long long* stamps,

@@ -1858,7 +1858,7 @@ int vs_k1_probe(vs_index* ix, const float* q_dev, int64_t nq, int32_t screen, in
 
 int vs_set_k1_schedule(int32_t schedule) {
     return guarded([&] {
-        if (schedule < 0 || schedule > 2) throw VsError(VS_ERR_ARG, "K1 schedule: 0, 1 or 2");
+        if (schedule != 0 && schedule != 1) throw VsError(VS_ERR_ARG, "K1 schedule: 0 or 1");
         set_k1_schedule(schedule);
     });
 }

@@ -34,7 +34,6 @@ hipError_t launch_k1_probe(int variant, int dt, const ScreenArgs& a, const uint8
             case VS_K1P_FULL_MS: return launch_one<DT_I8, PR_FULL, 1, false>(a, qt, nqb, st);
             case VS_K1P_FULL_PRIO: return launch_one<DT_I8, PR_FULL, 0, true>(a, qt, nqb, st);
             case VS_K1P_FULL_MS_PRIO: return launch_one<DT_I8, PR_FULL, 1, true>(a, qt, nqb, st);
-            case VS_K1P_FULL_MSIL: return launch_one<DT_I8, PR_FULL, 2, false>(a, qt, nqb, st);
             default: return hipErrorInvalidValue;
         }
     }

@@ -636,8 +636,7 @@ namespace vs {
 
 // the K1 int8 inner-product direct screen's schedule (vs_set_k1_schedule; vs_screen.h screen_direct
 // SCHED): 0 = barrier at the head of every K-step; 1 = the mid-step barrier (cfg3 K1 3.68 -> 3.50 ms,
-// profiles/r06_k1_decomposition.json); 2 = the mid-step barrier with the tile epilogue interleaved
-// into the next tile's first K-step.  (The bf16 / f16 direct screen keeps the head barrier: the
+// profiles/r06_k1_decomposition.json).  (The bf16 / f16 direct screen keeps the head barrier: the
 // mid-step form measured no faster there, its loop bound by the half-line loads.)
 static std::atomic<int> g_k1_sched{1};
 void set_k1_schedule(int s) { g_k1_sched.store(s); }
@@ -645,10 +644,6 @@ int k1_schedule() { return g_k1_sched.load(std::memory_order_relaxed); }
 
 bool i8_direct_ok(int dpad8) { return dpad8 % (64 * I8D_U) == 0 && dpad8 >= 2 * 64 * I8D_U; }
 bool d16_direct_ok(int dpad) { return dpad % (CH * I8D_U) == 0 && dpad >= 2 * CH * I8D_U; }
-
-__global__ void __launch_bounds__(512, 2) k_screen_i8d_il(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
-    screen_direct<DT_I8, METRIC_IP, false, 16, false, PR_NONE, 2>(a, qt, nqb);
-}
 
 // ... over group-residual codes (a corpus stored cluster by cluster): every key + <mu_g, q>
 // (inner product; the seed pass adds the same terms to its maxima)
@@ -2165,10 +2160,9 @@ static hipError_t launch_mfma_dt(int dt, const ScreenArgs& a, const uint8_t* qt,
             }
             // (the L2 form keeps the head barrier: under the mid-step schedule its ||x||^2 state
             // spills past the 256 VGPRs of two waves per SIMD)
-            const int sch = k1_schedule();
             void (*fn)(ScreenArgs, const uint8_t*, int) =
                 a.metric != METRIC_IP ? k_screen_i8d<METRIC_L2>
-                                      : sch == 2 ? k_screen_i8d_il : sch == 1 ? k_screen_i8d_ms<METRIC_IP> : k_screen_i8d<METRIC_IP>;
+                                      : k1_schedule() == 1 ? k_screen_i8d_ms<METRIC_IP> : k_screen_i8d<METRIC_IP>;
             set_lds_attr((const void*)fn, I8D_LDS);
             hipLaunchKernelGGL(fn, dim3(a.G), dim3(MF_THREADS), I8D_LDS, st, a, qt, nqb);
             return hipGetLastError();

@@ -724,8 +724,8 @@ constexpr int I8D_RES_LDS = 2 * MFMA_QB * 4;  // group residuals: <mu_g, q> of t
 
 // K-step kinds of the mid-step-barrier schedule (vs_i8_asm.h MS_*): F/N first K-step of a tile or
 // not, O/P the step's first 4 fragment reads its own or prefetched, P/N prefetch the next step's
-enum { MS_FON = 0, MS_NOP = 1, MS_NPP = 2, MS_NPN = 3, MS_NON = 4 };
-template <int DT, int KIND, bool NT>
+enum { MS_FON = 0, MS_NOP = 1, MS_NPP = 2, MS_NPN = 3 };
+template <int DT, int KIND>
 __device__ __forceinline__ void ms_step(intx4 (&acc)[2][16], intx4 (&bt)[4], uint32_t slot_lds, uint32_t next_lds,
                                         intx4& A0, intx4& A1, intx4& AN0, intx4& AN1, const uint8_t* qs0,
                                         const uint8_t* qs1, uint32_t ql0, uint32_t ql1, const uint8_t* cs) {
@@ -734,14 +734,10 @@ __device__ __forceinline__ void ms_step(intx4 (&acc)[2][16], intx4 (&bt)[4], uin
         if constexpr (KIND == MS_FON) P_##FON(A0, A1, AN0, AN1, qs0, qs1, ql0, ql1, cs); \
         else if constexpr (KIND == MS_NOP) P_##NOP(A0, A1, AN0, AN1, qs0, qs1, ql0, ql1, cs); \
         else if constexpr (KIND == MS_NPP) P_##NPP(A0, A1, AN0, AN1, qs0, qs1, ql0, ql1, cs); \
-        else if constexpr (KIND == MS_NON) P_##NON(A0, A1, AN0, AN1, qs0, qs1, ql0, ql1, cs); \
         else P_##NPN(A0, A1, AN0, AN1, qs0, qs1, ql0, ql1, cs);                        \
     } while (0)
-    if constexpr (DT == DT_I8) MS_KINDS(MS_I8_);
-    else if constexpr (DT == DT_BF16 && NT) MS_KINDS(MS_BF_NT_);
-    else if constexpr (DT == DT_BF16) MS_KINDS(MS_BF_DF_);
-    else if constexpr (NT) MS_KINDS(MS_HF_NT_);
-    else MS_KINDS(MS_HF_DF_);
+    static_assert(DT == DT_I8, "the mid-step barrier: the int8 screen");
+    MS_KINDS(MS_I8_);
 #undef MS_KINDS
 }
 
@@ -760,10 +756,6 @@ __device__ __forceinline__ void ms_step(intx4 (&acc)[2][16], intx4 (&bt)[4], uin
 // pairs 7 and 8 of a K-step and the issue of the K-step 3 ahead between pairs 8-11, and the next
 // K-step's first fragment reads are issued at the end of the step, so the matrix pipe keeps working
 // across every barrier (DESIGN §5 "K1 int8, mid-step barrier").
-// SCHED 2 = the mid-step barrier with the tile epilogue interleaved into the next tile's first
-// K-step (int8 inner product): before MFMA pair n of that step overwrites query column n's
-// accumulators, the loop code tests column n of the previous tile and stages its records, so the
-// epilogue's VALU work runs beside the MFMAs of the partner wave instead of between K-steps.
 // PROBE (diagnostic builds of the loop, vs_k1probe.hip; 0 in the product): per workgroup
 // s_memtime / s_memrealtime stamps around the loop into a.stamps, and PR_LOADS = the loads and the
 // barriers only, PR_LDS = + the query-fragment reads, PR_MFMA = + the MFMAs (no epilogue), PR_FULL =
@@ -777,9 +769,7 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
     static_assert(!(MAP && I8), "the mapped scan serves bf16 / f16 lists");
     static_assert(!RES || (I8 && !MAP && !L2), "group residuals: the int8 flat inner-product main pass");
     static_assert(NG == 16 || (NG == 4 && MAP), "narrow query tiles: mapped scans only");
-    static_assert(SCHED == 0 || (!MAP && !RES && NG == 16), "the mid-step barrier: flat shards");
-    static_assert(SCHED != 2 || (I8 && !L2), "the interleaved epilogue: the int8 inner-product screen");
-    constexpr bool IL = SCHED == 2;
+    static_assert(SCHED == 0 || (I8 && !MAP && !RES && NG == 16), "the mid-step barrier: int8 flat shards");
     static_assert(SCHED == 0 || PROBE == PR_NONE || PROBE == PR_FULL, "the mid-step barrier: whole-loop probes");
     constexpr bool EPI = PROBE == PR_NONE || PROBE == PR_FULL;  // the tile epilogue runs
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -1035,201 +1025,19 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
     do {                                                                                               \
         asm volatile("s_waitcnt vmcnt(8)" : "+v"(A[U_][0]), "+v"(A[U_][1]) : : "memory");            \
         const MsIssue is_ = ms_prep(((U_) + I8D_P) & 3);                                               \
-        ms_step<DT, KIND_, (((U_) + I8D_P) & 1) != 0>(acc, bt, ring + (uint32_t)((U_) * 16384) + lane_off, \
+        ms_step<DT, KIND_>(acc, bt, ring + (uint32_t)((U_) * 16384) + lane_off,                \
                                                      ring + (uint32_t)((((U_) + 1) & 3) * 16384) + lane_off, \
                                                      A[U_][0], A[U_][1], A[((U_) + I8D_P) & 3][0],          \
                                                      A[((U_) + I8D_P) & 3][1], is_.qs0, is_.qs1, is_.ql0,   \
                                                      is_.ql1, is_.cs);                                     \
     } while (0)
-    if constexpr (SCHED >= 1) {
+    if constexpr (SCHED == 1) {
         // the issue above left K-steps 0..2 in flight; step 0's query block must have landed in every
         // wave before its first fragment read
         if (t1 > t0) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
-        if constexpr (IL) {  // step 0's first fragments (every tile's step 0 takes them prefetched)
-            if (t1 > t0)
-                asm volatile("ds_read_b128 %0, %4 offset:0\n\tds_read_b128 %1, %4 offset:1024\n\t"
-                             "ds_read_b128 %2, %4 offset:2048\n\tds_read_b128 %3, %4 offset:3072"
-                             : "+v"(bt[0]), "+v"(bt[1]), "+v"(bt[2]), "+v"(bt[3]) : "v"(ring + lane_off) : "memory");
-        }
     }
-    // ---- SCHED 2: the tile epilogue in pieces (the previous tile's, inside the next tile's step 0) ----
-    struct EpState {
-        int64_t rowbase, idbase;
-        const uint32_t* rx;
-        float smax, smin, bmax;
-        int qlane, olane, par;
-        bool edge;
-    };
-    auto ep_setup = [&](int tt) -> EpState {
-        EpState e;
-        int olane;  // asm-opaque lane id: lane-derived indices are not hoisted out of the K loop
-        asm volatile("v_mov_b32 %0, %1" : "=v"(olane) : "v"(lane));
-        e.olane = olane;
-        e.qlane = olane & 15;
-        e.rowbase = ltile(tt) * TR;
-        e.idbase = e.rowbase;
-        e.par = tt & 1;
-        e.rx = rowx + (tt & 1) * TR;
-        e.edge = e.rowbase + TR > a.n_valid;
-        const int rw0 = wid * 32 + (olane >> 4) * 4;
-        const uint4 w0 = *(const uint4*)(e.rx + rw0), w1 = *(const uint4*)(e.rx + rw0 + 16);
-        const uint32_t w8[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
-        e.smax = e.smin = __uint_as_float(w8[0] << 16);
-        e.bmax = __uint_as_float(w8[0] & 0xFFFF0000u);
-#pragma unroll
-        for (int j = 1; j < 8; ++j) {
-            e.smax = fmaxf(e.smax, __uint_as_float(w8[j] << 16));
-            e.smin = fminf(e.smin, __uint_as_float(w8[j] << 16));
-            e.bmax = fmaxf(e.bmax, __uint_as_float(w8[j] & 0xFFFF0000u));
-        }
-        return e;
-    };
-    // keys of the staged records, one per lane (as the epilogue's drain below)
-    auto ep_drain = [&](const EpState& e, int nrec) {
-        __builtin_amdgcn_wave_barrier();
-        if (lane < nrec) {
-            const int meta = rmeta[lane];
-            const int n = meta & 15, sl = meta >> 4;
-            const int q = 16 * n + (sl & 15);
-            const int r0 = wid * 32 + (sl >> 4) * 4;
-            const intx4 c0 = rec[2 * lane], c1 = rec[2 * lane + 1];
-            const uint4 w0 = *(const uint4*)(e.rx + r0), w1 = *(const uint4*)(e.rx + r0 + 16);
-            const int cc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-            const uint32_t w8[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
-            const float4 f = qrec[q];
-            float v[8];
-            uint32_t mh = 0;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int row = r0 + (j >> 2) * 16 + (j & 3);
-                const float x = __builtin_fmaf(__uint_as_float(w8[j] & 0xFFFF0000u), f.y,
-                                               (float)cc[j] * __uint_as_float(w8[j] << 16)) * f.x;
-                v[j] = e.rowbase + row >= a.n_valid ? __builtin_nanf("") : x;
-                mh |= (v[j] >= f.z ? 1u : 0u) << j;
-            }
-            if (mh) {
-                flag[2 + e.par] = 1;
-                const u64 tk = thr_key[q];
-                float* sv = (float*)(rec + 2 * lane);
-                *(float4*)(sv) = make_float4(v[0], v[1], v[2], v[3]);
-                *(float4*)(sv + 4) = make_float4(v[4], v[5], v[6], v[7]);
-                while (mh) {
-                    const int j = __builtin_ctz(mh);
-                    mh &= mh - 1u;
-                    const u64 key = mk_key(sv[j], (uint32_t)(e.idbase + r0 + (j >> 2) * 16 + (j & 3)));
-                    if (key <= tk) continue;
-                    const int ps = atomicAdd(&flag[1], 1);
-                    if (ps < MF_POOL) {
-                        pool_key[ps] = key;
-                        pool_q[ps] = q;
-                        continue;
-                    }
-                    const int slot = atomicAdd(&cnt[q], 1);
-                    if (slot < a.cap) cand[(size_t)q * a.cap + slot] = key;
-                }
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
-    };
-    // column N of the tile: the bound test of its 8 keys (as the epilogue's) and its records staged
-    auto ep_column = [&](const EpState& e, auto N, const float4 f, int& nrec) {
-        constexpr int n = decltype(N)::value;
-        const int mi = max(max(max(acc[0][n][0], acc[0][n][1]), max(acc[0][n][2], acc[0][n][3])),
-                           max(max(acc[1][n][0], acc[1][n][1]), max(acc[1][n][2], acc[1][n][3])));
-        const float fm = (float)mi;
-        const float b = __builtin_fmaf(e.bmax, f.y, fmaxf(e.smax * fm, e.smin * fm)) * f.x;
-        const bool go = b >= f.z || e.edge;
-        const u64 bal = __ballot(go);
-        if (bal == 0ull) return;
-        const int c = __popcll(bal);
-        if (nrec + c > I8D_REC) {
-            ep_drain(e, nrec);
-            nrec = 0;
-        }
-        if (go) {
-            const int slot = nrec + lane_prefix(bal);
-            rec[2 * slot] = acc[0][n];
-            rec[2 * slot + 1] = acc[1][n];
-            rmeta[slot] = n | (e.olane << 4);
-        }
-        nrec += c;
-    };
     for (int ti = t0; ti < t1; ++ti) {
-        if constexpr (IL) {
-            // step 0: the previous tile's epilogue column by column, each before the MFMA pair that
-            // overwrites that column
-            asm volatile("s_waitcnt vmcnt(8)" : "+v"(A[0][0]), "+v"(A[0][1]) : : "memory");
-            const MsIssue is_ = ms_prep(I8D_P);
-            const uint32_t slot_lds = ring + lane_off;
-            const bool ep = ti > t0;
-            EpState es{};
-            float4 fq = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            int nrec = 0;
-            if (ep) {
-                asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // (MFMA -> VALU reads)
-                es = ep_setup(ti - 1);
-                fq = qrec[es.qlane];
-            }
-#define I8D_IL(N_, ...)                                                                  \
-    do {                                                                                 \
-        float4 fn_ = fq;                                                                 \
-        if (ep) {                                                                        \
-            if constexpr ((N_) < 15) fn_ = qrec[16 * ((N_) + 1) + es.qlane];            \
-            ep_column(es, std::integral_constant<int, (N_)>{}, fq, nrec);                \
-        }                                                                                \
-        MSIL_I8_##N_(acc[0][(N_) & 15], acc[1][(N_) & 15], A[0][0], A[0][1], __VA_ARGS__); \
-        fq = fn_;                                                                        \
-    } while (0)
-#define I8D_IL0(N_)                                                                      \
-    do {                                                                                 \
-        float4 fn_ = fq;                                                                 \
-        if (ep) {                                                                        \
-            fn_ = qrec[16 * ((N_) + 1) + es.qlane];                                      \
-            ep_column(es, std::integral_constant<int, (N_)>{}, fq, nrec);                \
-        }                                                                                \
-        MSIL_I8_##N_(acc[0][N_], acc[1][N_], A[0][0], A[0][1]);                          \
-        fq = fn_;                                                                        \
-    } while (0)
-            I8D_IL0(0);
-            I8D_IL0(1);
-            I8D_IL0(2);
-            I8D_IL0(3);
-            I8D_IL0(4);
-            I8D_IL0(5);
-            I8D_IL0(6);
-            I8D_IL0(7);
-            I8D_IL(8, is_.qs0, is_.ql0);
-            I8D_IL(9, is_.qs1, is_.ql1);
-            I8D_IL(10, A[3][0], is_.cs);
-            I8D_IL(11, A[3][1], is_.cs);
-            I8D_IL0(12);
-            I8D_IL0(13);
-            I8D_IL0(14);
-            if (ep) ep_column(es, std::integral_constant<int, 15>{}, fq, nrec);
-            MSIL_I8_15N(acc[0][15], acc[1][15], A[0][0], A[0][1]);
-#undef I8D_IL
-#undef I8D_IL0
-            if (ep && nrec) ep_drain(es, nrec);
-            I8D_MS(1, MS_NON);
-            if (check_pending) {  // the previous tile's inserts (step 0 + its drain) are complete in
-                check_pending = false;  // every wave: they precede step 1's barrier
-                compaction_check(ti);
-            }
-            I8D_MS(2, MS_NOP);
-            I8D_MS(3, MS_NPP);
-            for (int ks0 = I8D_U; ks0 < nks; ks0 += I8D_U) {
-                I8D_MS(0, MS_NPP);
-                I8D_MS(1, MS_NPP);
-                I8D_MS(2, MS_NPP);
-                I8D_MS(3, MS_NPP);  // (the tile's last step prefetches the next tile's step 0)
-            }
-            if (ti + 1 < t1) {  // the epilogue of this tile runs in the next tile's step 0
-                check_pending = true;
-                continue;
-            }
-            // the last tile: its epilogue below; the prefetch of its last step has landed first
-            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(bt[0]), "+v"(bt[1]), "+v"(bt[2]), "+v"(bt[3]) : : "memory");
-        } else if constexpr (SCHED == 1) {
+        if constexpr (SCHED == 1) {
             I8D_MS(0, MS_FON);
             if (check_pending) {
                 check_pending = false;
@@ -1477,8 +1285,7 @@ template <int METRIC>
 __global__ void __launch_bounds__(512, 2) k_screen_i8d_ms(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
     screen_direct<DT_I8, METRIC, false, 16, false, PR_NONE, 1>(a, qt, nqb);
 }
-// ... and with the interleaved epilogue (SCHED 2; inner product)
-__global__ void __launch_bounds__(512, 2) k_screen_i8d_il(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb);
+
 // One launch for every list scan: a workgroup whose query tile holds <= 32 queries runs the narrow
 // form (64 columns = 32 queries x (hi, lo): a quarter of the MFMAs, a quarter of the tile's L2
 // footprint), the others the full 256-column form (two separately allocated code paths; the

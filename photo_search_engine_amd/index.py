@@ -208,8 +208,7 @@ class FlatIndex:
                                       stream or None, ctypes.byref(ms)))
         return float(ms.value)
 
-    K1_PROBES = {"loads": 0, "lds": 1, "mfma": 2, "full": 3, "full_ms": 4, "full_prio": 5, "full_ms_prio": 6,
-                 "full_msil": 7}
+    K1_PROBES = {"loads": 0, "lds": 1, "mfma": 2, "full": 3, "full_ms": 4, "full_prio": 5, "full_ms_prio": 6}
 
     def k1_probe(self, q_ptr: int, nq: int, screen: str, variant: str, zero_queries: bool, reps: int = 5,
                  stream: Optional[int] = None):
@@ -271,7 +270,7 @@ def merge_shards_device(metric_type: int, S_ptr: int, I_ptr: int, G: int, nq: in
 def set_k1_schedule(schedule: int) -> None:
     """The K-step schedule of the int8 inner-product direct screen, process-wide (include/vs.h
     ``vs_set_k1_schedule``): 0 = a barrier at the head of every K-step, 1 (default) = the mid-step
-    barrier, 2 = the mid-step barrier with the tile epilogue interleaved.  Results are identical."""
+    barrier.  Results are identical."""
     check(_lib.load().vs_set_k1_schedule(int(schedule)))
 
 

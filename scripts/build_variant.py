@@ -23,13 +23,14 @@ def main(patch_file, name):
         s = open(p).read()
         assert s.count(old) == 1, (f, old[:80], s.count(old))
         open(p, "w").write(s.replace(old, new))
-    objs = []
-    for f in sorted(glob.glob(os.path.join(OUT, "*.hip"))):
+    objs, procs = [], []
+    for f in sorted(glob.glob(os.path.join(OUT, "*.hip"))):  # (compiled concurrently)
         o = f[:-4] + ".o"
-        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17",
-                        "-Wno-unused-result", "-Wno-unused-value", "-Wno-inline-asm", "-c", f, "-o", o], check=True,
-                       stderr=subprocess.DEVNULL)
+        procs.append(subprocess.Popen(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17",
+                                       "-Wno-unused-result", "-Wno-unused-value", "-Wno-inline-asm", "-c", f, "-o", o],
+                                      stderr=subprocess.DEVNULL))
         objs.append(o)
+    assert all(p.wait() == 0 for p in procs), "variant build failed"
     lib = os.path.join(ROOT, "diag", name + ".so")
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", lib] + objs, check=True)
     shutil.rmtree(OUT, ignore_errors=True)

@@ -24,8 +24,6 @@ barrier:
   pairs 8-15, the 2 query LDS-DMAs and 2 corpus loads of the K-step 3 ahead between them -> [the
   next step's first 4 fragment reads from its slot (P) | none (N)].  F = first K-step of a tile
   (src2 = 0).
-  MSIL_I8_<n>: pair n of a tile's first K-step when the previous tile's epilogue is interleaved
-  into it (see il_pair).
 
 Usage: python scripts/gen_i8_asm.py > photo_search_engine_amd/csrc/vs_i8_asm.h
 """
@@ -93,48 +91,6 @@ def ms_step(op: str, first: bool, own: bool, pre: bool, nt: bool) -> str:
     return "\\n\\t".join(lines)
 
 
-def il_pair(n: int, op: str = "v_mfma_i32_16x16x64_i8", pre: bool = True) -> str:
-    """MFMA pair n of a tile's first K-step in the mid-step schedule with the previous tile's epilogue
-    interleaved (the pair overwrites column n's accumulators; the loop code tests column n first):
-    its 4-ahead fragment read, the barrier before pair 8, the issue pieces after pairs 8-11, and
-    after pair 15 the next step's first 4 fragment reads.  The step's own first 4 fragments were
-    prefetched by the previous tile's last step."""
-    lines = []
-    if n == 8:
-        lines += ["s_waitcnt vmcnt(6)", "s_barrier"]
-    issued = min(16, n + RA)
-    lines.append(f"s_waitcnt lgkmcnt({issued - (n + 1)})")
-    for m in range(2):
-        lines.append(f"{op} %[c{m}], %[a{m}], %[b{n % RA}], 0")
-    if n + RA < 16:
-        lines.append(f"ds_read_b128 %[b{n % RA}], %[addr] offset:{(n + RA) * 1024}")
-    vm = {8: ["s_mov_b32 m0, %[ql]", "s_nop 0", "global_load_lds_dwordx4 %[qs], off"],
-          9: ["s_mov_b32 m0, %[ql]", "s_nop 0", "global_load_lds_dwordx4 %[qs], off"],
-          10: ["global_load_dwordx4 %[an], %[cs], off nt"],
-          11: ["global_load_dwordx4 %[an], %[cs], off offset:1024 nt"]}
-    lines += vm.get(n, [])
-    if n == 15 and pre:
-        for j in range(RA):
-            lines.append(f"ds_read_b128 %[b{j}], %[naddr] offset:{j * 1024}")
-    body_ = "\\n\\t".join(lines)
-    outs = ['[c0] "+v"(C0_)', '[c1] "+v"(C1_)'] + [f'[b{i}] "+v"(bt[{i}])' for i in range(RA)]
-    ins = ['[a0] "v"(A0_)', '[a1] "v"(A1_)', '[addr] "v"(slot_lds)']
-    args = "C0_, C1_, A0_, A1_"
-    if n in (8, 9):
-        ins += ['[qs] "v"(QS_)', '[ql] "s"(QL_)']
-        args += ", QS_, QL_"
-    elif n in (10, 11):
-        outs.append('[an] "+v"(AN_)')
-        ins.append('[cs] "v"(CS_)')
-        args += ", AN_, CS_"
-    elif n == 15 and pre:
-        ins.append('[naddr] "v"(next_lds)')
-    clob = '"memory", "m0"' if n in (8, 9) else '"memory"'
-    return (f'#define MSIL_I8_{n}{"" if pre or n != 15 else "N"}({args}) asm volatile("{body_}" : '
-            f'{", ".join(outs)} : {", ".join(ins)} : '
-            f'{clob})')
-
-
 def ms_macro(name: str, op: str, first: bool, own: bool, pre: bool, nt: bool, a2: int) -> str:
     outs = ", ".join([f'[c{m}_{n}] "+v"(acc[{m}][{n}])' for m in range(2) for n in range(16)] +
                      [f'[b{i}] "+v"(bt[{i}])' for i in range(RA)] + ['[an0] "+v"(AN0_)', '[an1] "+v"(AN1_)'])
@@ -173,19 +129,7 @@ if __name__ == "__main__":
     print(macro("HFD_STEP_N4", False, False, "v_mfma_f32_16x16x32_f16", 4))
     print(macro("HFD_STEP0_N4", True, False, "v_mfma_f32_16x16x32_f16", 4))
     print(lds_only())
-    # the first K-step of a tile with the previous tile's epilogue interleaved, pair by pair (int8)
-    for n in range(16):
-        print(il_pair(n))
-    print(il_pair(15, pre=False))  # MSIL_I8_15N: no prefetch of the next step's fragments
-    # mid-step-barrier K-steps: int8 (corpus loads nt, fragments 1 KiB apart) and bf16 / f16 (the
-    # K-step reads one half of each row's 128 B line: the first half default policy, the second nt;
-    # fragments 16 rows x 128 B = 2 KiB apart)
-    for tag, op, a2, nts in (("I8", "v_mfma_i32_16x16x64_i8", 1024, (True,)),
-                             ("BF", "v_mfma_f32_16x16x32_bf16", 2048, (False, True)),
-                             ("HF", "v_mfma_f32_16x16x32_f16", 2048, (False, True))):
-        for nt in nts:
-            pol = "" if tag == "I8" else ("_NT" if nt else "_DF")
-            for first, own, pre in ((True, True, False), (False, True, True), (False, False, True), (False, False, False),
-                                    (False, True, False)):
-                nm = f"MS_{tag}{pol}_{'F' if first else 'N'}{'O' if own else 'P'}{'P' if pre else 'N'}"
-                print(ms_macro(nm, op, first, own, pre, nt, a2))
+    # mid-step-barrier K-steps of the int8 screen (corpus loads nt, fragments 1 KiB apart)
+    for first, own, pre in ((True, True, False), (False, True, True), (False, False, True), (False, False, False)):
+        nm = f"MS_I8_{'F' if first else 'N'}{'O' if own else 'P'}{'P' if pre else 'N'}"
+        print(ms_macro(nm, "v_mfma_i32_16x16x64_i8", first, own, pre, True, 1024))

@@ -7,9 +7,9 @@ every threshold at +inf (no survivors), on the real packed query tile and on a z
   lds    -- + the query-fragment LDS reads
   mfma   -- + the 32 MFMAs per wave and K-step (no tile epilogue)
   full   -- + the epilogue's bound test (the product kernel's loop)
-  full_ms, full_msil, full_prio, full_ms_prio -- the whole loop under the mid-step-barrier schedule,
-            the same with the tile epilogue interleaved into the next tile's first K-step, static
-            priority for waves 4-7 (the schedules compared)
+  full_ms, full_prio, full_ms_prio -- the whole loop under the mid-step-barrier schedule / static
+            priority for waves 4-7 (the schedules compared; a form with the tile epilogue interleaved
+            into the next tile's first K-step was measured too and removed: profiles/r06_k1_decompose_il.log)
 Each workgroup stamps s_memtime (shader cycles) and s_memrealtime (100 MHz) around its loop, so a
 launch splits into cycles per workgroup and the clock it held.  Between rounds the product search
 runs (the same steps bench.py times), so the probes see the board in the product's thermal state.
@@ -44,7 +44,7 @@ def main() -> int:
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--heat-s", type=float, default=2.0, help="product searches before each round (s)")
-    ap.add_argument("--variants", default="loads,lds,mfma,full,full_ms,full_msil")
+    ap.add_argument("--variants", default="loads,lds,mfma,full,full_ms,full_prio,full_ms_prio")
     ap.add_argument("--native-variants", default="loads,mfma,full")
     ap.add_argument("--out", default="gpurun_out/k1_decomposition.json")
     args = ap.parse_args()

@@ -35,10 +35,16 @@ for s in ${STEPS:-decomp}; do
     cfg3) run bench_cfg3 600 python bench.py ;;
     ab3) abloop cfg3 2 --steps 20 --warmup 3 ;;
     ab3n) abloop cfg3n 2 --screen native --steps 10 --warmup 3 ;;
-    full2) VS_TEST_K1_SCHEDULE=2 run pytest_gpu_sched2 900 $PYT tests -m gpu ;;
-    direct2) VS_TEST_K1_SCHEDULE=2 run pytest_direct_sched2 600 $PYT tests/test_gpu_int8_direct.py tests/test_gpu_int8_screen.py tests/test_gpu_baseline_shapes.py -k "not cfg4_full" -m gpu ;;
-    ab12) ABS="1 2" abloop cfg3_12 2 --steps 20 --warmup 3 ;;
-    ab812) ABS="1 2" abloop shard8_12 2 --shard-of 8 --steps 30 ;;
+    ab) for i in 1 2; do for lib in $ABLIBS; do
+           VS_LIB_PATH=$lib timeout -k 10 300 python bench.py $ABARGS --no-cpu-baseline > gpurun_out/ab.tmp 2>&1
+           rc=$?; echo "$lib $(tail -1 gpurun_out/ab.tmp)" >> gpurun_out/ab_$ABNAME.txt
+           if [ $rc -ne 0 ]; then cp gpurun_out/ab.tmp gpurun_out/ab_${ABNAME}_fail.log; echo "step ab rc=$rc" >> gpurun_out/steps.log; exit $rc; fi
+         done; done; echo "step ab rc=0" >> gpurun_out/steps.log ;;
+    trace8) mkdir -p gpurun_out/trace8 && run trace8 300 rocprofv3 --kernel-trace -d gpurun_out/trace8 -o t --output-format csv -- python bench.py --shard-of 8 --steps 10 --warmup 3 --no-cpu-baseline && \
+      python scripts/trace_tail.py $(ls gpurun_out/trace8/*/t_kernel_trace.csv gpurun_out/trace8/t_kernel_trace.csv 2>/dev/null | head -1) 80 "vs::|copyBuffer|nccl|rccl|Kernel" > gpurun_out/trace8_tail.txt && rm -rf gpurun_out/trace8 ;;
+    trace3) mkdir -p gpurun_out/trace3 && run trace3 300 rocprofv3 --kernel-trace -d gpurun_out/trace3 -o t --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline && \
+      python scripts/trace_tail.py $(ls gpurun_out/trace3/*/t_kernel_trace.csv gpurun_out/trace3/t_kernel_trace.csv 2>/dev/null | head -1) 60 "vs::|copyBuffer|Kernel" > gpurun_out/trace3_tail.txt && rm -rf gpurun_out/trace3 ;;
+    full0) VS_TEST_K1_SCHEDULE=0 run pytest_gpu_sched0 900 $PYT tests -m gpu ;;
     ab8) abloop shard8 2 --shard-of 8 --steps 30 ;;
     shard8) run bench_shard8 300 python bench.py --shard-of 8 --steps 30 --no-cpu-baseline ;;
     cfg2) run bench_cfg2 300 python bench.py --workload cfg2 --no-cpu-baseline ;;
