@@ -470,7 +470,10 @@ def _kernel_name(kind: str, dtype: str, d: int, n_local: int = 0, metric: str = 
     if kind == "full_scan":
         return "k_full_scan"
     if kind == "mfma_i8" and dpad % 256 == 0 and dpad >= 512:
-        return "k_screen_i8d_res" if residual and metric == "ip" else "k_screen_i8d"
+        if residual and metric == "ip":
+            return "k_screen_i8d_res"
+        from photo_search_engine_amd.index import k1_schedule  # (inner product: the mid-step form)
+        return "k_screen_i8d_ms" if metric == "ip" and k1_schedule() == 1 else "k_screen_i8d"
     if kind == "mfma" and dtype in ("bf16", "f16") and dpad % 128 == 0 and dpad >= 256:
         return "k_screen_d16"
     return f"k_screen_{kind}"

@@ -729,7 +729,10 @@ __global__ void __launch_bounds__(256) k_screen_gemv(ScreenArgs a, const float* 
 #pragma unroll
                 for (int qi = 0; qi < NQ; ++qi) acc[r][qi] = 0.0f;
             }
-#pragma unroll 2
+            // (int8: 4 chunks per unrolled pass keep twice the loads in flight of the 64 B row
+            // pieces: cfg2 GEMV 0.2834 -> 0.2806 ms, profiles/r06_ab_cfg2_gemv.txt)
+            constexpr int CU = I8 ? 4 : 2;
+#pragma unroll CU
             for (int c = 0; c < nch; ++c) {
                 float qv[NQ][EPU];
 #pragma unroll

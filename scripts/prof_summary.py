@@ -83,7 +83,8 @@ def main():
         summary["kernels"][f"{name} grid={grid}"] = flat
     # the bench's dominant screen (its roofline kernel; the seed pass's <.., true> variant excluded)
     kind = (bench_line or {}).get("roofline", {}).get("kernel", "")
-    pat = {"k_screen_i8d": ("k_screen_i8d",), "k_screen_mfma_i8": ("k_screen_mfma<3,", "k_screen_i8d"),
+    pat = {"k_screen_i8d": ("k_screen_i8d",), "k_screen_i8d_ms": ("k_screen_i8d_ms",),
+           "k_screen_mfma_i8": ("k_screen_mfma<3,", "k_screen_i8d"),
            "k_screen_mfma": ("k_screen_mfma<",), "k_screen_gemv_i8": ("k_screen_gemv<3,",),
            "k_screen_gemv": ("k_screen_gemv<",)}
     screens = {k: v for k, v in summary["kernels"].items()
@@ -101,7 +102,7 @@ def main():
                    "profiled_kernel_ms": t["dur_s"] * 1e3, "clock_ghz": t.get("clock_ghz"),
                    "source": f"profiles/{tag}_pmc.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes)"}
         suffix = "" if cfg["n_local"] == cfg.get("N") else f"_n{cfg['n_local']}"
-        kname = {"k_screen_i8d": "k_screen_mfma_i8"}.get(kind, kind)  # (the bench's traffic lookup key)
+        kname = {"k_screen_i8d": "k_screen_mfma_i8", "k_screen_i8d_ms": "k_screen_mfma_i8"}.get(kind, kind)  # (the bench's traffic lookup key)
         with open(os.path.join(prof, f"traffic_{cfg['workload']}_{kname.replace('k_screen_', '')}{suffix}.json"), "w") as f:
             json.dump(traffic, f, indent=1)
         summary["dominant"] = traffic

@@ -48,6 +48,15 @@ for s in ${STEPS:-decomp}; do
     ab8) abloop shard8 2 --shard-of 8 --steps 30 ;;
     shard8) run bench_shard8 300 python bench.py --shard-of 8 --steps 30 --no-cpu-baseline ;;
     cfg2) run bench_cfg2 300 python bench.py --workload cfg2 --no-cpu-baseline ;;
+    cfg1) run bench_cfg1 300 python bench.py --workload cfg1 --steps 1000 --warmup 50 ;;
+    shard2) run bench_shard2 300 python bench.py --shard-of 2 --steps 20 --no-cpu-baseline ;;
+    shard4) run bench_shard4 300 python bench.py --shard-of 4 --steps 30 --no-cpu-baseline ;;
+    cfg5skew) run bench_cfg5_skew 900 python bench.py --workload cfg5 --skew 1.1 --steps 10 --warmup 2 ;;
+    cfg4) run bench_cfg4 900 python bench.py --workload cfg4 --steps 10 --warmup 3 --no-cpu-baseline ;;
+    mix10) run bench_mix10 600 python bench.py --data mixture-sorted --sigma 1.0 --warmup 8 --no-cpu-baseline ;;
+    mix05) run bench_mix05 600 python bench.py --data mixture-sorted --sigma 0.5 --warmup 8 --no-cpu-baseline ;;
+    profcfg3) TAG=${PTAG:-r06_final_cfg3} ARGS="--steps 20 --warmup 3 --no-cpu-baseline" PASSES=sq timeout -k 10 1100 bash scripts/gpu_prof.sh > gpurun_out/prof_cfg3.log 2>&1
+      rc=$?; echo "step profcfg3 rc=$rc" >> gpurun_out/steps.log; if fatal $rc || [ $rc -ne 0 ]; then exit $rc; fi ;;
     prof3) mkdir -p gpurun_out/prof3 && run prof3 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof3 -o run --output-format csv -- python bench.py --steps 30 --warmup 1 --no-cpu-baseline ;;
     *) echo "unknown step $s" >> gpurun_out/steps.log; exit 2 ;;
   esac
