@@ -454,7 +454,7 @@ double i8_union_target(int k, double sampled, double n) {
 // returns its arguments in *keep for vs_search_device_phase_b
 void search_block_i8(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float* D, int64_t* I, double* S64,
                      int* cert, int64_t id_offset, hipStream_t st, int phase = 0, int KA1 = 0,
-                     RefineArgs* keep = nullptr, int ostride = 1, bool prepack = false) {
+                     RefineArgs* keep = nullptr, int ostride = 1, bool prepack = false, int kwin = 0) {
     const int64_t tiles = (ix->ntotal + TR - 1) / TR;
     ScreenArgs a{};
     a.corpus = ix->data8;
@@ -515,7 +515,7 @@ void search_block_i8(vs_index* ix, Ctx* c, const float* q, int nqb, int k, float
     a.gcnt = c->gcnt.as<int>();
     a.thr0 = nullptr;
     auto seed_rank_of = [&](double sampled, int M) {
-        double target = i8_union_target(k, sampled, (double)ix->ntotal);
+        double target = i8_union_target(kwin > 0 ? kwin : k, sampled, (double)ix->ntotal);
         {
             std::lock_guard<std::mutex> g(ix->h_mu);
             target *= (double)(1 << ix->i8_log2);
@@ -1162,8 +1162,11 @@ vs_pending* vs::search_phase_a(vs_index* ix, const float* q_dev, int64_t nq, int
         // lists together hold the global k-th best of what they scored
         const int share = (k + world - 1) / world;
         p->ka = (int)std::min<int64_t>(round_up(2 * k + 24, 8), round_up(2 * share + 24, 8));
+        // the seed's union covers this shard's share of the global window: phase B certifies the
+        // unlisted rows against the global floor (~ the global k-th best), and the shard's rows
+        // within the int8 error budget of it are ~1/world of the whole window (iid shards)
         search_block_i8(ix, c, q_dev, (int)nq, k, nullptr, I_a, S_a, c->cert.as<int>(), id_offset, st, 1, p->ka,
-                        &p->r, stride, true);
+                        &p->r, stride, true, share);
     } else {
         c->outS.ensure((size_t)nq * k * sizeof(double));
         c->outI.ensure((size_t)nq * k * sizeof(int64_t));

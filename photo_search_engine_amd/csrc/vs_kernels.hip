@@ -495,11 +495,14 @@ __global__ void __launch_bounds__(256) k_pack_qtile_i8(const float* __restrict__
                                                         int* __restrict__ gcnt, u64* __restrict__ drop,
                                                         int* __restrict__ fails, const unsigned* __restrict__ l2max,
                                                         float gamma, NativeTile nat) {
-    const int lane = threadIdx.x & 63;
-    const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (r >= MFMA_QB) return;
-    if (fails && r == 0 && lane == 0) fails[0] = fails[1] = 0;
-    if (lane == 0) {
+    // one workgroup per query (256 threads over its d elements; a query's pack is a chain of
+    // reductions, so 4x the waves per query shorten the launch)
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int r = blockIdx.x;
+    __shared__ float s_mx[4];
+    __shared__ double s_red[4][5];
+    if (fails && r == 0 && tid == 0) fails[0] = fails[1] = 0;
+    if (tid == 0) {
         gcnt[r] = 0;
         drop[r] = 0ull;
         if constexpr (NDT != 0) {
@@ -508,24 +511,27 @@ __global__ void __launch_bounds__(256) k_pack_qtile_i8(const float* __restrict__
         }
     }
     // The codes need not be the nearest (the error norm below is measured from the codes chosen), so
-    // v * (1 / t) replaces the division; d <= 2048 (the common case): the lane's values are loaded
-    // once, in one burst, and kept in registers for the second pass.
-    constexpr int PL = 32;
+    // v * (1 / t) replaces the division; d <= 2048 (the common case): the thread's values are loaded
+    // once and kept in registers for the second pass.
+    constexpr int PL = 8;
     float vv[PL];
     float mx = 0.0f;
-    const bool cached = dpad8 <= 64 * PL;
+    const bool cached = dpad8 <= 256 * PL && (NDT == 0 || nat.dpad <= 256 * PL);
     if (cached) {
 #pragma unroll
         for (int j = 0; j < PL; ++j) {
-            const int i = lane + 64 * j;
+            const int i = tid + 256 * j;
             vv[j] = (r < nqb && i < d) ? q[(int64_t)r * d + i] : 0.0f;
             mx = fmaxf(mx, fabsf(vv[j]));
         }
     } else if (r < nqb) {
-        for (int i = lane; i < d; i += 64) mx = fmaxf(mx, fabsf(q[(int64_t)r * d + i]));
+        for (int i = tid; i < d; i += 256) mx = fmaxf(mx, fabsf(q[(int64_t)r * d + i]));
     }
 #pragma unroll
     for (int s = 32; s > 0; s >>= 1) mx = fmaxf(mx, __shfl_xor(mx, s, 64));
+    if (lane == 0) s_mx[w] = mx;
+    __syncthreads();
+    mx = fmaxf(fmaxf(s_mx[0], s_mx[1]), fmaxf(s_mx[2], s_mx[3]));
     const float t = mx / 127.0f;
     const float inv = t > 0.0f ? 1.0f / t : 0.0f;
     double e2 = 0.0, n2 = 0.0, c2 = 0.0;
@@ -540,40 +546,51 @@ __global__ void __launch_bounds__(256) k_pack_qtile_i8(const float* __restrict__
     if (cached) {
 #pragma unroll
         for (int j = 0; j < PL; ++j) {
-            const int i = lane + 64 * j;
+            const int i = tid + 256 * j;
             if (i < dpad8) one(i, vv[j]);
         }
     } else {
-        for (int i = lane; i < dpad8; i += 64) one(i, (r < nqb && i < d) ? q[(int64_t)r * d + i] : 0.0f);
+        for (int i = tid; i < dpad8; i += 256) one(i, (r < nqb && i < d) ? q[(int64_t)r * d + i] : 0.0f);
     }
+    double n2n = 0.0, e2n = 0.0;
     if constexpr (NDT != 0) {  // the native tile (k_pack_qtile<NDT>'s layout and qinfo)
-        double n2n = 0.0, e2n = 0.0;
         auto nat_one = [&](int i, float v) {
             const float st = round_store<NDT>(v, nat.qt + (int64_t)(i >> 5) * MFMA_QB * 64 + (int64_t)r * 64 + (i & 31) * 2);
             n2n += (double)st * st;
             const double df = (double)st - (double)v;
             e2n += df * df;
         };
-        if (cached && nat.dpad <= 64 * PL) {
+        if (cached) {
 #pragma unroll
             for (int j = 0; j < PL; ++j) {
-                const int i = lane + 64 * j;
+                const int i = tid + 256 * j;
                 if (i < nat.dpad) nat_one(i, i < d ? vv[j] : 0.0f);
             }
         } else {
-            for (int i = lane; i < nat.dpad; i += 64) nat_one(i, (r < nqb && i < d) ? q[(int64_t)r * d + i] : 0.0f);
+            for (int i = tid; i < nat.dpad; i += 256) nat_one(i, (r < nqb && i < d) ? q[(int64_t)r * d + i] : 0.0f);
         }
-        n2n = wave_sum_f64(n2n);
-        e2n = wave_sum_f64(e2n);
-        if (lane == 0 && r < nqb) {
+    }
+    {  // the five sums over the workgroup (fp64), finished by thread 0
+        const double v5[5] = {wave_sum_f64(e2), wave_sum_f64(n2), wave_sum_f64(c2), wave_sum_f64(n2n),
+                              wave_sum_f64(e2n)};
+        if (lane == 0)
+#pragma unroll
+            for (int j = 0; j < 5; ++j) s_red[w][j] = v5[j];
+        __syncthreads();
+        if (tid != 0) return;
+        e2 = s_red[0][0] + s_red[1][0] + s_red[2][0] + s_red[3][0];
+        n2 = s_red[0][1] + s_red[1][1] + s_red[2][1] + s_red[3][1];
+        c2 = s_red[0][2] + s_red[1][2] + s_red[2][2] + s_red[3][2];
+        n2n = s_red[0][3] + s_red[1][3] + s_red[2][3] + s_red[3][3];
+        e2n = s_red[0][4] + s_red[1][4] + s_red[2][4] + s_red[3][4];
+    }
+    if constexpr (NDT != 0) {
+        if (r < nqb) {
             nat.qinfo[2 * r] = (float)(sqrt(n2n) * (1.0 + 1e-6)) + 1e-30f;
             nat.qinfo[2 * r + 1] = (float)(sqrt(e2n) * (1.0 + 1e-6));
         }
     }
-    e2 = wave_sum_f64(e2);
-    n2 = wave_sum_f64(n2);
-    c2 = wave_sum_f64(c2);
-    if (lane == 0 && r < nqb) {
+    if (r < nqb) {
         const float qn = f32_up(sqrt(n2) * (1.0 + 1e-9));
         const double eq = sqrt(e2) * (1.0 + 1e-9);
         const double qh = sqrt(c2) * (double)t * (1.0 + 1e-9);  // ||t_q c_q||
@@ -649,6 +666,9 @@ bool d16_direct_ok(int dpad) { return dpad % (CH * I8D_U) == 0 && dpad >= 2 * CH
 // (inner product; the seed pass adds the same terms to its maxima)
 __global__ void __launch_bounds__(512, 2) k_screen_i8d_res(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
     screen_direct<DT_I8, METRIC_IP, false, 16, true>(a, qt, nqb);
+}
+__global__ void __launch_bounds__(512, 2) k_screen_i8d_res_ms(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
+    screen_direct<DT_I8, METRIC_IP, false, 16, true, PR_NONE, 1>(a, qt, nqb);
 }
 
 
@@ -2098,16 +2118,16 @@ hipError_t launch_pack_qtile_i8(const float* q, int nqb, int d, int dpad8, uint8
                                 const unsigned* l2max, float gamma, const NativeTile* nat) {
     const NativeTile none{};
     if (!nat) {
-        hipLaunchKernelGGL(k_pack_qtile_i8<0>, dim3(MFMA_QB / 4), dim3(256), 0, st, q, nqb, d, dpad8, qt, qfac, qeps,
+        hipLaunchKernelGGL(k_pack_qtile_i8<0>, dim3(MFMA_QB), dim3(256), 0, st, q, nqb, d, dpad8, qt, qfac, qeps,
                            maxes, gcnt, drop, fails, l2max, gamma, none);
         return hipGetLastError();
     }
     if (!nat->qt || !nat->qinfo || !nat->gcnt || !nat->drop || nat->dpad % 32 != 0) return hipErrorInvalidValue;
     if (nat->dt == DT_BF16)
-        hipLaunchKernelGGL(k_pack_qtile_i8<DT_BF16>, dim3(MFMA_QB / 4), dim3(256), 0, st, q, nqb, d, dpad8, qt, qfac,
+        hipLaunchKernelGGL(k_pack_qtile_i8<DT_BF16>, dim3(MFMA_QB), dim3(256), 0, st, q, nqb, d, dpad8, qt, qfac,
                            qeps, maxes, gcnt, drop, fails, l2max, gamma, *nat);
     else if (nat->dt == DT_F16)
-        hipLaunchKernelGGL(k_pack_qtile_i8<DT_F16>, dim3(MFMA_QB / 4), dim3(256), 0, st, q, nqb, d, dpad8, qt, qfac,
+        hipLaunchKernelGGL(k_pack_qtile_i8<DT_F16>, dim3(MFMA_QB), dim3(256), 0, st, q, nqb, d, dpad8, qt, qfac,
                            qeps, maxes, gcnt, drop, fails, l2max, gamma, *nat);
     else
         return hipErrorInvalidValue;
@@ -2157,8 +2177,9 @@ static hipError_t launch_mfma_dt(int dt, const ScreenArgs& a, const uint8_t* qt,
             if (a.seed_acc || a.tile_stride != 0) return hipErrorInvalidValue;
             if (a.gT) {  // group residuals (inner product)
                 if (a.metric != METRIC_IP) return hipErrorInvalidValue;
-                set_lds_attr((const void*)k_screen_i8d_res, I8D_LDS + I8D_RES_LDS);
-                hipLaunchKernelGGL(k_screen_i8d_res, dim3(a.G), dim3(MF_THREADS), I8D_LDS + I8D_RES_LDS, st, a, qt, nqb);
+                void (*rf)(ScreenArgs, const uint8_t*, int) = k1_schedule() == 1 ? k_screen_i8d_res_ms : k_screen_i8d_res;
+                set_lds_attr((const void*)rf, I8D_LDS + I8D_RES_LDS);
+                hipLaunchKernelGGL(rf, dim3(a.G), dim3(MF_THREADS), I8D_LDS + I8D_RES_LDS, st, a, qt, nqb);
                 return hipGetLastError();
             }
             // (the L2 form keeps the head barrier: under the mid-step schedule its ||x||^2 state

@@ -769,7 +769,7 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
     static_assert(!(MAP && I8), "the mapped scan serves bf16 / f16 lists");
     static_assert(!RES || (I8 && !MAP && !L2), "group residuals: the int8 flat inner-product main pass");
     static_assert(NG == 16 || (NG == 4 && MAP), "narrow query tiles: mapped scans only");
-    static_assert(SCHED == 0 || (I8 && !MAP && !RES && NG == 16), "the mid-step barrier: int8 flat shards");
+    static_assert(SCHED == 0 || (I8 && !MAP && NG == 16), "the mid-step barrier: int8 flat shards");
     static_assert(SCHED == 0 || PROBE == PR_NONE || PROBE == PR_FULL, "the mid-step barrier: whole-loop probes");
     constexpr bool EPI = PROBE == PR_NONE || PROBE == PR_FULL;  // the tile epilogue runs
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -998,8 +998,13 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
     };
     auto ms_prep = [&](int set) -> MsIssue {
         MsIssue r;
-        if ((I8 || L2) && iks == nks - 1 && iti < t1)
-            glds4(side_src + pg * TR + lane, __builtin_amdgcn_readfirstlane(side_dst + (uint32_t)((iti & 1) * 1024)));
+        if ((I8 || L2) && iks == nks - 1 && iti < t1) {  // (as I8D_ISSUE)
+            if (!t_wave)
+                glds4(side_src + pg * TR + lane, __builtin_amdgcn_readfirstlane(side_dst + (uint32_t)((iti & 1) * 1024)));
+            else
+                glds4(side_src + ((iti + 1 < t1 ? phys(iti + 1) : pg) * TR / I8_GROUP_ROWS) * MFMA_QB + lane,
+                      __builtin_amdgcn_readfirstlane(side_dst + (uint32_t)(((iti + 1) & 1) * 1024)));
+        }
         const uint32_t qbase = __builtin_amdgcn_readfirstlane(ring + (uint32_t)(set * 16384 + wid * 1024));
         r.ql0 = qbase;
         r.ql1 = __builtin_amdgcn_readfirstlane(qbase + 8192u);
@@ -1042,6 +1047,11 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
             if (check_pending) {
                 check_pending = false;
                 compaction_check(ti);
+            }
+            if constexpr (RES) {  // this tile's <mu_g, q> into qrec .w (every wave is past step 0's
+                int otid;         // barrier: done with the previous tile's epilogue)
+                asm volatile("v_mov_b32 %0, %1" : "=v"(otid) : "v"(tid));
+                if (otid < MFMA_QB) qrec[otid].w = tlds[(ti & 1) * MFMA_QB + otid];
             }
             I8D_MS(1, MS_NOP);
             I8D_MS(2, MS_NPP);
@@ -1280,7 +1290,7 @@ template <int DT, int METRIC>
 __global__ void __launch_bounds__(512, 2) k_screen_d16(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
     screen_direct<DT, METRIC>(a, qt, nqb);
 }
-// the int8 main pass under the mid-step-barrier schedule (SCHED 1; vs_set_k1_schedule)
+// the int8 main passes under the mid-step-barrier schedule (SCHED 1; vs_set_k1_schedule)
 template <int METRIC>
 __global__ void __launch_bounds__(512, 2) k_screen_i8d_ms(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
     screen_direct<DT_I8, METRIC, false, 16, false, PR_NONE, 1>(a, qt, nqb);

@@ -44,6 +44,7 @@ for s in ${STEPS:-decomp}; do
       python scripts/trace_tail.py $(ls gpurun_out/trace8/*/t_kernel_trace.csv gpurun_out/trace8/t_kernel_trace.csv 2>/dev/null | head -1) 80 "vs::|copyBuffer|nccl|rccl|Kernel" > gpurun_out/trace8_tail.txt && rm -rf gpurun_out/trace8 ;;
     trace3) mkdir -p gpurun_out/trace3 && run trace3 300 rocprofv3 --kernel-trace -d gpurun_out/trace3 -o t --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline && \
       python scripts/trace_tail.py $(ls gpurun_out/trace3/*/t_kernel_trace.csv gpurun_out/trace3/t_kernel_trace.csv 2>/dev/null | head -1) 60 "vs::|copyBuffer|Kernel" > gpurun_out/trace3_tail.txt && rm -rf gpurun_out/trace3 ;;
+    dist) run pytest_dist 600 $PYT tests/test_gpu_distributed.py tests/test_gpu_multi_device.py tests/test_gpu_int8_direct.py tests/test_gpu_int8_clustered.py -m gpu ;;
     full0) VS_TEST_K1_SCHEDULE=0 run pytest_gpu_sched0 900 $PYT tests -m gpu ;;
     ab8) abloop shard8 2 --shard-of 8 --steps 30 ;;
     shard8) run bench_shard8 300 python bench.py --shard-of 8 --steps 30 --no-cpu-baseline ;;
