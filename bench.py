@@ -81,6 +81,8 @@ def parse():
     ap.add_argument("--no-recall", action="store_true", help="cfg5: skip the exact ground truth (profiling runs)")
     ap.add_argument("--skew", type=float, default=0.0,
                     help="cfg5: Zipf exponent of the cluster sizes (0 = equal-sized clusters; 1.1 = a heavy head)")
+    ap.add_argument("--ivf-qtile", default="split", choices=["plain", "split"],
+                    help="cfg5: query tiles of the MFMA list scans' first pass (the other mode runs beside)")
     ap.add_argument("--ivf-scan", default="auto", choices=["auto", "gemv", "mfma"],
                     help="cfg5: list-scan kernels (auto: MFMA screen for lists probed by many queries; "
                          "with auto the GEMV-only scan is timed too and reported beside it)")
@@ -470,10 +472,11 @@ def _kernel_name(kind: str, dtype: str, d: int, n_local: int = 0, metric: str = 
     if kind == "full_scan":
         return "k_full_scan"
     if kind == "mfma_i8" and dpad % 256 == 0 and dpad >= 512:
+        from photo_search_engine_amd.index import k1_schedule  # (inner product: the mid-step forms)
+        ms = "_ms" if metric == "ip" and k1_schedule() == 1 else ""
         if residual and metric == "ip":
-            return "k_screen_i8d_res"
-        from photo_search_engine_amd.index import k1_schedule  # (inner product: the mid-step form)
-        return "k_screen_i8d_ms" if metric == "ip" and k1_schedule() == 1 else "k_screen_i8d"
+            return "k_screen_i8d_res" + ms
+        return "k_screen_i8d" + ms
     if kind == "mfma" and dtype in ("bf16", "f16") and dpad % 128 == 0 and dpad >= 256:
         return "k_screen_d16"
     return f"k_screen_{kind}"
@@ -823,6 +826,7 @@ def run_ivf(args):
         ix.search_device(q.data_ptr(), nq, k, D.data_ptr(), I.data_ptr(), S.data_ptr(), nprobe, stream)
 
     ix.set_scan(args.ivf_scan)
+    ix.set_query_tiles(args.ivf_qtile)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -861,6 +865,27 @@ def run_ivf(args):
                        "identical_results": bool(np.array_equal(I.cpu().numpy(), Ig) and
                                                  np.array_equal(S.cpu().numpy(), Sg0))}
         ix.set_scan(args.ivf_scan)
+    qtile_beside = None
+    if mfma_lists > 0:  # the other query-tile mode of the MFMA list scans on the same batch, beside
+        Sg0 = S.cpu().numpy()
+        other = "split" if args.ivf_qtile == "plain" else "plain"
+        ix.set_query_tiles(other)
+        step()
+        torch.cuda.synchronize()
+        ix.set_timing(True)
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        el1 = time.perf_counter() - t1
+        ix.set_timing(False)
+        kms1, _ = ix.timing_fetch()
+        qtile_beside = {"qtile": other, "ms_per_step": round(el1 * 1e3 / args.steps, 4),
+                        "scan_ms": round(float(np.mean(kms1)), 4),
+                        "uncertified_first_pass": ix.last_search_detail()[1],
+                        "identical_results": bool(np.array_equal(I.cpu().numpy(), Ig) and
+                                                  np.array_equal(S.cpu().numpy(), Sg0))}
+        ix.set_query_tiles(args.ivf_qtile)
 
     # probes (exact coarse top-nprobe) and per-batch scan volume, for the CPU baseline
     cf = FlatIndex(d, "ip", dtype, device=0)
@@ -947,7 +972,7 @@ def run_ivf(args):
         "config": {"workload": args.workload, "desc": desc, "N": N, "d": d, "batch": nq, "k": k, "nlist": nlist,
                    "nprobe": nprobe, "list_rows_min_max": [int(sizes.min()), int(sizes.max())],
                    "list_rows_median": int(np.median(sizes)), "skew": args.skew,
-                   "list_scan": args.ivf_scan, "mfma_list_scans": mfma_lists,
+                   "list_scan": args.ivf_scan, "mfma_query_tiles": args.ivf_qtile, "mfma_list_scans": mfma_lists,
                    "scan_bytes_read": {"mfma": mfma_bytes, "gemv": gemv_bytes},
                    "parallelism": "1 GPU"},
         "roofline": {
@@ -963,6 +988,7 @@ def run_ivf(args):
         },
         "uncertified_first_pass": uncert,
         "gemv_scan": gemv_beside,
+        "mfma_query_tiles_beside": qtile_beside,
         "build_s": round(t_build, 2),
         "recall@10": round(hit / (nq * 10.0), 6) if parts_S else None,
         "probed_recall@10": round(got / max(need, 1), 6) if parts_S else None,

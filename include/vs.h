@@ -309,6 +309,16 @@ int vs_ivf_timing_fetch(vs_ivf* ivf, float* ms, double* bytes_scanned, int cap);
 #define VS_IVF_SCAN_GEMV 1
 #define VS_IVF_SCAN_MFMA 2
 int vs_ivf_set_scan(vs_ivf* ivf, int mode);
+/* Query tiles of the MFMA list scans' first pass (results are identical either way):
+ * VS_IVF_QTILE_SPLIT (default) packs (hi, lo) parts of each query (128 queries a tile, two MFMA
+ * columns per query); VS_IVF_QTILE_PLAIN packs each query once, rounded to the list dtype (256
+ * queries a tile; lists probed by <= 64 queries take the narrow 64-column form), its ~2^8 x wider
+ * rounding margin taken by the certificate, so more queries may need a re-search.  Re-search
+ * rounds always pack split tiles; plain tiles need the direct form (padded dim a multiple of 128),
+ * otherwise split tiles are used. */
+#define VS_IVF_QTILE_PLAIN 0
+#define VS_IVF_QTILE_SPLIT 1
+int vs_ivf_set_query_tiles(vs_ivf* ivf, int mode);
 int vs_ivf_last_search_stats(const vs_ivf* ivf, int* mfma_lists, int* uncertified, double* bytes_read);
 
 /* ==== HNSW graph search ===================================================

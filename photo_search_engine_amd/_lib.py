@@ -131,6 +131,7 @@ _SIGS = {
     "vs_ivf_set_timing": (ctypes.c_int, [_vp, ctypes.c_int]),
     "vs_ivf_timing_fetch": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int]),
     "vs_ivf_set_scan": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "vs_ivf_set_query_tiles": (ctypes.c_int, [_vp, ctypes.c_int]),
     "vs_ivf_last_search_stats": (ctypes.c_int, [_vp, _vp, _vp, _vp]),
     # HNSW graph search
     "vs_hnsw_create": (ctypes.c_int, [_vp, _c_i64, _vp, _vp, _vp, _vp, ctypes.c_int32, ctypes.c_int32,

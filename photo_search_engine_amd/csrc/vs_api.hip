@@ -146,6 +146,8 @@ struct vs_index {
     hipEvent_t h_ev = nullptr;
     int h_pending = 0;          // 0 none, 1 int8 batch, 2 native batch in flight
     int h_nq = 0;               // queries of that batch
+    int h_clean = 0;            // consecutive clean readbacks (past kHealthCleanRun: every kHealthStride-th batch read)
+    unsigned h_seq = 0;         // batches noted since
     int i8_route = 0;           // searches still routed to the native screen
     int seed_log2 = 0, seed_clean = 0;
     int i8_log2 = 0, i8_clean = 0;  // int8 union depth: 2^i8_log2 times the target (dense corpora)
@@ -380,6 +382,7 @@ void health_poll(vs_index* ix) {
             --ix->seed_log2;
             ix->seed_clean = 0;
         }
+        ix->h_clean = f > 0 ? 0 : ix->h_clean + 1;
         ix->h_pending = 0;
     }
     (void)hipGetLastError();  // (hipEventQuery's "not ready" is no error)
@@ -403,9 +406,14 @@ double seed_scale(vs_index* ix) {
 }
 // after a first-pass batch (kind 1 int8, 2 native): read its failure count back behind it on the
 // stream (one readback in flight per index)
+// A long clean run reads back only every kHealthStride-th batch (a readback is a copy launch and ~10
+// us of the 8-shard step); the first failing readback returns to every batch.
+constexpr int kHealthCleanRun = 16;
+constexpr unsigned kHealthStride = 4;
 void health_note(vs_index* ix, Ctx* c, hipStream_t st, int kind, int nq) {
     std::lock_guard<std::mutex> g(ix->h_mu);
     if (ix->h_pending) return;
+    if (ix->h_clean >= kHealthCleanRun && (++ix->h_seq % kHealthStride) != 0) return;
     if (!ix->h_fails) {
         HIP_CHECK(hipHostMalloc((void**)&ix->h_fails, sizeof(unsigned), hipHostMallocDefault));
         HIP_CHECK(hipEventCreateWithFlags(&ix->h_ev, hipEventDisableTiming));

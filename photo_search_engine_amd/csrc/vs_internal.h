@@ -262,16 +262,17 @@ bool i8_direct_ok(int dpad8);
 bool d16_direct_ok(int dpad);
 // the same screen over pages of a page pool (IVF lists; bf16 / f16, unseeded, a.Kp <= MFMA_KP_MAX):
 // a.G workgroups, each with its own descriptor (a.wg_desc): <= MFMA_MAP_TILES pages of one list
-// (a.tile_map), one split query tile of <= 128 queries (qt + index * MFMA_QB * dpad * 2, made by
-// launch_pack_qtile_split); survivors appended to glist rows a.qmap[...].  Descriptors are
-// validated on the host (check_map_desc) before the launch.
-hipError_t launch_screen_mfma_mapped(int dt, const ScreenArgs& a, const uint8_t* qt, hipStream_t st);
+// (a.tile_map), one query tile of <= 128 split queries or <= 256 plain ones (qt + index * MFMA_QB *
+// dpad * 2, made by launch_pack_qtile_split); survivors appended to glist rows a.qmap[...].
+// Descriptors are validated on the host (check_map_desc) before the launch.  plain: the direct
+// form only (d16_direct_ok).
+hipError_t launch_screen_mfma_mapped(int dt, const ScreenArgs& a, const uint8_t* qt, bool plain, hipStream_t st);
 // host check of one descriptor against the launch (tile map length, query tiles, qmap length)
-bool check_map_desc(const int* desc, int64_t tmap_len, int n_qtiles, int64_t qmap_len);
-// every split query tile of the launch at once: tile y packs the sinfo[2y + 1] (1..128) queries
-// qidx[sinfo[2y] ..] of q (host-checked by the caller)
+bool check_map_desc(const int* desc, int64_t tmap_len, int n_qtiles, int64_t qmap_len, bool plain);
+// every query tile of the launch at once: tile y packs the sinfo[2y + 1] (1..128 split, 1..256
+// plain) queries qidx[sinfo[2y] ..] of q (host-checked by the caller)
 hipError_t launch_pack_qtile_split(int dt, const float* q, const int* qidx, const int* sinfo, int ntiles, int d,
-                                   int dpad, uint8_t* qt, float* qinfo, hipStream_t st);
+                                   int dpad, uint8_t* qt, float* qinfo, bool plain, hipStream_t st);
 hipError_t launch_screen_gemv(int dt, const ScreenArgs& a, const float* qp, int nqb, int nqpad, hipStream_t st);
 
 // one merge stage: in[(s*qstride + q)*Kp + j], s < nseg  ->  out[(b*nq + q)*Kp + j]

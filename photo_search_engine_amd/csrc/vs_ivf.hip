@@ -54,6 +54,7 @@ struct vs_ivf {
     int n_mdesc = 0;          // per query tile (offset into mqidx, queries)
     DevBuf rq, rD, rI, rS;  // re-search of uncertified queries: gathered queries and their outputs  // MFMA list scans: query indices, query tile, workspaces
     int scan_mode = VS_IVF_SCAN_AUTO;
+    int qtile_mode = VS_IVF_QTILE_SPLIT;  // MFMA list scans' first-pass query tiles
     int last_mfma_lists = 0;  // first pass of the last search: MFMA list scans ...
     int last_uncert = 0;      // ... and queries its certificate rejected (re-searched deeper)
     int cur_mfma_lists = 0;
@@ -81,15 +82,15 @@ void check_ivf(const vs_ivf* ix) {
 }
 
 // A list probed by nql queries costs the GEMV scan ceil(nql / IVF_QG) reads of its pages (items of
-// <= 8 queries, each re-reading the list from HBM); the MFMA screen reads them once per 128
-// queries (split query tiles), in the one launch shared by all MFMA scans.  Rates measured on
-// MI355X: GEMV scan ~76% of HBM peak on evenly probed lists, bf16 MFMA screen ~50%.
-bool mfma_scan_pays(const vs_ivf* ix, int64_t np, int nql) {
+// <= 8 queries, each re-reading the list from HBM); the MFMA screen reads them once per query tile
+// (qb = 128 split or 256 plain queries), in the one launch shared by all MFMA scans.  Rates
+// measured on MI355X: GEMV scan ~76% of HBM peak on evenly probed lists, bf16 MFMA screen ~50%.
+bool mfma_scan_pays(const vs_ivf* ix, int64_t np, int nql, int qb) {
     if (ix->dtype == DT_F32 || nql <= 1 || ix->scan_mode == VS_IVF_SCAN_GEMV) return false;
     if (ix->scan_mode == VS_IVF_SCAN_MFMA) return true;
     const double B = (double)tile_bytes(ix->dpad, ix->dtype);
     const double t_gemv = (double)((nql + IVF_QG - 1) / IVF_QG) * (double)np * B / 6.0e12;
-    const double t_mfma = (double)((nql + MFMA_QB / 2 - 1) / (MFMA_QB / 2)) * (double)np * B / 4.0e12;
+    const double t_mfma = (double)((nql + qb - 1) / qb) * (double)np * B / 4.0e12;
     return t_mfma < t_gemv;
 }
 
@@ -258,20 +259,27 @@ void search_core(vs_ivf* ix, const float* q_dev, int64_t nq, int k, int nprobe, 
     std::vector<int> cls_items[4];
     std::vector<int64_t> per_q((size_t)nq, 0);  // candidate keys each query's list can receive
     double bytes = 0.0;
-    // MFMA list scans: one split query tile (<= 128 queries, offset q0 into mq) over a list
+    // MFMA list scans: one query tile (<= qb queries, offset q0 into mq) over a list: split (hi, lo)
+    // tiles of 128 queries (margin ~2^-17 ||q|| ||x||), or in the first pass under
+    // VS_IVF_QTILE_PLAIN, plain tiles where the direct form serves (256 queries a tile, one MFMA
+    // column per query; their query-rounding margin, ~2^-9 ||q|| ||x||, goes to the certificate;
+    // cfg5 Zipf 1.1: scans 1.4% faster, but one query in 256 fails the wider margin and its
+    // re-search -- every probed list scanned again for it -- costs 4.4 ms).
     struct MScan { int l, q0, nqb; };
     std::vector<MScan> mscans;
     std::vector<int> mq;  // query indices of every MFMA scan's block
     int64_t mtiles = 0;   // pages all MFMA scans read
     const bool mfma_ok = Kp <= MFMA_KP_MAX;
+    const bool plain = first_pass && ix->qtile_mode == VS_IVF_QTILE_PLAIN && d16_direct_ok(ix->dpad);
+    const int qb = plain ? MFMA_QB : MFMA_QB / 2;
     for (int l = 0; l < ix->nlist; ++l) {
         const int nql = (int)lq[l].size();
         const int np = (int)ix->pages[l].size();
         if (nql == 0 || np == 0) continue;
         bytes += (double)ix->list_n[l] * ix->d * ix->es;
-        if (mfma_ok && mfma_scan_pays(ix, np, nql)) {
-            for (int b0 = 0; b0 < nql; b0 += MFMA_QB / 2) {  // split query tiles: 128 queries
-                const int nb = std::min(MFMA_QB / 2, nql - b0);
+        if (mfma_ok && mfma_scan_pays(ix, np, nql, qb)) {
+            for (int b0 = 0; b0 < nql; b0 += qb) {
+                const int nb = std::min(qb, nql - b0);
                 mscans.push_back({l, (int)mq.size(), nb});
                 mq.insert(mq.end(), lq[l].begin() + b0, lq[l].begin() + b0 + nb);
                 mtiles += np;
@@ -408,12 +416,12 @@ void search_core(vs_ivf* ix, const float* q_dev, int64_t nq, int k, int nprobe, 
         const int64_t tmap_len = ix->page_off_h.back();
         for (const Wg& w : wgs) {
             const int g[MAP_DESC] = {w.tm_off, w.nt, w.t0, w.nvalid, w.qti, w.qoff, w.nqb, 0};
-            if (!check_map_desc(g, tmap_len, (int)mscans.size(), (int64_t)mq.size()))
+            if (!check_map_desc(g, tmap_len, (int)mscans.size(), (int64_t)mq.size(), plain))
                 throw VsError(VS_ERR_INTERNAL, "IVF MFMA scan: invalid workgroup descriptor");
             desc.insert(desc.end(), g, g + MAP_DESC);
         }
         for (const MScan& m : mscans) {  // the query tiles' (offset into mq, queries), after the descriptors
-            if (m.nqb < 1 || m.nqb > MFMA_QB / 2 || m.q0 < 0 || m.q0 + m.nqb > (int)mq.size())
+            if (m.nqb < 1 || m.nqb > qb || m.q0 < 0 || m.q0 + m.nqb > (int)mq.size())
                 throw VsError(VS_ERR_INTERNAL, "IVF MFMA scan: invalid query tile");
             desc.push_back(m.q0);
             desc.push_back(m.nqb);
@@ -518,11 +526,11 @@ void search_core(vs_ivf* ix, const float* q_dev, int64_t nq, int k, int nprobe, 
         const size_t qtb = (size_t)MFMA_QB * ix->dpad * 2;  // one query tile
         ix->mqtile.ensure(qtb * mscans.size());
         const int G = ix->n_mdesc;
-        ix->mcand.ensure((size_t)G * (MFMA_QB / 2) * MFMA_CAP * sizeof(u64));
+        ix->mcand.ensure((size_t)G * qb * MFMA_CAP * sizeof(u64));
         // the query tiles (and their queries' margins in qinfo), one launch
         HIP_CHECK(launch_pack_qtile_split(ix->dtype, q_dev, ix->mqidx.as<int>(), ix->mdesc.as<int>() + (size_t)G * MAP_DESC,
                                           (int)mscans.size(), ix->d, ix->dpad, ix->mqtile.as<uint8_t>(),
-                                          ix->qinfo.as<float>(), st));
+                                          ix->qinfo.as<float>(), plain, st));
         ScreenArgs sa{};
         sa.corpus = ix->data;
         sa.dpad = ix->dpad;
@@ -539,7 +547,7 @@ void search_core(vs_ivf* ix, const float* q_dev, int64_t nq, int k, int nprobe, 
         sa.tile_map = ix->d_list_pages.as<int>();
         sa.qmap = ix->mqidx.as<int>();
         sa.wg_desc = ix->mdesc.as<int>();
-        HIP_CHECK(launch_screen_mfma_mapped(ix->dtype, sa, ix->mqtile.as<uint8_t>(), st));
+        HIP_CHECK(launch_screen_mfma_mapped(ix->dtype, sa, ix->mqtile.as<uint8_t>(), plain, st));
     }
     size_t off = 0;
     if (concurrent) {
@@ -939,6 +947,15 @@ int vs_ivf_set_scan(vs_ivf* ix, int mode) {
             throw VsError(VS_ERR_ARG, "unknown IVF scan mode");
         std::lock_guard<std::mutex> g(ix->search_mtx);
         ix->scan_mode = mode;
+    });
+}
+
+int vs_ivf_set_query_tiles(vs_ivf* ix, int mode) {
+    return guarded([&] {
+        check_ivf(ix);
+        if (mode != VS_IVF_QTILE_PLAIN && mode != VS_IVF_QTILE_SPLIT) throw VsError(VS_ERR_ARG, "unknown IVF query-tile mode");
+        std::lock_guard<std::mutex> g(ix->search_mtx);
+        ix->qtile_mode = mode;
     });
 }
 

@@ -233,9 +233,12 @@ __global__ void __launch_bounds__(256) k_pack_qtile(const float* __restrict__ q,
 // as hi = round(q) in tile row wn*128 + (jj/16)*32 + jj%16 and lo = round(q - hi) 16 rows further,
 // so the screen sums two MFMA accumulators per query.  Query j is q[qidx[j]]; its qinfo entry
 // becomes the max of what is there and (||hi|| + ||lo||, ||q - hi - lo||) (fp64, rounded up).
+// PLAIN: up to 256 queries, query j = hi alone in tile row j (qinfo: (||hi||, ||q - hi||)): half the
+// MFMAs per query, a margin ~2^8 x wider (the refine's certificate takes it; re-search rounds pack
+// split tiles).
 // One launch packs every tile: tile y = blockIdx.y takes queries qidx[sinfo[2y] ..] (sinfo[2y + 1]
 // of them) into qt + y * MFMA_QB * dpad * 2.
-template <int DT>
+template <int DT, bool PLAIN>
 __global__ void __launch_bounds__(256) k_pack_qtile_split(const float* __restrict__ q, const int* __restrict__ qidx,
                                                            const int* __restrict__ sinfo, int d, int dpad,
                                                            uint8_t* __restrict__ qt, float* __restrict__ qinfo) {
@@ -245,8 +248,8 @@ __global__ void __launch_bounds__(256) k_pack_qtile_split(const float* __restric
     const int lane = threadIdx.x & 63;
     const int c = blockIdx.x * 4 + (threadIdx.x >> 6);  // tile row
     if (c >= MFMA_QB) return;
-    const int wn = c >> 7, ni = (c >> 4) & 7, part = ni & 1;
-    const int j = wn * 64 + (ni >> 1) * 16 + (c & 15);
+    const int wn = c >> 7, ni = (c >> 4) & 7, part = PLAIN ? 0 : ni & 1;
+    const int j = PLAIN ? c : wn * 64 + (ni >> 1) * 16 + (c & 15);
     const bool real = j < nqb;
     const int64_t qr = real ? (int64_t)qidx[j] : 0;
     double h2 = 0.0, l2 = 0.0, e2 = 0.0;
@@ -254,7 +257,7 @@ __global__ void __launch_bounds__(256) k_pack_qtile_split(const float* __restric
     for (int i = lane; i < dpad; i += 64) {
         const float v = (real && i < d) ? q[qr * d + i] : 0.0f;
         const float hi = round_only<DT>(v);
-        const float lo = round_only<DT>(v - hi);  // v - hi is exact in fp32
+        const float lo = PLAIN ? 0.0f : round_only<DT>(v - hi);  // v - hi is exact in fp32
         round_store<DT>(part ? lo : hi, qt + (int64_t)(i >> 5) * MFMA_QB * 64 + (int64_t)c * 64 + (i & 31) * 2);
         h2 += (double)hi * hi;
         l2 += (double)lo * lo;
@@ -682,7 +685,10 @@ __global__ void __launch_bounds__(512, 2) k_screen_i8d_res_ms(ScreenArgs a, cons
 // rounding, certified in k_refine).
 // SPLIT: work items of 256 / SPLIT rows (a tile in SPLIT row blocks, each wave 64 / SPLIT rows of
 // it): corpora of fewer tiles than resident blocks reach more CUs (cfg1: 40 tiles)
-template <int DT, int NQ, int SPLIT = 1>
+// QL: the queries staged in LDS once per workgroup (dynamic LDS, NQ x dpad fp32), read from there
+// per chunk instead of from L1/L2: half the vector-memory instructions of the loop, and the query
+// values no longer held across the unrolled chunks (fewer VGPRs)
+template <int DT, int NQ, int SPLIT = 1, bool QL = false>
 __global__ void __launch_bounds__(256) k_screen_gemv(ScreenArgs a, const float* __restrict__ qp, int nqb) {
     constexpr bool I8 = DT == DT_I8;
     constexpr int ES = DT == DT_F32 ? 4 : I8 ? 1 : 2;
@@ -703,10 +709,13 @@ __global__ void __launch_bounds__(256) k_screen_gemv(ScreenArgs a, const float* 
     __shared__ int red[8];
     __shared__ int tile_s;
 
+    extern __shared__ __attribute__((aligned(16))) float qsh[];  // QL: [NQ][dpad]
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int unit = lane % LPR, rsub = lane / LPR;
     const int blk = blockIdx.x;
     const int items = a.tiles * SPLIT;
+    if constexpr (QL)
+        for (int i = tid; i < NQ * a.dpad / 4; i += 256) ((float4*)qsh)[i] = ((const float4*)qp)[i];
     const int t0 = (int)((int64_t)items * blk / a.G);
     const int t1 = (int)((int64_t)items * (blk + 1) / a.G);
     if (tid < NQ) {
@@ -757,10 +766,12 @@ __global__ void __launch_bounds__(256) k_screen_gemv(ScreenArgs a, const float* 
                 float qv[NQ][EPU];
 #pragma unroll
                 for (int qi = 0; qi < NQ; ++qi) {
-                    const float4* qs = (const float4*)(qp + (int64_t)qi * a.dpad + c * CHK + unit * EPU);
+                    const int64_t qo = (int64_t)qi * a.dpad + c * CHK + unit * EPU;
 #pragma unroll
                     for (int h = 0; h < EPU / 4; ++h) {
-                        float4 t = qs[h];
+                        float4 t;
+                        if constexpr (QL) t = ((const float4*)(qsh + qo))[h];
+                        else t = ((const float4*)(qp + qo))[h];
                         qv[qi][4 * h + 0] = t.x; qv[qi][4 * h + 1] = t.y;
                         qv[qi][4 * h + 2] = t.z; qv[qi][4 * h + 3] = t.w;
                     }
@@ -2071,15 +2082,21 @@ hipError_t launch_pack_qtile(int dt, const float* q, int nqb, int d, int dpad, u
 }
 
 hipError_t launch_pack_qtile_split(int dt, const float* q, const int* qidx, const int* sinfo, int ntiles, int d,
-                                   int dpad, uint8_t* qt, float* qinfo, hipStream_t st) {
+                                   int dpad, uint8_t* qt, float* qinfo, bool plain, hipStream_t st) {
     if (ntiles <= 0 || ntiles > 65535 || !qidx || !sinfo) return hipErrorInvalidValue;
     const dim3 grid(MFMA_QB / 4, ntiles);
-    if (dt == DT_BF16)
-        hipLaunchKernelGGL(k_pack_qtile_split<DT_BF16>, grid, dim3(256), 0, st, q, qidx, sinfo, d, dpad, qt, qinfo);
-    else if (dt == DT_F16)
-        hipLaunchKernelGGL(k_pack_qtile_split<DT_F16>, grid, dim3(256), 0, st, q, qidx, sinfo, d, dpad, qt, qinfo);
-    else
+#define VS_PACK_SPLIT(DT_, P_) \
+    hipLaunchKernelGGL((k_pack_qtile_split<DT_, P_>), grid, dim3(256), 0, st, q, qidx, sinfo, d, dpad, qt, qinfo)
+    if (dt == DT_BF16) {
+        if (plain) VS_PACK_SPLIT(DT_BF16, true);
+        else VS_PACK_SPLIT(DT_BF16, false);
+    } else if (dt == DT_F16) {
+        if (plain) VS_PACK_SPLIT(DT_F16, true);
+        else VS_PACK_SPLIT(DT_F16, false);
+    } else {
         return hipErrorInvalidValue;
+    }
+#undef VS_PACK_SPLIT
     return hipGetLastError();
 }
 
@@ -2221,34 +2238,39 @@ hipError_t launch_screen_mfma(int dt, const ScreenArgs& a, const uint8_t* qt, in
 }
 
 template <int DT, int METRIC>
-static void launch_mapped_one(const ScreenArgs& a, const uint8_t* qt, hipStream_t st) {
+static void launch_mapped_one(const ScreenArgs& a, const uint8_t* qt, bool plain, hipStream_t st) {
+    if (plain) {  // plain query tiles: the direct form only (checked by the caller)
+        set_lds_attr((const void*)k_screen_d16_mapped<DT, METRIC, true>, I8D_LDS_MAP);
+        hipLaunchKernelGGL((k_screen_d16_mapped<DT, METRIC, true>), dim3(a.G), dim3(MF_THREADS), I8D_LDS_MAP, st, a, qt, 0);
+        return;
+    }
     if (d16_direct_ok(a.dpad)) {  // the direct form (corpus fragments HBM -> VGPRs; narrow tiles inside)
-        set_lds_attr((const void*)k_screen_d16_mapped<DT, METRIC>, I8D_LDS_MAP);
-        hipLaunchKernelGGL((k_screen_d16_mapped<DT, METRIC>), dim3(a.G), dim3(MF_THREADS), I8D_LDS_MAP, st, a, qt, 0);
+        set_lds_attr((const void*)k_screen_d16_mapped<DT, METRIC, false>, I8D_LDS_MAP);
+        hipLaunchKernelGGL((k_screen_d16_mapped<DT, METRIC, false>), dim3(a.G), dim3(MF_THREADS), I8D_LDS_MAP, st, a, qt, 0);
         return;
     }
     set_lds_attr((const void*)k_screen_mfma_mapped<DT, METRIC>, MF_LDS_MAP);
     hipLaunchKernelGGL((k_screen_mfma_mapped<DT, METRIC>), dim3(a.G), dim3(MF_THREADS), MF_LDS_MAP, st, a, qt, 0);
 }
-bool check_map_desc(const int* g, int64_t tmap_len, int n_qtiles, int64_t qmap_len) {
+bool check_map_desc(const int* g, int64_t tmap_len, int n_qtiles, int64_t qmap_len, bool plain) {
     const int64_t tm_off = g[0], nt = g[1], t0 = g[2], nvalid = g[3], qti = g[4], qoff = g[5], nqb = g[6];
     // tiles [t0, t0 + nt) of a segment of nvalid rows, each holding at least one of its rows (the
     // kernel masks rows >= nvalid); page-table, query-tile and qmap slices in range
     return nt >= 1 && nt <= MFMA_MAP_TILES && tm_off >= 0 && tm_off + nt <= tmap_len && t0 >= 0 &&
            (t0 + nt - 1) * TR < nvalid && nvalid <= INT32_MAX && qti >= 0 && qti < n_qtiles && nqb >= 1 &&
-           nqb <= MFMA_QB / 2 && qoff >= 0 && qoff + nqb <= qmap_len;
+           nqb <= (plain ? MFMA_QB : MFMA_QB / 2) && qoff >= 0 && qoff + nqb <= qmap_len;
 }
-hipError_t launch_screen_mfma_mapped(int dt, const ScreenArgs& a, const uint8_t* qt, hipStream_t st) {
+hipError_t launch_screen_mfma_mapped(int dt, const ScreenArgs& a, const uint8_t* qt, bool plain, hipStream_t st) {
     // the launch contract the kernel relies on (descriptors: check_map_desc, by the caller)
     if (!a.tile_map || !a.qmap || !a.wg_desc || a.thr0 || a.seed_acc || a.tile_stride != 0 || a.gate || a.G <= 0 ||
-        a.Kp > MFMA_KP_MAX || a.cap != MFMA_CAP || a.lcap < a.Kp)
+        a.Kp > MFMA_KP_MAX || a.cap != MFMA_CAP || a.lcap < a.Kp || (plain && !d16_direct_ok(a.dpad)))
         return hipErrorInvalidValue;
     if (dt == DT_BF16) {
-        if (a.metric == METRIC_IP) launch_mapped_one<DT_BF16, METRIC_IP>(a, qt, st);
-        else launch_mapped_one<DT_BF16, METRIC_L2>(a, qt, st);
+        if (a.metric == METRIC_IP) launch_mapped_one<DT_BF16, METRIC_IP>(a, qt, plain, st);
+        else launch_mapped_one<DT_BF16, METRIC_L2>(a, qt, plain, st);
     } else if (dt == DT_F16) {
-        if (a.metric == METRIC_IP) launch_mapped_one<DT_F16, METRIC_IP>(a, qt, st);
-        else launch_mapped_one<DT_F16, METRIC_L2>(a, qt, st);
+        if (a.metric == METRIC_IP) launch_mapped_one<DT_F16, METRIC_IP>(a, qt, plain, st);
+        else launch_mapped_one<DT_F16, METRIC_L2>(a, qt, plain, st);
     } else {
         return hipErrorInvalidValue;
     }
@@ -2260,7 +2282,10 @@ static int gemv_occ(int nqpad) {
     int n = 0;
     hipError_t e = hipSuccess;
     switch (nqpad) {
-        case 1: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_screen_gemv<DT, 1>, 256, 0); break;
+        case 1:  // (int8: the QL form, its LDS at the largest query it takes)
+            if constexpr (DT == DT_I8) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_screen_gemv<DT, 1, 1, true>, 256, 4096 * 4);
+            else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_screen_gemv<DT, 1>, 256, 0);
+            break;
         case 2: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_screen_gemv<DT, 2>, 256, 0); break;
         case 4: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_screen_gemv<DT, 4>, 256, 0); break;
         default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_screen_gemv<DT, 8>, 256, 0); break;
@@ -2279,6 +2304,11 @@ int gemv_blocks_per_cu(int dt, int nqpad) {
 
 template <int DT, int SPLIT>
 static void launch_gemv_split(const ScreenArgs& a, const float* qp, int nqb, int nqpad, hipStream_t st) {
+    // (int8, one query: the query in LDS, k_screen_gemv QL)
+    if (DT == DT_I8 && nqpad == 1 && a.dpad <= 4096) {
+        hipLaunchKernelGGL((k_screen_gemv<DT, 1, SPLIT, true>), dim3(a.G), dim3(256), (size_t)a.dpad * 4, st, a, qp, nqb);
+        return;
+    }
     switch (nqpad) {
         case 1: hipLaunchKernelGGL((k_screen_gemv<DT, 1, SPLIT>), dim3(a.G), dim3(256), 0, st, a, qp, nqb); break;
         case 2: hipLaunchKernelGGL((k_screen_gemv<DT, 2, SPLIT>), dim3(a.G), dim3(256), 0, st, a, qp, nqb); break;

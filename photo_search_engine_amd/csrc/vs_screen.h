@@ -749,8 +749,11 @@ __device__ __forceinline__ void ms_step(intx4 (&acc)[2][16], intx4 (&bt)[4], uin
 // workgroup's descriptor (list segment, query tile, qmap slice), its page table in LDS (one lookup
 // per tile), keys carrying storage slots, split (hi, lo) query columns summed in the epilogue.
 // NG: query column groups of 16 (16 = the 256-column tile; 4 = a narrow tile of 64 columns for
-// mapped scans of lists probed by <= 32 queries: a quarter of the MFMAs, and the query DMAs read
-// only the tile's first 64 rows, so the L2 holds a quarter of each tile)
+// mapped scans of lists probed by <= 32 queries (<= 64 plain): a quarter of the MFMAs, and the query
+// DMAs read only the tile's first 64 rows, so the L2 holds a quarter of each tile)
+// PLAINQ (MAP only): the query tile holds one rounded copy of each query per column (k_pack_qtile_split
+// <DT, true>): twice the queries per tile, no pair sums; the wider query-rounding margin is the
+// refine's (qinfo).
 // SCHED: 0 = one s_waitcnt + s_barrier at the head of every K-step, then the issue of the K-step 3
 // ahead, then its MFMAs; 1 = the mid-step barrier (vs_i8_asm.h MS_*): the barrier sits between MFMA
 // pairs 7 and 8 of a K-step and the issue of the K-step 3 ahead between pairs 8-11, and the next
@@ -762,10 +765,12 @@ __device__ __forceinline__ void ms_step(intx4 (&acc)[2][16], intx4 (&bt)[4], uin
 // the whole loop (the host sets every threshold to +inf: the epilogue's bound test, no survivor).
 enum { PR_NONE = 0, PR_LOADS = 1, PR_LDS = 2, PR_MFMA = 3, PR_FULL = 4 };
 template <int DT, int METRIC, bool MAP = false, int NG = 16, bool RES = false, int PROBE = PR_NONE, int SCHED = 0,
-          bool PRIO = false>
+          bool PRIO = false, bool PLAINQ = false>
 __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
     constexpr bool L2 = METRIC == METRIC_L2;
     constexpr bool I8 = DT == DT_I8;
+    static_assert(!PLAINQ || MAP, "plain query tiles: mapped scans");
+    constexpr bool SPLITQ = MAP && !PLAINQ;  // (hi, lo) column pairs per query
     static_assert(!(MAP && I8), "the mapped scan serves bf16 / f16 lists");
     static_assert(!RES || (I8 && !MAP && !L2), "group residuals: the int8 flat inner-product main pass");
     static_assert(NG == 16 || (NG == 4 && MAP), "narrow query tiles: mapped scans only");
@@ -849,7 +854,7 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
     }
     const int nks = a.dpad / (I8 ? 64 : CH);
     const int64_t tbytes = (int64_t)TR * a.dpad * (I8 ? 1 : 2);
-    u64* cand = a.cand + (size_t)blk * (MAP ? MFMA_QB / 2 : MFMA_QB) * a.cap;
+    u64* cand = a.cand + (size_t)blk * (SPLITQ ? MFMA_QB / 2 : MFMA_QB) * a.cap;
     const int trigger = a.cap - TR;
     const uint32_t ring = lds_addr(smem);
     const uint32_t rowx_lds = lds_addr((const uint8_t*)rowx);
@@ -1184,10 +1189,10 @@ __device__ __forceinline__ void screen_direct(ScreenArgs a, const uint8_t* __res
             }
             __builtin_amdgcn_wave_barrier();
         };
-        // MAP: query p = columns 2p (hi) + 2p + 1 (lo): their fp32 sums, in place of the hi column
-        // (p = 0..7: the 128 queries of the split tile; columns 8..15 then hold nothing used)
-        constexpr int NCOL = MAP ? NG / 2 : NG;
-        if constexpr (MAP) {
+        // split MAP: query p = columns 2p (hi) + 2p + 1 (lo): their fp32 sums, in place of the hi
+        // column (p = 0..7: the 128 queries of the split tile; columns 8..15 then hold nothing used)
+        constexpr int NCOL = SPLITQ ? NG / 2 : NG;
+        if constexpr (SPLITQ) {
 #pragma unroll
             for (int p = 0; p < NG / 2; ++p)
 #pragma unroll
@@ -1296,14 +1301,16 @@ __global__ void __launch_bounds__(512, 2) k_screen_i8d_ms(ScreenArgs a, const ui
     screen_direct<DT_I8, METRIC, false, 16, false, PR_NONE, 1>(a, qt, nqb);
 }
 
-// One launch for every list scan: a workgroup whose query tile holds <= 32 queries runs the narrow
-// form (64 columns = 32 queries x (hi, lo): a quarter of the MFMAs, a quarter of the tile's L2
-// footprint), the others the full 256-column form (two separately allocated code paths; the
+// One launch for every list scan: a workgroup whose query tile fits 64 columns runs the narrow
+// form (32 queries x (hi, lo), or 64 plain queries: a quarter of the MFMAs, a quarter of the tile's
+// L2 footprint), the others the full 256-column form (two separately allocated code paths; the
 // choice is per workgroup, outside either K loop).
-template <int DT, int METRIC>
+template <int DT, int METRIC, bool PLAINQ>
 __global__ void __launch_bounds__(512, 2) k_screen_d16_mapped(ScreenArgs a, const uint8_t* __restrict__ qt, int nqb) {
-    if (a.wg_desc[(size_t)blockIdx.x * MAP_DESC + 6] <= 32) screen_direct<DT, METRIC, true, 4>(a, qt, nqb);
-    else screen_direct<DT, METRIC, true, 16>(a, qt, nqb);
+    if (a.wg_desc[(size_t)blockIdx.x * MAP_DESC + 6] <= (PLAINQ ? 64 : 32))
+        screen_direct<DT, METRIC, true, 4, false, PR_NONE, 0, false, PLAINQ>(a, qt, nqb);
+    else
+        screen_direct<DT, METRIC, true, 16, false, PR_NONE, 0, false, PLAINQ>(a, qt, nqb);
 }
 constexpr int I8D_LDS_MAP = I8D_LDS + MFMA_MAP_TILES * 4;  // + the workgroup's page table
 static_assert(I8D_LDS_MAP <= 160 * 1024, "LDS budget (direct mapped screen)");

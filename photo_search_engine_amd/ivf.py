@@ -163,6 +163,16 @@ class IVFFlatIndex:
             raise ValueError(f"scan mode must be one of {sorted(self._SCANS)}")
         check(self._L.vs_ivf_set_scan(self._h, self._SCANS[mode]))
 
+    _QTILES = {"plain": 0, "split": 1}
+
+    def set_query_tiles(self, mode: str) -> None:
+        """Query tiles of the MFMA list scans' first pass: "split" (default: (hi, lo) parts, 128 a
+        tile) or "plain" (each query rounded once, 256 a tile, the wider rounding margin certified
+        by the refine).  Results are identical in both modes (include/vs.h vs_ivf_set_query_tiles)."""
+        if mode not in self._QTILES:
+            raise ValueError(f"query-tile mode must be one of {sorted(self._QTILES)}")
+        check(self._L.vs_ivf_set_query_tiles(self._h, self._QTILES[mode]))
+
     def last_search_stats(self) -> Tuple[int, int]:
         """First pass of the last search: (MFMA list scans, queries re-searched for their certificate)."""
         return self.last_search_detail()[:2]

@@ -44,6 +44,7 @@ for s in ${STEPS:-decomp}; do
       python scripts/trace_tail.py $(ls gpurun_out/trace8/*/t_kernel_trace.csv gpurun_out/trace8/t_kernel_trace.csv 2>/dev/null | head -1) 80 "vs::|copyBuffer|nccl|rccl|Kernel" > gpurun_out/trace8_tail.txt && rm -rf gpurun_out/trace8 ;;
     trace3) mkdir -p gpurun_out/trace3 && run trace3 300 rocprofv3 --kernel-trace -d gpurun_out/trace3 -o t --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline && \
       python scripts/trace_tail.py $(ls gpurun_out/trace3/*/t_kernel_trace.csv gpurun_out/trace3/t_kernel_trace.csv 2>/dev/null | head -1) 60 "vs::|copyBuffer|Kernel" > gpurun_out/trace3_tail.txt && rm -rf gpurun_out/trace3 ;;
+    ivf) run pytest_ivf 600 $PYT tests/test_gpu_ivf.py tests/test_gpu_baseline_shapes.py -m gpu -k "ivf or cfg5" ;;
     dist) run pytest_dist 600 $PYT tests/test_gpu_distributed.py tests/test_gpu_multi_device.py tests/test_gpu_int8_direct.py tests/test_gpu_int8_clustered.py -m gpu ;;
     full0) VS_TEST_K1_SCHEDULE=0 run pytest_gpu_sched0 900 $PYT tests -m gpu ;;
     ab8) abloop shard8 2 --shard-of 8 --steps 30 ;;
@@ -56,6 +57,8 @@ for s in ${STEPS:-decomp}; do
     cfg4) run bench_cfg4 900 python bench.py --workload cfg4 --steps 10 --warmup 3 --no-cpu-baseline ;;
     mix10) run bench_mix10 600 python bench.py --data mixture-sorted --sigma 1.0 --warmup 8 --no-cpu-baseline ;;
     mix05) run bench_mix05 600 python bench.py --data mixture-sorted --sigma 0.5 --warmup 8 --no-cpu-baseline ;;
+    profcfg2) TAG=r06_cfg2 ARGS="--workload cfg2 --steps 200 --warmup 20 --no-cpu-baseline" PASSES="sq lds" timeout -k 10 1100 bash scripts/gpu_prof.sh > gpurun_out/prof_cfg2.log 2>&1
+      rc=$?; echo "step profcfg2 rc=$rc" >> gpurun_out/steps.log; if fatal $rc || [ $rc -ne 0 ]; then exit $rc; fi ;;
     profcfg3) TAG=${PTAG:-r06_final_cfg3} ARGS="--steps 20 --warmup 3 --no-cpu-baseline" PASSES=sq timeout -k 10 1100 bash scripts/gpu_prof.sh > gpurun_out/prof_cfg3.log 2>&1
       rc=$?; echo "step profcfg3 rc=$rc" >> gpurun_out/steps.log; if fatal $rc || [ $rc -ne 0 ]; then exit $rc; fi ;;
     prof3) mkdir -p gpurun_out/prof3 && run prof3 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof3 -o run --output-format csv -- python bench.py --steps 30 --warmup 1 --no-cpu-baseline ;;

@@ -182,3 +182,58 @@ def test_ivf_mfma_skewed_lists_mixed_scans(IVF):
     _check(ix, x_st, ix.centroids(), q[:1], 20, 3, "ip")
     assert ix.last_mfma_lists == 0
     ix.close()
+
+
+@pytest.mark.parametrize("metric", ["ip", "l2"])
+def test_ivf_mfma_plain_query_tiles(IVF, metric):
+    # the direct mapped form (padded dim a multiple of 128): plain query tiles (256 queries a tile,
+    # lists probed by <= 64 queries on the narrow 64-column form) and split (hi, lo) tiles (128 a
+    # tile, narrow up to 32) return the same exact answer as the oracle; 300 queries probing both
+    # lists: 2 x 2 plain tiles vs 2 x 3 split tiles; 50 queries: the narrow plain form
+    d, N, nlist, k = 256, 60_000, 2, 10
+    x = O.synth_rows(O.SEED_CORPUS, 0, N, d, True, "bf16")
+    ix = IVF(d, nlist, metric, "bf16")
+    ix.set_centroids(IO.sample_centroids(x, nlist, 4))
+    ix.add_synthetic(O.SEED_CORPUS, 0, N, True)
+    q = O.synth_rows(O.SEED_QUERIES, 0, 300, d, True, "f32")
+    ix.set_scan("mfma")
+    out = {}
+    for mode, nq, scans in (("plain", 300, 4), ("split", 300, 6), ("plain", 50, 2), ("split", 50, 2)):
+        ix.set_query_tiles(mode)
+        D, I, _ = _check(ix, x, ix.centroids(), q[:nq], k, 2, metric)
+        assert ix.last_search_stats()[0] == scans
+        out[(mode, nq)] = (D, I)
+    for nq in (300, 50):
+        np.testing.assert_array_equal(out[("plain", nq)][1], out[("split", nq)][1])
+        np.testing.assert_array_equal(out[("plain", nq)][0], out[("split", nq)][0])
+    with pytest.raises(ValueError):
+        ix.set_query_tiles("hi-lo")
+    ix.close()
+
+
+def test_ivf_plain_query_tiles_tight_clusters_researched(IVF):
+    # rows within ~1e-3 of their centroid: the 10th and 32nd best scores of a query differ by less
+    # than the plain tile's query-rounding margin (~2^-9 ||q|| ||x||), so the first pass leaves
+    # queries uncertified; their re-search packs split tiles (margin ~2^-17) and certifies them --
+    # the answer is the oracle's either way
+    rng = np.random.default_rng(11)
+    d, nlist, N, nq, k = 256, 4, 40_000, 96, 10
+    c = rng.standard_normal((nlist, d)).astype(np.float32)
+    c /= np.linalg.norm(c, axis=1, keepdims=True)
+    cid = rng.integers(0, nlist, N)
+    x = c[cid] + 1e-3 * rng.standard_normal((N, d)).astype(np.float32)
+    ix = IVF(d, nlist, "ip", "bf16")
+    ix.set_centroids(c)
+    ix.add(x)
+    x_st = O.round_dtype(x, "bf16")
+    q = c[rng.integers(0, nlist, nq)] + 0.05 * rng.standard_normal((nq, d)).astype(np.float32)
+    ix.set_scan("mfma")
+    ix.set_query_tiles("plain")
+    D, I, _ = _check(ix, x_st, ix.centroids(), q, k, 2, "ip")
+    assert ix.last_search_stats()[1] > 0  # re-searched on split tiles
+    ix.set_query_tiles("split")
+    D2, I2, _ = _check(ix, x_st, ix.centroids(), q, k, 2, "ip")
+    assert ix.last_search_stats()[1] == 0
+    np.testing.assert_array_equal(I2, I)
+    np.testing.assert_array_equal(D2, D)
+    ix.close()
