@@ -895,10 +895,12 @@ __global__ void __launch_bounds__(256) k_screen_gemv(ScreenArgs a, const float* 
 // ------------------------------------------------------------------------------------------------
 // One work item (list l, pages [p0, p1), nqi <= NQ queries) of the IVF scan, by one 256-thread
 // block.  Shared state (thresholds, counts, query ids) is the caller's; the block is synchronised
-// on entry and exit.
-template <int DT, int NQ>
+// on entry and exit.  QL: the item's NQ queries staged in LDS (qsh, NQ x dpad fp32) and read from
+// there per chunk, instead of 2 NQ global loads per lane and chunk beside the corpus loads.
+template <int DT, int NQ, bool QL = false>
 __device__ __forceinline__ void ivf_scan_item(const IvfScanArgs& a, const int* itm, u64* cand, u64* thr_key,
-                                              float* thr_f, int* cnt, int* qid, int* red, int* off_s) {
+                                              float* thr_f, int* cnt, int* qid, int* red, int* off_s,
+                                              float* qsh = nullptr) {
     constexpr int ES = DT == DT_F32 ? 4 : 2;
     constexpr int CE = CHB / ES;  // elements per chunk
     constexpr int CB = CHB;
@@ -923,6 +925,14 @@ __device__ __forceinline__ void ivf_scan_item(const IvfScanArgs& a, const int* i
         qid[tid] = real ? itm[4 + tid] : itm[4];
     }
     __syncthreads();
+    if constexpr (QL) {  // (padding slots: copies of the item's first query, as qid)
+        const int n4 = a.dpad / 4;
+        for (int i = tid; i < NQ * n4; i += 256) {
+            const int qi = i / n4, j = i - qi * n4;
+            ((float4*)qsh)[i] = ((const float4*)(a.qp + (int64_t)qid[qi] * a.dpad))[j];
+        }
+        __syncthreads();
+    }
     const int64_t ln = a.list_n[l];
     const int pbase = a.page_off[l];
     for (int p = p0; p < p1; ++p) {
@@ -941,10 +951,11 @@ __device__ __forceinline__ void ivf_scan_item(const IvfScanArgs& a, const int* i
                 float qv[NQ][EPU];
 #pragma unroll
                 for (int qi = 0; qi < NQ; ++qi) {
-                    const float4* qs = (const float4*)(a.qp + (int64_t)qid[qi] * a.dpad + c * CE + unit * EPU);
 #pragma unroll
                     for (int h = 0; h < EPU / 4; ++h) {
-                        float4 t = qs[h];
+                        float4 t;
+                        if constexpr (QL) t = ((const float4*)(qsh + qi * a.dpad + c * CE + unit * EPU))[h];
+                        else t = ((const float4*)(a.qp + (int64_t)qid[qi] * a.dpad + c * CE + unit * EPU))[h];
                         qv[qi][4 * h + 0] = t.x; qv[qi][4 * h + 1] = t.y;
                         qv[qi][4 * h + 2] = t.z; qv[qi][4 * h + 3] = t.w;
                     }
@@ -1032,8 +1043,9 @@ __device__ __forceinline__ void ivf_scan_item(const IvfScanArgs& a, const int* i
 // All query-count classes in ONE persistent launch with dynamic item fetch (an atomic counter):
 // the host orders items most expensive class first, so no per-class launch tail idles the HBM
 // stream and no block waits on a static share of heavier items.
-template <int DT>
+template <int DT, bool QL>
 __global__ void __launch_bounds__(256, 3) k_ivf_scan_dyn(IvfScanArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float qsh[];  // QL: [IVF_QG][dpad]
     __shared__ u64 thr_key[IVF_QG];
     __shared__ float thr_f[IVF_QG];
     __shared__ int cnt[IVF_QG];
@@ -1049,10 +1061,10 @@ __global__ void __launch_bounds__(256, 3) k_ivf_scan_dyn(IvfScanArgs a) {
         if (it >= a.n_items) break;  // block-uniform: every wave leaves here, the queue is drained
         const int* itm = a.items + (size_t)it * IVF_ITEM_INTS;
         const int nqi = itm[3];
-        if (nqi <= 1) ivf_scan_item<DT, 1>(a, itm, cand, thr_key, thr_f, cnt, qid, red, &off_s);
-        else if (nqi <= 2) ivf_scan_item<DT, 2>(a, itm, cand, thr_key, thr_f, cnt, qid, red, &off_s);
-        else if (nqi <= 4) ivf_scan_item<DT, 4>(a, itm, cand, thr_key, thr_f, cnt, qid, red, &off_s);
-        else ivf_scan_item<DT, IVF_QG>(a, itm, cand, thr_key, thr_f, cnt, qid, red, &off_s);
+        if (nqi <= 1) ivf_scan_item<DT, 1, QL>(a, itm, cand, thr_key, thr_f, cnt, qid, red, &off_s, qsh);
+        else if (nqi <= 2) ivf_scan_item<DT, 2, QL>(a, itm, cand, thr_key, thr_f, cnt, qid, red, &off_s, qsh);
+        else if (nqi <= 4) ivf_scan_item<DT, 4, QL>(a, itm, cand, thr_key, thr_f, cnt, qid, red, &off_s, qsh);
+        else ivf_scan_item<DT, IVF_QG, QL>(a, itm, cand, thr_key, thr_f, cnt, qid, red, &off_s, qsh);
     }
 }
 
@@ -2484,9 +2496,18 @@ hipError_t launch_ivf_scan(int dt, int nq_class, const IvfScanArgs& a, int grid,
 hipError_t launch_ivf_scan_dyn(int dt, const IvfScanArgs& a, int grid, hipStream_t st) {
     if (a.n_items <= 0 || grid <= 0) return hipSuccess;
     if (!a.next_item) return hipErrorInvalidValue;
-    if (dt == DT_F32) hipLaunchKernelGGL(k_ivf_scan_dyn<DT_F32>, dim3(grid), dim3(256), 0, st, a);
-    else if (dt == DT_BF16) hipLaunchKernelGGL(k_ivf_scan_dyn<DT_BF16>, dim3(grid), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL(k_ivf_scan_dyn<DT_F16>, dim3(grid), dim3(256), 0, st, a);
+    // the queries in LDS when an item's IVF_QG of them fit 48 KiB (3 resident workgroups per CU, as
+    // the VGPR budget allows; d <= 1536)
+    const size_t ql = (size_t)IVF_QG * a.dpad * 4;
+    if (ql <= 48 * 1024) {
+        if (dt == DT_F32) hipLaunchKernelGGL((k_ivf_scan_dyn<DT_F32, true>), dim3(grid), dim3(256), ql, st, a);
+        else if (dt == DT_BF16) hipLaunchKernelGGL((k_ivf_scan_dyn<DT_BF16, true>), dim3(grid), dim3(256), ql, st, a);
+        else hipLaunchKernelGGL((k_ivf_scan_dyn<DT_F16, true>), dim3(grid), dim3(256), ql, st, a);
+        return hipGetLastError();
+    }
+    if (dt == DT_F32) hipLaunchKernelGGL((k_ivf_scan_dyn<DT_F32, false>), dim3(grid), dim3(256), 0, st, a);
+    else if (dt == DT_BF16) hipLaunchKernelGGL((k_ivf_scan_dyn<DT_BF16, false>), dim3(grid), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((k_ivf_scan_dyn<DT_F16, false>), dim3(grid), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 
