@@ -707,7 +707,7 @@ void search_block(vs_index* ix, Ctx* c, const float* q, int nqb, int k, int Kp, 
         const int dpadq = gemv_i8 ? ix->dpad8 : ix->dpad;
         // work-queue tiles over exactly the resident blocks; a corpus of at most num_cu / 2 tiles
         // (cfg1: 40) would leave most CUs idle: its work items are quarter tiles (GEMV_SPLIT)
-        const int64_t resident = (int64_t)ix->num_cu * (gemv_dyn() ? gemv_blocks_per_cu(sdt, QB) : 8);
+        const int64_t resident = (int64_t)ix->num_cu * (gemv_dyn() ? gemv_blocks_per_cu(sdt, QB, dpadq) : 8);
         a.gemv_split = tiles <= ix->num_cu / 2 ? GEMV_SPLIT : 1;
         a.G = (int)std::min<int64_t>(tiles * a.gemv_split, resident);
         // one query: each block keeps only Kb < Kp keys and publishes the key below which it dropped

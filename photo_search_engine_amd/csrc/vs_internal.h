@@ -222,7 +222,7 @@ struct ScreenArgs {
 };
 constexpr int MAP_DESC = 8;
 constexpr int MFMA_MAP_TILES = 256;  // mapped screen: logical tiles per workgroup (its LDS page table)
-int gemv_blocks_per_cu(int dt, int nqpad);  // resident k_screen_gemv blocks per CU (occupancy API)
+int gemv_blocks_per_cu(int dt, int nqpad, int dpad);  // resident k_screen_gemv blocks per CU (occupancy API)
 
 // ---- launchers (vs_kernels.hip) -------------------------------------------------------------
 hipError_t launch_pack_rows(int dt, const float* src, int64_t n, int d, int dpad, uint8_t* data, int64_t lrow0,

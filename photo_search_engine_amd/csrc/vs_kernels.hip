@@ -2289,36 +2289,48 @@ hipError_t launch_screen_mfma_mapped(int dt, const ScreenArgs& a, const uint8_t*
     return hipGetLastError();
 }
 
-template <int DT>
+// the GEMV's queries go to LDS (k_screen_gemv QL) when the padded class's fp32 rows fit this many
+// bytes (one query up to d = 4096; occupancy below is taken at this size, which the VGPR budget
+// limits before the LDS does)
+constexpr size_t kGemvQlBytes = 16384;
+static bool gemv_ql(int nqpad, int dpad) { return (size_t)nqpad * dpad * 4 <= kGemvQlBytes; }
+template <int DT, bool QL>
 static int gemv_occ(int nqpad) {
     int n = 0;
     hipError_t e = hipSuccess;
+    const size_t lds = QL ? kGemvQlBytes : 0;
     switch (nqpad) {
-        case 1:  // (int8: the QL form, its LDS at the largest query it takes)
-            if constexpr (DT == DT_I8) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_screen_gemv<DT, 1, 1, true>, 256, 4096 * 4);
-            else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_screen_gemv<DT, 1>, 256, 0);
-            break;
-        case 2: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_screen_gemv<DT, 2>, 256, 0); break;
-        case 4: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_screen_gemv<DT, 4>, 256, 0); break;
-        default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_screen_gemv<DT, 8>, 256, 0); break;
+        case 1: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_screen_gemv<DT, 1, 1, QL>, 256, lds); break;
+        case 2: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_screen_gemv<DT, 2, 1, QL>, 256, lds); break;
+        case 4: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_screen_gemv<DT, 4, 1, QL>, 256, lds); break;
+        default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_screen_gemv<DT, 8, 1, QL>, 256, lds); break;
     }
     return e == hipSuccess && n > 0 ? n : 4;
 }
-int gemv_blocks_per_cu(int dt, int nqpad) {
-    static int cache[4][9] = {};  // benign race: idempotent
+template <int DT>
+static int gemv_occ_dt(int q, bool ql) { return ql ? gemv_occ<DT, true>(q) : gemv_occ<DT, false>(q); }
+int gemv_blocks_per_cu(int dt, int nqpad, int dpad) {
+    static int cache[4][9][2] = {};  // benign race: idempotent
     const int q = nqpad <= 1 ? 1 : nqpad <= 2 ? 2 : nqpad <= 4 ? 4 : 8;
-    int& v = cache[dt][q];
+    const bool ql = gemv_ql(q, dpad);
+    int& v = cache[dt][q][ql ? 1 : 0];
     if (!v)
-        v = dt == DT_F32 ? gemv_occ<DT_F32>(q) : dt == DT_BF16 ? gemv_occ<DT_BF16>(q)
-            : dt == DT_I8 ? gemv_occ<DT_I8>(q) : gemv_occ<DT_F16>(q);
+        v = dt == DT_F32 ? gemv_occ_dt<DT_F32>(q, ql) : dt == DT_BF16 ? gemv_occ_dt<DT_BF16>(q, ql)
+            : dt == DT_I8 ? gemv_occ_dt<DT_I8>(q, ql) : gemv_occ_dt<DT_F16>(q, ql);
     return v;
 }
 
 template <int DT, int SPLIT>
 static void launch_gemv_split(const ScreenArgs& a, const float* qp, int nqb, int nqpad, hipStream_t st) {
-    // (int8, one query: the query in LDS, k_screen_gemv QL)
-    if (DT == DT_I8 && nqpad == 1 && a.dpad <= 4096) {
-        hipLaunchKernelGGL((k_screen_gemv<DT, 1, SPLIT, true>), dim3(a.G), dim3(256), (size_t)a.dpad * 4, st, a, qp, nqb);
+    const int q = nqpad <= 1 ? 1 : nqpad <= 2 ? 2 : nqpad <= 4 ? 4 : 8;
+    if (gemv_ql(q, a.dpad)) {  // the queries in LDS (k_screen_gemv QL)
+        const size_t lds = (size_t)q * a.dpad * 4;
+        switch (q) {
+            case 1: hipLaunchKernelGGL((k_screen_gemv<DT, 1, SPLIT, true>), dim3(a.G), dim3(256), lds, st, a, qp, nqb); break;
+            case 2: hipLaunchKernelGGL((k_screen_gemv<DT, 2, SPLIT, true>), dim3(a.G), dim3(256), lds, st, a, qp, nqb); break;
+            case 4: hipLaunchKernelGGL((k_screen_gemv<DT, 4, SPLIT, true>), dim3(a.G), dim3(256), lds, st, a, qp, nqb); break;
+            default: hipLaunchKernelGGL((k_screen_gemv<DT, 8, SPLIT, true>), dim3(a.G), dim3(256), lds, st, a, qp, nqb); break;
+        }
         return;
     }
     switch (nqpad) {

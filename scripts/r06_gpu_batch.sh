@@ -40,6 +40,11 @@ for s in ${STEPS:-decomp}; do
            rc=$?; echo "$lib $(tail -1 gpurun_out/ab.tmp)" >> gpurun_out/ab_$ABNAME.txt
            if [ $rc -ne 0 ]; then cp gpurun_out/ab.tmp gpurun_out/ab_${ABNAME}_fail.log; echo "step ab rc=$rc" >> gpurun_out/steps.log; exit $rc; fi
          done; done; echo "step ab rc=0" >> gpurun_out/steps.log ;;
+    abprod) for i in 1 2; do for lib in $ABLIBS; do
+           VS_LIB_PATH=$lib timeout -k 10 300 python scripts/product_latency.py $PRODARGS > gpurun_out/ab.tmp 2>&1
+           rc=$?; echo "$lib $(tail -1 gpurun_out/ab.tmp)" >> gpurun_out/abprod_$ABNAME.txt
+           if [ $rc -ne 0 ]; then cp gpurun_out/ab.tmp gpurun_out/abprod_${ABNAME}_fail.log; echo "step abprod rc=$rc" >> gpurun_out/steps.log; exit $rc; fi
+         done; done; echo "step abprod rc=0" >> gpurun_out/steps.log ;;
     trace8) mkdir -p gpurun_out/trace8 && run trace8 300 rocprofv3 --kernel-trace -d gpurun_out/trace8 -o t --output-format csv -- python bench.py --shard-of 8 --steps 10 --warmup 3 --no-cpu-baseline && \
       python scripts/trace_tail.py $(ls gpurun_out/trace8/*/t_kernel_trace.csv gpurun_out/trace8/t_kernel_trace.csv 2>/dev/null | head -1) 80 "vs::|copyBuffer|nccl|rccl|Kernel" > gpurun_out/trace8_tail.txt && rm -rf gpurun_out/trace8 ;;
     trace3) mkdir -p gpurun_out/trace3 && run trace3 300 rocprofv3 --kernel-trace -d gpurun_out/trace3 -o t --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline && \
