@@ -27,7 +27,8 @@ Normalisation stays on the host in numpy, bit-identical to the reference
 Environment knobs (new, optional): ``VECTOR_DEVICE`` (GPU ordinal, default 0), ``VECTOR_DEVICES``
 (e.g. ``0,1,2,3,4,5,6,7``: one index over those GPUs of this process, include/vs.h vs_multi_*),
 ``VECTOR_DTYPE`` (f32 | bf16 | f16 storage, default f32 = the reference's storage precision),
-``VECTOR_SCREEN`` (native | int8: the batched-search screen, either metric) and
+``VECTOR_SCREEN`` (int8 | native: the screen in front of the exact refine, either metric; default
+int8 -- the certified int8 pre-screen, same exact results) and
 ``VECTOR_HNSW_SEARCH`` (exact | graph: how an ``index_type="hnsw"`` store searches).
 """
 from __future__ import annotations
@@ -57,9 +58,11 @@ def _default_index_factory(dimension: int, metric: str):
     else:
         device = int(devices[0]) if devices else int(os.environ.get("VECTOR_DEVICE", "0") or 0)
         index = FlatIndex(dimension, metric=kind, dtype=dtype, device=device)
-    screen = (os.environ.get("VECTOR_SCREEN", "") or "").strip().lower()
-    if screen:
-        index.set_screen(screen)
+    # the certified int8 pre-screen unless VECTOR_SCREEN=native: results are exact either way (the
+    # refine scores every candidate canonically and a certificate covers the rest), and the index
+    # routes batches back to the native screen by itself on data denser than the int8 margins
+    screen = (os.environ.get("VECTOR_SCREEN", "") or "").strip().lower() or "int8"
+    index.set_screen(screen)
     return index
 
 

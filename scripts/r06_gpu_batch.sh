@@ -59,6 +59,7 @@ for s in ${STEPS:-decomp}; do
     shard2) run bench_shard2 300 python bench.py --shard-of 2 --steps 20 --no-cpu-baseline ;;
     shard4) run bench_shard4 300 python bench.py --shard-of 4 --steps 30 --no-cpu-baseline ;;
     cfg5skew) run bench_cfg5_skew 900 python bench.py --workload cfg5 --skew 1.1 --steps 10 --warmup 2 ;;
+    prod) run product_latency_int8 300 python scripts/product_latency.py --calls 300 --screen int8 && run product_latency_native 300 python scripts/product_latency.py --calls 300 --screen native ;;
     cfg5) run bench_cfg5 900 python bench.py --workload cfg5 --steps 10 --warmup 2 ;;
     cfg4) run bench_cfg4 900 python bench.py --workload cfg4 --steps 10 --warmup 3 --no-cpu-baseline ;;
     mix10) run bench_mix10 600 python bench.py --data mixture-sorted --sigma 1.0 --warmup 8 --no-cpu-baseline ;;

@@ -28,7 +28,7 @@ def hip_factory():
     assert vsmod._index_factory is vsmod._default_index_factory  # the HIP index, no substitute
 
 
-@pytest.mark.parametrize("screen", ["", "int8"])
+@pytest.mark.parametrize("screen", ["native", "int8"])
 @pytest.mark.parametrize("metric", ["cosine", "l2"])
 def test_vector_store_cfg1_matches_reference_wrapper(data, monkeypatch, tmp_path, metric, screen):
     monkeypatch.setenv("VECTOR_SCREEN", screen)
@@ -44,7 +44,7 @@ def test_vector_store_cfg1_matches_reference_wrapper(data, monkeypatch, tmp_path
     s2.index.close()
 
 
-@pytest.mark.parametrize("screen", ["", "int8"])
+@pytest.mark.parametrize("screen", ["native", "int8"])
 def test_vector_store_cfg1_bf16_rows(data, monkeypatch, tmp_path, screen):
     monkeypatch.setenv("VECTOR_DTYPE", "bf16")
     monkeypatch.setenv("VECTOR_SCREEN", screen)
